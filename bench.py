@@ -1,0 +1,190 @@
+"""Benchmark: CEM planning throughput (candidate-timesteps/s) on the BASELINE.json workload.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 3]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A "step" is one CEMPlanner.plan() call (I iterations of proposal draw -> rollout ->
+elite top-K -> refit, plus the final mean's rollout) on the cheetah-run config (BASELINE.json
+configs[2]: N=4096, H=30, 17/6, 3x512 MLP, I=5, K=N/10) with synthetic random weights.
+value = I * N_total * H * K_steps / (max over ranks of the timed wall clock).
+With N GPUs each rank owns 4096 candidates (weak scaling: N_total = 4096 * N); one RCCL
+all-gather of returns per CEM iteration.
+
+Extra objects on the JSON line:
+  roofline     -- the rollout kernel (dominant): algorithmic MLP FLOP per launch / average launch
+                  time from HIP events recorded on the launch stream around every rollout launch of
+                  the timed region; peak = fp32 MFMA dense 157.3 TFLOP/s (MI355X_MICROARCH.md).
+  cpu_baseline -- the CPU oracle (NumPy restatement of the reference rollout + CEM refit), rank 0,
+                  N=1 only, on a bounded sample; a reported baseline, not the target.
+  parity       -- iteration-0 returns of 256 sampled candidates re-computed by the CPU oracle.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "mujoco-mbrl_amd"))
+sys.path.insert(0, REPO)
+
+PEAK_FP32_MFMA_TFLOPS = 157.3
+ITERATIONS = 5
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=3, help="SURVEY.md §8d config id (default: cheetah-run CEM)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-bytes", type=float, default=None,
+                    help="HBM bytes per rollout launch from a rocprofv3 PMC pass (profiles/)")
+    return ap.parse_args()
+
+
+def cpu_baseline(cfg_id, budget_s=20.0):
+    """Time the CPU oracle (rank 0, N=1 only) on a bounded sample of the same workload."""
+    from oracle import cem as ocem
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    except Exception:  # pragma: no cover
+        cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    p = ocem.synth_problem(cfg_id)
+    cfg = p["cfg"]
+    N, H = cfg["N"], cfg["H"]
+    # sample: whole CEM plans at the full N and H while they fit the budget, else fewer candidates
+    t0 = time.perf_counter()
+    ocem.cem_plan(p, num_iterations=1, record=False)
+    one_iter = time.perf_counter() - t0
+    n_sample = N if one_iter * ITERATIONS <= budget_s else max(64, int(N * budget_s / (one_iter * ITERATIONS)))
+    plans, elapsed = 0, 0.0
+    while elapsed < budget_s / 2 and plans < 3:
+        t0 = time.perf_counter()
+        ocem.cem_plan(p, N=n_sample, num_iterations=ITERATIONS, record=False)
+        elapsed += time.perf_counter() - t0
+        plans += 1
+    value = ITERATIONS * n_sample * H * plans / elapsed
+    return dict(value=value, unit="candidate-timesteps/s", cores=int(cores), kind="port",
+                sample=f"{plans} full CEM plan(s) (I={ITERATIONS}, N={n_sample}, H={H}) of the NumPy oracle "
+                       f"(oracle/cem.py), fp32, {elapsed:.1f} s")
+
+
+def parity_sample(prob, res, n=256):
+    from oracle import cem as ocem
+    from oracle.philox import cem_actions
+    p = ocem.synth_problem(prob["cfg_id"])
+    cfg = p["cfg"]
+    H, a = cfg["H"], cfg["a"]
+    idx = np.sort(np.random.default_rng(0).choice(res["returns"].shape[1], size=n, replace=False))
+    A = cem_actions(np.zeros((H, a), np.float32), np.full((H, a), 0.5, np.float32), -1.0, 1.0, p["rng_seed"], 0, idx)
+    ref = ocem.ensemble_returns(ocem.rollout(p["model"], p["norm"], p["cost"], p["s0"], A)).astype(np.float64)
+    got = res["returns"][0].cpu().numpy()[idx].astype(np.float64)
+    return dict(return_mae=float(np.mean(np.abs(got - ref))),
+                return_max_rel_err=float(np.max(np.abs(got - ref) / np.maximum(np.abs(ref), 1.0))),
+                sample=f"iteration-0 returns of {n} candidates vs CPU oracle")
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from mbrl_amd import CEMPlanner, synthetic
+    prob = synthetic.make_problem(args.config)
+    prob["cfg_id"] = args.config
+    cfg = prob["cfg"]
+    n_local, H, E = cfg["N"], cfg["H"], cfg["E"]
+    N = n_local * world
+    K = N // 10
+    kw = dict(num_candidates=N, num_elites=K, num_iterations=ITERATIONS, alpha=0.1, seed=prob["rng_seed"],
+              distributed=world > 1, device=dev)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    def plan(**extra):
+        return CEMPlanner.plan_detailed(prob["s0"], prob["model"], prob["cost"], prob["sample_action"], H, **kw, **extra)
+
+    first = plan(record=True)           # also warms the weight pack / workspaces
+    for _ in range(max(0, args.warmup - 1)):
+        plan()
+    events = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(ITERATIONS)] for _ in range(args.steps)]
+    for ev in events:          # torch creates events lazily: record once so the C ABI gets live handles
+        for s_, e_ in ev:
+            s_.record()
+            e_.record()
+    barrier()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        plan(rollout_events=events[k])
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    rollout_ms = [s.elapsed_time(e) for ev in events for (s, e) in ev]
+    avg_rollout_s = float(np.mean(rollout_ms)) / 1e3
+
+    cand_steps = ITERATIONS * N * H * args.steps
+    value = cand_steps / elapsed
+    flop_launch = n_local * H * synthetic.flop_per_candidate_step(cfg)
+    achieved = flop_launch / avg_rollout_s / 1e12
+    traffic = args.traffic_bytes
+    if traffic is None:
+        prof = os.path.join(REPO, "profiles", "rollout_traffic.json")
+        if os.path.exists(prof):
+            try:
+                traffic = json.load(open(prof)).get(cfg["name"])
+            except Exception:  # pragma: no cover
+                traffic = None
+    out = {
+        "metric": "candidate-timesteps/sec (CEM NxH rollout)",
+        "value": value,
+        "unit": "candidate-timesteps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (random nn.Linear-law weights, PCG64 seed 1000+config; Philox proposals)",
+        "config": {"workload": f"{cfg['name']} CEM N={N} H={H} s={cfg['s']} a={cfg['a']} "
+                               f"{cfg['L']}x{cfg['W']} MLP E={E} I={ITERATIONS} K={K}",
+                   "candidates_per_gpu": n_local, "horizon": H, "iterations": ITERATIONS, "elites": K,
+                   "parallelism": f"candidates sharded x{world}" if world > 1 else "single GPU"},
+        "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / PEAK_FP32_MFMA_TFLOPS, "traffic": traffic,
+                     "kernel": "rollout_kernel", "avg_launch_ms": avg_rollout_s * 1e3,
+                     "flop_per_launch": flop_launch},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["parity"] = parity_sample(prob, first)
+        out["cpu_baseline"] = cpu_baseline(args.config)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

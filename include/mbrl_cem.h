@@ -1,0 +1,174 @@
+/*
+ * mbrl_cem.h -- C ABI of the MI355X (gfx950) MPC/CEM planning hot path.
+ *
+ * This is the drop-in boundary under the reference's planner API. The reference is pure
+ * Python/PyTorch-CPU and has no FFI of its own; each entry point below replaces
+ * one piece of the reference's Python call chain, cited per function. The Python host layer
+ * (mujoco-mbrl_amd/mbrl_amd) binds these with ctypes (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *   - All tensor pointers are DEVICE pointers (caller-owned HBM, e.g. torch tensors' data_ptr()),
+ *     fp32 row-major unless stated; index buffers are int64 (torch.long).
+ *   - Nothing here allocates or frees device memory, synchronises the device, or retains a pointer
+ *     after it returns; scratch comes from the caller's workspace. Every call is stream-ordered on
+ *     `stream` (a hipStream_t) and may be captured into a HIP graph.
+ *   - Return value: MBRL_OK (0) or a negative MBRL_E* code; mbrl_last_error() then holds a
+ *     thread-local message. The Python layer turns a nonzero code into RuntimeError, matching the
+ *     reference's exceptions-only convention.
+ *   - No HIP call happens at library load (fork safety: parallel.py:1-2,20-52 pickles planners
+ *     into forkserver workers).
+ */
+#ifndef MBRL_CEM_H
+#define MBRL_CEM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MBRL_ABI_VERSION 1
+
+typedef struct ihipStream_t* mbrl_stream_t; /* == hipStream_t */
+typedef struct ihipEvent_t* mbrl_event_t;   /* == hipEvent_t  */
+
+enum {
+    MBRL_OK = 0,
+    MBRL_EINVAL = -1,        /* bad argument (null pointer, non-positive size, K > N, ...) */
+    MBRL_EUNSUPPORTED = -2,  /* shape outside what the kernels are built for */
+    MBRL_EHIP = -3,          /* a HIP runtime call failed */
+    MBRL_EWORKSPACE = -4     /* workspace too small */
+};
+
+/* Cost kinds. GOAL_STATE = state_action_cost(SmoothAbsLoss, CoshLoss), agents.py:182-183,231. */
+enum { MBRL_COST_GOAL_STATE = 0 };
+
+/* Ordering of NaN returns in elite selection. */
+enum {
+    MBRL_NAN_LAST = 0,  /* np.argsort(kind="stable") order: NaN after every number (CEM elites)     */
+    MBRL_NAN_FIRST = 1  /* np.argmin order: the first NaN wins (RandomShootingPlanner, planners.py:184) */
+};
+
+/* Dynamics MLP shape: Linear(s+a -> W), ReLU, [Linear(W -> W), ReLU] x (L-1), Linear(W -> s).
+ * models.py:96-110 (Model, L = 2) generalised to L hidden layers; E ensemble members. */
+typedef struct {
+    int32_t state_dim;  /* s  (observation dim, env_wrappers.py:86 flat 'observations') */
+    int32_t action_dim; /* a */
+    int32_t hidden;     /* W  (any >= 1; zero-padded inside the packed stream) */
+    int32_t n_hidden;   /* L >= 1 */
+    int32_t ensemble;   /* E >= 1 */
+} mbrl_mlp_shape;
+
+/* Normalisation affine, TransitionsDataset.normalize_field / unnormalize_field (data.py:255-260),
+ * bound as in agents.py:219-230. A zero flag = that keyword was None in the reference call. */
+typedef struct {
+    const float* obs_mean;  /* [s] */
+    const float* obs_std;   /* [s] */
+    const float* act_mean;  /* [a] */
+    const float* act_std;   /* [a] */
+    int32_t normalize_state;
+    int32_t unnormalize_state;
+    int32_t normalize_action;
+    int32_t _pad;
+} mbrl_norm;
+
+/* Per-step cost on the (s_{t+1}, a_t) pair (planners.py:210). */
+typedef struct {
+    int32_t kind;             /* MBRL_COST_GOAL_STATE */
+    int32_t has_state_cost;   /* SmoothAbsLoss term present (models.py:244-259) */
+    int32_t has_action_cost;  /* CoshLoss term present (models.py:262-272) */
+    int32_t _pad;
+    const float* weights;     /* [s] SmoothAbsLoss.weights */
+    const float* goal;        /* [s] SmoothAbsLoss.goal_state */
+    float alpha_state;        /* SmoothAbsLoss.alpha (default 0.4) */
+    float alpha_action;       /* CoshLoss.alpha (default 0.25) */
+} mbrl_cost;
+
+/* CEM proposal: a[t][n][d] = clip(mu[t][d] + sigma[t][d] * eps, lo, hi), eps from Philox4x32-10
+ * keyed by `seed`, counter (n + n_offset, t, iteration, d >> 2). Bounds follow the reference's
+ * dim-0 action bounds [max(min[0],-3), min(max[0],3)] (env_wrappers.py:52-55). */
+typedef struct {
+    uint64_t seed;
+    int32_t iteration;
+    int32_t _pad;
+    const float* mu;     /* [H][a] */
+    const float* sigma;  /* [H][a] */
+    float lo;
+    float hi;
+} mbrl_sampler;
+
+typedef struct {
+    int32_t N;            /* candidates (global; == local when not sharded) */
+    int32_t H;            /* horizon */
+    int32_t K;            /* elites */
+    int32_t iterations;   /* I */
+    float alpha;          /* refit smoothing: mu <- alpha*mu + (1-alpha)*mu' */
+    float lo, hi;         /* action bounds */
+    float init_mu;        /* initial mean (0) */
+    float init_sigma;     /* initial std ((hi-lo)/4) */
+    int32_t _pad;
+    uint64_t seed;
+} mbrl_cem_params;
+
+int mbrl_abi_version(void);
+const char* mbrl_last_error(void);
+
+/* ---- model upload: replaces the per-call nn.Linear weight reads of Model._forward (models.py:106-110) */
+size_t mbrl_mlp_packed_bytes(const mbrl_mlp_shape* shape);
+/* weights[e*(L+1)+l] / biases[...]: DEVICE pointers to nn.Linear weight [out][in] and bias [out],
+ * passed in a HOST array. Writes the fragment-ordered weight stream the rollout kernel reads. */
+int mbrl_mlp_pack(const mbrl_mlp_shape* shape, const float* const* weights, const float* const* biases,
+                  void* packed, mbrl_stream_t stream);
+
+/* ---- rollout + cost: replaces RandomShootingPlanner._generate_trajectories' model/cost loop
+ * (planners.py:199-210) and DynamicsModel.forward (models.py:13-29) on its batch.
+ * s0: [s] broadcast to every candidate (planners.py:204) or [N][s] when s0_per_candidate.
+ * actions: [H][N][a] time-major (planners.py:200,207) or NULL to draw from `sampler`.
+ * costs: [E][N] per-member return sum_t cost(s_{t+1}, a_t), summed sequentially in t.
+ * actions_out: [H][N][a] or NULL. states_out: [E][H][N][s] or NULL.
+ * n_offset: global index of local candidate 0 (rank shard offset; keys the RNG). */
+int mbrl_rollout_cost(const mbrl_mlp_shape* shape, const void* packed, const mbrl_norm* norm,
+                      const mbrl_cost* cost, const float* s0, int32_t s0_per_candidate,
+                      const float* actions, const mbrl_sampler* sampler, int32_t N, int32_t H,
+                      int32_t n_offset, float* costs, float* actions_out, float* states_out,
+                      mbrl_stream_t stream);
+
+/* ---- selection: replaces np.argmin (planners.py:184) and adds CEM's stable top-K.
+ * returns[n] = (sum_e costs[e][n]) / E (sequential in e; = costs[0][n] when E == 1).
+ * elite_idx[0..K): the K smallest (return, index) pairs, written in ASCENDING candidate index.
+ * returns_out: [N] or NULL. workspace: >= mbrl_select_workspace_bytes(N). */
+size_t mbrl_select_workspace_bytes(int32_t N);
+int mbrl_select_elites(const float* costs, int32_t E, int32_t N, int32_t K, int32_t nan_policy,
+                       int64_t* elite_idx, float* returns_out, void* workspace, size_t ws_bytes,
+                       mbrl_stream_t stream);
+
+/* ---- CEM refit (not in the reference). Regenerates each elite's actions from
+ * the counter RNG (so every rank can refit from the global elite list with no moment collective),
+ * sums them in the canonical chunked order, writes mu' / sigma' ([H][a]). */
+size_t mbrl_refit_workspace_bytes(int32_t H, int32_t a, int32_t K);
+int mbrl_cem_refit(const mbrl_sampler* sampler, int32_t H, int32_t a, const int64_t* elite_idx,
+                   int32_t K, float alpha, float* mu_out, float* sigma_out, void* workspace,
+                   size_t ws_bytes, mbrl_stream_t stream);
+
+/* ---- proposal draw only (generic-callable path and RNG parity): actions_out [H][N][a]. */
+int mbrl_sample_actions(const mbrl_sampler* sampler, int32_t H, int32_t a, int32_t N, int32_t n_offset,
+                        float* actions_out, mbrl_stream_t stream);
+
+/* ---- whole single-GPU CEM plan: I x (rollout -> select -> refit), then the final mean's rollout.
+ * mu / sigma: [H][a] final distribution. actions_out: [H][a] = clip(mu, lo, hi);
+ * states_out: [H][s] rollout of actions_out (ensemble mean over members).
+ * cost_hist [I][E][N], returns_hist [I][N], elite_hist [I][K]: optional per-iteration records (NULL = off).
+ * rollout_events: NULL or 2*I events; pair i brackets iteration i's rollout launch on `stream`. */
+size_t mbrl_cem_workspace_bytes(const mbrl_mlp_shape* shape, const mbrl_cem_params* params);
+int mbrl_cem_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_norm* norm,
+                  const mbrl_cost* cost, const float* s0, const mbrl_cem_params* params,
+                  float* mu, float* sigma, float* actions_out, float* states_out,
+                  float* cost_hist, float* returns_hist, int64_t* elite_hist,
+                  mbrl_event_t* rollout_events, void* workspace, size_t ws_bytes,
+                  mbrl_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MBRL_CEM_H */

@@ -1,0 +1,560 @@
+// Weight packing, elite selection, CEM refit, proposal sampling and the extern "C" ABI
+// (include/mbrl_cem.h).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdarg.h>
+#include <stdio.h>
+
+#include <string>
+
+#include "../../include/mbrl_cem.h"
+#include "mbrl_internal.h"
+#include "mbrl_rng.h"
+
+namespace mbrl {
+
+static thread_local std::string g_err;
+
+static int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+static int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+static int hip_check(hipError_t e, const char* what) {
+    if (e == hipSuccess) return MBRL_OK;
+    return fail(MBRL_EHIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+// ------------------------------------------------------------------------------------------------
+// Weight packing: nn.Linear [out][in] -> fragment stream (see rollout.hip header)
+// ------------------------------------------------------------------------------------------------
+// Hidden-type layer (layer 0 or W->W): chunk kc holds K rows 16kc..16kc+15 for this wave's T tiles.
+__global__ void pack_hidden_kernel(const float* __restrict__ w, int in_real, int out_real, int nkc, int T,
+                                   float* __restrict__ dst /* chunk base */) {
+    const size_t total = (size_t)nkc * 4 * T * 64 * 4;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const int s = (int)(i & 3);
+        const int lane = (int)((i >> 2) & 63);
+        const size_t frag = i >> 8;           // (kc * 4 + wave) * T + j
+        const int j = (int)(frag % T);
+        const int wave = (int)((frag / T) & 3);
+        const int kc = (int)(frag / T / 4);
+        const int n = wave * 16 * T + 16 * j + (lane & 15);
+        const int k = 16 * kc + 4 * (lane >> 4) + s;
+        dst[i] = (n < out_real && k < in_real) ? w[(size_t)n * in_real + k] : 0.0f;
+    }
+}
+
+// Output layer: chunk j = output tile j; fragment kc covers this wave's K rows w*16T + 16kc + ...
+__global__ void pack_out_kernel(const float* __restrict__ w, int in_real, int out_real, int NOT, int T,
+                                float* __restrict__ dst) {
+    const size_t total = (size_t)NOT * 4 * T * 64 * 4;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const int s = (int)(i & 3);
+        const int lane = (int)((i >> 2) & 63);
+        const size_t frag = i >> 8;           // (j * 4 + wave) * T + kc
+        const int kc = (int)(frag % T);
+        const int wave = (int)((frag / T) & 3);
+        const int j = (int)(frag / T / 4);
+        const int n = 16 * j + (lane & 15);
+        const int k = wave * 16 * T + 16 * kc + 4 * (lane >> 4) + s;
+        dst[i] = (n < out_real && k < in_real) ? w[(size_t)n * in_real + k] : 0.0f;
+    }
+}
+
+__global__ void pack_bias_kernel(const float* __restrict__ b, int n_real, int n_pad, float* __restrict__ dst) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n_pad; i += gridDim.x * blockDim.x)
+        dst[i] = i < n_real ? b[i] : 0.0f;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Block scan helper (exclusive), blockDim.x multiple of 64, <= 1024
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* lds_waves, uint32_t* total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) lds_waves[wave] = x;
+    __syncthreads();
+    if (wave == 0) {
+        uint32_t w = lane < nw ? lds_waves[lane] : 0u;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(w, o, 64);
+            if (lane >= o) w += y;
+        }
+        if (lane < nw) lds_waves[lane] = w;  // inclusive wave prefix
+    }
+    __syncthreads();
+    const uint32_t before = wave > 0 ? lds_waves[wave - 1] : 0u;
+    *total = lds_waves[nw - 1];
+    __syncthreads();
+    return before + x - v;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Elite selection: returns -> order keys -> radix select of the K-th key -> stable tie break by
+// index -> compaction in ascending index order. One workgroup of 1024 threads (N is small:
+// 1e3..3e4 candidates; the pass is a few microseconds).
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t order_key(float v, int nan_policy) {
+    if (v != v) return nan_policy == MBRL_NAN_LAST ? 0xFFFFFFFFu : 0u;
+    if (v == 0.0f) v = 0.0f;  // -0.0 ties with +0.0, as in NumPy's comparisons
+    const uint32_t b = __float_as_uint(v);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+
+__global__ void __launch_bounds__(1024) select_kernel(const float* __restrict__ costs, int E, int N, int K,
+                                                      int nan_policy, int64_t* __restrict__ elite_idx,
+                                                      float* __restrict__ returns_out, uint32_t* __restrict__ keys) {
+    __shared__ uint32_t hist[256];
+    __shared__ uint32_t scan_ws[16];
+    __shared__ uint32_t sel[3];  // prefix, bucket, remaining k
+    const int tid = threadIdx.x, nt = blockDim.x;
+    for (int n = tid; n < N; n += nt) {
+        float r = costs[n];
+        if (E > 1) {
+            for (int e = 1; e < E; ++e) r = __fadd_rn(r, costs[(size_t)e * N + n]);
+            r = __fdiv_rn(r, (float)E);
+        }
+        if (returns_out) returns_out[n] = r;
+        keys[n] = order_key(r, nan_policy);
+    }
+    uint32_t prefix = 0, mask = 0, kk = (uint32_t)K;
+    __syncthreads();
+    for (int shift = 24; shift >= 0; shift -= 8) {
+        if (tid < 256) hist[tid] = 0;
+        __syncthreads();
+        for (int n = tid; n < N; n += nt) {
+            const uint32_t k = keys[n];
+            if ((k & mask) == prefix) atomicAdd(&hist[(k >> shift) & 255u], 1u);
+        }
+        __syncthreads();
+        uint32_t tot;
+        const uint32_t h = tid < 256 ? hist[tid] : 0u;
+        const uint32_t before = block_exclusive_scan(h, scan_ws, &tot);
+        if (tid < 256 && before < kk && before + h >= kk) { sel[0] = (uint32_t)tid; sel[1] = before; }
+        __syncthreads();
+        prefix |= sel[0] << shift;
+        mask |= 0xFFu << shift;
+        kk -= sel[1];
+        __syncthreads();
+    }
+    // prefix = K-th smallest key; kk = how many of the keys equal to it are elites (lowest index first)
+    const int seg = (N + nt - 1) / nt;
+    const int n0 = tid * seg, n1 = min(N, n0 + seg);
+    uint32_t eq = 0;
+    for (int n = n0; n < n1; ++n) eq += keys[n] == prefix;
+    uint32_t tot;
+    uint32_t eq_before = block_exclusive_scan(eq, scan_ws, &tot);
+    uint32_t cnt = 0;
+    for (int n = n0; n < n1; ++n) {
+        const uint32_t k = keys[n];
+        if (k < prefix) ++cnt;
+        else if (k == prefix) { if (eq_before < kk) ++cnt; ++eq_before; }
+    }
+    eq_before -= eq;
+    uint32_t pos = block_exclusive_scan(cnt, scan_ws, &tot);
+    for (int n = n0; n < n1; ++n) {
+        const uint32_t k = keys[n];
+        bool take = false;
+        if (k < prefix) take = true;
+        else if (k == prefix) { take = eq_before < kk; ++eq_before; }
+        if (take && pos < (uint32_t)K) elite_idx[pos++] = n;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// CEM refit. gather: regenerate every elite's a_t from the counter RNG into aelite[t][e][a].
+// refit: canonical chunked sums (ELITE_CHUNK = 32, oracle/cem.py:chunked_sum) -> mean, population
+// variance -> alpha-smoothed mu / sigma. All float ops correctly rounded, no contraction.
+// ------------------------------------------------------------------------------------------------
+constexpr int ELITE_CHUNK = 32;
+
+__global__ void gather_elites_kernel(uint64_t seed, int iteration, const float* __restrict__ mu,
+                                     const float* __restrict__ sigma, float lo, float hi, int a,
+                                     const int64_t* __restrict__ elite_idx, int K, float* __restrict__ aelite) {
+    const int t = blockIdx.y;
+    const int G = (a + 3) >> 2;
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= K * G) return;
+    const int e = idx / G, g = idx - (idx / G) * G;
+    float z[4];
+    cem_normal4(seed, (uint32_t)elite_idx[e], (uint32_t)t, (uint32_t)iteration, (uint32_t)g, z);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int d = 4 * g + j;
+        if (d < a) aelite[((size_t)t * K + e) * a + d] = cem_action(mu[t * a + d], sigma[t * a + d], z[j], lo, hi);
+    }
+}
+
+__global__ void refit_kernel(const float* __restrict__ aelite, int a, int K, float alpha, float oma,
+                             const float* __restrict__ mu, const float* __restrict__ sigma,
+                             float* __restrict__ mu_out, float* __restrict__ sigma_out) {
+#pragma clang fp contract(off)
+    extern __shared__ float part[];  // [nch][a]
+    __shared__ float mean[64];
+    const int t = blockIdx.x;
+    const int nch = (K + ELITE_CHUNK - 1) / ELITE_CHUNK;
+    const float* A = aelite + (size_t)t * K * a;
+    for (int pass = 0; pass < 2; ++pass) {
+        for (int idx = threadIdx.x; idx < nch * a; idx += blockDim.x) {
+            const int c = idx / a, d = idx - (idx / a) * a;
+            const int e0 = c * ELITE_CHUNK, e1 = min(K, e0 + ELITE_CHUNK);
+            float acc = 0.f;
+            for (int e = e0; e < e1; ++e) {
+                float v = A[(size_t)e * a + d];
+                if (pass == 1) { const float df = __fadd_rn(v, -mean[d]); v = __fmul_rn(df, df); }
+                acc = (e == e0) ? v : __fadd_rn(acc, v);
+            }
+            part[c * a + d] = acc;
+        }
+        __syncthreads();
+        if ((int)threadIdx.x < a) {
+            const int d = threadIdx.x;
+            float tot = part[d];
+            for (int c = 1; c < nch; ++c) tot = __fadd_rn(tot, part[c * a + d]);
+            const float m = __fdiv_rn(tot, (float)K);
+            if (pass == 0) {
+                mean[d] = m;
+            } else {
+                const float mu0 = mu[t * a + d], s0 = sigma[t * a + d];
+                mu_out[t * a + d] = __fadd_rn(__fmul_rn(alpha, mu0), __fmul_rn(oma, mean[d]));
+                const float v = __fadd_rn(__fmul_rn(alpha, __fmul_rn(s0, s0)), __fmul_rn(oma, m));
+                sigma_out[t * a + d] = __fsqrt_rn(v);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void sample_kernel(uint64_t seed, int iteration, const float* __restrict__ mu,
+                              const float* __restrict__ sigma, float lo, float hi, int H, int a, int N,
+                              int n_offset, float* __restrict__ out) {
+    const int G = (a + 3) >> 2;
+    const size_t total = (size_t)H * N * G;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const int g = (int)(i % G);
+        const int n = (int)((i / G) % N);
+        const int t = (int)(i / G / N);
+        float z[4];
+        cem_normal4(seed, (uint32_t)(n_offset + n), (uint32_t)t, (uint32_t)iteration, (uint32_t)g, z);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int d = 4 * g + j;
+            if (d < a) out[((size_t)t * N + n) * a + d] = cem_action(mu[t * a + d], sigma[t * a + d], z[j], lo, hi);
+        }
+    }
+}
+
+__global__ void fill2_kernel(float* __restrict__ x, float vx, float* __restrict__ y, float vy, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) { x[i] = vx; y[i] = vy; }
+}
+
+__global__ void finalize_kernel(const float* __restrict__ mu_src, const float* __restrict__ sg_src, float lo,
+                                float hi, int n, float* __restrict__ mu, float* __restrict__ sigma,
+                                float* __restrict__ actions) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        const float m = mu_src[i];
+        if (mu) mu[i] = m;
+        if (sigma) sigma[i] = sg_src[i];
+        actions[i] = fminf(fmaxf(m, lo), hi);
+    }
+}
+
+__global__ void member_mean_kernel(const float* __restrict__ src, int E, int n, float* __restrict__ dst) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        float acc = src[i];
+        for (int e = 1; e < E; ++e) acc = __fadd_rn(acc, src[(size_t)e * n + i]);
+        dst[i] = E > 1 ? __fdiv_rn(acc, (float)E) : acc;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Host helpers
+// ------------------------------------------------------------------------------------------------
+static int shape_geometry(const mbrl_mlp_shape* sh, Geometry* g) {
+    if (!sh) return fail(MBRL_EINVAL, "shape is NULL");
+    if (!make_geometry(sh->state_dim, sh->action_dim, sh->hidden, sh->n_hidden, sh->ensemble, g))
+        return fail(MBRL_EUNSUPPORTED, "unsupported MLP shape s=%d a=%d W=%d L=%d E=%d (need all >= 1, W <= 1024)",
+                    sh->state_dim, sh->action_dim, sh->hidden, sh->n_hidden, sh->ensemble);
+    return MBRL_OK;
+}
+
+static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+static int rollout_impl(const Geometry& g, const void* packed, const mbrl_norm* norm, const mbrl_cost* cost,
+                        const float* s0, int s0_per_cand, const float* actions, const mbrl_sampler* sampler,
+                        int N, int H, int n_offset, float* costs, float* actions_out, float* states_out,
+                        hipStream_t stream) {
+    if (!packed || !s0 || !costs) return fail(MBRL_EINVAL, "packed, s0 and costs must be non-NULL");
+    if (N < 1 || H < 1) return fail(MBRL_EINVAL, "N=%d H=%d must be >= 1", N, H);
+    if (!actions && !sampler) return fail(MBRL_EINVAL, "need either actions or a sampler");
+    if (n_offset < 0) return fail(MBRL_EINVAL, "n_offset=%d < 0", n_offset);
+    RolloutArgs A{};
+    A.packed = static_cast<const float*>(packed);
+    A.member_stride = g.member_stride;
+    A.stream_floats = g.stream_floats;
+    A.s = g.s; A.a = g.a; A.L = g.L; A.Wpad = g.Wpad; A.K0C = g.K0C; A.NOT = g.NOT; A.E = g.E;
+    A.chunks_per_step = g.C; A.lda = g.lda; A.pw = g.pw; A.k0pad_extra = 16 * g.K0C - g.s - g.a;
+    A.N = N; A.H = H; A.n_offset = n_offset;
+    if (norm) {
+        A.obs_mean = norm->obs_mean; A.obs_std = norm->obs_std;
+        A.act_mean = norm->act_mean; A.act_std = norm->act_std;
+        A.norm_s = norm->normalize_state; A.unnorm_s = norm->unnormalize_state; A.norm_a = norm->normalize_action;
+        if ((A.norm_s || A.unnorm_s) && (!A.obs_mean || !A.obs_std))
+            return fail(MBRL_EINVAL, "state normalisation requested without obs_mean/obs_std");
+        if (A.norm_a && (!A.act_mean || !A.act_std))
+            return fail(MBRL_EINVAL, "action normalisation requested without act_mean/act_std");
+    }
+    if (cost) {
+        if (cost->kind != MBRL_COST_GOAL_STATE) return fail(MBRL_EUNSUPPORTED, "cost kind %d", cost->kind);
+        A.has_sc = cost->has_state_cost; A.has_ac = cost->has_action_cost;
+        A.cw = cost->weights; A.goal = cost->goal;
+        A.alpha_s = cost->alpha_state; A.alpha_s2 = cost->alpha_state * cost->alpha_state;
+        A.alpha_a = cost->alpha_action; A.alpha_a2 = cost->alpha_action * cost->alpha_action;
+        if (A.has_sc && (!A.cw || !A.goal)) return fail(MBRL_EINVAL, "state cost without weights/goal");
+    }
+    A.s0 = s0; A.s0_per_cand = s0_per_cand;
+    A.actions = actions;
+    if (!actions) {
+        A.seed = sampler->seed; A.iteration = sampler->iteration;
+        A.mu = sampler->mu; A.sigma = sampler->sigma; A.lo = sampler->lo; A.hi = sampler->hi;
+        if (!A.mu || !A.sigma) return fail(MBRL_EINVAL, "sampler mu/sigma NULL");
+    }
+    A.costs = costs; A.actions_out = actions_out; A.states_out = states_out;
+    // Tile height: two 16-row blocks per workgroup halve the weight stream per FLOP once there are
+    // enough candidates to still give every CU a workgroup.
+    int R = (N >= 2 * 16 * 256 && g.T <= 8) ? 2 : 1;
+    const int G = (g.a + 3) / 4;
+    if (16 * R * G > 192) R = 1;
+    if (16 * G > 192) return fail(MBRL_EUNSUPPORTED, "action_dim %d too large (max 48)", g.a);
+    if (rollout_lds_bytes(A, 16 * R) > 160 * 1024) {
+        R = 1;
+        if (rollout_lds_bytes(A, 16) > 160 * 1024)
+            return fail(MBRL_EUNSUPPORTED, "LDS footprint %zu B exceeds 160 KiB", rollout_lds_bytes(A, 16));
+    }
+    return hip_check(launch_rollout(A, g.T, R, stream), "rollout launch");
+}
+
+static int select_impl(const float* costs, int E, int N, int K, int nan_policy, int64_t* elite_idx,
+                       float* returns_out, void* ws, size_t ws_bytes, hipStream_t stream) {
+    if (!costs || !elite_idx || !ws) return fail(MBRL_EINVAL, "costs, elite_idx and workspace must be non-NULL");
+    if (N < 1 || K < 1 || K > N || E < 1) return fail(MBRL_EINVAL, "need 1 <= K (%d) <= N (%d), E >= 1", K, N);
+    if (ws_bytes < align256((size_t)N * 4)) return fail(MBRL_EWORKSPACE, "select workspace %zu < %zu", ws_bytes, align256((size_t)N * 4));
+    hipLaunchKernelGGL(select_kernel, dim3(1), dim3(1024), 0, stream, costs, E, N, K, nan_policy, elite_idx,
+                       returns_out, static_cast<uint32_t*>(ws));
+    return hip_check(hipGetLastError(), "select launch");
+}
+
+static int refit_impl(const mbrl_sampler* sp, int H, int a, const int64_t* elite_idx, int K, float alpha,
+                      float* aelite, float* mu_out, float* sigma_out, hipStream_t stream) {
+    if (!sp || !sp->mu || !sp->sigma || !elite_idx || !mu_out || !sigma_out || !aelite)
+        return fail(MBRL_EINVAL, "refit: NULL argument");
+    if (H < 1 || a < 1 || a > 64 || K < 1) return fail(MBRL_EINVAL, "refit: H=%d a=%d K=%d", H, a, K);
+    if ((size_t)((K + ELITE_CHUNK - 1) / ELITE_CHUNK) * a * sizeof(float) > 64 * 1024)
+        return fail(MBRL_EUNSUPPORTED, "refit: K=%d x a=%d exceeds the refit kernel's LDS", K, a);
+    const int G = (a + 3) / 4;
+    hipLaunchKernelGGL(gather_elites_kernel, dim3((K * G + 255) / 256, H), dim3(256), 0, stream, sp->seed,
+                       sp->iteration, sp->mu, sp->sigma, sp->lo, sp->hi, a, elite_idx, K, aelite);
+    const int nch = (K + ELITE_CHUNK - 1) / ELITE_CHUNK;
+    const float oma = 1.0f - alpha;
+    hipLaunchKernelGGL(refit_kernel, dim3(H), dim3(256), (size_t)nch * a * sizeof(float), stream, aelite, a, K,
+                       alpha, oma, sp->mu, sp->sigma, mu_out, sigma_out);
+    return hip_check(hipGetLastError(), "refit launch");
+}
+
+}  // namespace mbrl
+
+using namespace mbrl;
+
+// ================================================================================================
+// extern "C" ABI
+// ================================================================================================
+extern "C" {
+
+int mbrl_abi_version(void) { return MBRL_ABI_VERSION; }
+
+const char* mbrl_last_error(void) { return g_err.c_str(); }
+
+size_t mbrl_mlp_packed_bytes(const mbrl_mlp_shape* shape) {
+    Geometry g;
+    if (shape_geometry(shape, &g) != MBRL_OK) return 0;
+    return g.member_stride * (size_t)g.E * sizeof(float);
+}
+
+int mbrl_mlp_pack(const mbrl_mlp_shape* shape, const float* const* weights, const float* const* biases,
+                  void* packed, mbrl_stream_t stream_) {
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
+    Geometry g;
+    int rc = shape_geometry(shape, &g);
+    if (rc) return rc;
+    if (!weights || !biases || !packed) return fail(MBRL_EINVAL, "pack: NULL argument");
+    const int nl = g.L + 1;
+    for (int e = 0; e < g.E; ++e) {
+        float* base = static_cast<float*>(packed) + (size_t)e * g.member_stride;
+        float* bias_base = base + g.stream_floats;
+        size_t chunk = 0;
+        for (int l = 0; l < nl; ++l) {
+            const float* w = weights[e * nl + l];
+            const float* b = biases[e * nl + l];
+            if (!w || !b) return fail(MBRL_EINVAL, "pack: NULL weight/bias for member %d layer %d", e, l);
+            float* dst = base + chunk * 1024 * g.T;
+            if (l < g.L) {
+                const int in_real = l == 0 ? g.s + g.a : g.W;
+                const int nkc = l == 0 ? g.K0C : 4 * g.T;
+                hipLaunchKernelGGL(pack_hidden_kernel, dim3(256), dim3(256), 0, stream, w, in_real, g.W, nkc, g.T, dst);
+                hipLaunchKernelGGL(pack_bias_kernel, dim3(4), dim3(256), 0, stream, b, g.W, g.Wpad, bias_base + (size_t)l * g.Wpad);
+                chunk += nkc;
+            } else {
+                hipLaunchKernelGGL(pack_out_kernel, dim3(256), dim3(256), 0, stream, w, g.W, g.s, g.NOT, g.T, dst);
+                hipLaunchKernelGGL(pack_bias_kernel, dim3(1), dim3(256), 0, stream, b, g.s, 16 * g.NOT,
+                                   bias_base + (size_t)g.L * g.Wpad);
+                chunk += g.NOT;
+            }
+        }
+    }
+    return hip_check(hipGetLastError(), "pack launch");
+}
+
+int mbrl_rollout_cost(const mbrl_mlp_shape* shape, const void* packed, const mbrl_norm* norm, const mbrl_cost* cost,
+                      const float* s0, int32_t s0_per_candidate, const float* actions, const mbrl_sampler* sampler,
+                      int32_t N, int32_t H, int32_t n_offset, float* costs, float* actions_out, float* states_out,
+                      mbrl_stream_t stream) {
+    Geometry g;
+    int rc = shape_geometry(shape, &g);
+    if (rc) return rc;
+    return rollout_impl(g, packed, norm, cost, s0, s0_per_candidate, actions, sampler, N, H, n_offset, costs,
+                        actions_out, states_out, reinterpret_cast<hipStream_t>(stream));
+}
+
+size_t mbrl_select_workspace_bytes(int32_t N) { return align256((size_t)(N > 0 ? N : 1) * 4); }
+
+int mbrl_select_elites(const float* costs, int32_t E, int32_t N, int32_t K, int32_t nan_policy, int64_t* elite_idx,
+                       float* returns_out, void* workspace, size_t ws_bytes, mbrl_stream_t stream) {
+    return select_impl(costs, E, N, K, nan_policy, elite_idx, returns_out, workspace, ws_bytes,
+                       reinterpret_cast<hipStream_t>(stream));
+}
+
+size_t mbrl_refit_workspace_bytes(int32_t H, int32_t a, int32_t K) {
+    return align256((size_t)(H > 0 ? H : 1) * (K > 0 ? K : 1) * (a > 0 ? a : 1) * sizeof(float));
+}
+
+int mbrl_cem_refit(const mbrl_sampler* sampler, int32_t H, int32_t a, const int64_t* elite_idx, int32_t K, float alpha,
+                   float* mu_out, float* sigma_out, void* workspace, size_t ws_bytes, mbrl_stream_t stream) {
+    if (!workspace) return fail(MBRL_EINVAL, "refit: workspace is NULL");
+    if (ws_bytes < mbrl_refit_workspace_bytes(H, a, K))
+        return fail(MBRL_EWORKSPACE, "refit workspace %zu < %zu", ws_bytes, mbrl_refit_workspace_bytes(H, a, K));
+    return refit_impl(sampler, H, a, elite_idx, K, alpha, static_cast<float*>(workspace), mu_out, sigma_out,
+                      reinterpret_cast<hipStream_t>(stream));
+}
+
+int mbrl_sample_actions(const mbrl_sampler* sampler, int32_t H, int32_t a, int32_t N, int32_t n_offset,
+                        float* actions_out, mbrl_stream_t stream) {
+    if (!sampler || !sampler->mu || !sampler->sigma || !actions_out) return fail(MBRL_EINVAL, "sample: NULL argument");
+    if (H < 1 || a < 1 || N < 1 || n_offset < 0) return fail(MBRL_EINVAL, "sample: bad sizes");
+    const size_t total = (size_t)H * N * ((a + 3) / 4);
+    const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+    hipLaunchKernelGGL(sample_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                       sampler->seed, sampler->iteration, sampler->mu, sampler->sigma, sampler->lo, sampler->hi,
+                       H, a, N, n_offset, actions_out);
+    return hip_check(hipGetLastError(), "sample launch");
+}
+
+// Workspace layout for mbrl_cem_plan.
+struct PlanWs {
+    float *costs, *mu[2], *sigma[2], *aelite, *states, *tmp_cost;
+    int64_t* elites;
+    uint32_t* keys;
+    size_t bytes;
+};
+
+static PlanWs plan_ws(const Geometry& g, const mbrl_cem_params* p, void* base) {
+    PlanWs w{};
+    char* b = static_cast<char*>(base);
+    size_t o = 0;
+    auto take = [&](size_t n) { void* r = b ? b + o : nullptr; o += align256(n); return r; };
+    const size_t Ha = (size_t)p->H * g.a;
+    w.costs = (float*)take((size_t)g.E * p->N * 4);
+    w.mu[0] = (float*)take(Ha * 4); w.mu[1] = (float*)take(Ha * 4);
+    w.sigma[0] = (float*)take(Ha * 4); w.sigma[1] = (float*)take(Ha * 4);
+    w.aelite = (float*)take((size_t)p->H * p->K * g.a * 4);
+    w.states = (float*)take((size_t)g.E * p->H * g.s * 4);
+    w.tmp_cost = (float*)take((size_t)g.E * 4);
+    w.elites = (int64_t*)take((size_t)p->K * 8);
+    w.keys = (uint32_t*)take((size_t)p->N * 4);
+    w.bytes = o;
+    return w;
+}
+
+size_t mbrl_cem_workspace_bytes(const mbrl_mlp_shape* shape, const mbrl_cem_params* params) {
+    Geometry g;
+    if (shape_geometry(shape, &g) != MBRL_OK || !params) return 0;
+    return plan_ws(g, params, nullptr).bytes;
+}
+
+int mbrl_cem_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_norm* norm, const mbrl_cost* cost,
+                  const float* s0, const mbrl_cem_params* p, float* mu, float* sigma, float* actions_out,
+                  float* states_out, float* cost_hist, float* returns_hist, int64_t* elite_hist,
+                  mbrl_event_t* rollout_events, void* workspace, size_t ws_bytes, mbrl_stream_t stream_) {
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
+    Geometry g;
+    int rc = shape_geometry(shape, &g);
+    if (rc) return rc;
+    if (!p) return fail(MBRL_EINVAL, "params is NULL");
+    if (p->N < 1 || p->H < 1 || p->K < 1 || p->K > p->N || p->iterations < 1)
+        return fail(MBRL_EINVAL, "bad CEM params N=%d H=%d K=%d I=%d", p->N, p->H, p->K, p->iterations);
+    if (!actions_out || !states_out || !workspace) return fail(MBRL_EINVAL, "actions_out/states_out/workspace NULL");
+    PlanWs w = plan_ws(g, p, workspace);
+    if (ws_bytes < w.bytes) return fail(MBRL_EWORKSPACE, "workspace %zu < %zu", ws_bytes, w.bytes);
+    const int Ha = p->H * g.a;
+    hipLaunchKernelGGL(fill2_kernel, dim3((Ha + 255) / 256), dim3(256), 0, stream, w.mu[0], p->init_mu, w.sigma[0],
+                       p->init_sigma, Ha);
+    int cur = 0;
+    for (int it = 0; it < p->iterations; ++it) {
+        mbrl_sampler sp{};
+        sp.seed = p->seed; sp.iteration = it; sp.mu = w.mu[cur]; sp.sigma = w.sigma[cur]; sp.lo = p->lo; sp.hi = p->hi;
+        float* costs = cost_hist ? cost_hist + (size_t)it * g.E * p->N : w.costs;
+        int64_t* elites = elite_hist ? elite_hist + (size_t)it * p->K : w.elites;
+        float* rets = returns_hist ? returns_hist + (size_t)it * p->N : nullptr;
+        if (rollout_events) {
+            rc = hip_check(hipEventRecord(reinterpret_cast<hipEvent_t>(rollout_events[2 * it]), stream), "event");
+            if (rc) return rc;
+        }
+        rc = rollout_impl(g, packed, norm, cost, s0, 0, nullptr, &sp, p->N, p->H, 0, costs, nullptr, nullptr, stream);
+        if (rc) return rc;
+        if (rollout_events) {
+            rc = hip_check(hipEventRecord(reinterpret_cast<hipEvent_t>(rollout_events[2 * it + 1]), stream), "event");
+            if (rc) return rc;
+        }
+        rc = select_impl(costs, g.E, p->N, p->K, MBRL_NAN_LAST, elites, rets, w.keys, align256((size_t)p->N * 4), stream);
+        if (rc) return rc;
+        rc = refit_impl(&sp, p->H, g.a, elites, p->K, p->alpha, w.aelite, w.mu[cur ^ 1], w.sigma[cur ^ 1], stream);
+        if (rc) return rc;
+        cur ^= 1;
+    }
+    hipLaunchKernelGGL(finalize_kernel, dim3((Ha + 255) / 256), dim3(256), 0, stream, w.mu[cur], w.sigma[cur], p->lo,
+                       p->hi, Ha, mu, sigma, actions_out);
+    // final mean's rollout -> predicted states [E][H][1][s], then the member mean
+    rc = rollout_impl(g, packed, norm, cost, s0, 0, actions_out, nullptr, 1, p->H, 0, w.tmp_cost, nullptr, w.states,
+                      stream);
+    if (rc) return rc;
+    const int Hs = p->H * g.s;
+    hipLaunchKernelGGL(member_mean_kernel, dim3((Hs + 255) / 256), dim3(256), 0, stream, w.states, g.E, Hs, states_out);
+    return hip_check(hipGetLastError(), "plan launch");
+}
+
+}  // extern "C"

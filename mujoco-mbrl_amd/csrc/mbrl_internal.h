@@ -1,0 +1,111 @@
+// Internal kernel-argument structs and the geometry shared by the pack kernels, the rollout kernel
+// and the host launcher. Not part of the public ABI (include/mbrl_cem.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace mbrl {
+
+// Packed-stream geometry for one MLP shape (DESIGN.md §2 "weight stream").
+struct Geometry {
+    int s, a, W, L, E;
+    int T;          // 16-column tiles per wave per hidden layer; Wpad = 64 * T
+    int Wpad;
+    int K0C;        // layer-0 K chunks of 16 (even)
+    int NOT;        // output tiles of 16 (even)
+    int C;          // chunks per step = K0C + (L-1)*4T + NOT
+    int lda;        // LDS activation row stride (floats)
+    int pw;         // LDS output-partial row stride (floats)
+    size_t stream_floats;  // C * 1024 * T
+    size_t bias_floats;    // L * Wpad + 16 * NOT
+    size_t member_stride;  // floats per ensemble member (64-float aligned)
+};
+
+inline int round_even(int x) { return (x + 1) & ~1; }
+
+inline bool make_geometry(int s, int a, int W, int L, int E, Geometry* g) {
+    if (s < 1 || a < 1 || W < 1 || L < 1 || E < 1) return false;
+    int T = 1;
+    while (64 * T < W) T *= 2;
+    if (T > 16) return false;
+    g->s = s; g->a = a; g->W = W; g->L = L; g->E = E;
+    g->T = T;
+    g->Wpad = 64 * T;
+    g->K0C = round_even((s + a + 15) / 16);
+    g->NOT = round_even((s + 15) / 16);
+    if (g->NOT > 2 * 4 * T * 4) return false;
+    g->C = g->K0C + (L - 1) * 4 * T + g->NOT;
+    const int k0 = 16 * g->K0C;
+    g->lda = (g->Wpad > k0 ? g->Wpad : k0) + 4;
+    g->pw = 16 * g->NOT + 4;
+    g->stream_floats = (size_t)g->C * 1024 * T;
+    g->bias_floats = (size_t)L * g->Wpad + 16 * (size_t)g->NOT;
+    g->member_stride = (g->stream_floats + g->bias_floats + 63) / 64 * 64;
+    return true;
+}
+
+struct RolloutArgs {
+    const float* packed;
+    size_t member_stride;
+    size_t stream_floats;
+    int s, a, L, Wpad, K0C, NOT, E, chunks_per_step, lda, pw, k0pad_extra;
+    int N, H, n_offset;
+    const float *obs_mean, *obs_std, *act_mean, *act_std;
+    int norm_s, unnorm_s, norm_a;
+    const float *cw, *goal;
+    float alpha_s, alpha_s2, alpha_a, alpha_a2;
+    int has_sc, has_ac;
+    const float* s0;
+    int s0_per_cand;
+    const float* actions;  // given [H][N][a] or nullptr -> sampled
+    uint64_t seed;
+    int iteration;
+    const float* mu;
+    const float* sigma;
+    float lo, hi;
+    float* costs;
+    float* actions_out;
+    float* states_out;
+};
+
+struct LdsMap {
+    float *act, *part, *sterm, *aterm, *obs_mean, *obs_std, *act_mean, *act_std, *goal, *cw, *hbias, *mu,
+        *sigma;
+    size_t total_floats;
+};
+
+__host__ __device__ inline size_t lds_round4(size_t x) { return (x + 3) & ~(size_t)3; }
+
+__host__ __device__ inline LdsMap lds_map(const RolloutArgs& A, float* base, int M) {
+    LdsMap L;
+    size_t o = 0;
+    auto take = [&](size_t n) { float* p = base ? base + o : nullptr; o += lds_round4(n); return p; };
+    L.act = take((size_t)M * A.lda);
+    L.part = take((size_t)4 * M * A.pw);
+    L.sterm = take((size_t)M * A.s);
+    L.aterm = take((size_t)2 * M * A.a);
+    L.obs_mean = take(A.s);
+    L.obs_std = take(A.s);
+    L.act_mean = take(A.a);
+    L.act_std = take(A.a);
+    L.goal = take(A.s);
+    L.cw = take(A.s);
+    L.hbias = take((size_t)A.L * A.Wpad + 16 * (size_t)A.NOT);
+    L.mu = take(A.actions ? 0 : (size_t)A.H * A.a);
+    L.sigma = take(A.actions ? 0 : (size_t)A.H * A.a);
+    L.total_floats = o;
+    return L;
+}
+
+// At least 82 KiB so that one workgroup owns a CU: 256 workgroups of N = 4096 then land one per CU
+// instead of doubling up on some CUs (the kernel is sized for one wave per SIMD).
+inline size_t rollout_lds_bytes(const RolloutArgs& A, int M) {
+    const size_t need = lds_map(A, nullptr, M).total_floats * sizeof(float);
+    const size_t floor_bytes = 82 * 1024;
+    return need > floor_bytes ? need : floor_bytes;
+}
+
+hipError_t launch_rollout(const RolloutArgs& A, int T, int R, hipStream_t stream);
+
+}  // namespace mbrl

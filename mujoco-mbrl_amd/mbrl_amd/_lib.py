@@ -1,0 +1,123 @@
+"""ctypes binding of the HIP extension's C ABI (include/mbrl_cem.h).
+
+The library is built in-tree (`make -C mujoco-mbrl_amd`, or `__graft_entry__.build()`) and loaded
+from this directory. There is no fallback: if the library is missing every fused entry point
+raises, so a GPU run can never silently take a CPU path.
+
+torch is imported first on purpose: torch's bundled libamdhip64 and /opt/rocm's share the soname
+libamdhip64.so.7, so the extension binds to the runtime torch already loaded and the stream handles
+it receives (torch.cuda.current_stream().cuda_stream) are valid for it.
+"""
+import ctypes
+import os
+from ctypes import POINTER, c_float, c_int32, c_int64, c_size_t, c_uint64, c_void_p
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmbrl_cem.so")
+
+MBRL_OK = 0
+MBRL_COST_GOAL_STATE = 0
+MBRL_NAN_LAST = 0
+MBRL_NAN_FIRST = 1
+
+# Every symbol include/mbrl_cem.h declares (tests/test_abi.py checks the two lists agree).
+EXPORTED = (
+    "mbrl_abi_version", "mbrl_last_error", "mbrl_mlp_packed_bytes", "mbrl_mlp_pack",
+    "mbrl_rollout_cost", "mbrl_select_workspace_bytes", "mbrl_select_elites",
+    "mbrl_refit_workspace_bytes", "mbrl_cem_refit", "mbrl_sample_actions",
+    "mbrl_cem_workspace_bytes", "mbrl_cem_plan",
+)
+
+
+class MlpShape(ctypes.Structure):
+    _fields_ = [("state_dim", c_int32), ("action_dim", c_int32), ("hidden", c_int32),
+                ("n_hidden", c_int32), ("ensemble", c_int32)]
+
+
+class Norm(ctypes.Structure):
+    _fields_ = [("obs_mean", c_void_p), ("obs_std", c_void_p), ("act_mean", c_void_p),
+                ("act_std", c_void_p), ("normalize_state", c_int32), ("unnormalize_state", c_int32),
+                ("normalize_action", c_int32), ("_pad", c_int32)]
+
+
+class Cost(ctypes.Structure):
+    _fields_ = [("kind", c_int32), ("has_state_cost", c_int32), ("has_action_cost", c_int32),
+                ("_pad", c_int32), ("weights", c_void_p), ("goal", c_void_p),
+                ("alpha_state", c_float), ("alpha_action", c_float)]
+
+
+class Sampler(ctypes.Structure):
+    _fields_ = [("seed", c_uint64), ("iteration", c_int32), ("_pad", c_int32), ("mu", c_void_p),
+                ("sigma", c_void_p), ("lo", c_float), ("hi", c_float)]
+
+
+class CemParams(ctypes.Structure):
+    _fields_ = [("N", c_int32), ("H", c_int32), ("K", c_int32), ("iterations", c_int32),
+                ("alpha", c_float), ("lo", c_float), ("hi", c_float), ("init_mu", c_float),
+                ("init_sigma", c_float), ("_pad", c_int32), ("seed", c_uint64)]
+
+
+_lib = None
+
+
+def load():
+    """Load (once) and type the extension. Raises ImportError if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"mbrl_amd HIP extension not found at {LIB_PATH}; build it with "
+            "`make -C mujoco-mbrl_amd` or `python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = ctypes.CDLL(LIB_PATH)
+    P = c_void_p
+    sig = {
+        "mbrl_abi_version": (c_int32, []),
+        "mbrl_last_error": (ctypes.c_char_p, []),
+        "mbrl_mlp_packed_bytes": (c_size_t, [POINTER(MlpShape)]),
+        "mbrl_mlp_pack": (c_int32, [POINTER(MlpShape), POINTER(c_void_p), POINTER(c_void_p), P, P]),
+        "mbrl_rollout_cost": (c_int32, [POINTER(MlpShape), P, POINTER(Norm), POINTER(Cost), P, c_int32, P,
+                                        POINTER(Sampler), c_int32, c_int32, c_int32, P, P, P, P]),
+        "mbrl_select_workspace_bytes": (c_size_t, [c_int32]),
+        "mbrl_select_elites": (c_int32, [P, c_int32, c_int32, c_int32, c_int32, P, P, P, c_size_t, P]),
+        "mbrl_refit_workspace_bytes": (c_size_t, [c_int32, c_int32, c_int32]),
+        "mbrl_cem_refit": (c_int32, [POINTER(Sampler), c_int32, c_int32, P, c_int32, c_float, P, P, P,
+                                     c_size_t, P]),
+        "mbrl_sample_actions": (c_int32, [POINTER(Sampler), c_int32, c_int32, c_int32, c_int32, P, P]),
+        "mbrl_cem_workspace_bytes": (c_size_t, [POINTER(MlpShape), POINTER(CemParams)]),
+        "mbrl_cem_plan": (c_int32, [POINTER(MlpShape), P, POINTER(Norm), POINTER(Cost), P, POINTER(CemParams),
+                                    P, P, P, P, P, P, P, P, P, c_size_t, P]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.mbrl_abi_version() != 1:
+        raise ImportError(f"mbrl_amd ABI version mismatch: {lib.mbrl_abi_version()} != 1")
+    _lib = lib
+    return lib
+
+
+def check(rc, what):
+    if rc != MBRL_OK:
+        msg = load().mbrl_last_error()
+        raise RuntimeError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    return None if t is None else c_void_p(t.data_ptr())
+
+
+def stream_handle(device=None):
+    return c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_gpu(t):
+    if not t.is_cuda:
+        raise RuntimeError("mbrl_amd fused path needs CUDA (HIP) tensors; got a CPU tensor")
+
+
+__all__ = ["load", "check", "ptr", "stream_handle", "MlpShape", "Norm", "Cost", "Sampler", "CemParams",
+           "EXPORTED", "MBRL_NAN_LAST", "MBRL_NAN_FIRST", "MBRL_COST_GOAL_STATE", "c_int64"]

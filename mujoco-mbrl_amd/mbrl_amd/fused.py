@@ -1,0 +1,327 @@
+"""Recognise the reference's model / cost / sampler closures and drive the HIP extension.
+
+The planners receive opaque callables: the model is
+functools.partial(model, normalize_state=partial(normalize_field, field_name="observations",
+stats=S), normalize_action=..., unnormalize_state=...) (agents.py:219-230), the cost is
+functools.partial(state_action_cost, state_cost=SmoothAbsLoss, action_cost=CoshLoss)
+(agents.py:231) and sample_action is functools.partial(_sample_action, action_spec=spec)
+(agents.py:233). This module unpacks those closures (partial.func / .keywords) into the POD
+descriptors of include/mbrl_cem.h. Anything it does not recognise returns None and the planner
+takes its generic path (the callables run on device tensors; selection and refit still run in
+the HIP extension).
+
+Device state is cached per module: packed weights are re-packed only when a parameter changes
+(torch's in-place version counter moves on every optimizer.step()).
+"""
+import functools
+import weakref
+
+import numpy as np
+import torch
+
+from . import _lib
+from .models import CoshLoss, EnsembleModel, Model, SmoothAbsLoss
+
+
+# ------------------------------------------------------------------------------------------------
+# introspection
+# ------------------------------------------------------------------------------------------------
+def _unpartial(f):
+    kw = {}
+    while isinstance(f, functools.partial):
+        kw = {**f.keywords, **kw}
+        f = f.func
+    return f, kw
+
+
+def _linear_layers(module):
+    """(members, L, W, s, a) for a recognised dynamics module, else None. members = list of lists of
+    nn.Linear. Accepts this package's Model / EnsembleModel and the reference's models.Model
+    (duck-typed: linear1..linear3 + ReLU activation_fn + noise None)."""
+    if isinstance(module, EnsembleModel):
+        members = [m.linears() for m in module.members]
+        m0 = module.members[0]
+        return members, m0.n_hidden, m0.hidden_units, m0.state_dim, m0.action_dim
+    if isinstance(module, Model):
+        if module.noise is not None:
+            return None
+        return [module.linears()], module.n_hidden, module.hidden_units, module.state_dim, module.action_dim
+    names = [n for n in ("linear1", "linear2", "linear3") if isinstance(getattr(module, n, None), torch.nn.Linear)]
+    if (type(module).__name__ == "Model" and len(names) == 3 and not hasattr(module, "linear4")
+            and isinstance(getattr(module, "activation_fn", None), torch.nn.ReLU)
+            and getattr(module, "noise", None) is None):
+        lins = [module.linear1, module.linear2, module.linear3]
+        W = lins[0].out_features
+        s = lins[2].out_features
+        a = lins[0].in_features - s
+        if lins[1].in_features == W and lins[1].out_features == W and lins[2].in_features == W and a >= 1:
+            return [lins], 2, W, s, a
+    return None
+
+
+def _field_stats(norm_fn, expect_name):
+    """(field_name, mean, std) of partial(normalize_field|unnormalize_field, field_name=, stats=)."""
+    if norm_fn is None:
+        return None
+    f, kw = _unpartial(norm_fn)
+    if getattr(f, "__name__", "") != expect_name or "field_name" not in kw or "stats" not in kw:
+        return False
+    try:
+        st = kw["stats"][kw["field_name"]]
+        return kw["field_name"], torch.as_tensor(st["mean"]), torch.as_tensor(st["std"])
+    except (KeyError, TypeError):
+        return False
+
+
+def describe_norm(normalize_state, normalize_action, unnormalize_state, s, a):
+    ns = _field_stats(normalize_state, "normalize_field")
+    us = _field_stats(unnormalize_state, "unnormalize_field")
+    na = _field_stats(normalize_action, "normalize_field")
+    if ns is False or us is False or na is False:
+        return None
+    obs = ns or us
+    if ns and us and not (torch.equal(ns[1].float(), us[1].float()) and torch.equal(ns[2].float(), us[2].float())):
+        return None  # one obs-stat pair serves both directions in the kernel
+    if obs and (obs[1].numel() != s or obs[2].numel() != s):
+        return None
+    if na and (na[1].numel() != a or na[2].numel() != a):
+        return None
+    return dict(obs_mean=obs[1] if obs else None, obs_std=obs[2] if obs else None,
+                act_mean=na[1] if na else None, act_std=na[2] if na else None,
+                normalize_state=bool(ns), unnormalize_state=bool(us), normalize_action=bool(na))
+
+
+def describe_model(model):
+    """Model callable -> dict(module, layers, L, W, s, a, norm) or None."""
+    f, kw = _unpartial(model)
+    if set(kw) - {"normalize_state", "normalize_action", "unnormalize_state"}:
+        return None
+    layers = _linear_layers(f) if isinstance(f, torch.nn.Module) else None
+    if layers is None:
+        return None
+    members, L, W, s, a = layers
+    norm = describe_norm(kw.get("normalize_state"), kw.get("normalize_action"), kw.get("unnormalize_state"), s, a)
+    if norm is None:
+        return None
+    return dict(module=f, members=members, L=L, W=W, s=s, a=a, E=len(members), norm=norm)
+
+
+def describe_cost(cost, s):
+    """partial(state_action_cost, state_cost=SmoothAbsLoss, action_cost=CoshLoss) -> dict or None."""
+    f, kw = _unpartial(cost)
+    if getattr(f, "__name__", "") != "state_action_cost" or set(kw) != {"state_cost", "action_cost"}:
+        return None
+    sc, ac = kw["state_cost"], kw["action_cost"]
+    if not (isinstance(sc, SmoothAbsLoss) or type(sc).__name__ == "SmoothAbsLoss"):
+        return None
+    if not (isinstance(ac, CoshLoss) or type(ac).__name__ == "CoshLoss"):
+        return None
+    if sc.goal_state is None:
+        return None
+    goal = torch.as_tensor(sc.goal_state, dtype=torch.float32).flatten()
+    w = torch.as_tensor(sc.weights, dtype=torch.float32).flatten()
+    if goal.numel() == 1:
+        goal = goal.expand(s)
+    if w.numel() == 1:
+        w = w.expand(s)
+    if goal.numel() != s or w.numel() != s:
+        return None
+    def raw_key(x):
+        return _tensor_key(x) if torch.is_tensor(x) else ("v", float(np.asarray(x).ravel()[0]), np.size(x))
+    return dict(weights=w.contiguous(), goal=goal.contiguous(), alpha_state=float(sc.alpha),
+                alpha_action=float(ac.alpha), key=(raw_key(sc.weights), raw_key(sc.goal_state),
+                                                   float(sc.alpha), float(ac.alpha)))
+
+
+def describe_sampler(sample_action):
+    """partial(_sample_action, action_spec=spec) -> (lo, hi, a) or None."""
+    f, kw = _unpartial(sample_action)
+    spec = kw.get("action_spec")
+    if spec is None or getattr(f, "__name__", "") not in ("_sample_action", "sample_action"):
+        return None
+    lo = max(float(spec.minimum[0]), -3.0)
+    hi = min(float(spec.maximum[0]), 3.0)
+    return lo, hi, int(spec.shape[0])
+
+
+# ------------------------------------------------------------------------------------------------
+# device caches
+# ------------------------------------------------------------------------------------------------
+_PACKED = weakref.WeakKeyDictionary()   # module -> (key, packed tensor)
+
+
+def _param_key(members, device):
+    return (str(device),) + tuple((p.data_ptr(), p._version) for lins in members for lin in lins
+                                  for p in (lin.weight, lin.bias))
+
+
+def mlp_shape(desc):
+    return _lib.MlpShape(desc["s"], desc["a"], desc["W"], desc["L"], desc["E"])
+
+
+def packed_weights(desc, device):
+    """Packed fragment stream of desc's module on `device` (cached until a parameter changes)."""
+    module, members = desc["module"], desc["members"]
+    key = _param_key(members, device)
+    hit = _PACKED.get(module)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    lib = _lib.load()
+    shape = mlp_shape(desc)
+    nbytes = lib.mbrl_mlp_packed_bytes(ctypes_ref(shape))
+    if nbytes == 0:
+        raise RuntimeError(f"unsupported MLP shape for the HIP path: {desc['s']}/{desc['a']} W={desc['W']} L={desc['L']}")
+    packed = torch.empty(nbytes // 4, dtype=torch.float32, device=device)
+    keep, wp, bp = [], [], []
+    for lins in members:
+        for lin in lins:
+            w = lin.weight.detach().to(device=device, dtype=torch.float32).contiguous()
+            b = lin.bias.detach().to(device=device, dtype=torch.float32).contiguous()
+            keep += [w, b]
+            wp.append(w.data_ptr())
+            bp.append(b.data_ptr())
+    n = len(wp)
+    warr = (_lib.c_void_p * n)(*wp)
+    barr = (_lib.c_void_p * n)(*bp)
+    with torch.cuda.device(device):
+        _lib.check(lib.mbrl_mlp_pack(ctypes_ref(shape), warr, barr, _lib.ptr(packed), _lib.stream_handle(device)),
+                   "mbrl_mlp_pack")
+        # the temporaries in `keep` must outlive the pack kernels
+        torch.cuda.current_stream(device).synchronize()
+    _PACKED[module] = (key, packed)
+    return packed
+
+
+def ctypes_ref(x):
+    import ctypes
+    return ctypes.byref(x)
+
+
+def _dev(t, device):
+    return None if t is None else t.detach().to(device=device, dtype=torch.float32).contiguous()
+
+
+class DeviceProblem:
+    """Device-resident descriptors for one (model, cost) pair; holds the tensors the POD structs point at."""
+
+    def __init__(self, mdesc, cdesc, device):
+        self.mdesc, self.cdesc, self.device = mdesc, cdesc, device
+        self.shape = mlp_shape(mdesc)
+        self.packed = packed_weights(mdesc, device)
+        n = mdesc["norm"]
+        self._norm_t = [_dev(n[k], device) for k in ("obs_mean", "obs_std", "act_mean", "act_std")]
+        self.norm = _lib.Norm(*[_lib.ptr(t) for t in self._norm_t], int(n["normalize_state"]),
+                              int(n["unnormalize_state"]), int(n["normalize_action"]), 0)
+        if cdesc is not None:
+            self._cost_t = [_dev(cdesc["weights"], device), _dev(cdesc["goal"], device)]
+            self.cost = _lib.Cost(_lib.MBRL_COST_GOAL_STATE, 1, 1, 0, _lib.ptr(self._cost_t[0]),
+                                  _lib.ptr(self._cost_t[1]), cdesc["alpha_state"], cdesc["alpha_action"])
+        else:
+            self._cost_t = []
+            self.cost = _lib.Cost(_lib.MBRL_COST_GOAL_STATE, 0, 0, 0, None, None, 0.0, 0.0)
+
+
+def _tensor_key(t):
+    return None if t is None else (t.data_ptr(), t._version, t.device.type, tuple(t.shape))
+
+
+_PROBLEMS = {}
+
+
+def device_problem(mdesc, cdesc, device):
+    """Cached DeviceProblem: rebuilt only when weights, statistics or cost parameters change."""
+    n = mdesc["norm"]
+    key = (id(mdesc["module"]), _param_key(mdesc["members"], device),
+           tuple(_tensor_key(n[k]) for k in ("obs_mean", "obs_std", "act_mean", "act_std")),
+           (n["normalize_state"], n["unnormalize_state"], n["normalize_action"]),
+           None if cdesc is None else cdesc["key"])
+    hit = _PROBLEMS.get(key)
+    if hit is not None and hit[0]() is mdesc["module"]:
+        return hit[1]
+    prob = DeviceProblem(mdesc, cdesc, device)
+    if len(_PROBLEMS) > 64:
+        _PROBLEMS.clear()
+    _PROBLEMS[key] = (weakref.ref(mdesc["module"]), prob)
+    return prob
+
+
+# ------------------------------------------------------------------------------------------------
+# thin wrappers over the C ABI (all on the current stream of `device`)
+# ------------------------------------------------------------------------------------------------
+def rollout(prob, s0, N, H, *, actions=None, sampler=None, n_offset=0, s0_per_candidate=False,
+            costs=None, actions_out=None, states_out=None):
+    lib = _lib.load()
+    dev = prob.device
+    E = prob.mdesc["E"]
+    if costs is None:
+        costs = torch.empty((E, N), dtype=torch.float32, device=dev)
+    _lib.check(lib.mbrl_rollout_cost(ctypes_ref(prob.shape), _lib.ptr(prob.packed), ctypes_ref(prob.norm),
+                                     ctypes_ref(prob.cost), _lib.ptr(s0), int(s0_per_candidate), _lib.ptr(actions),
+                                     ctypes_ref(sampler) if sampler is not None else None, N, H, n_offset,
+                                     _lib.ptr(costs), _lib.ptr(actions_out), _lib.ptr(states_out),
+                                     _lib.stream_handle(dev)), "mbrl_rollout_cost")
+    return costs
+
+
+def select(costs, K, nan_policy=_lib.MBRL_NAN_LAST, returns_out=None, workspace=None):
+    """costs: [E, N] device tensor -> elite indices [K] (int64, ascending)."""
+    lib = _lib.load()
+    E, N = costs.shape
+    dev = costs.device
+    elites = torch.empty(K, dtype=torch.int64, device=dev)
+    need = lib.mbrl_select_workspace_bytes(N)
+    if workspace is None or workspace.numel() < need:
+        workspace = torch.empty(need, dtype=torch.uint8, device=dev)
+    _lib.check(lib.mbrl_select_elites(_lib.ptr(costs), E, N, K, nan_policy, _lib.ptr(elites), _lib.ptr(returns_out),
+                                      _lib.ptr(workspace), workspace.numel(), _lib.stream_handle(dev)),
+               "mbrl_select_elites")
+    return elites
+
+
+def refit(sampler, H, a, elites, alpha, mu_out, sigma_out, workspace=None):
+    lib = _lib.load()
+    dev = mu_out.device
+    K = elites.numel()
+    need = lib.mbrl_refit_workspace_bytes(H, a, K)
+    if workspace is None or workspace.numel() < need:
+        workspace = torch.empty(need, dtype=torch.uint8, device=dev)
+    _lib.check(lib.mbrl_cem_refit(ctypes_ref(sampler), H, a, _lib.ptr(elites), K, float(alpha), _lib.ptr(mu_out),
+                                  _lib.ptr(sigma_out), _lib.ptr(workspace), workspace.numel(),
+                                  _lib.stream_handle(dev)), "mbrl_cem_refit")
+
+
+def sample_actions(sampler, H, a, N, n_offset, out):
+    lib = _lib.load()
+    _lib.check(lib.mbrl_sample_actions(ctypes_ref(sampler), H, a, N, n_offset, _lib.ptr(out),
+                                       _lib.stream_handle(out.device)), "mbrl_sample_actions")
+    return out
+
+
+def make_sampler(seed, iteration, mu, sigma, lo, hi):
+    return _lib.Sampler(int(seed) & 0xFFFFFFFFFFFFFFFF, int(iteration), 0, _lib.ptr(mu), _lib.ptr(sigma),
+                        float(lo), float(hi))
+
+
+# ------------------------------------------------------------------------------------------------
+# DynamicsModel.forward on device (one step, per-row start states)
+# ------------------------------------------------------------------------------------------------
+def try_forward(module, state, action, normalize_action, normalize_state, unnormalize_state):
+    layers = _linear_layers(module)
+    if layers is None or isinstance(module, EnsembleModel):
+        return None
+    members, L, W, s, a = layers
+    if state.dim() != 2 or action.dim() != 2 or state.shape[1] != s or action.shape[1] != a \
+            or state.shape[0] != action.shape[0] or state.dtype != torch.float32 or action.dtype != torch.float32:
+        return None
+    norm = describe_norm(normalize_state, normalize_action, unnormalize_state, s, a)
+    if norm is None:
+        return None
+    desc = dict(module=module, members=members, L=L, W=W, s=s, a=a, E=1, norm=norm)
+    dev = state.device
+    prob = device_problem(desc, None, dev)
+    B = state.shape[0]
+    st = state.contiguous()
+    act = action.contiguous().view(1, B, a)
+    out = torch.empty((1, 1, B, s), dtype=torch.float32, device=dev)
+    rollout(prob, st, B, 1, actions=act, s0_per_candidate=True, states_out=out)
+    return out.view(B, s)

@@ -1,0 +1,167 @@
+"""Dynamics models and costs with the reference's API (/root/reference/src/mbrl/models.py).
+
+`DynamicsModel.forward(state, action, normalize_action=None, normalize_state=None,
+unnormalize_state=None)` keeps the reference contract (models.py:13-29). On CUDA tensors with
+autograd off it runs the one-step batch through the same HIP rollout kernel the planners use
+(H = 1, per-row start states); otherwise (training, CPU tensors) it is plain PyTorch, exactly the
+reference's arithmetic.
+"""
+import functools
+
+import torch
+import torch.nn as nn
+
+
+class DynamicsModel(nn.Module):
+    """models.py:8-29."""
+
+    def __init__(self):
+        super().__init__()
+        self.train_iterations = 0
+
+    def forward(self, state, action, normalize_action=None, normalize_state=None, unnormalize_state=None):
+        if state.is_cuda and not torch.is_grad_enabled() and getattr(self, "noise", None) is None:
+            from . import fused
+            out = fused.try_forward(self, state, action, normalize_action, normalize_state, unnormalize_state)
+            if out is not None:
+                return out
+        if normalize_action:
+            action = normalize_action(action)
+        if normalize_state:
+            state = normalize_state(state)
+        x = torch.cat([state, action], dim=1)
+        out = self._forward(x)
+        if unnormalize_state:
+            out = unnormalize_state(out)
+        return out
+
+
+class Model(DynamicsModel):
+    """models.py:96-110 generalised to `n_hidden` Linear-ReLU layers (default 2 = the reference).
+
+    Layers are named linear1 .. linear{n_hidden+1} so an n_hidden=2 state_dict loads into the
+    reference's Model and vice versa."""
+
+    def __init__(self, state_dim, action_dim, hidden_units=50, noise=None, n_hidden=2):
+        super().__init__()
+        self.state_dim, self.action_dim = state_dim, action_dim
+        self.hidden_units, self.n_hidden = hidden_units, n_hidden
+        dims = [state_dim + action_dim] + [hidden_units] * n_hidden + [state_dim]
+        for i, (fi, fo) in enumerate(zip(dims[:-1], dims[1:])):
+            setattr(self, f"linear{i + 1}", nn.Linear(fi, fo))
+        self.activation_fn = nn.ReLU()
+        self.noise = noise
+
+    def linears(self):
+        return [getattr(self, f"linear{i + 1}") for i in range(self.n_hidden + 1)]
+
+    def _forward(self, x):
+        lins = self.linears()
+        for lin in lins[:-1]:
+            x = self.activation_fn(lin(x))
+        x = lins[-1](x)
+        return x if self.noise is None else x + torch.randn_like(x) * self.noise
+
+
+class EnsembleModel(DynamicsModel):
+    """PETS-style ensemble of E `Model`s (not in the reference; BASELINE.json config 5).
+
+    The CEM planner rolls every member out on the same actions and scores a candidate by the mean
+    of the members' returns. Called directly, forward() returns the member-mean next state."""
+
+    def __init__(self, members):
+        super().__init__()
+        self.members = nn.ModuleList(members)
+        m0 = self.members[0]
+        for m in self.members:
+            if not isinstance(m, Model) or (m.state_dim, m.action_dim, m.hidden_units, m.n_hidden) != \
+                    (m0.state_dim, m0.action_dim, m0.hidden_units, m0.n_hidden):
+                raise ValueError("EnsembleModel members must be Models of one shape")
+        self.state_dim, self.action_dim = m0.state_dim, m0.action_dim
+        self.hidden_units, self.n_hidden = m0.hidden_units, m0.n_hidden
+        self.noise = None
+
+    def _forward(self, x):
+        return torch.stack([m._forward(x) for m in self.members]).mean(0)
+
+
+class ModelWithReward(nn.Module):
+    """models.py:125-163 (shared trunk, state head linear3, reward head linear4). The planners run
+    it through the generic callable path (RewardAgent's reward-as-cost wiring, agents.py:342-366)."""
+
+    def __init__(self, state_dim, action_dim, hidden_units=200):
+        super().__init__()
+        self.train_iterations = 0
+        self.linear1 = nn.Linear(state_dim + action_dim, hidden_units)
+        self.linear2 = nn.Linear(hidden_units, hidden_units)
+        self.linear3 = nn.Linear(hidden_units, state_dim)
+        self.linear4 = nn.Linear(hidden_units, 1)
+        self.activation_fn = nn.ReLU()
+
+    def _forward(self, x):
+        x = self.activation_fn(self.linear1(x))
+        x = self.activation_fn(self.linear2(x))
+        return self.linear3(x), self.linear4(x)
+
+    def forward(self, state, action, normalize_state=None, unnormalize_state=None, normalize_action=None,
+                unnormalize_reward=None):
+        if normalize_action:
+            action = normalize_action(action)
+        if normalize_state:
+            state = normalize_state(state)
+        x = torch.cat([state, action], dim=1)
+        state, reward = self._forward(x)
+        if unnormalize_reward:
+            reward = unnormalize_reward(reward)
+        if unnormalize_state:
+            state = unnormalize_state(state)
+        return state, reward
+
+
+class StateCost(nn.Module):
+    goal_state = None
+
+    def set_goal_state(self, goal_state):
+        self.goal_state = goal_state
+
+
+class SmoothAbsLoss(StateCost):
+    """models.py:244-259: sum_d sqrt((w_d (x_d - g_d))^2 + alpha^2) - alpha."""
+
+    def __init__(self, weights, goal_state, alpha=0.4):
+        super().__init__()
+        self.alpha = alpha
+        self.weights = weights
+        self.goal_state = goal_state
+
+    def forward(self, x):
+        x = x - self.goal_state
+        return torch.sum(torch.sqrt((x * self.weights) ** 2 + self.alpha ** 2) - self.alpha, dim=-1)
+
+
+class CoshLoss(nn.Module):
+    """models.py:262-272: alpha^2 * mean_d(cosh(a_d / alpha) - 1)."""
+
+    def __init__(self, alpha=0.25):
+        super().__init__()
+        self.alpha = alpha
+
+    def forward(self, x):
+        return (self.alpha ** 2) * torch.mean(torch.cosh(x / self.alpha) - 1, dim=-1)
+
+
+def state_action_cost(state, action, state_cost, action_cost):
+    """agents.py:182-183."""
+    return state_cost(state) + action_cost(action)
+
+
+def compose(a, b):
+    """agents.py:300-304."""
+    def ab(*args, **kwargs):
+        return b(a(*args, **kwargs))
+    return ab
+
+
+def goal_state_cost(state_cost, action_cost):
+    """The cost GoalStateAgent hands the planner (agents.py:231)."""
+    return functools.partial(state_action_cost, state_cost=state_cost, action_cost=action_cost)

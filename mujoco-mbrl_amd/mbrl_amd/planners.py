@@ -1,0 +1,296 @@
+"""Planners with the reference's static `plan()` API (/root/reference/src/mbrl/planners.py:14-25).
+
+    plan(initial_state, model, cost, sample_action, horizon, initial_trajectory=None, **kwargs)
+        -> (states [H, s], actions [H, a])
+
+The class itself (not an instance) is what agents pass around (experiment.py:15-26, agents.py:48),
+kwargs are read as kwargs.get(name, Cls.defaults[name]) (planners.py:141,153-155), and
+`initial_trajectory` is accepted and ignored exactly as the reference's random-shooting planner
+ignores it (planners.py:166-187).
+
+RandomShootingPlanner -- the reference's planner (planners.py:140-216), same sampling call and
+    argmin semantics, rollout + cost + argmin on the GPU.
+CEMPlanner            -- the CEM hot path of BASELINE.json: I iterations of
+    Philox proposal -> persistent MFMA rollout -> stable top-K -> alpha-smoothed Gaussian refit.
+    With torch.distributed initialised and distributed=True, candidates are sharded over ranks:
+    one RCCL all-gather of the per-candidate returns per iteration; every rank then runs the same
+    deterministic selection and refit (the refit regenerates elite actions from the counter RNG,
+    so no moment collective is needed and the result is bit-identical for any rank count).
+
+Both take the fused path when fused.describe_* recognise the model / cost closures; otherwise the
+user's callables run on device tensors (reference semantics, planners.py:199-210) and selection /
+refit still run in the HIP extension.
+"""
+import numpy as np
+import torch
+
+from . import _lib, fused
+
+
+class ModelPlanner:
+    """planners.py:14-25."""
+
+    @staticmethod
+    def plan(initial_state, model, cost, sample_action, horizon, initial_trajectory=None, **kwargs):
+        raise NotImplementedError
+
+
+def _device(kwargs):
+    dev = kwargs.get("device")
+    if dev is None:
+        if not torch.cuda.is_available():
+            raise RuntimeError("mbrl_amd planners need a ROCm GPU (torch.cuda.is_available() is False)")
+        dev = torch.device("cuda", torch.cuda.current_device())
+    return torch.device(dev)
+
+
+def _to_host(x, keep_device):
+    return x if keep_device else x.cpu()
+
+
+def _generic_costs(model, cost, s0, actions, H, N):
+    """planners.py:199-210 with the caller's callables on device tensors. actions [H, N, a] on device.
+    Returns costs [1, N] (sequential sum over t) and states [H, N, s]."""
+    s = s0.shape[0]
+    states = torch.empty((H, N, s), dtype=torch.float32, device=actions.device)
+    cur = s0.unsqueeze(0).repeat_interleave(N, dim=0)
+    with torch.no_grad():
+        for t in range(H):
+            cur = model(cur, actions[t])
+            states[t] = cur
+        c = cost(states.reshape(H * N, s), actions.reshape(H * N, -1)).reshape(H, N)
+        total = c[0].clone()
+        for t in range(1, H):
+            total = total + c[t]
+    return total.reshape(1, N).contiguous(), states
+
+
+class RandomShootingPlanner(ModelPlanner):
+    """planners.py:140-216 on the GPU."""
+    defaults = dict(num_trajectories=1000)
+
+    @staticmethod
+    def plan(initial_state, model, cost, sample_action, horizon, initial_trajectory=None, **kwargs):
+        num_trajectories = kwargs.get("num_trajectories", RandomShootingPlanner.defaults["num_trajectories"])
+        return RandomShootingPlanner._plan(initial_state, model, cost, sample_action, horizon, initial_trajectory,
+                                           num_trajectories, **kwargs)
+
+    @staticmethod
+    def _plan(initial_state, model, cost, sample_action, horizon, initial_trajectory, num_trajectories, **kwargs):
+        dev = _device(kwargs)
+        N, H = int(num_trajectories), int(horizon)
+        # planners.py:200: one draw of N*H actions from the caller's sampler (host RNG), time-major
+        action_list = sample_action(batch_size=N * H)
+        a = action_list.shape[1]
+        with torch.cuda.device(dev):
+            acts = action_list.to(device=dev, dtype=torch.float32).reshape(H, N, a).contiguous()
+            s0 = initial_state.to(device=dev, dtype=torch.float32).contiguous()
+            mdesc = fused.describe_model(model)
+            cdesc = fused.describe_cost(cost, mdesc["s"]) if mdesc is not None else None
+            if mdesc is not None and cdesc is not None and mdesc["E"] == 1 and mdesc["a"] == a:
+                prob = fused.device_problem(mdesc, cdesc, dev)
+                states = torch.empty((1, H, N, mdesc["s"]), dtype=torch.float32, device=dev)
+                costs = fused.rollout(prob, s0, N, H, actions=acts, states_out=states)
+                states = states[0]
+            else:
+                costs, states = _generic_costs(model, cost, s0, acts, H, N)
+            idx = fused.select(costs, 1, nan_policy=_lib.MBRL_NAN_FIRST)   # np.argmin, planners.py:184
+            i = idx[0]
+            out_states = states[:, i]
+            out_actions = acts[:, i]
+            keep = kwargs.get("return_device", False)
+            return _to_host(out_states, keep), _to_host(out_actions, keep)
+
+
+class CEMPlanner(ModelPlanner):
+    """Cross-entropy method over action sequences (not in the reference).
+
+    kwargs (defaults): num_candidates (1000), num_elites (None -> num_candidates // 10),
+    num_iterations (5), alpha (0.1), seed (None -> drawn from the global NumPy RNG, like the
+    reference's sampler), init_std (None -> (hi - lo) / 4), action_bounds (None -> from
+    sample_action's action_spec, else (-1, 1)), distributed (False), return_device (False).
+    Returns the final Gaussian mean (clipped) and its predicted states (ensemble mean)."""
+    defaults = dict(num_candidates=1000, num_elites=None, num_iterations=5, alpha=0.1, seed=None, init_std=None,
+                    action_bounds=None, distributed=False, return_device=False)
+
+    @staticmethod
+    def plan(initial_state, model, cost, sample_action, horizon, initial_trajectory=None, **kwargs):
+        res = CEMPlanner.plan_detailed(initial_state, model, cost, sample_action, horizon, initial_trajectory,
+                                       **kwargs)
+        return res["states"], res["actions"]
+
+    @staticmethod
+    def _settings(sample_action, horizon, kwargs):
+        d = CEMPlanner.defaults
+        g = lambda k: kwargs.get(k, d[k])  # noqa: E731
+        N = int(g("num_candidates"))
+        K = g("num_elites")
+        K = max(1, N // 10) if K is None else int(K)
+        bounds = g("action_bounds")
+        sdesc = fused.describe_sampler(sample_action) if sample_action is not None else None
+        if bounds is None:
+            bounds = (sdesc[0], sdesc[1]) if sdesc is not None else (-1.0, 1.0)
+        lo, hi = float(bounds[0]), float(bounds[1])
+        init_std = g("init_std")
+        init_std = float(np.float32(hi - lo) / np.float32(4.0)) if init_std is None else float(init_std)
+        seed = g("seed")
+        if seed is None:
+            seed = int(np.random.randint(0, 2 ** 62, dtype=np.int64))
+        if not 1 <= K <= N:
+            raise ValueError(f"need 1 <= num_elites ({K}) <= num_candidates ({N})")
+        return dict(N=N, K=K, H=int(horizon), I=int(g("num_iterations")), alpha=float(g("alpha")), lo=lo, hi=hi,
+                    init_std=init_std, seed=seed, distributed=bool(g("distributed")),
+                    keep=bool(g("return_device")), record=bool(kwargs.get("record", False)),
+                    events=kwargs.get("rollout_events"), adim=sdesc[2] if sdesc else None)
+
+    @staticmethod
+    def plan_detailed(initial_state, model, cost, sample_action, horizon, initial_trajectory=None, **kwargs):
+        """plan() plus diagnostics: dict(states, actions, mu, sigma[, costs, returns, elites per iteration])."""
+        dev = _device(kwargs)
+        st = CEMPlanner._settings(sample_action, horizon, kwargs)
+        with torch.cuda.device(dev):
+            s0 = initial_state.to(device=dev, dtype=torch.float32).contiguous()
+            mdesc = fused.describe_model(model)
+            cdesc = fused.describe_cost(cost, mdesc["s"]) if mdesc is not None else None
+            ws = None
+            if st["distributed"] and torch.distributed.is_available() and torch.distributed.is_initialized() \
+                    and torch.distributed.get_world_size() > 1:
+                ws = torch.distributed.get_world_size()
+            if mdesc is not None and cdesc is not None:
+                prob = fused.device_problem(mdesc, cdesc, dev)
+                if ws is None:
+                    res = _cem_fused_single(prob, s0, st)
+                else:
+                    res = _cem_fused_sharded(prob, s0, st, ws)
+            else:
+                a = st["adim"]
+                if a is None:
+                    a = sample_action(batch_size=1).shape[1]
+                res = _cem_generic(model, cost, s0, st, a, dev)
+            res["states"] = _to_host(res["states"], st["keep"])
+            res["actions"] = _to_host(res["actions"], st["keep"])
+            return res
+
+
+_WS = {}
+
+
+def _workspace(key, nbytes, device):
+    buf = _WS.get(key)
+    if buf is None or buf.numel() < nbytes or buf.device != device:
+        buf = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=device)
+        _WS[key] = buf
+    return buf
+
+
+def _cem_fused_single(prob, s0, st):
+    """One C-ABI call: mbrl_cem_plan (every iteration stream-ordered, no host sync)."""
+    lib = _lib.load()
+    dev = prob.device
+    md = prob.mdesc
+    N, K, H, I = st["N"], st["K"], st["H"], st["I"]
+    a, s, E = md["a"], md["s"], md["E"]
+    params = _lib.CemParams(N, H, K, I, st["alpha"], st["lo"], st["hi"], 0.0, st["init_std"], 0,
+                            int(st["seed"]) & 0xFFFFFFFFFFFFFFFF)
+    need = lib.mbrl_cem_workspace_bytes(fused.ctypes_ref(prob.shape), fused.ctypes_ref(params))
+    ws = _workspace(("cem", str(dev)), need, dev)
+    mu = torch.empty((H, a), dtype=torch.float32, device=dev)
+    sigma = torch.empty((H, a), dtype=torch.float32, device=dev)
+    actions = torch.empty((H, a), dtype=torch.float32, device=dev)
+    states = torch.empty((H, s), dtype=torch.float32, device=dev)
+    rec = st["record"]
+    cost_hist = torch.empty((I, E, N), dtype=torch.float32, device=dev) if rec else None
+    ret_hist = torch.empty((I, N), dtype=torch.float32, device=dev) if rec else None
+    elite_hist = torch.empty((I, K), dtype=torch.int64, device=dev) if rec else None
+    events = st["events"]
+    ev_arr = None
+    if events is not None:
+        ev_arr = (_lib.c_void_p * (2 * I))(*[e.cuda_event for pair in events for e in pair])
+    _lib.check(lib.mbrl_cem_plan(fused.ctypes_ref(prob.shape), _lib.ptr(prob.packed), fused.ctypes_ref(prob.norm),
+                                 fused.ctypes_ref(prob.cost), _lib.ptr(s0), fused.ctypes_ref(params), _lib.ptr(mu),
+                                 _lib.ptr(sigma), _lib.ptr(actions), _lib.ptr(states), _lib.ptr(cost_hist),
+                                 _lib.ptr(ret_hist), _lib.ptr(elite_hist), ev_arr, _lib.ptr(ws), ws.numel(),
+                                 _lib.stream_handle(dev)), "mbrl_cem_plan")
+    out = dict(states=states, actions=actions, mu=mu, sigma=sigma)
+    if rec:
+        out.update(costs=cost_hist, returns=ret_hist, elites=elite_hist)
+    return out
+
+
+def _cem_fused_sharded(prob, s0, st, world):
+    """Candidates [r*N/G, (r+1)*N/G) on rank r; per iteration: local rollout -> RCCL all-gather of
+    the [E, N/G] costs -> replicated selection + refit (identical on every rank)."""
+    import torch.distributed as dist
+    dev = prob.device
+    md = prob.mdesc
+    N, K, H, I = st["N"], st["K"], st["H"], st["I"]
+    a, s, E = md["a"], md["s"], md["E"]
+    rank = dist.get_rank()
+    if N % world:
+        raise ValueError(f"num_candidates {N} must divide evenly over {world} ranks")
+    Nl = N // world
+    mu = torch.zeros((H, a), dtype=torch.float32, device=dev)
+    sigma = torch.full((H, a), st["init_std"], dtype=torch.float32, device=dev)
+    mu_n, sigma_n = torch.empty_like(mu), torch.empty_like(sigma)
+    local = torch.empty((E, Nl), dtype=torch.float32, device=dev)
+    gathered = torch.empty((world, E, Nl), dtype=torch.float32, device=dev)
+    rec = st["record"]
+    hist = dict(costs=[], returns=[], elites=[])
+    events = st["events"]
+    for it in range(I):
+        sp = fused.make_sampler(st["seed"], it, mu, sigma, st["lo"], st["hi"])
+        if events is not None:
+            events[it][0].record()
+        fused.rollout(prob, s0, Nl, H, sampler=sp, n_offset=rank * Nl, costs=local)
+        if events is not None:
+            events[it][1].record()
+        dist.all_gather_into_tensor(gathered, local)
+        costs = gathered.permute(1, 0, 2).reshape(E, N) if E > 1 else gathered.reshape(1, N)
+        rets = torch.empty(N, dtype=torch.float32, device=dev) if rec else None
+        elites = fused.select(costs, K, returns_out=rets,
+                              workspace=_workspace(("sel", str(dev)), _lib.load().mbrl_select_workspace_bytes(N), dev))
+        fused.refit(sp, H, a, elites, st["alpha"], mu_n, sigma_n,
+                    workspace=_workspace(("refit", str(dev)), _lib.load().mbrl_refit_workspace_bytes(H, a, K), dev))
+        mu, mu_n = mu_n, mu
+        sigma, sigma_n = sigma_n, sigma
+        if rec:
+            hist["costs"].append(costs.clone())
+            hist["returns"].append(rets)
+            hist["elites"].append(elites)
+    actions = mu.clamp(st["lo"], st["hi"]).contiguous()
+    states_e = torch.empty((E, H, 1, s), dtype=torch.float32, device=dev)
+    fused.rollout(prob, s0, 1, H, actions=actions.view(H, 1, a), states_out=states_e)
+    states = states_e[:, :, 0, :].mean(0) if E > 1 else states_e[0, :, 0, :]
+    out = dict(states=states, actions=actions, mu=mu, sigma=sigma)
+    if rec:
+        out.update({k: torch.stack(v) for k, v in hist.items()})
+    return out
+
+
+def _cem_generic(model, cost, s0, st, a, dev):
+    """CEM with opaque callables: HIP proposal draw, the callables on device tensors, HIP select/refit."""
+    N, K, H, I = st["N"], st["K"], st["H"], st["I"]
+    mu = torch.zeros((H, a), dtype=torch.float32, device=dev)
+    sigma = torch.full((H, a), st["init_std"], dtype=torch.float32, device=dev)
+    mu_n, sigma_n = torch.empty_like(mu), torch.empty_like(sigma)
+    acts = torch.empty((H, N, a), dtype=torch.float32, device=dev)
+    hist = dict(costs=[], returns=[], elites=[])
+    for it in range(I):
+        sp = fused.make_sampler(st["seed"], it, mu, sigma, st["lo"], st["hi"])
+        fused.sample_actions(sp, H, a, N, 0, acts)
+        costs, _ = _generic_costs(model, cost, s0, acts, H, N)
+        rets = torch.empty(N, dtype=torch.float32, device=dev)
+        elites = fused.select(costs, K, returns_out=rets)
+        fused.refit(sp, H, a, elites, st["alpha"], mu_n, sigma_n)
+        mu, mu_n = mu_n, mu
+        sigma, sigma_n = sigma_n, sigma
+        if st["record"]:
+            hist["costs"].append(costs.clone())
+            hist["returns"].append(rets)
+            hist["elites"].append(elites)
+    actions = mu.clamp(st["lo"], st["hi"]).contiguous()
+    _, states = _generic_costs(model, cost, s0, actions.view(H, 1, a), H, 1)
+    out = dict(states=states[:, 0, :], actions=actions, mu=mu, sigma=sigma)
+    if st["record"]:
+        out.update({k: torch.stack(v) for k, v in hist.items()})
+    return out

@@ -1,0 +1,62 @@
+"""Synthetic random-weight dynamics problems at BASELINE.json's named shapes.
+
+There are no checkpoints or datasets offline, so the bench and the smoke test plan on random
+weights drawn with nn.Linear's init law (U(-1/sqrt(fan_in), 1/sqrt(fan_in))) from NumPy PCG64,
+seed = 1000 + config id; normalisation mean ~ U(-0.5, 0.5), std ~ U(0.5, 2) (seed + 1);
+s0, goal ~ N(0, 1) (seed + 2); CEM proposal seed = seed + 3. The CPU oracle draws the identical
+arrays independently (oracle/cem.py:synth_problem; tests/test_host.py checks the two agree).
+"""
+import functools
+
+import numpy as np
+import torch
+
+from . import data, env, models
+
+# id: (name, obs dim, action dim, hidden width, hidden layers, candidates, horizon, ensemble)
+CONFIGS = {
+    1: dict(name="cartpole-swingup-rs", s=5, a=1, W=256, L=2, N=128, H=12, E=1),
+    2: dict(name="cartpole-swingup-cem", s=5, a=1, W=256, L=2, N=1024, H=20, E=1),
+    3: dict(name="cheetah-run-cem", s=17, a=6, W=512, L=3, N=4096, H=30, E=1),
+    4: dict(name="walker-walk-cem", s=24, a=6, W=512, L=3, N=16384, H=30, E=1),
+    5: dict(name="humanoid-stand-cem-ens5", s=67, a=21, W=512, L=3, N=32768, H=50, E=5),
+}
+
+
+def flop_per_candidate_step(cfg):
+    """Algorithmic MLP FLOP per candidate per step, times the ensemble size."""
+    s, a, W, L, E = cfg["s"], cfg["a"], cfg["W"], cfg["L"], cfg["E"]
+    return 2 * (W * (s + a) + (L - 1) * W * W + W * s) * E
+
+
+def make_problem(config_id, **overrides):
+    cfg = dict(CONFIGS[config_id])
+    cfg.update(overrides)
+    seed = 1000 + config_id
+    s, a, W, L, E = cfg["s"], cfg["a"], cfg["W"], cfg["L"], cfg["E"]
+    rng = np.random.Generator(np.random.PCG64(seed))
+    dims = [s + a] + [W] * L + [s]
+    members = []
+    for _ in range(E):
+        m = models.Model(s, a, hidden_units=W, n_hidden=L)
+        with torch.no_grad():
+            for lin, fi, fo in zip(m.linears(), dims[:-1], dims[1:]):
+                bound = 1.0 / np.sqrt(fi)
+                lin.weight.copy_(torch.from_numpy(rng.uniform(-bound, bound, size=(fo, fi)).astype(np.float32)))
+                lin.bias.copy_(torch.from_numpy(rng.uniform(-bound, bound, size=(fo,)).astype(np.float32)))
+        members.append(m)
+    module = members[0] if E == 1 else models.EnsembleModel(members)
+    rn = np.random.Generator(np.random.PCG64(seed + 1))
+    stats = {"observations": {"mean": torch.from_numpy(rn.uniform(-0.5, 0.5, size=s).astype(np.float32)),
+                              "std": torch.from_numpy(rn.uniform(0.5, 2.0, size=s).astype(np.float32))},
+             "actions": {"mean": torch.from_numpy(rn.uniform(-0.5, 0.5, size=a).astype(np.float32)),
+                         "std": torch.from_numpy(rn.uniform(0.5, 2.0, size=a).astype(np.float32))}}
+    rs = np.random.Generator(np.random.PCG64(seed + 2))
+    s0 = torch.from_numpy(rs.standard_normal(s).astype(np.float32))
+    goal = torch.from_numpy(rs.standard_normal(s).astype(np.float32))
+    ds = data.TransitionsDataset(stats)
+    model_fn = functools.partial(module, **ds.normalizers())                          # agents.py:224-230
+    cost_fn = models.goal_state_cost(models.SmoothAbsLoss(torch.ones(s), goal, 0.4), models.CoshLoss(0.25))
+    sample_action = env.sample_action_fn(env.BoundedActionSpec(a, -1.0, 1.0))          # agents.py:233
+    return dict(cfg=cfg, module=module, model=model_fn, cost=cost_fn, sample_action=sample_action, s0=s0,
+                goal=goal, stats=stats, rng_seed=seed + 3)

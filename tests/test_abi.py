@@ -1,0 +1,91 @@
+"""CPU: the C-ABI library loads without a GPU, exports exactly what include/mbrl_cem.h declares,
+and the ctypes structs match the C layout (checked against gcc on the header itself)."""
+import ctypes
+import os
+import re
+import subprocess
+import tempfile
+
+import pytest
+
+from conftest import REPO
+
+HEADER = os.path.join(REPO, "include", "mbrl_cem.h")
+
+
+def declared_functions():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(mbrl_[a-z_0-9]+)\s*\(", txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    from mbrl_amd import _lib
+    lib = _lib.load()
+    decl = declared_functions()
+    assert decl == sorted(_lib.EXPORTED)
+    for name in decl:
+        assert hasattr(lib, name), name
+    assert lib.mbrl_abi_version() == 1
+
+
+def test_no_gpu_needed_for_sizing_calls():
+    from mbrl_amd import _lib
+    lib = _lib.load()
+    sh = _lib.MlpShape(17, 6, 512, 3, 1)
+    # 68 chunks x 8 KiB per wave x 4 waves + biases (3*512 + 32), 64-float aligned
+    assert lib.mbrl_mlp_packed_bytes(ctypes.byref(sh)) == ((68 * 8192 + 3 * 512 + 32 + 63) // 64 * 64) * 4
+    bad = _lib.MlpShape(17, 6, 4096, 3, 1)
+    assert lib.mbrl_mlp_packed_bytes(ctypes.byref(bad)) == 0
+    assert lib.mbrl_select_workspace_bytes(4096) >= 4096 * 4
+    assert lib.mbrl_refit_workspace_bytes(30, 6, 409) >= 30 * 6 * 409 * 4
+    p = _lib.CemParams(4096, 30, 409, 5, 0.1, -1.0, 1.0, 0.0, 0.5, 0, 1)
+    assert lib.mbrl_cem_workspace_bytes(ctypes.byref(sh), ctypes.byref(p)) > 4096 * 4
+
+
+def test_errors_are_reported_not_crashing():
+    from mbrl_amd import _lib
+    lib = _lib.load()
+    sh = _lib.MlpShape(0, 6, 512, 3, 1)
+    rc = lib.mbrl_mlp_pack(ctypes.byref(sh), None, None, None, None)
+    assert rc == -2
+    assert b"unsupported MLP shape" in lib.mbrl_last_error()
+    rc = lib.mbrl_select_elites(None, 1, 10, 20, 0, None, None, None, 0, None)
+    assert rc == -1
+
+
+STRUCTS = {
+    "MlpShape": ("mbrl_mlp_shape", ["state_dim", "action_dim", "hidden", "n_hidden", "ensemble"]),
+    "Norm": ("mbrl_norm", ["obs_mean", "obs_std", "act_mean", "act_std", "normalize_state", "unnormalize_state",
+                           "normalize_action"]),
+    "Cost": ("mbrl_cost", ["kind", "has_state_cost", "has_action_cost", "weights", "goal", "alpha_state",
+                           "alpha_action"]),
+    "Sampler": ("mbrl_sampler", ["seed", "iteration", "mu", "sigma", "lo", "hi"]),
+    "CemParams": ("mbrl_cem_params", ["N", "H", "K", "iterations", "alpha", "lo", "hi", "init_mu", "init_sigma",
+                                      "seed"]),
+}
+
+
+def test_ctypes_layout_matches_c_header():
+    from mbrl_amd import _lib
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void){"]
+    for py, (c, fields) in STRUCTS.items():
+        lines.append(f'printf("{py} sizeof %zu\\n", sizeof({c}));')
+        for f in fields:
+            lines.append(f'printf("{py} {f} %zu\\n", offsetof({c}, {f}));')
+    lines.append("return 0;}")
+    with tempfile.TemporaryDirectory() as d:
+        src, exe = os.path.join(d, "l.c"), os.path.join(d, "l")
+        open(src, "w").write("\n".join(lines))
+        try:
+            subprocess.run(["gcc", "-std=c99", "-o", exe, src], check=True, capture_output=True)
+        except (FileNotFoundError, subprocess.CalledProcessError) as e:  # pragma: no cover
+            pytest.skip(f"gcc unavailable: {e}")
+        out = subprocess.run([exe], check=True, capture_output=True, text=True).stdout.split("\n")
+    for line in filter(None, out):
+        py, field, val = line.split()
+        cls = getattr(_lib, py)
+        if field == "sizeof":
+            assert ctypes.sizeof(cls) == int(val), py
+        else:
+            assert getattr(cls, field).offset == int(val), (py, field)

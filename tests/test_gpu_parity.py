@@ -1,0 +1,276 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle and the reference's golden
+vectors. Bars: bit-exact for the RNG draw, elite index sets, argmin and the refit's mu / sigma;
+returns within 1e-5 relative (BASELINE.json north_star) against max(|ref|, 1)."""
+import functools
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import cem as ocem
+from oracle.philox import cem_actions
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-5
+DEV = "cuda:0"
+
+
+def rel_err(x, ref):
+    x = x.detach().cpu().numpy() if torch.is_tensor(x) else np.asarray(x)
+    return float(np.max(np.abs(x.astype(np.float64) - ref) / np.maximum(np.abs(ref), 1.0)))
+
+
+def build(problem):
+    """mbrl_amd model / cost / sampler closures wired exactly as GoalStateAgent (agents.py:219-233)."""
+    from mbrl_amd import data, env, models
+    cfg = problem["cfg"]
+    s, a, W, L = cfg["s"], cfg["a"], cfg["W"], cfg["L"]
+    members = []
+    for layers in problem["model"]:
+        m = models.Model(s, a, hidden_units=W, n_hidden=L)
+        with torch.no_grad():
+            for lin, (w, b) in zip(m.linears(), layers):
+                lin.weight.copy_(torch.from_numpy(w))
+                lin.bias.copy_(torch.from_numpy(b))
+        members.append(m)
+    module = members[0] if len(members) == 1 else models.EnsembleModel(members)
+    nm = problem["norm"]
+    ds = data.TransitionsDataset({"observations": {"mean": torch.from_numpy(nm["obs_mean"]),
+                                                   "std": torch.from_numpy(nm["obs_std"])},
+                                  "actions": {"mean": torch.from_numpy(nm["act_mean"]),
+                                              "std": torch.from_numpy(nm["act_std"])}})
+    model_fn = functools.partial(module, **ds.normalizers())
+    c = problem["cost"]
+    cost_fn = models.goal_state_cost(models.SmoothAbsLoss(torch.from_numpy(c["weights"]), torch.from_numpy(c["goal"]),
+                                                          c["alpha_state"]), models.CoshLoss(c["alpha_action"]))
+    sample_action = env.sample_action_fn(env.BoundedActionSpec(a, -1.0, 1.0))
+    return module, model_fn, cost_fn, sample_action
+
+
+def device_problem(problem):
+    from mbrl_amd import fused
+    _, model_fn, cost_fn, _ = build(problem)
+    md = fused.describe_model(model_fn)
+    cd = fused.describe_cost(cost_fn, md["s"])
+    assert md is not None and cd is not None, "closures not recognised by the fused path"
+    return fused.device_problem(md, cd, torch.device(DEV))
+
+
+# ------------------------------------------------------------------------------------------------ RNG
+@pytest.mark.parametrize("a,N,H,it,offset", [(1, 1000, 12, 0, 0), (6, 4096, 30, 3, 0), (21, 257, 5, 4, 4096),
+                                             (5, 33, 3, 1, 7)])
+def test_proposal_draw_bit_exact(a, N, H, it, offset):
+    from mbrl_amd import fused
+    rng = np.random.default_rng(a * 131 + N)
+    mu = rng.uniform(-0.5, 0.5, size=(H, a)).astype(np.float32)
+    sg = rng.uniform(0.1, 0.9, size=(H, a)).astype(np.float32)
+    mu_d, sg_d = torch.from_numpy(mu).to(DEV), torch.from_numpy(sg).to(DEV)
+    out = torch.empty((H, N, a), dtype=torch.float32, device=DEV)
+    seed = 0x1234_5678_9ABC + a
+    fused.sample_actions(fused.make_sampler(seed, it, mu_d, sg_d, -1.0, 1.0), H, a, N, offset, out)
+    ref = cem_actions(mu, sg, -1.0, 1.0, seed, it, np.arange(offset, offset + N))
+    assert np.array_equal(out.cpu().numpy(), ref)
+
+
+# ------------------------------------------------------------------------------------------------ rollout
+@pytest.mark.parametrize("cid,over", [(2, dict(N=1000, H=20)), (3, dict(N=300, H=30)), (4, dict(N=200, H=7)),
+                                      (5, dict(N=40, H=6)), (2, dict(N=1, H=3)), (3, dict(N=17, H=2))])
+def test_rollout_costs_and_states_given_actions(cid, over):
+    from mbrl_amd import fused
+    p = ocem.synth_problem(cid, **over)
+    N, H, a, s, E = over["N"], over["H"], p["cfg"]["a"], p["cfg"]["s"], p["cfg"]["E"]
+    A = cem_actions(np.zeros((H, a), np.float32), np.full((H, a), 0.5, np.float32), -1, 1, 11, 0, np.arange(N))
+    ref_costs, ref_states = ocem.rollout(p["model"], p["norm"], p["cost"], p["s0"], A, store_states=True)
+    prob = device_problem(p)
+    states = torch.empty((E, H, N, s), dtype=torch.float32, device=DEV)
+    costs = fused.rollout(prob, torch.from_numpy(p["s0"]).to(DEV), N, H, actions=torch.from_numpy(A).to(DEV),
+                          states_out=states)
+    torch.cuda.synchronize()
+    assert rel_err(costs, ref_costs) < RTOL
+    assert np.allclose(states.cpu().numpy(), ref_states, rtol=1e-4, atol=1e-4)
+
+
+def test_rollout_sampled_matches_given():
+    """In-kernel Philox draw == the standalone draw: same costs and the same recorded actions."""
+    from mbrl_amd import _lib, fused
+    p = ocem.synth_problem(3, N=500, H=9)
+    prob = device_problem(p)
+    N, H, a = 500, 9, 6
+    mu = torch.full((H, a), 0.1, device=DEV)
+    sg = torch.full((H, a), 0.4, device=DEV)
+    sp = fused.make_sampler(77, 2, mu, sg, -1.0, 1.0)
+    acts = torch.empty((H, N, a), device=DEV)
+    s0 = torch.from_numpy(p["s0"]).to(DEV)
+    c1 = fused.rollout(prob, s0, N, H, sampler=sp, actions_out=acts)
+    c2 = fused.rollout(prob, s0, N, H, actions=acts.clone())
+    torch.cuda.synchronize()
+    ref = cem_actions(mu.cpu().numpy(), sg.cpu().numpy(), -1, 1, 77, 2, np.arange(N))
+    assert np.array_equal(acts.cpu().numpy(), ref)
+    assert torch.equal(c1, c2)
+    assert _lib is not None
+
+
+def test_dynamics_forward_matches_oracle_step():
+    p = ocem.synth_problem(4)
+    module, model_fn, _, _ = build(p)
+    rng = np.random.default_rng(5)
+    B = 333
+    s = rng.standard_normal((B, 24)).astype(np.float32)
+    a = rng.uniform(-1, 1, (B, 6)).astype(np.float32)
+    with torch.no_grad():
+        out = model_fn(torch.from_numpy(s).to(DEV), torch.from_numpy(a).to(DEV))
+    ref = ocem.dynamics_step(p["model"][0], p["norm"], s, a)
+    assert np.allclose(out.cpu().numpy(), ref, rtol=1e-5, atol=1e-5)
+    from mbrl_amd import fused
+    assert fused._PACKED.get(module) is not None, "forward did not take the HIP path"
+
+
+# ------------------------------------------------------------------------------------------------ select / refit
+def test_select_matches_stable_argsort_with_ties_nan_and_signed_zero():
+    from mbrl_amd import _lib, fused
+    rng = np.random.default_rng(0)
+    for N, K in [(1, 1), (10, 3), (1000, 100), (4096, 409), (32768, 3276), (5000, 5000)]:
+        r = rng.integers(0, 50, size=N).astype(np.float32)      # heavy ties
+        if N >= 10:
+            r[rng.integers(0, N, size=N // 10 + 1)] = np.nan
+            r[rng.integers(0, N, size=3)] = -0.0
+            r[rng.integers(0, N, size=3)] = 0.0
+            r[rng.integers(0, N, size=2)] = -np.inf
+        el = fused.select(torch.from_numpy(r).to(DEV).view(1, N), K)
+        assert np.array_equal(el.cpu().numpy(), ocem.select_elites(r, K)), (N, K)
+        am = fused.select(torch.from_numpy(r).to(DEV).view(1, N), 1, nan_policy=_lib.MBRL_NAN_FIRST)
+        assert int(am[0]) == ocem.rs_argmin(r), N
+
+
+def test_select_ensemble_mean():
+    from mbrl_amd import fused
+    rng = np.random.default_rng(1)
+    c = rng.uniform(100, 200, size=(5, 3000)).astype(np.float32)
+    ret = torch.empty(3000, device=DEV)
+    el = fused.select(torch.from_numpy(c).to(DEV), 300, returns_out=ret)
+    r = ocem.ensemble_returns(c)
+    assert np.array_equal(ret.cpu().numpy(), r)
+    assert np.array_equal(el.cpu().numpy(), ocem.select_elites(r, 300))
+
+
+@pytest.mark.parametrize("H,a,N,K", [(30, 6, 4096, 409), (50, 21, 2000, 200), (12, 1, 128, 1), (7, 5, 100, 100)])
+def test_refit_bit_exact(H, a, N, K):
+    from mbrl_amd import fused
+    rng = np.random.default_rng(H + a)
+    mu = rng.uniform(-0.3, 0.3, size=(H, a)).astype(np.float32)
+    sg = rng.uniform(0.2, 0.6, size=(H, a)).astype(np.float32)
+    elites = np.sort(rng.choice(N, size=K, replace=False)).astype(np.int64)
+    mu_d, sg_d = torch.from_numpy(mu).to(DEV), torch.from_numpy(sg).to(DEV)
+    mo, so = torch.empty_like(mu_d), torch.empty_like(sg_d)
+    sp = fused.make_sampler(4242, 1, mu_d, sg_d, -1.0, 1.0)
+    fused.refit(sp, H, a, torch.from_numpy(elites).to(DEV), 0.1, mo, so)
+    A = cem_actions(mu, sg, -1, 1, 4242, 1, elites)                # [H, K, a]
+    rm, rs = ocem.refit(mu, sg, np.ascontiguousarray(A.transpose(1, 0, 2)), 0.1)
+    assert np.array_equal(mo.cpu().numpy(), rm)
+    assert np.array_equal(so.cpu().numpy(), rs)
+
+
+# ------------------------------------------------------------------------------------------------ whole planners
+CEM_CASES = [("config2_cem", 2, {}), ("config3_cem", 3, {}), ("config4_cem_N2048", 4, dict(N=2048)),
+             ("config5_cem_N256_H20", 5, dict(N=256, H=20))]
+
+
+@pytest.mark.parametrize("name,cid,over", CEM_CASES, ids=[c[0] for c in CEM_CASES])
+def test_cem_plan_against_reference_golden(golden, name, cid, over):
+    from mbrl_amd import CEMPlanner
+    g = golden(name)
+    p = ocem.synth_problem(cid, **over)
+    _, model_fn, cost_fn, sample_action = build(p)
+    res = CEMPlanner.plan_detailed(torch.from_numpy(p["s0"]), model_fn, cost_fn, sample_action, int(g["H"]),
+                                   num_candidates=int(g["N"]), num_elites=int(g["K"]),
+                                   num_iterations=int(g["I"]), alpha=float(g["alpha"]), seed=p["rng_seed"],
+                                   record=True)
+    for it in range(int(g["I"])):
+        assert rel_err(res["returns"][it], g["returns"][it]) < RTOL, f"iteration {it}"
+        assert np.array_equal(res["elites"][it].cpu().numpy(), g["elites"][it]), f"iteration {it}"
+    assert np.array_equal(res["mu"].cpu().numpy(), g["mu"][-1])
+    assert np.array_equal(res["sigma"].cpu().numpy(), g["sigma"][-1])
+    assert np.array_equal(res["actions"].numpy(), g["final_actions"])
+    assert np.allclose(res["states"].numpy(), g["final_states"], rtol=1e-4, atol=1e-4)
+
+
+def test_random_shooting_planner_against_reference_golden(golden):
+    """Config 1 through the public API with the reference's sampler semantics and global NumPy RNG."""
+    from mbrl_amd import RandomShootingPlanner
+    g = golden("config1_rs")
+    p = ocem.synth_problem(1)
+    _, model_fn, cost_fn, sample_action = build(p)
+    np.random.seed(int(g["np_seed"]))
+    states, actions = RandomShootingPlanner.plan(torch.from_numpy(p["s0"]), model_fn, cost_fn, sample_action,
+                                                 p["cfg"]["H"], None, num_trajectories=p["cfg"]["N"])
+    assert np.array_equal(actions.numpy(), g["plan_actions"])
+    assert np.allclose(states.numpy(), g["plan_states"], rtol=1e-5, atol=1e-5)
+
+
+def test_random_shooting_toy_known_answer(golden):
+    """test_random_shooting.py:5-25 through the generic callable path (HIP argmin)."""
+    from mbrl_amd import RandomShootingPlanner
+    world_size, goal = 10, torch.tensor(9, dtype=torch.float)
+
+    def model(states, actions):
+        return torch.fmod((torch.fmod(states + actions, world_size) + world_size), world_size)
+
+    def sample_action(batch_size):
+        return torch.randint(low=-1, high=2, size=(batch_size, 1), dtype=torch.float)
+
+    def cost(states, actions):
+        return torch.abs(states - goal.to(states.device))
+
+    torch.manual_seed(0)
+    states, actions = RandomShootingPlanner.plan(torch.tensor([2], dtype=torch.float), model, cost, sample_action, 5,
+                                                 None, num_trajectories=1000)
+    assert states.numpy().ravel().tolist() == [1.0, 0.0, 9.0, 9.0, 8.0]
+    assert float(torch.abs(states - 9).sum()) == 18.0
+
+
+def test_cem_generic_path_matches_fused():
+    """Opaque callables (generic path) and recognised closures (fused path) agree on the elite sets."""
+    from mbrl_amd import CEMPlanner
+    p = ocem.synth_problem(2, N=512, H=10)
+    _, model_fn, cost_fn, sample_action = build(p)
+    kw = dict(num_candidates=512, num_iterations=3, seed=5, record=True)
+    fused_res = CEMPlanner.plan_detailed(torch.from_numpy(p["s0"]), model_fn, cost_fn, sample_action, 10, **kw)
+    opaque_model = lambda s, a: model_fn(s, a)        # noqa: E731  (not introspectable)
+    opaque_cost = lambda s, a: cost_fn(s, a)          # noqa: E731
+    gen = CEMPlanner.plan_detailed(torch.from_numpy(p["s0"]), opaque_model, opaque_cost, sample_action, 10, **kw)
+    for it in range(3):
+        assert rel_err(gen["returns"][it], fused_res["returns"][it].cpu().numpy()) < RTOL
+        assert torch.equal(gen["elites"][it], fused_res["elites"][it])
+
+
+# ------------------------------------------------------------------------------------------------ full sizes
+@pytest.mark.parametrize("cid", [3, 4, 5])
+def test_full_size_plan_sampled_candidates(cid):
+    """BASELINE configs at full N/H/E: every iteration's returns for 48 random candidates are
+    recomputed by the oracle from the counter RNG (size-independent check), elites are exactly the
+    stable top-K of the device returns, and the plan is deterministic across calls."""
+    from mbrl_amd import CEMPlanner
+    p = ocem.synth_problem(cid)
+    cfg = p["cfg"]
+    N, H, a = cfg["N"], cfg["H"], cfg["a"]
+    _, model_fn, cost_fn, sample_action = build(p)
+    kw = dict(num_candidates=N, num_iterations=3, seed=p["rng_seed"], record=True)
+    res = CEMPlanner.plan_detailed(torch.from_numpy(p["s0"]), model_fn, cost_fn, sample_action, H, **kw)
+    res2 = CEMPlanner.plan_detailed(torch.from_numpy(p["s0"]), model_fn, cost_fn, sample_action, H, **kw)
+    assert torch.equal(res["returns"], res2["returns"]) and torch.equal(res["mu"], res2["mu"])
+    rng = np.random.default_rng(cid)
+    mu = np.zeros((H, a), np.float32)
+    sg = np.full((H, a), 0.5, np.float32)
+    K = N // 10
+    for it in range(3):
+        rets = res["returns"][it].cpu().numpy()
+        elites = res["elites"][it].cpu().numpy()
+        assert np.array_equal(elites, ocem.select_elites(rets, K))
+        idx = np.sort(rng.choice(N, size=48, replace=False))
+        A = cem_actions(mu, sg, -1, 1, p["rng_seed"], it, idx)
+        ref = ocem.ensemble_returns(ocem.rollout(p["model"], p["norm"], p["cost"], p["s0"], A))
+        assert rel_err(rets[idx], ref) < RTOL, f"iteration {it}"
+        Ael = cem_actions(mu, sg, -1, 1, p["rng_seed"], it, elites)
+        mu, sg = ocem.refit(mu, sg, np.ascontiguousarray(Ael.transpose(1, 0, 2)), 0.1)
+    assert np.array_equal(res["mu"].cpu().numpy(), mu)
+    assert np.array_equal(res["sigma"].cpu().numpy(), sg)

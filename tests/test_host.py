@@ -1,0 +1,98 @@
+"""CPU: host-side logic -- synthetic inputs, closure recognition, model semantics, sharding layout."""
+import functools
+
+import numpy as np
+import torch
+
+from oracle import cem as ocem
+
+
+def test_synthetic_matches_oracle_generator():
+    from mbrl_amd import synthetic
+    for cid, over in [(1, {}), (3, {}), (5, dict(N=64, H=4))]:
+        prob = synthetic.make_problem(cid, **over)
+        p = ocem.synth_problem(cid, **over)
+        members = prob["module"].members if prob["cfg"]["E"] > 1 else [prob["module"]]
+        model = [[(l.weight.detach().numpy(), l.bias.detach().numpy()) for l in m.linears()] for m in members]
+        assert ocem.weights_sha256(model) == ocem.weights_sha256(p["model"])
+        assert np.array_equal(prob["s0"].numpy(), p["s0"])
+        assert np.array_equal(prob["goal"].numpy(), p["cost"]["goal"])
+        assert np.array_equal(prob["stats"]["actions"]["std"].numpy(), p["norm"]["act_std"])
+        assert prob["rng_seed"] == p["rng_seed"]
+
+
+def test_flop_per_candidate_step_matches_survey():
+    from mbrl_amd import synthetic
+    assert synthetic.flop_per_candidate_step(synthetic.CONFIGS[2]) == 136_704
+    assert synthetic.flop_per_candidate_step(synthetic.CONFIGS[3]) == 1_089_536
+    assert synthetic.flop_per_candidate_step(synthetic.CONFIGS[4]) == 1_103_872
+    assert synthetic.flop_per_candidate_step(synthetic.CONFIGS[5]) == 5 * 1_207_296
+
+
+def test_closure_recognition():
+    from mbrl_amd import fused, synthetic
+    prob = synthetic.make_problem(3)
+    md = fused.describe_model(prob["model"])
+    assert md is not None and (md["s"], md["a"], md["W"], md["L"], md["E"]) == (17, 6, 512, 3, 1)
+    assert md["norm"]["normalize_state"] and md["norm"]["unnormalize_state"] and md["norm"]["normalize_action"]
+    cd = fused.describe_cost(prob["cost"], 17)
+    assert cd is not None and cd["alpha_state"] == 0.4 and cd["alpha_action"] == 0.25
+    assert fused.describe_sampler(prob["sample_action"]) == (-1.0, 1.0, 6)
+    # anything opaque -> generic path
+    assert fused.describe_model(lambda s, a: s) is None
+    assert fused.describe_cost(lambda s, a: s, 17) is None
+    # a noisy model is not deterministic -> generic path
+    from mbrl_amd import models
+    noisy = models.Model(3, 1, 8, noise=0.1)
+    assert fused.describe_model(noisy) is None
+    ens = synthetic.make_problem(5, N=8, H=2)
+    assert fused.describe_model(ens["model"])["E"] == 5
+
+
+def test_reference_style_model_duck_typed():
+    """The reference's models.Model (linear1..3, ReLU, noise=None) is recognised by duck typing."""
+    from mbrl_amd import fused
+
+    class Model(torch.nn.Module):  # same attribute layout as /root/reference/src/mbrl/models.py:96-110
+        def __init__(self):
+            super().__init__()
+            self.linear1 = torch.nn.Linear(7, 50)
+            self.linear2 = torch.nn.Linear(50, 50)
+            self.linear3 = torch.nn.Linear(50, 5)
+            self.activation_fn = torch.nn.ReLU()
+            self.noise = None
+    md = fused.describe_model(Model())
+    assert (md["s"], md["a"], md["W"], md["L"]) == (5, 2, 50, 2)
+
+
+def test_model_cpu_forward_is_reference_arithmetic():
+    from mbrl_amd import synthetic
+    prob = synthetic.make_problem(4, N=8)
+    p = ocem.synth_problem(4, N=8)
+    rng = np.random.default_rng(2)
+    s = rng.standard_normal((64, 24)).astype(np.float32)
+    a = rng.uniform(-1, 1, (64, 6)).astype(np.float32)
+    with torch.no_grad():
+        out = prob["model"](torch.from_numpy(s), torch.from_numpy(a)).numpy()
+    assert np.allclose(out, ocem.dynamics_step(p["model"][0], p["norm"], s, a), rtol=1e-5, atol=1e-5)
+    c = prob["cost"](torch.from_numpy(s), torch.from_numpy(a)).numpy()
+    assert np.allclose(c, ocem.goal_state_cost(s, a, p["cost"]), rtol=1e-6)
+
+
+def test_sample_action_reference_semantics():
+    from mbrl_amd import env
+    spec = env.BoundedActionSpec(3, -5.0, 0.5)
+    np.random.seed(4)
+    x = env._sample_action(spec, batch_size=7)
+    np.random.seed(4)
+    ref = np.random.uniform(-3, 0.5, size=21).reshape(7, 3)
+    assert x.dtype == torch.float32 and x.shape == (7, 3)
+    assert np.array_equal(x.numpy(), ref.astype(np.float32))
+
+
+def test_model_state_dict_compatible_with_reference_layout():
+    from mbrl_amd import models
+    m = models.Model(5, 1, hidden_units=256)
+    assert sorted(m.state_dict()) == sorted(
+        [f"linear{i}.{p}" for i in (1, 2, 3) for p in ("weight", "bias")])
+    assert isinstance(functools.partial(m), functools.partial)
