@@ -124,7 +124,8 @@ int mbrl_mlp_pack(const mbrl_mlp_shape* shape, const float* const* weights, cons
 /* ---- rollout + cost: replaces RandomShootingPlanner._generate_trajectories' model/cost loop
  * (planners.py:199-210) and DynamicsModel.forward (models.py:13-29) on its batch.
  * s0: [s] broadcast to every candidate (planners.py:204) or [N][s] when s0_per_candidate.
- * actions: [H][N][a] time-major (planners.py:200,207) or NULL to draw from `sampler`.
+ * actions: [H][N][a] time-major (planners.py:200,207), or NULL to draw them from `sampler` into
+ *          actions_out first (actions_out is then required).
  * costs: [E][N] per-member return sum_t cost(s_{t+1}, a_t), summed sequentially in t.
  * actions_out: [H][N][a] or NULL. states_out: [E][H][N][s] or NULL.
  * n_offset: global index of local candidate 0 (rank shard offset; keys the RNG). */

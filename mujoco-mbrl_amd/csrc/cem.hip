@@ -296,6 +296,14 @@ static int shape_geometry(const mbrl_mlp_shape* sh, Geometry* g) {
 
 static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+static int sample_impl(const mbrl_sampler* sp, int H, int a, int N, int n_offset, float* out, hipStream_t stream) {
+    const size_t total = (size_t)H * N * ((a + 3) / 4);
+    const int blocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
+    hipLaunchKernelGGL(sample_kernel, dim3(blocks), dim3(256), 0, stream, sp->seed, sp->iteration, sp->mu, sp->sigma,
+                       sp->lo, sp->hi, H, a, N, n_offset, out);
+    return hip_check(hipGetLastError(), "sample launch");
+}
+
 static int rollout_impl(const Geometry& g, const void* packed, const mbrl_norm* norm, const mbrl_cost* cost,
                         const float* s0, int s0_per_cand, const float* actions, const mbrl_sampler* sampler,
                         int N, int H, int n_offset, float* costs, float* actions_out, float* states_out,
@@ -329,19 +337,23 @@ static int rollout_impl(const Geometry& g, const void* packed, const mbrl_norm* 
         if (A.has_sc && (!A.cw || !A.goal)) return fail(MBRL_EINVAL, "state cost without weights/goal");
     }
     A.s0 = s0; A.s0_per_cand = s0_per_cand;
-    A.actions = actions;
     if (!actions) {
-        A.seed = sampler->seed; A.iteration = sampler->iteration;
-        A.mu = sampler->mu; A.sigma = sampler->sigma; A.lo = sampler->lo; A.hi = sampler->hi;
-        if (!A.mu || !A.sigma) return fail(MBRL_EINVAL, "sampler mu/sigma NULL");
+        // CEM proposal: draw into actions_out first, then roll those actions out
+        if (!actions_out) return fail(MBRL_EINVAL, "a sampled rollout needs actions_out to hold the draw");
+        if (!sampler->mu || !sampler->sigma) return fail(MBRL_EINVAL, "sampler mu/sigma NULL");
+        int rc = sample_impl(sampler, H, g.a, N, n_offset, actions_out, stream);
+        if (rc) return rc;
+        actions = actions_out;
     }
-    A.costs = costs; A.actions_out = actions_out; A.states_out = states_out;
+    A.actions = actions;
+    A.costs = costs; A.states_out = states_out;
     // Tile height: two 16-row blocks per workgroup halve the weight stream per FLOP once there are
     // enough candidates to still give every CU a workgroup.
     int R = (N >= 2 * 16 * 256 && g.T <= 8) ? 2 : 1;
     const int G = (g.a + 3) / 4;
-    if (16 * R * G > 192) R = 1;
-    if (16 * G > 192) return fail(MBRL_EUNSUPPORTED, "action_dim %d too large (max 48)", g.a);
+    (void)G;
+    if (16 * R * g.a > 768) R = 1;
+    if (16 * g.a > 768) return fail(MBRL_EUNSUPPORTED, "action_dim %d too large (max 48)", g.a);
     if (rollout_lds_bytes(A, 16 * R) > 160 * 1024) {
         R = 1;
         if (rollout_lds_bytes(A, 16) > 160 * 1024)
@@ -466,17 +478,12 @@ int mbrl_sample_actions(const mbrl_sampler* sampler, int32_t H, int32_t a, int32
                         float* actions_out, mbrl_stream_t stream) {
     if (!sampler || !sampler->mu || !sampler->sigma || !actions_out) return fail(MBRL_EINVAL, "sample: NULL argument");
     if (H < 1 || a < 1 || N < 1 || n_offset < 0) return fail(MBRL_EINVAL, "sample: bad sizes");
-    const size_t total = (size_t)H * N * ((a + 3) / 4);
-    const int blocks = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
-    hipLaunchKernelGGL(sample_kernel, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                       sampler->seed, sampler->iteration, sampler->mu, sampler->sigma, sampler->lo, sampler->hi,
-                       H, a, N, n_offset, actions_out);
-    return hip_check(hipGetLastError(), "sample launch");
+    return sample_impl(sampler, H, a, N, n_offset, actions_out, reinterpret_cast<hipStream_t>(stream));
 }
 
 // Workspace layout for mbrl_cem_plan.
 struct PlanWs {
-    float *costs, *mu[2], *sigma[2], *aelite, *states, *tmp_cost;
+    float *costs, *mu[2], *sigma[2], *aelite, *states, *tmp_cost, *actions;
     int64_t* elites;
     uint32_t* keys;
     size_t bytes;
@@ -489,6 +496,7 @@ static PlanWs plan_ws(const Geometry& g, const mbrl_cem_params* p, void* base) {
     auto take = [&](size_t n) { void* r = b ? b + o : nullptr; o += align256(n); return r; };
     const size_t Ha = (size_t)p->H * g.a;
     w.costs = (float*)take((size_t)g.E * p->N * 4);
+    w.actions = (float*)take((size_t)p->H * p->N * g.a * 4);
     w.mu[0] = (float*)take(Ha * 4); w.mu[1] = (float*)take(Ha * 4);
     w.sigma[0] = (float*)take(Ha * 4); w.sigma[1] = (float*)take(Ha * 4);
     w.aelite = (float*)take((size_t)p->H * p->K * g.a * 4);
@@ -534,7 +542,7 @@ int mbrl_cem_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_no
             rc = hip_check(hipEventRecord(reinterpret_cast<hipEvent_t>(rollout_events[2 * it]), stream), "event");
             if (rc) return rc;
         }
-        rc = rollout_impl(g, packed, norm, cost, s0, 0, nullptr, &sp, p->N, p->H, 0, costs, nullptr, nullptr, stream);
+        rc = rollout_impl(g, packed, norm, cost, s0, 0, nullptr, &sp, p->N, p->H, 0, costs, w.actions, nullptr, stream);
         if (rc) return rc;
         if (rollout_events) {
             rc = hip_check(hipEventRecord(reinterpret_cast<hipEvent_t>(rollout_events[2 * it + 1]), stream), "event");

@@ -58,20 +58,14 @@ struct RolloutArgs {
     int has_sc, has_ac;
     const float* s0;
     int s0_per_cand;
-    const float* actions;  // given [H][N][a] or nullptr -> sampled
-    uint64_t seed;
-    int iteration;
-    const float* mu;
-    const float* sigma;
-    float lo, hi;
+    const float* actions;  // [H][N][a] (given, or drawn by the proposal kernel just before)
     float* costs;
     float* actions_out;
     float* states_out;
 };
 
 struct LdsMap {
-    float *act, *part, *sterm, *aterm, *obs_mean, *obs_std, *act_mean, *act_std, *goal, *cw, *hbias, *mu,
-        *sigma;
+    float *act, *act2, *part, *sterm, *aterm, *obs_mean, *obs_std, *act_mean, *act_std, *goal, *cw, *hbias;
     size_t total_floats;
 };
 
@@ -82,6 +76,7 @@ __host__ __device__ inline LdsMap lds_map(const RolloutArgs& A, float* base, int
     size_t o = 0;
     auto take = [&](size_t n) { float* p = base ? base + o : nullptr; o += lds_round4(n); return p; };
     L.act = take((size_t)M * A.lda);
+    L.act2 = take((size_t)M * A.lda);
     L.part = take((size_t)4 * M * A.pw);
     L.sterm = take((size_t)M * A.s);
     L.aterm = take((size_t)2 * M * A.a);
@@ -92,8 +87,6 @@ __host__ __device__ inline LdsMap lds_map(const RolloutArgs& A, float* base, int
     L.goal = take(A.s);
     L.cw = take(A.s);
     L.hbias = take((size_t)A.L * A.Wpad + 16 * (size_t)A.NOT);
-    L.mu = take(A.actions ? 0 : (size_t)A.H * A.a);
-    L.sigma = take(A.actions ? 0 : (size_t)A.H * A.a);
     L.total_floats = o;
     return L;
 }

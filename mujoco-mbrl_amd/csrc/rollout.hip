@@ -7,25 +7,31 @@
 //
 // Mapping:
 //   * one workgroup = 4 waves = M = 16*R candidates of one ensemble member, for all H steps; the
-//     candidates' activations live in LDS for the whole horizon (never touch HBM).
+//     candidates' activations live in LDS for the whole horizon (ping-pong buffers, never HBM).
 //   * every Linear is a chain of v_mfma_f32_16x16x4_f32 (exact fp32): wave w owns output columns
 //     [w*W/4, (w+1)*W/4) of each hidden layer (T = W/64 16-column tiles); the output layer splits
 //     K over the 4 waves and reduces through LDS.
 //   * weights are pre-packed (pack kernels in cem.hip) into the exact fragment order each wave
 //     consumes: one global_load_dwordx4 per lane = one 1 KiB coalesced B fragment. The per-step
 //     stream (~2.2 MB for 3x512) stays resident in every XCD's 4 MB L2; each wave streams its
-//     slice with a register double buffer that runs ahead across layer and step boundaries.
-//   * the step epilogue (unnormalise, goal cost, renormalise, next proposal draw from the Philox
-//     counter RNG) runs on the VALU from LDS; the per-candidate return is a register of thread m.
+//     slice through a register double buffer that runs one chunk (32 MFMAs) ahead across layer and
+//     step boundaries. sched_barrier pins the issue order so hipcc cannot sink the prefetch next to
+//     its use (it did: the unpinned build drained vmcnt(0) every chunk).
+//   * the A operand (activations) is read from LDS one chunk ahead as well.
+//   * candidate actions come from HBM ([H][N][a], written by the proposal kernel or given by the
+//     caller); a_{t+1} is loaded at the start of step t so its latency hides under the MFMAs.
+//   * the step epilogue (unnormalise, goal cost, renormalise) runs on the VALU out of LDS; per-row
+//     cost sums are wave shuffle reductions; the return is a register of the reducing lane.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "mbrl_internal.h"
-#include "mbrl_rng.h"
 
 namespace mbrl {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define MBRL_PIN() __builtin_amdgcn_sched_barrier(0)
 
 template <int T>
 __device__ __forceinline__ void load_chunk(f32x4 (&b)[T], const f32x4* __restrict__ p) {
@@ -33,14 +39,16 @@ __device__ __forceinline__ void load_chunk(f32x4 (&b)[T], const f32x4* __restric
     for (int j = 0; j < T; ++j) b[j] = p[j * 64];
 }
 
-// Hidden-type chunk: one 16-deep K slice x T output tiles.
-template <int T, int R>
-__device__ __forceinline__ void mma_hidden(f32x4 (&acc)[R][T], const f32x4 (&b)[T], const float* act,
-                                           int lda, int kc, int lane) {
-    f32x4 a[R];
+template <int R>
+__device__ __forceinline__ void read_a(f32x4 (&a)[R], const float* act, int lda, int kc, int lane) {
 #pragma unroll
     for (int r = 0; r < R; ++r)
         a[r] = *reinterpret_cast<const f32x4*>(act + (16 * r + (lane & 15)) * lda + 16 * kc + 4 * (lane >> 4));
+}
+
+// Hidden-type chunk: one 16-deep K slice x T output tiles (MFMAs on independent accumulators).
+template <int T, int R>
+__device__ __forceinline__ void mma_hidden(f32x4 (&acc)[R][T], const f32x4 (&a)[R], const f32x4 (&b)[T]) {
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -50,46 +58,51 @@ __device__ __forceinline__ void mma_hidden(f32x4 (&acc)[R][T], const f32x4 (&b)[
                 acc[r][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[r][s], b[j][s], acc[r][j], 0, 0, 0);
 }
 
-// Output-type chunk: one 16-column output tile over this wave's W/4-deep K range.
+// Output-type chunk: one 16-column output tile over this wave's W/4-deep K range; four accumulator
+// chains so consecutive MFMAs never wait on each other.
 template <int T, int R>
-__device__ __forceinline__ void mma_out(const f32x4 (&aout)[R][T], const f32x4 (&b)[T], float* part,
-                                        int pw, int tile, int lane) {
-    f32x4 o0[R], o1[R];
+__device__ __forceinline__ void mma_out(const f32x4 (&aout)[R][T], const f32x4 (&b)[T], float* part, int pw,
+                                        int tile, int lane) {
+    f32x4 o[R][4];
 #pragma unroll
-    for (int r = 0; r < R; ++r) { o0[r] = f32x4{0.f, 0.f, 0.f, 0.f}; o1[r] = o0[r]; }
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) o[r][s] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kc = 0; kc < T; ++kc)
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            o0[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(aout[r][kc][0], b[kc][0], o0[r], 0, 0, 0);
-            o1[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(aout[r][kc][1], b[kc][1], o1[r], 0, 0, 0);
-            o0[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(aout[r][kc][2], b[kc][2], o0[r], 0, 0, 0);
-            o1[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(aout[r][kc][3], b[kc][3], o1[r], 0, 0, 0);
-        }
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                o[r][s] = __builtin_amdgcn_mfma_f32_16x16x4f32(aout[r][kc][s], b[kc][s], o[r][s], 0, 0, 0);
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-            part[(16 * r + 4 * (lane >> 4) + i) * pw + 16 * tile + (lane & 15)] = o0[r][i] + o1[r][i];
+            part[(16 * r + 4 * (lane >> 4) + i) * pw + 16 * tile + (lane & 15)] =
+                (o[r][0][i] + o[r][1][i]) + (o[r][2][i] + o[r][3][i]);
 }
 
+// acc + bias -> ReLU -> next activation buffer; one barrier (ping-pong buffers).
 template <int T, int R>
-__device__ __forceinline__ void hidden_epilogue(f32x4 (&acc)[R][T], float* act, int lda, const float* hb,
-                                                int wave, int lane) {
-    __syncthreads();  // every wave has finished reading this layer's input
+__device__ __forceinline__ void hidden_store(const f32x4 (&acc)[R][T], const float (&bias)[T], float* out,
+                                             int lda, int wave, int lane) {
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
         for (int j = 0; j < T; ++j) {
             const int col = wave * 16 * T + 16 * j + (lane & 15);
-            const float bias = hb[col];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int row = 16 * r + 4 * (lane >> 4) + i;
-                act[row * lda + col] = fmaxf(acc[r][j][i] + bias, 0.0f);
-            }
+            for (int i = 0; i < 4; ++i)
+                out[(16 * r + 4 * (lane >> 4) + i) * lda + col] = fmaxf(acc[r][j][i] + bias[j], 0.0f);
         }
     __syncthreads();
+}
+
+template <int T>
+__device__ __forceinline__ void load_bias(float (&bias)[T], const float* hb, int wave, int lane) {
+#pragma unroll
+    for (int j = 0; j < T; ++j) bias[j] = hb[wave * 16 * T + 16 * j + (lane & 15)];
 }
 
 template <int T, int R>
@@ -100,46 +113,62 @@ __device__ __forceinline__ void zero_acc(f32x4 (&acc)[R][T]) {
         for (int j = 0; j < T; ++j) acc[r][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 }
 
-// Draw (or read) a_t for this tile's candidates, write the normalised action into the MLP input,
-// and stage its CoshLoss terms.  Threads 64..64+M*G (waves 1..3) so it overlaps phase B on wave 0.
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Per-thread slice of this tile's action block: items i = tid + 256*k of [M][a].
+constexpr int MAX_ACT_ITEMS = 3;  // M*a <= 768 (e.g. M=16, a<=48; M=32, a<=24)
+
 template <int R>
-__device__ __forceinline__ void stage_actions(const RolloutArgs& A, const LdsMap& L, int tile, int t) {
+__device__ __forceinline__ void fetch_actions(const RolloutArgs& A, int tile, int t, float (&av)[MAX_ACT_ITEMS]) {
     constexpr int M = 16 * R;
-    const int G = (A.a + 3) >> 2;
-    const int idx = (int)threadIdx.x - 64;
-    if (idx < 0 || idx >= M * G) return;
-    const int m = idx / G, g = idx - (idx / G) * G;
-    const int n = tile * M + m;
-    const bool valid = n < A.N;
-    float z[4] = {0.f, 0.f, 0.f, 0.f};
-    if (A.actions == nullptr)
-        cem_normal4(A.seed, (uint32_t)(A.n_offset + n), (uint32_t)t, (uint32_t)A.iteration, (uint32_t)g, z);
+#pragma unroll
+    for (int k = 0; k < MAX_ACT_ITEMS; ++k) {
+        const int i = (int)threadIdx.x + 256 * k;
+        av[k] = 0.f;
+        if (i < M * A.a) {
+            const int m = i / A.a, d = i - (i / A.a) * A.a;
+            const int n = tile * M + m;
+            if (n < A.N) av[k] = A.actions[((size_t)t * A.N + n) * A.a + d];
+        }
+    }
+}
+
+// a_t -> normalised MLP input columns [s, s+a) and CoshLoss terms.
+template <int R>
+__device__ __forceinline__ void stage_actions(const RolloutArgs& A, const LdsMap& L, float* act, int t,
+                                              const float (&av)[MAX_ACT_ITEMS]) {
+    constexpr int M = 16 * R;
     float* aterm = L.aterm + (t & 1) * M * A.a;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int d = 4 * g + j;
-        if (d >= A.a) break;
-        float av;
-        if (A.actions == nullptr)
-            av = cem_action(L.mu[t * A.a + d], L.sigma[t * A.a + d], z[j], A.lo, A.hi);
-        else
-            av = valid ? A.actions[((size_t)t * A.N + n) * A.a + d] : 0.0f;
-        L.act[m * A.lda + A.s + d] = A.norm_a ? (av - L.act_mean[d]) / L.act_std[d] : av;
-        aterm[m * A.a + d] = A.has_ac ? coshf(av / A.alpha_a) - 1.0f : 0.0f;
-        if (A.actions_out != nullptr && valid) A.actions_out[((size_t)t * A.N + n) * A.a + d] = av;
+    for (int k = 0; k < MAX_ACT_ITEMS; ++k) {
+        const int i = (int)threadIdx.x + 256 * k;
+        if (i < M * A.a) {
+            const int m = i / A.a, d = i - (i / A.a) * A.a;
+            act[m * A.lda + A.s + d] = A.norm_a ? (av[k] - L.act_mean[d]) / L.act_std[d] : av[k];
+            aterm[m * A.a + d] = A.has_ac ? coshf(av[k] / A.alpha_a) - 1.0f : 0.0f;
+        }
     }
 }
 
 template <int T, int R>
 __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
     constexpr int M = 16 * R;
+    constexpr int KH = 4 * T;  // K chunks of a hidden (W -> W) layer
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const LdsMap L = lds_map(A, smem, M);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int tile = blockIdx.x, e = blockIdx.y;
     const float* member = A.packed + (size_t)e * A.member_stride;
+    float* const actX = L.act;   // step input (layer 0) and every even layer's input
+    float* const actY = L.act2;
 
-    // ---- prologue: parameters into LDS, s0 into the MLP input
+    // ---- prologue: parameters into LDS, s0 and a_0 into the MLP input
+    float av[MAX_ACT_ITEMS];
+    fetch_actions<R>(A, tile, 0, av);
     for (int i = tid; i < A.s; i += 256) {
         L.obs_mean[i] = A.obs_mean ? A.obs_mean[i] : 0.f;
         L.obs_std[i] = A.obs_std ? A.obs_std[i] : 1.f;
@@ -152,20 +181,18 @@ __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
     }
     const float* bias_src = member + A.stream_floats;
     for (int i = tid; i < A.L * A.Wpad + 16 * A.NOT; i += 256) L.hbias[i] = bias_src[i];
-    if (A.actions == nullptr)
-        for (int i = tid; i < A.H * A.a; i += 256) { L.mu[i] = A.mu[i]; L.sigma[i] = A.sigma[i]; }
     __syncthreads();
     for (int i = tid; i < M * A.s; i += 256) {
         const int m = i / A.s, d = i - (i / A.s) * A.s;
         const int n = min(tile * M + m, A.N - 1);
         const float sv = A.s0_per_cand ? A.s0[(size_t)n * A.s + d] : A.s0[d];
-        L.act[m * A.lda + d] = A.norm_s ? (sv - L.obs_mean[d]) / L.obs_std[d] : sv;
+        actX[m * A.lda + d] = A.norm_s ? (sv - L.obs_mean[d]) / L.obs_std[d] : sv;
     }
     for (int i = tid; i < M * A.k0pad_extra; i += 256) {
         const int m = i / A.k0pad_extra, j = i - (i / A.k0pad_extra) * A.k0pad_extra;
-        L.act[m * A.lda + A.s + A.a + j] = 0.f;
+        actX[m * A.lda + A.s + A.a + j] = 0.f;
     }
-    stage_actions<R>(A, L, tile, 0);
+    stage_actions<R>(A, L, actX, 0, av);
     __syncthreads();
 
     // ---- weight stream: this wave's slice of chunk g is at wb + g * cs (f32x4 units)
@@ -175,34 +202,59 @@ __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
     auto chunk_ptr = [&](int g) { return wb + (size_t)(g < C ? g : g - C) * cs; };
 
     f32x4 bA[T], bB[T];
+    f32x4 aA[R], aB[R];
     f32x4 acc[R][T];
+    float bias[T];
     load_chunk<T>(bA, wb);
-    float total = 0.f;
-    const int KH = 4 * T;  // K chunks of a hidden (W -> W) layer
+    float total[M / 4];  // rows 4*wave + (i&3) + 16*(i>>2), held by every lane of the wave
+#pragma unroll
+    for (int i = 0; i < M / 4; ++i) total[i] = 0.f;
 
     for (int t = 0; t < A.H; ++t) {
         int g = 0;
-        // ---- layer 0: [s | a | 0-pad] -> W
+        // a_{t+1} from HBM now; consumed in this step's epilogue
+        if (t + 1 < A.H) fetch_actions<R>(A, tile, t + 1, av);
+        // ---- layer 0: actX [s | a | 0-pad] -> actY (W)
         zero_acc<T, R>(acc);
+        load_bias<T>(bias, L.hbias, wave, lane);
+        read_a<R>(aA, actX, A.lda, 0, lane);
         for (int kc = 0; kc < A.K0C; kc += 2) {
             load_chunk<T>(bB, chunk_ptr(g + 1));
-            mma_hidden<T, R>(acc, bA, L.act, A.lda, kc, lane);
+            read_a<R>(aB, actX, A.lda, kc + 1, lane);
+            MBRL_PIN();
+            mma_hidden<T, R>(acc, aA, bA);
+            MBRL_PIN();
             load_chunk<T>(bA, chunk_ptr(g + 2));
-            mma_hidden<T, R>(acc, bB, L.act, A.lda, kc + 1, lane);
+            if (kc + 2 < A.K0C) read_a<R>(aA, actX, A.lda, kc + 2, lane);
+            MBRL_PIN();
+            mma_hidden<T, R>(acc, aB, bB);
+            MBRL_PIN();
             g += 2;
         }
-        hidden_epilogue<T, R>(acc, L.act, A.lda, L.hbias, wave, lane);
-        // ---- hidden layers 1..L-1: W -> W
+        hidden_store<T, R>(acc, bias, actY, A.lda, wave, lane);
+        // ---- hidden layers 1..L-1 (W -> W), alternating Y->X->Y...
+        float* in = actY;
+        float* out = actX;
         for (int l = 1; l < A.L; ++l) {
             zero_acc<T, R>(acc);
+            load_bias<T>(bias, L.hbias + l * A.Wpad, wave, lane);
+            read_a<R>(aA, in, A.lda, 0, lane);
+#pragma unroll
             for (int kc = 0; kc < KH; kc += 2) {
                 load_chunk<T>(bB, chunk_ptr(g + 1));
-                mma_hidden<T, R>(acc, bA, L.act, A.lda, kc, lane);
+                read_a<R>(aB, in, A.lda, kc + 1, lane);
+                MBRL_PIN();
+                mma_hidden<T, R>(acc, aA, bA);
+                MBRL_PIN();
                 load_chunk<T>(bA, chunk_ptr(g + 2));
-                mma_hidden<T, R>(acc, bB, L.act, A.lda, kc + 1, lane);
+                if (kc + 2 < KH) read_a<R>(aA, in, A.lda, kc + 2, lane);
+                MBRL_PIN();
+                mma_hidden<T, R>(acc, aB, bB);
+                MBRL_PIN();
                 g += 2;
             }
-            hidden_epilogue<T, R>(acc, L.act, A.lda, L.hbias + l * A.Wpad, wave, lane);
+            hidden_store<T, R>(acc, bias, out, A.lda, wave, lane);
+            float* tmp = in; in = out; out = tmp;
         }
         // ---- output layer: W -> s, K split over the 4 waves, partials through LDS
         {
@@ -212,24 +264,28 @@ __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
 #pragma unroll
                 for (int kc = 0; kc < T; ++kc)
                     aout[r][kc] = *reinterpret_cast<const f32x4*>(
-                        L.act + (16 * r + (lane & 15)) * A.lda + wave * 16 * T + 16 * kc + 4 * (lane >> 4));
+                        in + (16 * r + (lane & 15)) * A.lda + wave * 16 * T + 16 * kc + 4 * (lane >> 4));
             float* part = L.part + wave * M * A.pw;
             for (int j = 0; j < A.NOT; j += 2) {
                 load_chunk<T>(bB, chunk_ptr(g + 1));
+                MBRL_PIN();
                 mma_out<T, R>(aout, bA, part, A.pw, j, lane);
+                MBRL_PIN();
                 load_chunk<T>(bA, chunk_ptr(g + 2));
+                MBRL_PIN();
                 mma_out<T, R>(aout, bB, part, A.pw, j + 1, lane);
+                MBRL_PIN();
                 g += 2;
             }
         }
         __syncthreads();
 
-        // ---- phase A: s_{t+1} = unnormalize(out), state-cost terms, next MLP input
+        // ---- epilogue A: s_{t+1} = unnormalize(out), state-cost terms, next MLP input into actX
         const float* bout = L.hbias + A.L * A.Wpad;
+        const int ws = M * A.pw;
         for (int i = tid; i < M * A.s; i += 256) {
             const int m = i / A.s, d = i - (i / A.s) * A.s;
             const int ro = m * A.pw + d;
-            const int ws = M * A.pw;
             const float o = L.part[ro] + L.part[ws + ro] + L.part[2 * ws + ro] + L.part[3 * ws + ro] + bout[d];
             const float sn = A.unnorm_s ? o * L.obs_std[d] + L.obs_mean[d] : o;
             float term = 0.f;
@@ -238,31 +294,37 @@ __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
                 term = sqrtf(x * x + A.alpha_s2) - A.alpha_s;
             }
             L.sterm[m * A.s + d] = term;
-            L.act[m * A.lda + d] = A.norm_s ? (sn - L.obs_mean[d]) / L.obs_std[d] : sn;
+            actX[m * A.lda + d] = A.norm_s ? (sn - L.obs_mean[d]) / L.obs_std[d] : sn;
             const int n = tile * M + m;
             if (A.states_out != nullptr && n < A.N)
                 A.states_out[(((size_t)e * A.H + t) * A.N + n) * A.s + d] = sn;
         }
         for (int i = tid; i < M * A.k0pad_extra; i += 256) {
             const int m = i / A.k0pad_extra, j = i - (i / A.k0pad_extra) * A.k0pad_extra;
-            L.act[m * A.lda + A.s + A.a + j] = 0.f;
+            actX[m * A.lda + A.s + A.a + j] = 0.f;
         }
+        if (t + 1 < A.H) stage_actions<R>(A, L, actX, t + 1, av);
         __syncthreads();
-        // ---- phase B (wave 0): per-candidate step cost, sequential return; phase C (waves 1-3): a_{t+1}
-        if (tid < M) {
+        // ---- epilogue B: per-row step cost by wave reductions (reads only sterm / aterm[t&1], which
+        // nothing rewrites before the next epilogue A, so no trailing barrier)
+        const float* aterm = L.aterm + (t & 1) * M * A.a;
+#pragma unroll
+        for (int i = 0; i < M / 4; ++i) {
+            const int m = 4 * wave + (i & 3) + 16 * (i >> 2);
             float sc = 0.f, ac = 0.f;
-            for (int d = 0; d < A.s; ++d) sc += L.sterm[tid * A.s + d];
-            const float* aterm = L.aterm + (t & 1) * M * A.a;
-            for (int d = 0; d < A.a; ++d) ac += aterm[tid * A.a + d];
-            ac = A.alpha_a2 * (ac / (float)A.a);
-            total += sc + ac;
+            for (int d = lane; d < A.s; d += 64) sc += L.sterm[m * A.s + d];
+            for (int d = lane; d < A.a; d += 64) ac += aterm[m * A.a + d];
+            sc = wave_sum(sc);
+            ac = wave_sum(ac);
+            total[i] += sc + A.alpha_a2 * (ac / (float)A.a);
         }
-        if (t + 1 < A.H) stage_actions<R>(A, L, tile, t + 1);
-        __syncthreads();
     }
-    if (tid < M) {
-        const int n = tile * M + tid;
-        if (n < A.N) A.costs[(size_t)e * A.N + n] = total;
+    if (lane == 0) {
+#pragma unroll
+        for (int i = 0; i < M / 4; ++i) {
+            const int n = tile * M + 4 * wave + (i & 3) + 16 * (i >> 2);
+            if (n < A.N) A.costs[(size_t)e * A.N + n] = total[i];
+        }
     }
 }
 

@@ -233,6 +233,7 @@ def _cem_fused_sharded(prob, s0, st, world):
     sigma = torch.full((H, a), st["init_std"], dtype=torch.float32, device=dev)
     mu_n, sigma_n = torch.empty_like(mu), torch.empty_like(sigma)
     local = torch.empty((E, Nl), dtype=torch.float32, device=dev)
+    acts = torch.empty((H, Nl, a), dtype=torch.float32, device=dev)
     gathered = torch.empty((world, E, Nl), dtype=torch.float32, device=dev)
     rec = st["record"]
     hist = dict(costs=[], returns=[], elites=[])
@@ -241,7 +242,7 @@ def _cem_fused_sharded(prob, s0, st, world):
         sp = fused.make_sampler(st["seed"], it, mu, sigma, st["lo"], st["hi"])
         if events is not None:
             events[it][0].record()
-        fused.rollout(prob, s0, Nl, H, sampler=sp, n_offset=rank * Nl, costs=local)
+        fused.rollout(prob, s0, Nl, H, sampler=sp, n_offset=rank * Nl, costs=local, actions_out=acts)
         if events is not None:
             events[it][1].record()
         dist.all_gather_into_tensor(gathered, local)
