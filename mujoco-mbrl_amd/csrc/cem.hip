@@ -68,6 +68,22 @@ __global__ void pack_out_kernel(const float* __restrict__ w, int in_real, int ou
     }
 }
 
+// Plain copies for traj.hip: transposed W^T [in][cols] (zero-padded columns) ...
+__global__ void pack_transposed_kernel(const float* __restrict__ w, int in_real, int out_real, int cols,
+                                       float* __restrict__ dst) {
+    const size_t total = (size_t)in_real * cols;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const int k = (int)(i / cols), n = (int)(i - (i / cols) * cols);
+        dst[i] = n < out_real ? w[(size_t)n * in_real + k] : 0.0f;
+    }
+}
+
+// ... and a straight copy (the output layer keeps nn.Linear's row-major [out][in]).
+__global__ void copy_kernel(const float* __restrict__ src, size_t n, float* __restrict__ dst) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        dst[i] = src[i];
+}
+
 __global__ void pack_bias_kernel(const float* __restrict__ b, int n_real, int n_pad, float* __restrict__ dst) {
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n_pad; i += gridDim.x * blockDim.x)
         dst[i] = i < n_real ? b[i] : 0.0f;
@@ -231,7 +247,7 @@ __global__ void refit_kernel(const float* __restrict__ aelite, int a, int K, flo
                 const float mu0 = mu[t * a + d], s0 = sigma[t * a + d];
                 mu_out[t * a + d] = __fadd_rn(__fmul_rn(alpha, mu0), __fmul_rn(oma, mean[d]));
                 const float v = __fadd_rn(__fmul_rn(alpha, __fmul_rn(s0, s0)), __fmul_rn(oma, m));
-                sigma_out[t * a + d] = __fsqrt_rn(v);
+                sigma_out[t * a + d] = exact_sqrt(v);
             }
         }
         __syncthreads();
@@ -362,6 +378,24 @@ static int rollout_impl(const Geometry& g, const void* packed, const mbrl_norm* 
     return hip_check(launch_rollout(A, g.T, R, stream), "rollout launch");
 }
 
+static int traj_impl(const Geometry& g, const void* packed, const mbrl_norm* norm, const float* s0,
+                     const float* actions, int H, float* states_out, hipStream_t stream) {
+    TrajArgs T{};
+    T.packed = static_cast<const float*>(packed);
+    T.member_stride = g.member_stride;
+    T.bias_off = g.stream_floats;
+    T.tw_base = g.stream_floats + g.bias_floats;
+    for (int l = 0; l <= g.L; ++l) T.tw_off[l] = g.tw_off[l];
+    T.s = g.s; T.a = g.a; T.W = g.W; T.Wpad = g.Wpad; T.L = g.L; T.H = H;
+    if (norm) {
+        T.obs_mean = norm->obs_mean; T.obs_std = norm->obs_std;
+        T.act_mean = norm->act_mean; T.act_std = norm->act_std;
+        T.norm_s = norm->normalize_state; T.unnorm_s = norm->unnormalize_state; T.norm_a = norm->normalize_action;
+    }
+    T.s0 = s0; T.actions = actions; T.states_out = states_out;
+    return hip_check(launch_traj(T, g.E, stream), "trajectory launch");
+}
+
 static int select_impl(const float* costs, int E, int N, int K, int nan_policy, int64_t* elite_idx,
                        float* returns_out, void* ws, size_t ws_bytes, hipStream_t stream) {
     if (!costs || !elite_idx || !ws) return fail(MBRL_EINVAL, "costs, elite_idx and workspace must be non-NULL");
@@ -425,16 +459,19 @@ int mbrl_mlp_pack(const mbrl_mlp_shape* shape, const float* const* weights, cons
             const float* b = biases[e * nl + l];
             if (!w || !b) return fail(MBRL_EINVAL, "pack: NULL weight/bias for member %d layer %d", e, l);
             float* dst = base + chunk * 1024 * g.T;
+            float* plain = base + g.stream_floats + g.bias_floats + g.tw_off[l];
             if (l < g.L) {
                 const int in_real = l == 0 ? g.s + g.a : g.W;
                 const int nkc = l == 0 ? g.K0C : 4 * g.T;
                 hipLaunchKernelGGL(pack_hidden_kernel, dim3(256), dim3(256), 0, stream, w, in_real, g.W, nkc, g.T, dst);
                 hipLaunchKernelGGL(pack_bias_kernel, dim3(4), dim3(256), 0, stream, b, g.W, g.Wpad, bias_base + (size_t)l * g.Wpad);
+                hipLaunchKernelGGL(pack_transposed_kernel, dim3(256), dim3(256), 0, stream, w, in_real, g.W, g.Wpad, plain);
                 chunk += nkc;
             } else {
                 hipLaunchKernelGGL(pack_out_kernel, dim3(256), dim3(256), 0, stream, w, g.W, g.s, g.NOT, g.T, dst);
                 hipLaunchKernelGGL(pack_bias_kernel, dim3(1), dim3(256), 0, stream, b, g.s, 16 * g.NOT,
                                    bias_base + (size_t)g.L * g.Wpad);
+                hipLaunchKernelGGL(copy_kernel, dim3(64), dim3(256), 0, stream, w, (size_t)g.s * g.W, plain);
                 chunk += g.NOT;
             }
         }
@@ -556,9 +593,8 @@ int mbrl_cem_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_no
     }
     hipLaunchKernelGGL(finalize_kernel, dim3((Ha + 255) / 256), dim3(256), 0, stream, w.mu[cur], w.sigma[cur], p->lo,
                        p->hi, Ha, mu, sigma, actions_out);
-    // final mean's rollout -> predicted states [E][H][1][s], then the member mean
-    rc = rollout_impl(g, packed, norm, cost, s0, 0, actions_out, nullptr, 1, p->H, 0, w.tmp_cost, nullptr, w.states,
-                      stream);
+    // final mean's rollout -> predicted states [E][H][s], then the member mean
+    rc = traj_impl(g, packed, norm, s0, actions_out, p->H, w.states, stream);
     if (rc) return rc;
     const int Hs = p->H * g.s;
     hipLaunchKernelGGL(member_mean_kernel, dim3((Hs + 255) / 256), dim3(256), 0, stream, w.states, g.E, Hs, states_out);

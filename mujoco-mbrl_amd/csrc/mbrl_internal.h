@@ -7,6 +7,8 @@
 
 namespace mbrl {
 
+constexpr int MAX_LAYERS = 4;  // hidden layers
+
 // Packed-stream geometry for one MLP shape (DESIGN.md §2 "weight stream").
 struct Geometry {
     int s, a, W, L, E;
@@ -19,13 +21,18 @@ struct Geometry {
     int pw;         // LDS output-partial row stride (floats)
     size_t stream_floats;  // C * 1024 * T
     size_t bias_floats;    // L * Wpad + 16 * NOT
+    // plain copies for the single-trajectory kernel (traj.hip): layer 0 and hidden layers
+    // transposed W^T [in][Wpad]; the output layer row-major [s][W]
+    int Opad;
+    size_t tw_off[MAX_LAYERS + 1];  // offsets inside the plain region
+    size_t tw_floats;
     size_t member_stride;  // floats per ensemble member (64-float aligned)
 };
 
 inline int round_even(int x) { return (x + 1) & ~1; }
 
 inline bool make_geometry(int s, int a, int W, int L, int E, Geometry* g) {
-    if (s < 1 || a < 1 || W < 1 || L < 1 || E < 1) return false;
+    if (s < 1 || a < 1 || W < 1 || L < 1 || L > MAX_LAYERS || E < 1) return false;
     int T = 1;
     while (64 * T < W) T *= 2;
     if (T > 16) return false;
@@ -41,7 +48,15 @@ inline bool make_geometry(int s, int a, int W, int L, int E, Geometry* g) {
     g->pw = 16 * g->NOT + 4;
     g->stream_floats = (size_t)g->C * 1024 * T;
     g->bias_floats = (size_t)L * g->Wpad + 16 * (size_t)g->NOT;
-    g->member_stride = (g->stream_floats + g->bias_floats + 63) / 64 * 64;
+    g->Opad = (s + 3) & ~3;
+    size_t o = 0;
+    g->tw_off[0] = o;
+    o += (size_t)(s + a) * g->Wpad;
+    for (int l = 1; l < L; ++l) { g->tw_off[l] = o; o += (size_t)W * g->Wpad; }
+    g->tw_off[L] = o;
+    o += (size_t)s * W;
+    g->tw_floats = o;
+    g->member_stride = (g->stream_floats + g->bias_floats + g->tw_floats + 63) / 64 * 64;
     return true;
 }
 
@@ -100,5 +115,21 @@ inline size_t rollout_lds_bytes(const RolloutArgs& A, int M) {
 }
 
 hipError_t launch_rollout(const RolloutArgs& A, int T, int R, hipStream_t stream);
+
+// Single-trajectory rollout (one candidate per ensemble member): the final CEM mean's predicted
+// states. Latency-bound, so VALU dot products over plain weight copies on one workgroup per member
+// instead of the 16-row MFMA tile (traj.hip).
+struct TrajArgs {
+    const float* packed;
+    size_t member_stride, bias_off, tw_base;
+    size_t tw_off[MAX_LAYERS + 1];
+    int s, a, W, Wpad, L, H;
+    const float *obs_mean, *obs_std, *act_mean, *act_std;
+    int norm_s, unnorm_s, norm_a;
+    const float* s0;
+    const float* actions;  // [H][a]
+    float* states_out;     // [E][H][s]
+};
+hipError_t launch_traj(const TrajArgs& A, int E, hipStream_t stream);
 
 }  // namespace mbrl

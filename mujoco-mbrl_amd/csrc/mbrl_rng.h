@@ -31,6 +31,25 @@ __device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1
 
 __device__ __forceinline__ float f32_from_bits(uint32_t b) { return __uint_as_float(b); }
 
+// Correctly rounded sqrt for finite x >= 0. gfx950's v_sqrt_f32 (what sqrtf / __fsqrt_rn lower to)
+// is not correctly rounded; NumPy's is. Start from it and fix the last bit against the exact
+// midpoints: squares of float32 values and of their midpoints are exact in fp64 (<= 50 bits).
+__device__ __forceinline__ float exact_sqrt(float x) {
+    if (!(x > 0.0f) || isinf(x)) return sqrtf(x);
+    float y = sqrtf(x);
+    const double xd = (double)x;
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+        const float lo = __uint_as_float(__float_as_uint(y) - 1u);
+        const float hi = __uint_as_float(__float_as_uint(y) + 1u);
+        const double mlo = 0.5 * ((double)lo + (double)y);
+        const double mhi = 0.5 * ((double)y + (double)hi);
+        if (xd < mlo * mlo) y = lo;
+        else if (xd > mhi * mhi) y = hi;
+    }
+    return y;
+}
+
 // ln(u), u in (0, 1]; mirrors oracle/philox.py:_log_f32 operation for operation.
 __device__ __forceinline__ float exact_log(float u) {
 #pragma clang fp contract(off)
@@ -82,7 +101,7 @@ __device__ __forceinline__ void box_muller(uint32_t x0, uint32_t x1, float& z0, 
 #pragma clang fp contract(off)
     const float u1 = __fmul_rn((float)((x0 >> 8) + 1u), 5.9604644775390625e-8f);  // (0, 1]
     const float u2 = __fmul_rn((float)(x1 >> 8), 5.9604644775390625e-8f);         // [0, 1)
-    const float r = __fsqrt_rn(__fmul_rn(-2.0f, exact_log(u1)));
+    const float r = exact_sqrt(__fmul_rn(-2.0f, exact_log(u1)));
     float sn, cs;
     exact_sincos_turn(u2, sn, cs);
     z0 = __fmul_rn(r, cs);

@@ -33,8 +33,10 @@ def test_no_gpu_needed_for_sizing_calls():
     from mbrl_amd import _lib
     lib = _lib.load()
     sh = _lib.MlpShape(17, 6, 512, 3, 1)
-    # 68 chunks x 8 KiB per wave x 4 waves + biases (3*512 + 32), 64-float aligned
-    assert lib.mbrl_mlp_packed_bytes(ctypes.byref(sh)) == ((68 * 8192 + 3 * 512 + 32 + 63) // 64 * 64) * 4
+    # 68 chunks x 8 KiB per wave x 4 waves + biases (3*512 + 32) + plain copies for the trajectory
+    # kernel (W^T of layer 0 and the two hidden layers, row-major output layer), 64-float aligned
+    plain = 23 * 512 + 2 * 512 * 512 + 17 * 512
+    assert lib.mbrl_mlp_packed_bytes(ctypes.byref(sh)) == ((68 * 8192 + 3 * 512 + 32 + plain + 63) // 64 * 64) * 4
     bad = _lib.MlpShape(17, 6, 4096, 3, 1)
     assert lib.mbrl_mlp_packed_bytes(ctypes.byref(bad)) == 0
     assert lib.mbrl_select_workspace_bytes(4096) >= 4096 * 4
