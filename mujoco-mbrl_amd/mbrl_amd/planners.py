@@ -71,9 +71,10 @@ class RandomShootingPlanner(ModelPlanner):
 
     @staticmethod
     def plan(initial_state, model, cost, sample_action, horizon, initial_trajectory=None, **kwargs):
-        num_trajectories = kwargs.get("num_trajectories", RandomShootingPlanner.defaults["num_trajectories"])
+        kw = dict(kwargs)
+        num_trajectories = kw.pop("num_trajectories", RandomShootingPlanner.defaults["num_trajectories"])
         return RandomShootingPlanner._plan(initial_state, model, cost, sample_action, horizon, initial_trajectory,
-                                           num_trajectories, **kwargs)
+                                           num_trajectories, **kw)
 
     @staticmethod
     def _plan(initial_state, model, cost, sample_action, horizon, initial_trajectory, num_trajectories, **kwargs):
