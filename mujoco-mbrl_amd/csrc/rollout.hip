@@ -33,6 +33,25 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 #define MBRL_PIN() __builtin_amdgcn_sched_barrier(0)
 
+// Diagnostic build only (make diag, -DMBRL_STAMPS): per-wave s_memtime sums per kernel segment,
+// written to a buffer set by mbrl_diag_set_stamps(). The timed kernel never contains stamps.
+#ifdef MBRL_STAMPS
+constexpr int NSEG = 8;
+__device__ unsigned long long* g_mbrl_stamps;
+#define STAMP(k)                                                   \
+    do {                                                           \
+        MBRL_PIN();                                                \
+        const unsigned long long _t = __builtin_amdgcn_s_memtime(); \
+        seg[k] += _t - tprev;                                      \
+        tprev = _t;                                                \
+        MBRL_PIN();                                                \
+    } while (0)
+#else
+#define STAMP(k) \
+    do {         \
+    } while (0)
+#endif
+
 template <int T>
 __device__ __forceinline__ void load_chunk(f32x4 (&b)[T], const f32x4* __restrict__ p) {
 #pragma unroll
@@ -209,6 +228,10 @@ __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
     float total[M / 4];  // rows 4*wave + (i&3) + 16*(i>>2), held by every lane of the wave
 #pragma unroll
     for (int i = 0; i < M / 4; ++i) total[i] = 0.f;
+#ifdef MBRL_STAMPS
+    unsigned long long seg[NSEG] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long tprev = __builtin_amdgcn_s_memtime();
+#endif
 
     for (int t = 0; t < A.H; ++t) {
         int g = 0;
@@ -231,7 +254,9 @@ __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
             MBRL_PIN();
             g += 2;
         }
+        STAMP(0);
         hidden_store<T, R>(acc, bias, actY, A.lda, wave, lane);
+        STAMP(1);
         // ---- hidden layers 1..L-1 (W -> W), alternating Y->X->Y...
         float* in = actY;
         float* out = actX;
@@ -253,7 +278,9 @@ __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
                 MBRL_PIN();
                 g += 2;
             }
+            STAMP(2);
             hidden_store<T, R>(acc, bias, out, A.lda, wave, lane);
+            STAMP(3);
             float* tmp = in; in = out; out = tmp;
         }
         // ---- output layer: W -> s, K split over the 4 waves, partials through LDS
@@ -278,7 +305,9 @@ __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
                 g += 2;
             }
         }
+        STAMP(4);
         __syncthreads();
+        STAMP(5);
 
         // ---- epilogue A: s_{t+1} = unnormalize(out), state-cost terms, next MLP input into actX
         const float* bout = L.hbias + A.L * A.Wpad;
@@ -305,6 +334,7 @@ __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
         }
         if (t + 1 < A.H) stage_actions<R>(A, L, actX, t + 1, av);
         __syncthreads();
+        STAMP(6);
         // ---- epilogue B: per-row step cost by wave reductions (reads only sterm / aterm[t&1], which
         // nothing rewrites before the next epilogue A, so no trailing barrier)
         const float* aterm = L.aterm + (t & 1) * M * A.a;
@@ -318,7 +348,15 @@ __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
             ac = wave_sum(ac);
             total[i] += sc + A.alpha_a2 * (ac / (float)A.a);
         }
+        STAMP(7);
     }
+#ifdef MBRL_STAMPS
+    if (lane == 0 && g_mbrl_stamps != nullptr) {
+        unsigned long long* dst = g_mbrl_stamps + (((size_t)e * gridDim.x + tile) * 4 + wave) * NSEG;
+#pragma unroll
+        for (int k = 0; k < NSEG; ++k) dst[k] = seg[k];
+    }
+#endif
     if (lane == 0) {
 #pragma unroll
         for (int i = 0; i < M / 4; ++i) {
@@ -354,3 +392,9 @@ hipError_t launch_rollout(const RolloutArgs& A, int T, int R, hipStream_t stream
 }
 
 }  // namespace mbrl
+
+#ifdef MBRL_STAMPS
+extern "C" int mbrl_diag_set_stamps(void* buf) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(mbrl::g_mbrl_stamps), &buf, sizeof(buf));
+}
+#endif

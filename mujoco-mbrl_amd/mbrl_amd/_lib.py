@@ -14,7 +14,8 @@ from ctypes import POINTER, c_float, c_int32, c_int64, c_size_t, c_uint64, c_voi
 
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmbrl_cem.so")
+LIB_PATH = os.environ.get("MBRL_AMD_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                          "libmbrl_cem.so")
 
 MBRL_OK = 0
 MBRL_COST_GOAL_STATE = 0

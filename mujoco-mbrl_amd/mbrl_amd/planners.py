@@ -49,16 +49,30 @@ def _to_host(x, keep_device):
 
 
 def _generic_costs(model, cost, s0, actions, H, N):
-    """planners.py:199-210 with the caller's callables on device tensors. actions [H, N, a] on device.
-    Returns costs [1, N] (sequential sum over t) and states [H, N, s]."""
+    """planners.py:199-210 with the caller's callables. actions [H, N, a] on the GPU.
+
+    The callables are opaque: they run on GPU tensors when they accept them, else (their own
+    parameters live on the host, e.g. a cost closing over CPU goal tensors as the reference's
+    agents build them) on host copies of the inputs. Returns costs [1, N] (sequential sum over t)
+    and states [H, N, s] on the GPU; selection and refit stay in the HIP extension."""
+    dev = actions.device
     s = s0.shape[0]
-    states = torch.empty((H, N, s), dtype=torch.float32, device=actions.device)
+
+    def call(fn, *args):
+        try:
+            return fn(*args).to(dev)
+        except RuntimeError as e:
+            if "device" not in str(e):
+                raise
+            return fn(*[x.cpu() for x in args]).to(dev)
+
+    states = torch.empty((H, N, s), dtype=torch.float32, device=dev)
     cur = s0.unsqueeze(0).repeat_interleave(N, dim=0)
     with torch.no_grad():
         for t in range(H):
-            cur = model(cur, actions[t])
+            cur = call(model, cur, actions[t])
             states[t] = cur
-        c = cost(states.reshape(H * N, s), actions.reshape(H * N, -1)).reshape(H, N)
+        c = call(cost, states.reshape(H * N, s), actions.reshape(H * N, -1)).reshape(H, N)
         total = c[0].clone()
         for t in range(1, H):
             total = total + c[t]

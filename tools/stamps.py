@@ -1,0 +1,56 @@
+"""Diagnostic: per-segment cycle shares of the rollout kernel from the -DMBRL_STAMPS build.
+
+    make -C mujoco-mbrl_amd diag && python tools/stamps.py [config_id]
+
+Only shares are meaningful (the stamps' own waits perturb the schedule); never quote its time."""
+import ctypes
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["MBRL_AMD_LIB"] = os.path.join(REPO, "mujoco-mbrl_amd", "mbrl_amd", "libmbrl_cem_diag.so")
+sys.path.insert(0, os.path.join(REPO, "mujoco-mbrl_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from mbrl_amd import _lib, fused, synthetic  # noqa: E402
+
+SEGS = ["layer0 mma", "layer0 store+bar", "hidden mma", "hidden store+bar", "output mma", "output bar",
+        "epilogue A+bar", "epilogue B"]
+
+
+def main():
+    cid = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    prob = synthetic.make_problem(cid)
+    cfg = prob["cfg"]
+    N, H, a, E = cfg["N"], cfg["H"], cfg["a"], cfg["E"]
+    lib = _lib.load()
+    lib.mbrl_diag_set_stamps.argtypes = [ctypes.c_void_p]
+    dev = torch.device("cuda", 0)
+    md = fused.describe_model(prob["model"])
+    cd = fused.describe_cost(prob["cost"], md["s"])
+    p = fused.device_problem(md, cd, dev)
+    tiles = (N + 15) // 16
+    buf = torch.zeros(E * tiles * 4 * len(SEGS), dtype=torch.int64, device=dev)
+    assert lib.mbrl_diag_set_stamps(buf.data_ptr()) == 0
+    mu = torch.zeros((H, a), device=dev)
+    sg = torch.full((H, a), 0.5, device=dev)
+    acts = torch.empty((H, N, a), device=dev)
+    s0 = prob["s0"].to(dev)
+    for _ in range(3):
+        fused.rollout(p, s0, N, H, sampler=fused.make_sampler(1, 0, mu, sg, -1, 1), actions_out=acts)
+    torch.cuda.synchronize()
+    st = buf.view(E * tiles * 4, len(SEGS)).cpu().numpy().astype(np.float64)
+    per_step = st.mean(0) / H
+    tot = per_step.sum()
+    print(f"config {cid}: mean cycles per step per wave {tot:.0f} (diag build; shares only)")
+    for name, v in zip(SEGS, per_step):
+        print(f"  {name:18s} {v:9.0f}  {100 * v / tot:5.1f}%")
+    mfma = 2176 if cid in (3, 4) else None
+    if mfma:
+        print(f"  ideal MFMA issue per step per wave: {mfma * 32} cycles")
+
+
+if __name__ == "__main__":
+    main()
