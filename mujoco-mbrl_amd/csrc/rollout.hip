@@ -66,6 +66,8 @@ __device__ __forceinline__ void read_a(f32x4 (&a)[R], const float* act, int lda,
 }
 
 // Hidden-type chunk: one 16-deep K slice x T output tiles (MFMAs on independent accumulators).
+// Weights are the A operand and activations the B operand (Y^T = W X^T), so lane l ends up with
+// 4 consecutive output features n0 + 4(l>>4) + i of candidate 16r + (l&15): a float4 row store.
 template <int T, int R>
 __device__ __forceinline__ void mma_hidden(f32x4 (&acc)[R][T], const f32x4 (&a)[R], const f32x4 (&b)[T]) {
 #pragma unroll
@@ -74,7 +76,7 @@ __device__ __forceinline__ void mma_hidden(f32x4 (&acc)[R][T], const f32x4 (&a)[
         for (int j = 0; j < T; ++j)
 #pragma unroll
             for (int r = 0; r < R; ++r)
-                acc[r][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[r][s], b[j][s], acc[r][j], 0, 0, 0);
+                acc[r][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[j][s], a[r][s], acc[r][j], 0, 0, 0);
 }
 
 // Output-type chunk: one 16-column output tile over this wave's W/4-deep K range; four accumulator
@@ -93,35 +95,34 @@ __device__ __forceinline__ void mma_out(const f32x4 (&aout)[R][T], const f32x4 (
         for (int s = 0; s < 4; ++s)
 #pragma unroll
             for (int r = 0; r < R; ++r)
-                o[r][s] = __builtin_amdgcn_mfma_f32_16x16x4f32(aout[r][kc][s], b[kc][s], o[r][s], 0, 0, 0);
+                o[r][s] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[kc][s], aout[r][kc][s], o[r][s], 0, 0, 0);
 #pragma unroll
     for (int r = 0; r < R; ++r)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            part[(16 * r + 4 * (lane >> 4) + i) * pw + 16 * tile + (lane & 15)] =
-                (o[r][0][i] + o[r][1][i]) + (o[r][2][i] + o[r][3][i]);
+        *reinterpret_cast<f32x4*>(part + (16 * r + (lane & 15)) * pw + 16 * tile + 4 * (lane >> 4)) =
+            (o[r][0] + o[r][1]) + (o[r][2] + o[r][3]);
 }
 
-// acc + bias -> ReLU -> next activation buffer; one barrier (ping-pong buffers).
+// acc + bias -> ReLU -> next activation buffer (float4 row stores); one barrier (ping-pong buffers).
 template <int T, int R>
-__device__ __forceinline__ void hidden_store(const f32x4 (&acc)[R][T], const float (&bias)[T], float* out,
+__device__ __forceinline__ void hidden_store(const f32x4 (&acc)[R][T], const f32x4 (&bias)[T], float* out,
                                              int lda, int wave, int lane) {
+    const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
         for (int j = 0; j < T; ++j) {
-            const int col = wave * 16 * T + 16 * j + (lane & 15);
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                out[(16 * r + 4 * (lane >> 4) + i) * lda + col] = fmaxf(acc[r][j][i] + bias[j], 0.0f);
+            f32x4 v = acc[r][j] + bias[j];
+            v = __builtin_elementwise_max(v, zero);
+            *reinterpret_cast<f32x4*>(out + (16 * r + (lane & 15)) * lda + wave * 16 * T + 16 * j + 4 * (lane >> 4)) = v;
         }
     __syncthreads();
 }
 
 template <int T>
-__device__ __forceinline__ void load_bias(float (&bias)[T], const float* hb, int wave, int lane) {
+__device__ __forceinline__ void load_bias(f32x4 (&bias)[T], const float* hb, int wave, int lane) {
 #pragma unroll
-    for (int j = 0; j < T; ++j) bias[j] = hb[wave * 16 * T + 16 * j + (lane & 15)];
+    for (int j = 0; j < T; ++j)
+        bias[j] = *reinterpret_cast<const f32x4*>(hb + wave * 16 * T + 16 * j + 4 * (lane >> 4));
 }
 
 template <int T, int R>
@@ -132,44 +133,54 @@ __device__ __forceinline__ void zero_acc(f32x4 (&acc)[R][T]) {
         for (int j = 0; j < T; ++j) acc[r][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 }
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+// Sum over the 16 lanes of a DPP row (row_ror 8, 4, 2, 1): every lane of the row gets the total.
+__device__ __forceinline__ float rowsum16(float v) {
+    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false));
+    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x124, 0xF, 0xF, false));
+    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x122, 0xF, 0xF, false));
+    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x121, 0xF, 0xF, false));
     return v;
 }
 
-// Per-thread slice of this tile's action block: items i = tid + 256*k of [M][a].
-constexpr int MAX_ACT_ITEMS = 3;  // M*a <= 768 (e.g. M=16, a<=48; M=32, a<=24)
+// Epilogue mapping: lane l of wave w owns candidate row m = 16r + 4w + (l >> 4) and the feature
+// slots d = (l & 15) + 16k of that row, so per-row reductions are one DPP row sum.
+constexpr int MAX_A_PER_LANE = 3;  // action_dim <= 48
 
+__device__ __forceinline__ int epi_row(int r, int wave, int lane) { return 16 * r + 4 * wave + (lane >> 4); }
+
+// a_t for this lane's (row, slots), loaded early and unconditionally (clamped indices) so hipcc
+// emits no branch-around-load with its vmcnt(0) (cdna_hip_programming.md §5, trap (c)).
 template <int R>
-__device__ __forceinline__ void fetch_actions(const RolloutArgs& A, int tile, int t, float (&av)[MAX_ACT_ITEMS]) {
+__device__ __forceinline__ void fetch_actions(const RolloutArgs& A, int tile, int t, int wave, int lane,
+                                              float (&av)[R][MAX_A_PER_LANE]) {
     constexpr int M = 16 * R;
 #pragma unroll
-    for (int k = 0; k < MAX_ACT_ITEMS; ++k) {
-        const int i = (int)threadIdx.x + 256 * k;
-        av[k] = 0.f;
-        if (i < M * A.a) {
-            const int m = i / A.a, d = i - (i / A.a) * A.a;
-            const int n = tile * M + m;
-            if (n < A.N) av[k] = A.actions[((size_t)t * A.N + n) * A.a + d];
-        }
+    for (int r = 0; r < R; ++r) {
+        const int n = min(tile * M + epi_row(r, wave, lane), A.N - 1);
+        const float* src = A.actions + ((size_t)t * A.N + n) * A.a;
+#pragma unroll
+        for (int k = 0; k < MAX_A_PER_LANE; ++k) av[r][k] = src[min((lane & 15) + 16 * k, A.a - 1)];
     }
 }
 
-// a_t -> normalised MLP input columns [s, s+a) and CoshLoss terms.
+// a_t -> normalised MLP input columns [s, s+a); returns this lane's share of sum_d (cosh(a_d/alpha)-1).
 template <int R>
-__device__ __forceinline__ void stage_actions(const RolloutArgs& A, const LdsMap& L, float* act, int t,
-                                              const float (&av)[MAX_ACT_ITEMS]) {
-    constexpr int M = 16 * R;
-    float* aterm = L.aterm + (t & 1) * M * A.a;
+__device__ __forceinline__ void stage_actions(const RolloutArgs& A, const LdsMap& L, float* act, int wave, int lane,
+                                              const float (&av)[R][MAX_A_PER_LANE], float (&acp)[R]) {
 #pragma unroll
-    for (int k = 0; k < MAX_ACT_ITEMS; ++k) {
-        const int i = (int)threadIdx.x + 256 * k;
-        if (i < M * A.a) {
-            const int m = i / A.a, d = i - (i / A.a) * A.a;
-            act[m * A.lda + A.s + d] = A.norm_a ? (av[k] - L.act_mean[d]) / L.act_std[d] : av[k];
-            aterm[m * A.a + d] = A.has_ac ? coshf(av[k] / A.alpha_a) - 1.0f : 0.0f;
+    for (int r = 0; r < R; ++r) {
+        const int m = epi_row(r, wave, lane);
+        float c = 0.f;
+#pragma unroll
+        for (int k = 0; k < MAX_A_PER_LANE; ++k) {
+            const int d = (lane & 15) + 16 * k;
+            if (d < A.a) {
+                const float x = av[r][k];
+                act[m * A.lda + A.s + d] = A.norm_a ? (x - L.act_mean[d]) / L.act_std[d] : x;
+                if (A.has_ac) c += coshf(x / A.alpha_a) - 1.0f;
+            }
         }
+        acp[r] = c;
     }
 }
 
@@ -186,8 +197,9 @@ __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
     float* const actY = L.act2;
 
     // ---- prologue: parameters into LDS, s0 and a_0 into the MLP input
-    float av[MAX_ACT_ITEMS];
-    fetch_actions<R>(A, tile, 0, av);
+    float av[R][MAX_A_PER_LANE];
+    float acp[R];  // this lane's share of the current step's CoshLoss sum, per row
+    fetch_actions<R>(A, tile, 0, wave, lane, av);
     for (int i = tid; i < A.s; i += 256) {
         L.obs_mean[i] = A.obs_mean ? A.obs_mean[i] : 0.f;
         L.obs_std[i] = A.obs_std ? A.obs_std[i] : 1.f;
@@ -211,7 +223,7 @@ __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
         const int m = i / A.k0pad_extra, j = i - (i / A.k0pad_extra) * A.k0pad_extra;
         actX[m * A.lda + A.s + A.a + j] = 0.f;
     }
-    stage_actions<R>(A, L, actX, 0, av);
+    stage_actions<R>(A, L, actX, wave, lane, av, acp);
     __syncthreads();
 
     // ---- weight stream: this wave's slice of chunk g is at wb + g * cs (f32x4 units)
@@ -223,11 +235,11 @@ __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
     f32x4 bA[T], bB[T];
     f32x4 aA[R], aB[R];
     f32x4 acc[R][T];
-    float bias[T];
+    f32x4 bias[T];
     load_chunk<T>(bA, wb);
-    float total[M / 4];  // rows 4*wave + (i&3) + 16*(i>>2), held by every lane of the wave
+    float total[R];  // return of row epi_row(r, wave, lane), held by the 16 lanes of that row
 #pragma unroll
-    for (int i = 0; i < M / 4; ++i) total[i] = 0.f;
+    for (int r = 0; r < R; ++r) total[r] = 0.f;
 #ifdef MBRL_STAMPS
     unsigned long long seg[NSEG] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long tprev = __builtin_amdgcn_s_memtime();
@@ -236,7 +248,7 @@ __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
     for (int t = 0; t < A.H; ++t) {
         int g = 0;
         // a_{t+1} from HBM now; consumed in this step's epilogue
-        if (t + 1 < A.H) fetch_actions<R>(A, tile, t + 1, av);
+        if (t + 1 < A.H) fetch_actions<R>(A, tile, t + 1, wave, lane, av);
         // ---- layer 0: actX [s | a | 0-pad] -> actY (W)
         zero_acc<T, R>(acc);
         load_bias<T>(bias, L.hbias, wave, lane);
@@ -309,46 +321,38 @@ __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
         __syncthreads();
         STAMP(5);
 
-        // ---- epilogue A: s_{t+1} = unnormalize(out), state-cost terms, next MLP input into actX
-        const float* bout = L.hbias + A.L * A.Wpad;
-        const int ws = M * A.pw;
-        for (int i = tid; i < M * A.s; i += 256) {
-            const int m = i / A.s, d = i - (i / A.s) * A.s;
-            const int ro = m * A.pw + d;
-            const float o = L.part[ro] + L.part[ws + ro] + L.part[2 * ws + ro] + L.part[3 * ws + ro] + bout[d];
-            const float sn = A.unnorm_s ? o * L.obs_std[d] + L.obs_mean[d] : o;
-            float term = 0.f;
-            if (A.has_sc) {
-                const float x = (sn - L.goal[d]) * L.cw[d];
-                term = sqrtf(x * x + A.alpha_s2) - A.alpha_s;
+        // ---- epilogue (one pass, no cross-wave traffic): s_{t+1} = unnormalize(out), goal cost of
+        // (s_{t+1}, a_t), next MLP input [norm(s_{t+1}) | norm(a_{t+1}) | 0-pad] into actX
+        {
+            const float* bout = L.hbias + A.L * A.Wpad;
+            const int ws = M * A.pw;
+            const int j = lane & 15;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int m = epi_row(r, wave, lane);
+                const int n = tile * M + m;
+                float sc = 0.f;
+                for (int d = j; d < A.s; d += 16) {
+                    const int ro = m * A.pw + d;
+                    const float o = L.part[ro] + L.part[ws + ro] + L.part[2 * ws + ro] + L.part[3 * ws + ro] + bout[d];
+                    const float sn = A.unnorm_s ? o * L.obs_std[d] + L.obs_mean[d] : o;
+                    if (A.has_sc) {
+                        const float x = (sn - L.goal[d]) * L.cw[d];
+                        sc += sqrtf(x * x + A.alpha_s2) - A.alpha_s;
+                    }
+                    actX[m * A.lda + d] = A.norm_s ? (sn - L.obs_mean[d]) / L.obs_std[d] : sn;
+                    if (A.states_out != nullptr && n < A.N)
+                        A.states_out[(((size_t)e * A.H + t) * A.N + n) * A.s + d] = sn;
+                }
+                for (int d = A.s + A.a + j; d < A.s + A.a + A.k0pad_extra; d += 16) actX[m * A.lda + d] = 0.f;
+                sc = rowsum16(sc);
+                const float ac = rowsum16(acp[r]);
+                total[r] += sc + A.alpha_a2 * (ac / (float)A.a);
             }
-            L.sterm[m * A.s + d] = term;
-            actX[m * A.lda + d] = A.norm_s ? (sn - L.obs_mean[d]) / L.obs_std[d] : sn;
-            const int n = tile * M + m;
-            if (A.states_out != nullptr && n < A.N)
-                A.states_out[(((size_t)e * A.H + t) * A.N + n) * A.s + d] = sn;
+            if (t + 1 < A.H) stage_actions<R>(A, L, actX, wave, lane, av, acp);
         }
-        for (int i = tid; i < M * A.k0pad_extra; i += 256) {
-            const int m = i / A.k0pad_extra, j = i - (i / A.k0pad_extra) * A.k0pad_extra;
-            actX[m * A.lda + A.s + A.a + j] = 0.f;
-        }
-        if (t + 1 < A.H) stage_actions<R>(A, L, actX, t + 1, av);
         __syncthreads();
         STAMP(6);
-        // ---- epilogue B: per-row step cost by wave reductions (reads only sterm / aterm[t&1], which
-        // nothing rewrites before the next epilogue A, so no trailing barrier)
-        const float* aterm = L.aterm + (t & 1) * M * A.a;
-#pragma unroll
-        for (int i = 0; i < M / 4; ++i) {
-            const int m = 4 * wave + (i & 3) + 16 * (i >> 2);
-            float sc = 0.f, ac = 0.f;
-            for (int d = lane; d < A.s; d += 64) sc += L.sterm[m * A.s + d];
-            for (int d = lane; d < A.a; d += 64) ac += aterm[m * A.a + d];
-            sc = wave_sum(sc);
-            ac = wave_sum(ac);
-            total[i] += sc + A.alpha_a2 * (ac / (float)A.a);
-        }
-        STAMP(7);
     }
 #ifdef MBRL_STAMPS
     if (lane == 0 && g_mbrl_stamps != nullptr) {
@@ -357,11 +361,11 @@ __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
         for (int k = 0; k < NSEG; ++k) dst[k] = seg[k];
     }
 #endif
-    if (lane == 0) {
+    if ((lane & 15) == 0) {
 #pragma unroll
-        for (int i = 0; i < M / 4; ++i) {
-            const int n = tile * M + 4 * wave + (i & 3) + 16 * (i >> 2);
-            if (n < A.N) A.costs[(size_t)e * A.N + n] = total[i];
+        for (int r = 0; r < R; ++r) {
+            const int n = tile * M + epi_row(r, wave, lane);
+            if (n < A.N) A.costs[(size_t)e * A.N + n] = total[r];
         }
     }
 }

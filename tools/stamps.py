@@ -17,7 +17,7 @@ import torch  # noqa: E402
 from mbrl_amd import _lib, fused, synthetic  # noqa: E402
 
 SEGS = ["layer0 mma", "layer0 store+bar", "hidden mma", "hidden store+bar", "output mma", "output bar",
-        "epilogue A+bar", "epilogue B"]
+        "epilogue+bar", "(unused)"]
 
 
 def main():
