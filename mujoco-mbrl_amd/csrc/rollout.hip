@@ -184,10 +184,15 @@ __device__ __forceinline__ void stage_actions(const RolloutArgs& A, const LdsMap
     }
 }
 
-template <int T, int R>
+// K0C / NOT > 0: compile-time layer-0 / output chunk counts, enabling a 4-deep weight ring with
+// static register slots (three chunks = ~3000 MFMA cycles of load cover). K0C == 0: runtime counts,
+// 2-deep ring (any shape).
+template <int T, int R, int K0C_T, int NOT_T>
 __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
     constexpr int M = 16 * R;
-    constexpr int KH = 4 * T;  // K chunks of a hidden (W -> W) layer
+    constexpr bool RING = K0C_T > 0;
+    constexpr int NB = RING ? 4 : 2;
+    static_assert(!RING || ((K0C_T + NOT_T) % NB == 0 && K0C_T % 2 == 0 && NOT_T % 2 == 0), "ring layout");
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const LdsMap L = lds_map(A, smem, M);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -232,11 +237,12 @@ __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
     const int C = A.chunks_per_step;
     auto chunk_ptr = [&](int g) { return wb + (size_t)(g < C ? g : g - C) * cs; };
 
-    f32x4 bA[T], bB[T];
-    f32x4 aA[R], aB[R];
+    f32x4 ring[NB][T];
+    f32x4 aAB[2][R];  // A fragments of chunks with even / odd index within the layer
     f32x4 acc[R][T];
     f32x4 bias[T];
-    load_chunk<T>(bA, wb);
+#pragma unroll
+    for (int q = 0; q < NB - 1; ++q) load_chunk<T>(ring[q], chunk_ptr(q));
     float total[R];  // return of row epi_row(r, wave, lane), held by the 16 lanes of that row
 #pragma unroll
     for (int r = 0; r < R; ++r) total[r] = 0.f;
@@ -245,6 +251,18 @@ __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
     unsigned long long tprev = __builtin_amdgcn_s_memtime();
 #endif
 
+// One chunk of a hidden-type layer: refill the slot chunk (c-1) vacated with chunk c+NB-1, read the
+// next A fragment, then the MFMAs of chunk c. SLOT must fold to a constant (unrolled loops).
+#define MBRL_HIDDEN_CHUNK(SLOT, KC, NK, IN)                                          \
+    do {                                                                             \
+        load_chunk<T>(ring[((SLOT) + NB - 1) % NB], chunk_ptr(g + NB - 1));          \
+        if ((KC) + 1 < (NK)) read_a<R>(aAB[((KC) + 1) & 1], IN, A.lda, (KC) + 1, lane);   \
+        MBRL_PIN();                                                                  \
+        mma_hidden<T, R>(acc, aAB[(KC) & 1], ring[SLOT]);                            \
+        MBRL_PIN();                                                                  \
+        ++g;                                                                         \
+    } while (0)
+
     for (int t = 0; t < A.H; ++t) {
         int g = 0;
         // a_{t+1} from HBM now; consumed in this step's epilogue
@@ -252,19 +270,16 @@ __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
         // ---- layer 0: actX [s | a | 0-pad] -> actY (W)
         zero_acc<T, R>(acc);
         load_bias<T>(bias, L.hbias, wave, lane);
-        read_a<R>(aA, actX, A.lda, 0, lane);
-        for (int kc = 0; kc < A.K0C; kc += 2) {
-            load_chunk<T>(bB, chunk_ptr(g + 1));
-            read_a<R>(aB, actX, A.lda, kc + 1, lane);
-            MBRL_PIN();
-            mma_hidden<T, R>(acc, aA, bA);
-            MBRL_PIN();
-            load_chunk<T>(bA, chunk_ptr(g + 2));
-            if (kc + 2 < A.K0C) read_a<R>(aA, actX, A.lda, kc + 2, lane);
-            MBRL_PIN();
-            mma_hidden<T, R>(acc, aB, bB);
-            MBRL_PIN();
-            g += 2;
+        read_a<R>(aAB[0], actX, A.lda, 0, lane);
+        if constexpr (RING) {
+#pragma unroll
+            for (int kc = 0; kc < K0C_T; ++kc) MBRL_HIDDEN_CHUNK(kc % NB, kc, K0C_T, actX);
+        } else {
+            for (int kc = 0; kc < A.K0C; kc += 2) {
+                MBRL_HIDDEN_CHUNK(0, 0, 2, actX + 16 * kc);
+                MBRL_HIDDEN_CHUNK(1, 1, 2, actX + 16 * kc);
+                if (kc + 2 < A.K0C) read_a<R>(aAB[0], actX, A.lda, kc + 2, lane);
+            }
         }
         STAMP(0);
         hidden_store<T, R>(acc, bias, actY, A.lda, wave, lane);
@@ -275,21 +290,11 @@ __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
         for (int l = 1; l < A.L; ++l) {
             zero_acc<T, R>(acc);
             load_bias<T>(bias, L.hbias + l * A.Wpad, wave, lane);
-            read_a<R>(aA, in, A.lda, 0, lane);
+            read_a<R>(aAB[0], in, A.lda, 0, lane);
+            constexpr int KH = 4 * T;  // 4T % NB == 0: every hidden layer starts on the same slot
+            constexpr int S0 = RING ? K0C_T % NB : 0;
 #pragma unroll
-            for (int kc = 0; kc < KH; kc += 2) {
-                load_chunk<T>(bB, chunk_ptr(g + 1));
-                read_a<R>(aB, in, A.lda, kc + 1, lane);
-                MBRL_PIN();
-                mma_hidden<T, R>(acc, aA, bA);
-                MBRL_PIN();
-                load_chunk<T>(bA, chunk_ptr(g + 2));
-                if (kc + 2 < KH) read_a<R>(aA, in, A.lda, kc + 2, lane);
-                MBRL_PIN();
-                mma_hidden<T, R>(acc, aB, bB);
-                MBRL_PIN();
-                g += 2;
-            }
+            for (int kc = 0; kc < KH; ++kc) MBRL_HIDDEN_CHUNK((S0 + kc) % NB, kc, KH, in);
             STAMP(2);
             hidden_store<T, R>(acc, bias, out, A.lda, wave, lane);
             STAMP(3);
@@ -305,17 +310,25 @@ __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
                     aout[r][kc] = *reinterpret_cast<const f32x4*>(
                         in + (16 * r + (lane & 15)) * A.lda + wave * 16 * T + 16 * kc + 4 * (lane >> 4));
             float* part = L.part + wave * M * A.pw;
-            for (int j = 0; j < A.NOT; j += 2) {
-                load_chunk<T>(bB, chunk_ptr(g + 1));
-                MBRL_PIN();
-                mma_out<T, R>(aout, bA, part, A.pw, j, lane);
-                MBRL_PIN();
-                load_chunk<T>(bA, chunk_ptr(g + 2));
-                MBRL_PIN();
-                mma_out<T, R>(aout, bB, part, A.pw, j + 1, lane);
-                MBRL_PIN();
-                g += 2;
+#define MBRL_OUT_CHUNK(SLOT, J)                                                   \
+    do {                                                                          \
+        load_chunk<T>(ring[((SLOT) + NB - 1) % NB], chunk_ptr(g + NB - 1));       \
+        MBRL_PIN();                                                               \
+        mma_out<T, R>(aout, ring[SLOT], part, A.pw, J, lane);                     \
+        MBRL_PIN();                                                               \
+        ++g;                                                                      \
+    } while (0)
+            if constexpr (RING) {
+                constexpr int S0 = K0C_T % NB;
+#pragma unroll
+                for (int j = 0; j < NOT_T; ++j) MBRL_OUT_CHUNK((S0 + j) % NB, j);
+            } else {
+                for (int j = 0; j < A.NOT; j += 2) {
+                    MBRL_OUT_CHUNK(0, j);
+                    MBRL_OUT_CHUNK(1, j + 1);
+                }
             }
+#undef MBRL_OUT_CHUNK
         }
         STAMP(4);
         __syncthreads();
@@ -354,6 +367,7 @@ __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
         __syncthreads();
         STAMP(6);
     }
+#undef MBRL_HIDDEN_CHUNK
 #ifdef MBRL_STAMPS
     if (lane == 0 && g_mbrl_stamps != nullptr) {
         unsigned long long* dst = g_mbrl_stamps + (((size_t)e * gridDim.x + tile) * 4 + wave) * NSEG;
@@ -370,25 +384,36 @@ __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
     }
 }
 
-template <int T, int R>
+template <int T, int R, int K0C_T, int NOT_T>
 static hipError_t launch_rollout_tr(const RolloutArgs& A, hipStream_t stream) {
     const int M = 16 * R;
     dim3 grid((A.N + M - 1) / M, A.E);
     const size_t lds = rollout_lds_bytes(A, M);
     static bool attr_set = false;  // raise the dynamic-LDS cap once per instantiation
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&rollout_kernel<T, R>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&rollout_kernel<T, R, K0C_T, NOT_T>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    hipLaunchKernelGGL((rollout_kernel<T, R>), grid, dim3(256), lds, stream, A);
+    hipLaunchKernelGGL((rollout_kernel<T, R, K0C_T, NOT_T>), grid, dim3(256), lds, stream, A);
     return hipGetLastError();
+}
+
+template <int T, int R>
+static hipError_t launch_rollout_t(const RolloutArgs& A, hipStream_t stream) {
+    if constexpr (T <= 8) {  // the 4-deep ring needs 4*T*4 VGPRs
+        if (A.K0C == 2 && A.NOT == 2) return launch_rollout_tr<T, R, 2, 2>(A, stream);
+        if (A.K0C == 6 && A.NOT == 6) return launch_rollout_tr<T, R, 6, 6>(A, stream);
+        if (A.K0C == 2 && A.NOT == 6) return launch_rollout_tr<T, R, 2, 6>(A, stream);
+        if (A.K0C == 6 && A.NOT == 2) return launch_rollout_tr<T, R, 6, 2>(A, stream);
+    }
+    return launch_rollout_tr<T, R, 0, 0>(A, stream);
 }
 
 hipError_t launch_rollout(const RolloutArgs& A, int T, int R, hipStream_t stream) {
 #define MBRL_CASE(TT, RR) \
-    if (T == TT && R == RR) return launch_rollout_tr<TT, RR>(A, stream);
+    if (T == TT && R == RR) return launch_rollout_t<TT, RR>(A, stream);
     MBRL_CASE(1, 1) MBRL_CASE(2, 1) MBRL_CASE(4, 1) MBRL_CASE(8, 1) MBRL_CASE(16, 1)
     MBRL_CASE(1, 2) MBRL_CASE(2, 2) MBRL_CASE(4, 2) MBRL_CASE(8, 2)
 #undef MBRL_CASE
