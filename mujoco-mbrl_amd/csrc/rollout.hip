@@ -33,6 +33,21 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 #define MBRL_PIN() __builtin_amdgcn_sched_barrier(0)
 
+// Spread a chunk's T weight loads (and the next A read) between its 4*T*R MFMAs: issued as one
+// burst they cost ~120 cycles of idle matrix pipe per chunk (stamps), issued in the MFMAs' shadow
+// they are free. Masks: 0x8 MFMA, 0x20 VMEM read, 0x100 DS read.
+template <int T, int R>
+__device__ __forceinline__ void interleave_loads() {
+    __builtin_amdgcn_sched_group_barrier(0x008, 2 * R, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, R, 0);
+#pragma unroll
+    for (int q = 0; q < T; ++q) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 2 * R, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2 * R, 0);
+    }
+}
+
 // Diagnostic build only (make diag, -DMBRL_STAMPS): per-wave s_memtime sums per kernel segment,
 // written to a buffer set by mbrl_diag_set_stamps(). The timed kernel never contains stamps.
 #ifdef MBRL_STAMPS
@@ -256,9 +271,9 @@ __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
 #define MBRL_HIDDEN_CHUNK(SLOT, KC, NK, IN)                                          \
     do {                                                                             \
         load_chunk<T>(ring[((SLOT) + NB - 1) % NB], chunk_ptr(g + NB - 1));          \
-        if ((KC) + 1 < (NK)) read_a<R>(aAB[((KC) + 1) & 1], IN, A.lda, (KC) + 1, lane);   \
-        MBRL_PIN();                                                                  \
+        if ((KC) + 1 < (NK)) read_a<R>(aAB[((KC) + 1) & 1], IN, A.lda, (KC) + 1, lane); \
         mma_hidden<T, R>(acc, aAB[(KC) & 1], ring[SLOT]);                            \
+        interleave_loads<T, R>();                                                    \
         MBRL_PIN();                                                                  \
         ++g;                                                                         \
     } while (0)
