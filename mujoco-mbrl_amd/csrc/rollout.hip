@@ -38,6 +38,9 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // they are free. Masks: 0x8 MFMA, 0x20 VMEM read, 0x100 DS read.
 template <int T, int R>
 __device__ __forceinline__ void interleave_loads() {
+#ifdef MBRL_NO_INTERLEAVE
+    return;
+#endif
     __builtin_amdgcn_sched_group_barrier(0x008, 2 * R, 0);
     __builtin_amdgcn_sched_group_barrier(0x100, R, 0);
 #pragma unroll
@@ -69,8 +72,14 @@ __device__ unsigned long long* g_mbrl_stamps;
 
 template <int T>
 __device__ __forceinline__ void load_chunk(f32x4 (&b)[T], const f32x4* __restrict__ p) {
+#ifdef MBRL_DIAG_NOLOAD  // timing ablation only: no weight stream (results are garbage)
+    (void)p;
+#pragma unroll
+    for (int j = 0; j < T; ++j) asm volatile("" : "+v"(b[j]));
+#else
 #pragma unroll
     for (int j = 0; j < T; ++j) b[j] = p[j * 64];
+#endif
 }
 
 template <int R>

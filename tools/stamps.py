@@ -8,7 +8,8 @@ import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["MBRL_AMD_LIB"] = os.path.join(REPO, "mujoco-mbrl_amd", "mbrl_amd", "libmbrl_cem_diag.so")
+os.environ["MBRL_AMD_LIB"] = os.path.join(REPO, "mujoco-mbrl_amd", "mbrl_amd",
+                                         os.environ.get("MBRL_DIAG_LIB", "libmbrl_cem_diag.so"))
 sys.path.insert(0, os.path.join(REPO, "mujoco-mbrl_amd"))
 
 import numpy as np  # noqa: E402
@@ -22,7 +23,8 @@ SEGS = ["layer0 mma", "layer0 store+bar", "hidden mma", "hidden store+bar", "out
 
 def main():
     cid = int(sys.argv[1]) if len(sys.argv) > 1 else 3
-    prob = synthetic.make_problem(cid)
+    over = {"N": int(sys.argv[2])} if len(sys.argv) > 2 else {}
+    prob = synthetic.make_problem(cid, **over)
     cfg = prob["cfg"]
     N, H, a, E = cfg["N"], cfg["H"], cfg["a"], cfg["E"]
     lib = _lib.load()
@@ -31,7 +33,8 @@ def main():
     md = fused.describe_model(prob["model"])
     cd = fused.describe_cost(prob["cost"], md["s"])
     p = fused.device_problem(md, cd, dev)
-    tiles = (N + 15) // 16
+    R = 2 if (N >= 2 * 16 * 256 and md["W"] <= 512) else 1
+    tiles = (N + 16 * R - 1) // (16 * R)
     buf = torch.zeros(E * tiles * 4 * len(SEGS), dtype=torch.int64, device=dev)
     assert lib.mbrl_diag_set_stamps(buf.data_ptr()) == 0
     mu = torch.zeros((H, a), device=dev)
@@ -44,12 +47,13 @@ def main():
     st = buf.view(E * tiles * 4, len(SEGS)).cpu().numpy().astype(np.float64)
     per_step = st.mean(0) / H
     tot = per_step.sum()
-    print(f"config {cid}: mean cycles per step per wave {tot:.0f} (diag build; shares only)")
+    print(f"config {cid} N={N} R={R} tiles={tiles}: mean cycles per step per wave {tot:.0f} (diag build; shares only)")
     for name, v in zip(SEGS, per_step):
         print(f"  {name:18s} {v:9.0f}  {100 * v / tot:5.1f}%")
-    mfma = 2176 if cid in (3, 4) else None
+    mfma = 2176 * R if cid in (3, 4) else None
     if mfma:
-        print(f"  ideal MFMA issue per step per wave: {mfma * 32} cycles")
+        print(f"  ideal MFMA issue per step per wave: {mfma * 32} cycles; hidden-loop efficiency "
+              f"{2048 * R * 32 / per_step[2]:.3f}")
 
 
 if __name__ == "__main__":
