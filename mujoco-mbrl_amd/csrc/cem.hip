@@ -190,6 +190,76 @@ __global__ void __launch_bounds__(1024) select_kernel(const float* __restrict__ 
     }
 }
 
+// Register-resident variant for N <= 1024 * KPT: thread t owns candidates [t*KPT, t*KPT + KPT);
+// radix histograms are private per wave (16 x 256 counters) so clustered returns (every candidate
+// sharing the top key byte, the common case) do not serialise on one LDS counter.
+template <int KPT>
+__global__ void __launch_bounds__(1024) select_reg_kernel(const float* __restrict__ costs, int E, int N, int K,
+                                                          int nan_policy, int64_t* __restrict__ elite_idx,
+                                                          float* __restrict__ returns_out) {
+    __shared__ uint32_t hist[16][256];
+    __shared__ uint32_t scan_ws[16];
+    __shared__ uint32_t sel[2];
+    const int tid = threadIdx.x, wave = tid >> 6;
+    const int n0 = tid * KPT;
+    uint32_t key[KPT];
+#pragma unroll
+    for (int k = 0; k < KPT; ++k) {
+        const int n = n0 + k;
+        key[k] = 0xFFFFFFFFu;
+        if (n < N) {
+            float r = costs[n];
+            if (E > 1) {
+                for (int e = 1; e < E; ++e) r = __fadd_rn(r, costs[(size_t)e * N + n]);
+                r = __fdiv_rn(r, (float)E);
+            }
+            if (returns_out) returns_out[n] = r;
+            key[k] = order_key(r, nan_policy);
+        }
+    }
+    uint32_t prefix = 0, mask = 0, kk = (uint32_t)K;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+        for (int i = tid; i < 16 * 256; i += 1024) (&hist[0][0])[i] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < KPT; ++k)
+            if (n0 + k < N && (key[k] & mask) == prefix) atomicAdd(&hist[wave][(key[k] >> shift) & 255u], 1u);
+        __syncthreads();
+        uint32_t h = 0;
+        if (tid < 256)
+#pragma unroll
+            for (int w = 0; w < 16; ++w) h += hist[w][tid];
+        uint32_t tot;
+        const uint32_t before = block_exclusive_scan(h, scan_ws, &tot);
+        if (tid < 256 && before < kk && before + h >= kk) { sel[0] = (uint32_t)tid; sel[1] = before; }
+        __syncthreads();
+        prefix |= sel[0] << shift;
+        mask |= 0xFFu << shift;
+        kk -= sel[1];
+        __syncthreads();
+    }
+    uint32_t eq = 0;
+#pragma unroll
+    for (int k = 0; k < KPT; ++k) eq += (n0 + k < N && key[k] == prefix);
+    uint32_t tot;
+    uint32_t eq_before = block_exclusive_scan(eq, scan_ws, &tot);
+    bool take[KPT];
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int k = 0; k < KPT; ++k) {
+        take[k] = false;
+        if (n0 + k < N) {
+            if (key[k] < prefix) take[k] = true;
+            else if (key[k] == prefix) { take[k] = eq_before < kk; ++eq_before; }
+        }
+        cnt += take[k];
+    }
+    uint32_t pos = block_exclusive_scan(cnt, scan_ws, &tot);
+#pragma unroll
+    for (int k = 0; k < KPT; ++k)
+        if (take[k] && pos < (uint32_t)K) elite_idx[pos++] = n0 + k;
+}
+
 // ------------------------------------------------------------------------------------------------
 // CEM refit. gather: regenerate every elite's a_t from the counter RNG into aelite[t][e][a].
 // refit: canonical chunked sums (ELITE_CHUNK = 32, oracle/cem.py:chunked_sum) -> mean, population
@@ -379,7 +449,8 @@ static int rollout_impl(const Geometry& g, const void* packed, const mbrl_norm* 
 }
 
 static int traj_impl(const Geometry& g, const void* packed, const mbrl_norm* norm, const float* s0,
-                     const float* actions, int H, float* states_out, hipStream_t stream) {
+                     const float* actions, int H, float* states_out, unsigned long long* xchg, size_t xchg_bytes,
+                     unsigned* status, hipStream_t stream) {
     TrajArgs T{};
     T.packed = static_cast<const float*>(packed);
     T.member_stride = g.member_stride;
@@ -393,6 +464,8 @@ static int traj_impl(const Geometry& g, const void* packed, const mbrl_norm* nor
         T.norm_s = norm->normalize_state; T.unnorm_s = norm->unnormalize_state; T.norm_a = norm->normalize_action;
     }
     T.s0 = s0; T.actions = actions; T.states_out = states_out;
+    if (xchg && status && traj_coop_supported(T, g.E) && xchg_bytes >= traj_coop_xchg_bytes(T, g.E))
+        return hip_check(launch_traj_coop(T, g.E, xchg, status, stream), "trajectory launch");
     return hip_check(launch_traj(T, g.E, stream), "trajectory launch");
 }
 
@@ -401,6 +474,14 @@ static int select_impl(const float* costs, int E, int N, int K, int nan_policy, 
     if (!costs || !elite_idx || !ws) return fail(MBRL_EINVAL, "costs, elite_idx and workspace must be non-NULL");
     if (N < 1 || K < 1 || K > N || E < 1) return fail(MBRL_EINVAL, "need 1 <= K (%d) <= N (%d), E >= 1", K, N);
     if (ws_bytes < align256((size_t)N * 4)) return fail(MBRL_EWORKSPACE, "select workspace %zu < %zu", ws_bytes, align256((size_t)N * 4));
+#define MBRL_SEL(KPT)                                                                                       \
+    if (N <= 1024 * (KPT)) {                                                                                \
+        hipLaunchKernelGGL(select_reg_kernel<KPT>, dim3(1), dim3(1024), 0, stream, costs, E, N, K, nan_policy, \
+                           elite_idx, returns_out);                                                         \
+        return hip_check(hipGetLastError(), "select launch");                                               \
+    }
+    MBRL_SEL(1) MBRL_SEL(2) MBRL_SEL(4) MBRL_SEL(8) MBRL_SEL(16) MBRL_SEL(32)
+#undef MBRL_SEL
     hipLaunchKernelGGL(select_kernel, dim3(1), dim3(1024), 0, stream, costs, E, N, K, nan_policy, elite_idx,
                        returns_out, static_cast<uint32_t*>(ws));
     return hip_check(hipGetLastError(), "select launch");
@@ -521,6 +602,9 @@ int mbrl_sample_actions(const mbrl_sampler* sampler, int32_t H, int32_t a, int32
 // Workspace layout for mbrl_cem_plan.
 struct PlanWs {
     float *costs, *mu[2], *sigma[2], *aelite, *states, *tmp_cost, *actions;
+    unsigned long long* xchg;
+    unsigned* status;
+    size_t xchg_bytes;
     int64_t* elites;
     uint32_t* keys;
     size_t bytes;
@@ -541,6 +625,9 @@ static PlanWs plan_ws(const Geometry& g, const mbrl_cem_params* p, void* base) {
     w.tmp_cost = (float*)take((size_t)g.E * 4);
     w.elites = (int64_t*)take((size_t)p->K * 8);
     w.keys = (uint32_t*)take((size_t)p->N * 4);
+    w.xchg_bytes = (size_t)g.E * 2 * g.Wpad * 8;
+    w.xchg = (unsigned long long*)take(w.xchg_bytes);
+    w.status = (unsigned*)take(16);
     w.bytes = o;
     return w;
 }
@@ -594,7 +681,7 @@ int mbrl_cem_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_no
     hipLaunchKernelGGL(finalize_kernel, dim3((Ha + 255) / 256), dim3(256), 0, stream, w.mu[cur], w.sigma[cur], p->lo,
                        p->hi, Ha, mu, sigma, actions_out);
     // final mean's rollout -> predicted states [E][H][s], then the member mean
-    rc = traj_impl(g, packed, norm, s0, actions_out, p->H, w.states, stream);
+    rc = traj_impl(g, packed, norm, s0, actions_out, p->H, w.states, w.xchg, w.xchg_bytes, w.status, stream);
     if (rc) return rc;
     const int Hs = p->H * g.s;
     hipLaunchKernelGGL(member_mean_kernel, dim3((Hs + 255) / 256), dim3(256), 0, stream, w.states, g.E, Hs, states_out);

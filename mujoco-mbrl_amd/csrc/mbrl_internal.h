@@ -132,4 +132,14 @@ struct TrajArgs {
 };
 hipError_t launch_traj(const TrajArgs& A, int E, hipStream_t stream);
 
+// Cooperative variant: P = Wpad/16 workgroups per member each own 16 hidden units of every W -> W
+// layer (slices LDS-resident); layer 0 and the output layer are computed redundantly by every
+// workgroup; hidden activations are all-gathered through tagged 8-byte granules in `xchg`
+// (E * 2 * Wpad granules, zeroed by the launcher before every launch). Needs P*E <= 256 and
+// s <= 64. `status` (one uint32, zeroed by the launcher) becomes nonzero if a bounded spin gave up.
+bool traj_coop_supported(const TrajArgs& A, int E);
+size_t traj_coop_xchg_bytes(const TrajArgs& A, int E);
+hipError_t launch_traj_coop(const TrajArgs& A, int E, unsigned long long* xchg, unsigned* status,
+                            hipStream_t stream);
+
 }  // namespace mbrl

@@ -129,7 +129,7 @@ def test_dynamics_forward_matches_oracle_step():
 def test_select_matches_stable_argsort_with_ties_nan_and_signed_zero():
     from mbrl_amd import _lib, fused
     rng = np.random.default_rng(0)
-    for N, K in [(1, 1), (10, 3), (1000, 100), (4096, 409), (32768, 3276), (5000, 5000)]:
+    for N, K in [(1, 1), (10, 3), (1000, 100), (4096, 409), (32768, 3276), (5000, 5000), (70001, 7000)]:
         r = rng.integers(0, 50, size=N).astype(np.float32)      # heavy ties
         if N >= 10:
             r[rng.integers(0, N, size=N // 10 + 1)] = np.nan
