@@ -119,103 +119,189 @@ hipError_t launch_traj(const TrajArgs& A, int E, hipStream_t stream) {
 namespace mbrl {
 
 // ------------------------------------------------------------------------------------------------
-// Cooperative single-trajectory rollout (see mbrl_internal.h). Hand-off protocol: R2 granules of
-// cdna_hip_programming.md §6 Guideline 16 -- each value travels as ONE aligned 8-byte
-// {tag = epoch, value} agent-scope atomic store; the consumer wave re-reads (agent-scope atomic
-// loads, L1-bypassing) until every tag equals the epoch. epoch = phase + 1, phase = t*(L-1) + l-1;
-// two buffers by phase parity (a workgroup cannot be two phases ahead of a reader: it must first
-// gather the phase in between, which needs everyone's publish that follows their read).
-// Every spin is bounded (s_memrealtime, 100 MHz); on timeout `status` is set and the kernel exits.
+// Cooperative single-trajectory rollout (see mbrl_internal.h).
+//
+// P = Wpad/16 workgroups per member, 512 threads each. Workgroup p owns hidden units
+// [16p, 16p+16) of every W -> W layer (those 16 rows LDS-resident, row stride W+32 so the two
+// half-waves of a wave read disjoint bank halves). Layer 0 and the output layer are computed
+// redundantly by every workgroup from REGISTER-resident weights (loaded once): thread u holds column
+// u of W0^T (K0 <= K0R values); thread (g = tid>>5, c = tid&31) holds Wout[g+16m][c+32i]. Every
+// step-invariant operand (normalised actions for all H steps, biases, normaliser statistics) is
+// staged in LDS at the start, so a step issues no global load except the hand-off sweeps.
+//
+// Hand-off: R2 granules of cdna_hip_programming.md §6 Guideline 16 -- each value travels as ONE
+// aligned 8-byte {tag = epoch, value} agent-scope atomic store to global memory; one wave re-reads
+// (agent-scope atomic loads, L1-bypassing) until every tag equals the epoch. epoch = phase + 1,
+// phase = t*(L-1) + l-1; two buffers by phase parity (a workgroup cannot be two phases ahead of a
+// reader: it must first gather the phase in between, which needs everyone's publish that follows
+// their read). Every spin is bounded (s_memrealtime, 100 MHz); on timeout `status` is set and the
+// kernel exits.
 // ------------------------------------------------------------------------------------------------
-constexpr int COOP_THREADS = 256;
+constexpr int COOP_THREADS = 512;
 constexpr int COOP_ROWS = 16;  // hidden units per workgroup per layer
+constexpr int COOP_MAX_W = 512;
 
 typedef unsigned long long u64;
 typedef __attribute__((address_space(1))) u64 gu64;
 
-__device__ __forceinline__ float rowsum16_t(float v) {
-    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false));
-    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x124, 0xF, 0xF, false));
-    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x122, 0xF, 0xF, false));
-    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x121, 0xF, 0xF, false));
+// Diagnostic build only (-DMBRL_STAMPS): per-workgroup s_memrealtime sums (10 ns ticks) of the
+// coop kernel's segments, written to a buffer set by mbrl_diag_set_traj_stamps().
+#ifdef MBRL_STAMPS
+constexpr int TRAJ_NSEG = 4;
+__device__ unsigned long long* g_mbrl_traj_stamps;
+#define TSTAMP(k)                                                      \
+    do {                                                               \
+        const unsigned long long _t = __builtin_amdgcn_s_memrealtime(); \
+        tseg[k] += _t - tprev;                                         \
+        tprev = _t;                                                    \
+    } while (0)
+#else
+#define TSTAMP(k) \
+    do {          \
+    } while (0)
+#endif
+
+// sum over the 32 lanes of a half-wave, fixed butterfly order (identical result in every lane)
+__device__ __forceinline__ float halfwave_sum(float v) {
+#pragma unroll
+    for (int o = 16; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
 
+struct CoopLds {
+    int rs;                         // slice row stride (floats)
+    size_t slices, x0, hA, hB, out, acts, hb, ob, om, os, flag, total;
+};
+
+__host__ __device__ inline CoopLds coop_lds(int s, int a, int W, int Wp, int L, int H) {
+    CoopLds m;
+    auto al4 = [](size_t n) { return (n + 3) & ~(size_t)3; };
+    m.rs = W + 32;
+    size_t o = 0;
+    m.slices = o; o += (size_t)(L - 1) * COOP_ROWS * m.rs;
+    m.x0 = o;     o += al4(s + a);
+    m.hA = o;     o += Wp;
+    m.hB = o;     o += Wp;
+    m.out = o;    o += al4(s);
+    m.acts = o;   o += al4((size_t)H * a);       // normalised actions, [H][a]
+    m.hb = o;     o += al4((size_t)(L - 1) * COOP_ROWS);  // my hidden biases
+    m.ob = o;     o += al4(s);                    // output bias
+    m.om = o;     o += al4(s);                    // obs mean
+    m.os = o;     o += al4(s);                    // obs std
+    m.flag = o;   o += 4;
+    m.total = o * sizeof(float);
+    return m;
+}
+
+template <int K0R, int SM>
 __global__ void __launch_bounds__(COOP_THREADS) traj_coop_kernel(const TrajArgs A, u64* __restrict__ xchg_all,
                                                                   unsigned* __restrict__ status) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int p = blockIdx.x, P = gridDim.x, e = blockIdx.y;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int Wp = A.Wpad, K0 = A.s + A.a;
-    float* slices = smem;                                      // [(L-1)][16][W]
-    float* x0 = slices + (size_t)(A.L - 1) * COOP_ROWS * A.W;  // [K0 padded to 4]
-    float* hA = x0 + ((K0 + 3) & ~3);                          // [Wp]
-    float* hB = hA + Wp;                                       // [Wp]
-    float* out = hB + Wp;                                      // [s rounded up to 4]
-    int& abort_flag = *reinterpret_cast<int*>(out + ((A.s + 3) & ~3));  // dynamic region (G17)
+    const int s = A.s, a = A.a, W = A.W, Wp = A.Wpad, K0 = s + a;
+    const CoopLds m = coop_lds(s, a, W, Wp, A.L, A.H);
+    float* slices = smem + m.slices;
+    float* x0 = smem + m.x0;
+    float* out = smem + m.out;
+    float* acts = smem + m.acts;
+    float* hb = smem + m.hb;
+    float* ob = smem + m.ob;
+    float* om = smem + m.om;
+    float* os = smem + m.os;
+    int& abort_flag = *reinterpret_cast<int*>(smem + m.flag);
     const float* member = A.packed + (size_t)e * A.member_stride;
     const float* bias = member + A.bias_off;
     const float* tw = member + A.tw_base;
-    u64* xchg = xchg_all + (size_t)e * 2 * Wp;
+    gu64* xchg = (gu64*)(xchg_all + (size_t)e * 2 * Wp);
 
+    // ---- one-time staging ----------------------------------------------------------------------
     if (tid == 0) abort_flag = 0;
-    // this workgroup's rows of every hidden W -> W layer: W_l[n][k] = W^T_l[k][n] (plain region);
-    // 16 consecutive threads read one 64-byte run of a W^T row
-    for (int l = 1; l < A.L; ++l) {
+    for (int l = 1; l < A.L; ++l) {      // my rows of W_l: W_l[n][k] = W^T_l[k][n]
         const float* wt = tw + A.tw_off[l];
-        float* dst = slices + (size_t)(l - 1) * COOP_ROWS * A.W;
-        for (int i = tid; i < COOP_ROWS * A.W; i += COOP_THREADS) {
+        float* dst = slices + (size_t)(l - 1) * COOP_ROWS * m.rs;
+        for (int i = tid; i < COOP_ROWS * W; i += COOP_THREADS) {
             const int k = i >> 4, o = i & 15;
-            dst[o * A.W + k] = wt[(size_t)k * Wp + p * COOP_ROWS + o];
+            dst[o * m.rs + k] = wt[(size_t)k * Wp + p * COOP_ROWS + o];
         }
     }
-    for (int d = tid; d < A.s; d += COOP_THREADS) {
+    for (int i = tid; i < A.H * a; i += COOP_THREADS) {
+        const int d = i % a;
+        const float av = A.actions[i];
+        acts[i] = A.norm_a ? (av - A.act_mean[d]) / A.act_std[d] : av;
+    }
+    for (int i = tid; i < (A.L - 1) * COOP_ROWS; i += COOP_THREADS)
+        hb[i] = bias[(size_t)(1 + i / COOP_ROWS) * Wp + p * COOP_ROWS + (i % COOP_ROWS)];
+    for (int d = tid; d < s; d += COOP_THREADS) {
+        ob[d] = bias[(size_t)A.L * Wp + d];
+        om[d] = A.obs_mean[d];
+        os[d] = A.obs_std[d];
         const float sv = A.s0[d];
         x0[d] = A.norm_s ? (sv - A.obs_mean[d]) / A.obs_std[d] : sv;
     }
+    // layer-0 column of unit u = tid (W^T_0 [K0][Wp]), zero past K0
+    float w0r[K0R];
+    const bool has_unit = tid < Wp;
+    const float b0 = has_unit ? bias[tid] : 0.0f;
+#pragma unroll
+    for (int k = 0; k < K0R; ++k)
+        w0r[k] = (has_unit && k < K0) ? tw[A.tw_off[0] + (size_t)k * Wp + tid] : 0.0f;
+    // output rows d = g + 16 mm, columns c + 32 i (Wout row-major [s][W]), zero past s / W
+    const int g = tid >> 5, c = tid & 31;
+    float wor[SM][COOP_MAX_W / 32];
+#pragma unroll
+    for (int mm = 0; mm < SM; ++mm)
+#pragma unroll
+        for (int i = 0; i < COOP_MAX_W / 32; ++i) {
+            const int d = g + 16 * mm, k = c + 32 * i;
+            wor[mm][i] = (d < s && k < W) ? tw[A.tw_off[A.L] + (size_t)d * W + k] : 0.0f;
+        }
     __syncthreads();
 
+#ifdef MBRL_STAMPS
+    unsigned long long tseg[TRAJ_NSEG] = {0, 0, 0, 0};
+    unsigned long long tprev = __builtin_amdgcn_s_memrealtime();
+#endif
     int phase = 0;
     for (int t = 0; t < A.H; ++t) {
-        for (int d = tid; d < A.a; d += COOP_THREADS) {
-            const float av = A.actions[t * A.a + d];
-            x0[A.s + d] = A.norm_a ? (av - A.act_mean[d]) / A.act_std[d] : av;
+        for (int d = tid; d < a; d += COOP_THREADS) x0[s + d] = acts[t * a + d];
+        __syncthreads();
+        float* cur = smem + m.hA;
+        float* nxt = smem + m.hB;
+        if (has_unit) {                                 // layer 0 (redundant in every workgroup)
+            float v = b0;
+#pragma unroll
+            for (int k = 0; k < K0R; ++k)
+                if (k < K0) v += w0r[k] * x0[k];
+            cur[tid] = fmaxf(v, 0.0f);
         }
         __syncthreads();
-        // layer 0, all Wp units (redundant in every workgroup): W^T_0 [K0][Wp], coalesced over n
-        for (int n = tid; n < Wp; n += COOP_THREADS) {
-            const float* w0 = tw + A.tw_off[0] + n;
-            float v = bias[n];
-            for (int k = 0; k < K0; ++k) v += w0[(size_t)k * Wp] * x0[k];
-            hA[n] = fmaxf(v, 0.0f);
-        }
-        __syncthreads();
-        float* cur = hA;
-        float* nxt = hB;
+        TSTAMP(0);
         for (int l = 1; l < A.L; ++l, ++phase) {
-            // my 16 units: row o = tid >> 4, lanes j = tid & 15 split K
-            const int o = tid >> 4, j = tid & 15;
-            const float* ws = slices + (size_t)(l - 1) * COOP_ROWS * A.W + (size_t)o * A.W;
+            // my 16 units: row g (half-wave), lanes c split K
+            const float* ws = slices + (size_t)(l - 1) * COOP_ROWS * m.rs + (size_t)g * m.rs;
             float v = 0.f;
-            for (int k = j; k < A.W; k += 16) v += ws[k] * cur[k];
-            v = rowsum16_t(v);
+#pragma unroll
+            for (int i = 0; i < COOP_MAX_W / 32; ++i)
+                if (c + 32 * i < W) v += ws[c + 32 * i] * cur[c + 32 * i];
+            v = halfwave_sum(v);
             const unsigned epoch = (unsigned)phase + 1u;
-            u64* buf = xchg + (size_t)(phase & 1) * Wp;
-            if (j == 0) {
-                const int n = p * COOP_ROWS + o;
-                const float y = fmaxf(v + bias[(size_t)l * Wp + n], 0.0f);
-                __hip_atomic_store(&buf[n], ((u64)epoch << 32) | __float_as_uint(y), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+            gu64* buf = xchg + (size_t)(phase & 1) * Wp;
+            if (c == 0) {
+                const float y = fmaxf(v + hb[(l - 1) * COOP_ROWS + g], 0.0f);
+                __hip_atomic_store(&buf[p * COOP_ROWS + g], ((u64)epoch << 32) | __float_as_uint(y),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
+            TSTAMP(1);
             // gather all P slices: wave 0 sweeps the granules until every tag matches
             if (wave == 0) {
                 const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
                 for (;;) {
                     bool ok = true;
                     for (int n = lane; n < P * COOP_ROWS; n += 64) {
-                        const u64 g = __hip_atomic_load(&buf[n], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        ok &= (unsigned)(g >> 32) == epoch;
-                        nxt[n] = __uint_as_float((unsigned)g);
+                        const u64 gv = __hip_atomic_load(&buf[n], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        ok &= (unsigned)(gv >> 32) == epoch;
+                        nxt[n] = __uint_as_float((unsigned)gv);
                     }
                     if (__all(ok)) break;
                     if (__builtin_amdgcn_s_memrealtime() - t_start > 20000000ull) {  // 200 ms
@@ -229,57 +315,87 @@ __global__ void __launch_bounds__(COOP_THREADS) traj_coop_kernel(const TrajArgs 
                 }
             }
             __syncthreads();
+            TSTAMP(2);
             if (abort_flag) return;
             float* tmp = cur; cur = nxt; nxt = tmp;
         }
-        // output layer (redundant): 16 lanes per output row, Wout row-major [s][W]
-        const float* wo = tw + A.tw_off[A.L];
-        const float* bo = bias + (size_t)A.L * Wp;
-        for (int base = 0; base < A.s; base += COOP_THREADS / 16) {
-            const int o = base + (tid >> 4), j = tid & 15;
+        // output layer (redundant): half-wave g owns rows g + 16 mm
+#pragma unroll
+        for (int mm = 0; mm < SM; ++mm) {
             float v = 0.f;
-            if (o < A.s)
-                for (int k = j; k < A.W; k += 16) v += wo[(size_t)o * A.W + k] * cur[k];
-            v = rowsum16_t(v);
-            if (j == 0 && o < A.s) out[o] = v + bo[o];
+#pragma unroll
+            for (int i = 0; i < COOP_MAX_W / 32; ++i)
+                if (c + 32 * i < W) v += wor[mm][i] * cur[c + 32 * i];
+            v = halfwave_sum(v);
+            const int d = g + 16 * mm;
+            if (c == 0 && d < s) out[d] = v + ob[d];
         }
         __syncthreads();
-        for (int d = tid; d < A.s; d += COOP_THREADS) {
-            const float sn = A.unnorm_s ? out[d] * A.obs_std[d] + A.obs_mean[d] : out[d];
-            if (p == 0) A.states_out[((size_t)e * A.H + t) * A.s + d] = sn;
-            x0[d] = A.norm_s ? (sn - A.obs_mean[d]) / A.obs_std[d] : sn;
+        for (int d = tid; d < s; d += COOP_THREADS) {
+            const float sn = A.unnorm_s ? out[d] * os[d] + om[d] : out[d];
+            if (p == 0) A.states_out[((size_t)e * A.H + t) * s + d] = sn;
+            x0[d] = A.norm_s ? (sn - om[d]) / os[d] : sn;
         }
-        // x0[s..s+a) is rewritten before the barrier at the top of the next step
+        // x0 is read again only after the barrier at the top of the next step
+        TSTAMP(3);
     }
+#ifdef MBRL_STAMPS
+    if (tid == 0 && g_mbrl_traj_stamps != nullptr)
+        for (int k = 0; k < TRAJ_NSEG; ++k)
+            g_mbrl_traj_stamps[((size_t)e * P + p) * TRAJ_NSEG + k] = tseg[k];
+#endif
+}
+
+// register budgets: (K0 <= 32, s <= 32) for cartpole / cheetah / walker, (K0 <= 96, s <= 80) humanoid
+static int coop_variant(const TrajArgs& A) {
+    const int K0 = A.s + A.a;
+    if (K0 <= 32 && A.s <= 32) return 0;
+    if (K0 <= 96 && A.s <= 80) return 1;
+    return -1;
 }
 
 bool traj_coop_supported(const TrajArgs& A, int E) {
     const int P = A.Wpad / COOP_ROWS;
-    const size_t lds = ((size_t)(A.L - 1) * COOP_ROWS * A.W + ((A.s + A.a + 3) & ~3) + 2 * A.Wpad +
-                        ((A.s + 3) & ~3) + 4) * 4;
-    return A.L >= 2 && A.W == A.Wpad && P * E <= 256 && lds <= 150 * 1024;
+    const CoopLds m = coop_lds(A.s, A.a, A.W, A.Wpad, A.L, A.H);
+    return A.L >= 2 && A.W == A.Wpad && A.Wpad <= COOP_MAX_W && P * E <= 256 && m.total <= 150 * 1024 &&
+           coop_variant(A) >= 0;
 }
 
 size_t traj_coop_xchg_bytes(const TrajArgs& A, int E) { return (size_t)E * 2 * A.Wpad * sizeof(u64); }
 
-hipError_t launch_traj_coop(const TrajArgs& A, int E, unsigned long long* xchg, unsigned* status,
-                            hipStream_t stream) {
-    const int P = A.Wpad / COOP_ROWS;
-    const size_t lds = ((size_t)(A.L - 1) * COOP_ROWS * A.W + ((A.s + A.a + 3) & ~3) + 2 * A.Wpad +
-                        ((A.s + 3) & ~3) + 4) * 4;
+template <int K0R, int SM>
+static hipError_t launch_coop_variant(const TrajArgs& A, int E, u64* xchg, unsigned* status, size_t lds,
+                                      hipStream_t stream) {
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(&traj_coop_kernel),
+        hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(&traj_coop_kernel<K0R, SM>),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (err != hipSuccess) return err;
         attr_set = true;
     }
+    hipLaunchKernelGGL((traj_coop_kernel<K0R, SM>), dim3(A.Wpad / COOP_ROWS, E), dim3(COOP_THREADS), lds, stream,
+                       A, xchg, status);
+    return hipGetLastError();
+}
+
+hipError_t launch_traj_coop(const TrajArgs& A, int E, unsigned long long* xchg, unsigned* status,
+                            hipStream_t stream) {
+    const CoopLds m = coop_lds(A.s, A.a, A.W, A.Wpad, A.L, A.H);
     hipError_t err = hipMemsetAsync(xchg, 0, traj_coop_xchg_bytes(A, E), stream);
     if (err != hipSuccess) return err;
     err = hipMemsetAsync(status, 0, sizeof(unsigned), stream);
     if (err != hipSuccess) return err;
-    hipLaunchKernelGGL(traj_coop_kernel, dim3(P, E), dim3(COOP_THREADS), lds, stream, A, xchg, status);
-    return hipGetLastError();
+    switch (coop_variant(A)) {
+        case 0: return launch_coop_variant<32, 2>(A, E, xchg, status, m.total, stream);
+        case 1: return launch_coop_variant<96, 5>(A, E, xchg, status, m.total, stream);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 }  // namespace mbrl
+
+#ifdef MBRL_STAMPS
+extern "C" int mbrl_diag_set_traj_stamps(void* buf) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(mbrl::g_mbrl_traj_stamps), &buf, sizeof(buf));
+}
+#endif

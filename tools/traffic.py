@@ -1,0 +1,46 @@
+"""Summarise tools/pmc.sh output (gpurun_out/pmc) into profiles/.
+
+    python tools/traffic.py <config-name> <round-tag>
+
+Writes profiles/<round>_rollout_pmc.csv (per-counter mean/min/max over the profiled rollout
+dispatches) and sets profiles/rollout_traffic.json[<config-name>] = HBM-side bytes per launch:
+2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes). The factor 2 is MI355X_MICROARCH.md's gfx950
+correction for wide coalesced reads (FETCH_SIZE counts 128-B requests as 64 B); WRITE_SIZE is exact
+for 16-B-per-lane stores. The first dispatch (cold caches) is excluded from the mean."""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    name, tag = sys.argv[1], sys.argv[2]
+    vals = collections.defaultdict(list)
+    kernel = None
+    for f in sorted(glob.glob(os.path.join(REPO, "gpurun_out", "pmc", "p*", "*counter_collection.csv"))):
+        for r in csv.DictReader(open(f)):
+            vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
+            kernel = r["Kernel_Name"]
+    out = os.path.join(REPO, "profiles", f"{tag}_rollout_pmc.csv")
+    with open(out, "w") as fh:
+        fh.write("kernel,counter,dispatches,mean_excl_first,min,max\n")
+        for k, v in sorted(vals.items()):
+            warm = v[1:] if len(v) > 1 else v
+            fh.write(f"\"{kernel}\",{k},{len(v)},{sum(warm) / len(warm):.1f},{min(v):.1f},{max(v):.1f}\n")
+    mean = {k: (sum(v[1:]) / len(v[1:]) if len(v) > 1 else v[0]) for k, v in vals.items()}
+    traffic = 2 * mean["FETCH_SIZE"] * 1024 + mean["WRITE_SIZE"] * 1024
+    tj = os.path.join(REPO, "profiles", "rollout_traffic.json")
+    d = json.load(open(tj)) if os.path.exists(tj) else {}
+    d[name] = traffic
+    d["_method"] = ("bytes per rollout launch = 2*FETCH_SIZE + WRITE_SIZE (KiB->B), mean over warm dispatches; "
+                    f"source {os.path.basename(out)}")
+    json.dump(d, open(tj, "w"), indent=1)
+    print(out, traffic)
+
+
+if __name__ == "__main__":
+    main()
