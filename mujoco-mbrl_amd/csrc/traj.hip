@@ -173,13 +173,13 @@ struct CoopLds {
     size_t slices, x0, hA, hB, out, acts, hb, ob, om, os, flag, total;
 };
 
-__host__ __device__ inline CoopLds coop_lds(int s, int a, int W, int Wp, int L, int H) {
+__host__ __device__ inline CoopLds coop_lds(int s, int a, int W, int Wp, int L, int H, int K0R) {
     CoopLds m;
     auto al4 = [](size_t n) { return (n + 3) & ~(size_t)3; };
     m.rs = W + 32;
     size_t o = 0;
     m.slices = o; o += (size_t)(L - 1) * COOP_ROWS * m.rs;
-    m.x0 = o;     o += al4(s + a);
+    m.x0 = o;     o += al4(K0R > s + a ? K0R : s + a);
     m.hA = o;     o += Wp;
     m.hB = o;     o += Wp;
     m.out = o;    o += al4(s);
@@ -193,14 +193,18 @@ __host__ __device__ inline CoopLds coop_lds(int s, int a, int W, int Wp, int L, 
     return m;
 }
 
-template <int K0R, int SM>
+// K0R: layer-0 inputs held per thread (>= s + a); SM: output rows per half-wave (16 SM >= s);
+// WI = W / 32: columns per lane of a 16-row dot (W == Wpad). All loops are unguarded: operands past
+// the real sizes are zero (weights) or finite zeros (x0 padding), so LDS reads issue in batches.
+template <int K0R, int SM, int WI>
 __global__ void __launch_bounds__(COOP_THREADS) traj_coop_kernel(const TrajArgs A, u64* __restrict__ xchg_all,
                                                                   unsigned* __restrict__ status) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int p = blockIdx.x, P = gridDim.x, e = blockIdx.y;
+    const int p = blockIdx.x, e = blockIdx.y;
+    [[maybe_unused]] const int P = gridDim.x;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int s = A.s, a = A.a, W = A.W, Wp = A.Wpad, K0 = s + a;
-    const CoopLds m = coop_lds(s, a, W, Wp, A.L, A.H);
+    const CoopLds m = coop_lds(s, a, W, Wp, A.L, A.H, K0R);
     float* slices = smem + m.slices;
     float* x0 = smem + m.x0;
     float* out = smem + m.out;
@@ -217,6 +221,8 @@ __global__ void __launch_bounds__(COOP_THREADS) traj_coop_kernel(const TrajArgs 
 
     // ---- one-time staging ----------------------------------------------------------------------
     if (tid == 0) abort_flag = 0;
+    for (int k = tid; k < K0R; k += COOP_THREADS) x0[k] = 0.0f;
+    __syncthreads();
     for (int l = 1; l < A.L; ++l) {      // my rows of W_l: W_l[n][k] = W^T_l[k][n]
         const float* wt = tw + A.tw_off[l];
         float* dst = slices + (size_t)(l - 1) * COOP_ROWS * m.rs;
@@ -248,11 +254,11 @@ __global__ void __launch_bounds__(COOP_THREADS) traj_coop_kernel(const TrajArgs 
         w0r[k] = (has_unit && k < K0) ? tw[A.tw_off[0] + (size_t)k * Wp + tid] : 0.0f;
     // output rows d = g + 16 mm, columns c + 32 i (Wout row-major [s][W]), zero past s / W
     const int g = tid >> 5, c = tid & 31;
-    float wor[SM][COOP_MAX_W / 32];
+    float wor[SM][WI];
 #pragma unroll
     for (int mm = 0; mm < SM; ++mm)
 #pragma unroll
-        for (int i = 0; i < COOP_MAX_W / 32; ++i) {
+        for (int i = 0; i < WI; ++i) {
             const int d = g + 16 * mm, k = c + 32 * i;
             wor[mm][i] = (d < s && k < W) ? tw[A.tw_off[A.L] + (size_t)d * W + k] : 0.0f;
         }
@@ -271,8 +277,7 @@ __global__ void __launch_bounds__(COOP_THREADS) traj_coop_kernel(const TrajArgs 
         if (has_unit) {                                 // layer 0 (redundant in every workgroup)
             float v = b0;
 #pragma unroll
-            for (int k = 0; k < K0R; ++k)
-                if (k < K0) v += w0r[k] * x0[k];
+            for (int k = 0; k < K0R; ++k) v += w0r[k] * x0[k];
             cur[tid] = fmaxf(v, 0.0f);
         }
         __syncthreads();
@@ -282,8 +287,7 @@ __global__ void __launch_bounds__(COOP_THREADS) traj_coop_kernel(const TrajArgs 
             const float* ws = slices + (size_t)(l - 1) * COOP_ROWS * m.rs + (size_t)g * m.rs;
             float v = 0.f;
 #pragma unroll
-            for (int i = 0; i < COOP_MAX_W / 32; ++i)
-                if (c + 32 * i < W) v += ws[c + 32 * i] * cur[c + 32 * i];
+            for (int i = 0; i < WI; ++i) v += ws[c + 32 * i] * cur[c + 32 * i];
             v = halfwave_sum(v);
             const unsigned epoch = (unsigned)phase + 1u;
             gu64* buf = xchg + (size_t)(phase & 1) * Wp;
@@ -296,12 +300,17 @@ __global__ void __launch_bounds__(COOP_THREADS) traj_coop_kernel(const TrajArgs 
             // gather all P slices: wave 0 sweeps the granules until every tag matches
             if (wave == 0) {
                 const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+                constexpr int GR = WI / 2;         // granules per lane: P * 16 = Wp = 32 WI
                 for (;;) {
+                    u64 gv[GR];
+#pragma unroll
+                    for (int q = 0; q < GR; ++q)    // all loads in flight before the first compare
+                        gv[q] = __hip_atomic_load(&buf[lane + 64 * q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     bool ok = true;
-                    for (int n = lane; n < P * COOP_ROWS; n += 64) {
-                        const u64 gv = __hip_atomic_load(&buf[n], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        ok &= (unsigned)(gv >> 32) == epoch;
-                        nxt[n] = __uint_as_float((unsigned)gv);
+#pragma unroll
+                    for (int q = 0; q < GR; ++q) {
+                        ok &= (unsigned)(gv[q] >> 32) == epoch;
+                        nxt[lane + 64 * q] = __uint_as_float((unsigned)gv[q]);
                     }
                     if (__all(ok)) break;
                     if (__builtin_amdgcn_s_memrealtime() - t_start > 20000000ull) {  // 200 ms
@@ -324,8 +333,7 @@ __global__ void __launch_bounds__(COOP_THREADS) traj_coop_kernel(const TrajArgs 
         for (int mm = 0; mm < SM; ++mm) {
             float v = 0.f;
 #pragma unroll
-            for (int i = 0; i < COOP_MAX_W / 32; ++i)
-                if (c + 32 * i < W) v += wor[mm][i] * cur[c + 32 * i];
+            for (int i = 0; i < WI; ++i) v += wor[mm][i] * cur[c + 32 * i];
             v = halfwave_sum(v);
             const int d = g + 16 * mm;
             if (c == 0 && d < s) out[d] = v + ob[d];
@@ -347,49 +355,56 @@ __global__ void __launch_bounds__(COOP_THREADS) traj_coop_kernel(const TrajArgs 
 }
 
 // register budgets: (K0 <= 32, s <= 32) for cartpole / cheetah / walker, (K0 <= 96, s <= 80) humanoid
-static int coop_variant(const TrajArgs& A) {
+static int coop_k0r(const TrajArgs& A) {
     const int K0 = A.s + A.a;
-    if (K0 <= 32 && A.s <= 32) return 0;
-    if (K0 <= 96 && A.s <= 80) return 1;
-    return -1;
+    if (K0 <= 32 && A.s <= 32) return 32;
+    if (K0 <= 96 && A.s <= 80) return 96;
+    return 0;
 }
 
 bool traj_coop_supported(const TrajArgs& A, int E) {
     const int P = A.Wpad / COOP_ROWS;
-    const CoopLds m = coop_lds(A.s, A.a, A.W, A.Wpad, A.L, A.H);
-    return A.L >= 2 && A.W == A.Wpad && A.Wpad <= COOP_MAX_W && P * E <= 256 && m.total <= 150 * 1024 &&
-           coop_variant(A) >= 0;
+    const int k0r = coop_k0r(A);
+    if (k0r == 0 || A.L < 2 || A.W != A.Wpad || A.Wpad > COOP_MAX_W || P * E > 256) return false;
+    return coop_lds(A.s, A.a, A.W, A.Wpad, A.L, A.H, k0r).total <= 150 * 1024;
 }
 
 size_t traj_coop_xchg_bytes(const TrajArgs& A, int E) { return (size_t)E * 2 * A.Wpad * sizeof(u64); }
 
-template <int K0R, int SM>
-static hipError_t launch_coop_variant(const TrajArgs& A, int E, u64* xchg, unsigned* status, size_t lds,
-                                      hipStream_t stream) {
+template <int K0R, int SM, int WI>
+static hipError_t launch_coop_variant(const TrajArgs& A, int E, u64* xchg, unsigned* status, hipStream_t stream) {
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(&traj_coop_kernel<K0R, SM>),
+        hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(&traj_coop_kernel<K0R, SM, WI>),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (err != hipSuccess) return err;
         attr_set = true;
     }
-    hipLaunchKernelGGL((traj_coop_kernel<K0R, SM>), dim3(A.Wpad / COOP_ROWS, E), dim3(COOP_THREADS), lds, stream,
-                       A, xchg, status);
+    const size_t lds = coop_lds(A.s, A.a, A.W, A.Wpad, A.L, A.H, K0R).total;
+    hipLaunchKernelGGL((traj_coop_kernel<K0R, SM, WI>), dim3(A.Wpad / COOP_ROWS, E), dim3(COOP_THREADS), lds,
+                       stream, A, xchg, status);
     return hipGetLastError();
+}
+
+template <int K0R, int SM>
+static hipError_t launch_coop_width(const TrajArgs& A, int E, u64* xchg, unsigned* status, hipStream_t stream) {
+    switch (A.Wpad) {
+        case 64: return launch_coop_variant<K0R, SM, 2>(A, E, xchg, status, stream);
+        case 128: return launch_coop_variant<K0R, SM, 4>(A, E, xchg, status, stream);
+        case 256: return launch_coop_variant<K0R, SM, 8>(A, E, xchg, status, stream);
+        case 512: return launch_coop_variant<K0R, SM, 16>(A, E, xchg, status, stream);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 hipError_t launch_traj_coop(const TrajArgs& A, int E, unsigned long long* xchg, unsigned* status,
                             hipStream_t stream) {
-    const CoopLds m = coop_lds(A.s, A.a, A.W, A.Wpad, A.L, A.H);
     hipError_t err = hipMemsetAsync(xchg, 0, traj_coop_xchg_bytes(A, E), stream);
     if (err != hipSuccess) return err;
     err = hipMemsetAsync(status, 0, sizeof(unsigned), stream);
     if (err != hipSuccess) return err;
-    switch (coop_variant(A)) {
-        case 0: return launch_coop_variant<32, 2>(A, E, xchg, status, m.total, stream);
-        case 1: return launch_coop_variant<96, 5>(A, E, xchg, status, m.total, stream);
-        default: return hipErrorInvalidValue;
-    }
+    return coop_k0r(A) == 32 ? launch_coop_width<32, 2>(A, E, xchg, status, stream)
+                             : launch_coop_width<96, 5>(A, E, xchg, status, stream);
 }
 
 }  // namespace mbrl
