@@ -156,6 +156,14 @@ int mbrl_cem_refit(const mbrl_sampler* sampler, int32_t H, int32_t a, const int6
 int mbrl_sample_actions(const mbrl_sampler* sampler, int32_t H, int32_t a, int32_t N, int32_t n_offset,
                         float* actions_out, mbrl_stream_t stream);
 
+/* ---- one trajectory per ensemble member: the states of a single action sequence (the final CEM
+ * mean; replaces the N=1 use of planners.py:199-210). actions [H][a]; states_out [H][s] = member
+ * mean; member_states_out [E][H][s] or NULL. workspace >= mbrl_trajectory_workspace_bytes. */
+size_t mbrl_trajectory_workspace_bytes(const mbrl_mlp_shape* shape, int32_t H);
+int mbrl_trajectory(const mbrl_mlp_shape* shape, const void* packed, const mbrl_norm* norm, const float* s0,
+                    const float* actions, int32_t H, float* states_out, float* member_states_out,
+                    void* workspace, size_t ws_bytes, mbrl_stream_t stream);
+
 /* ---- whole single-GPU CEM plan: I x (rollout -> select -> refit), then the final mean's rollout.
  * mu / sigma: [H][a] final distribution. actions_out: [H][a] = clip(mu, lo, hi);
  * states_out: [H][s] rollout of actions_out (ensemble mean over members).

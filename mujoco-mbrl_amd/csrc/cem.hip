@@ -599,6 +599,52 @@ int mbrl_sample_actions(const mbrl_sampler* sampler, int32_t H, int32_t a, int32
     return sample_impl(sampler, H, a, N, n_offset, actions_out, reinterpret_cast<hipStream_t>(stream));
 }
 
+// Workspace for mbrl_trajectory: per-member states, exchange granules, status word.
+struct TrajWs {
+    float* states;
+    unsigned long long* xchg;
+    unsigned* status;
+    size_t xchg_bytes, bytes;
+};
+
+static TrajWs traj_ws(const Geometry& g, int H, void* base) {
+    TrajWs w{};
+    char* b = static_cast<char*>(base);
+    size_t o = 0;
+    auto take = [&](size_t n) { void* r = b ? b + o : nullptr; o += align256(n); return r; };
+    w.xchg_bytes = (size_t)g.E * 2 * g.Wpad * 8;
+    w.xchg = (unsigned long long*)take(w.xchg_bytes);   // memset block first, 16-B multiple (G16)
+    w.status = (unsigned*)take(16);
+    w.states = (float*)take((size_t)g.E * H * g.s * 4);
+    w.bytes = o;
+    return w;
+}
+
+size_t mbrl_trajectory_workspace_bytes(const mbrl_mlp_shape* shape, int32_t H) {
+    Geometry g;
+    if (shape_geometry(shape, &g) != MBRL_OK || H < 1) return 0;
+    return traj_ws(g, H, nullptr).bytes;
+}
+
+int mbrl_trajectory(const mbrl_mlp_shape* shape, const void* packed, const mbrl_norm* norm, const float* s0,
+                    const float* actions, int32_t H, float* states_out, float* member_states_out, void* workspace,
+                    size_t ws_bytes, mbrl_stream_t stream_) {
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
+    Geometry g;
+    int rc = shape_geometry(shape, &g);
+    if (rc) return rc;
+    if (H < 1) return fail(MBRL_EINVAL, "trajectory: H=%d", H);
+    if (!packed || !s0 || !actions || !states_out || !workspace) return fail(MBRL_EINVAL, "trajectory: NULL argument");
+    TrajWs w = traj_ws(g, H, workspace);
+    if (ws_bytes < w.bytes) return fail(MBRL_EWORKSPACE, "trajectory workspace %zu < %zu", ws_bytes, w.bytes);
+    float* per_member = member_states_out ? member_states_out : w.states;
+    rc = traj_impl(g, packed, norm, s0, actions, H, per_member, w.xchg, w.xchg_bytes, w.status, stream);
+    if (rc) return rc;
+    const int Hs = H * g.s;
+    hipLaunchKernelGGL(member_mean_kernel, dim3((Hs + 255) / 256), dim3(256), 0, stream, per_member, g.E, Hs, states_out);
+    return hip_check(hipGetLastError(), "trajectory launch");
+}
+
 // Workspace layout for mbrl_cem_plan.
 struct PlanWs {
     float *costs, *mu[2], *sigma[2], *aelite, *states, *tmp_cost, *actions;

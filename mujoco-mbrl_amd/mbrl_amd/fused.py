@@ -290,6 +290,21 @@ def refit(sampler, H, a, elites, alpha, mu_out, sigma_out, workspace=None):
                                   _lib.stream_handle(dev)), "mbrl_cem_refit")
 
 
+def trajectory(prob, s0, actions, H, member_states=None, workspace=None):
+    """States [H, s] (ensemble mean) of ONE action sequence actions [H, a]; member_states [E, H, s] optional."""
+    lib = _lib.load()
+    dev = prob.device
+    states = torch.empty((H, prob.mdesc["s"]), dtype=torch.float32, device=dev)
+    need = lib.mbrl_trajectory_workspace_bytes(ctypes_ref(prob.shape), H)
+    if workspace is None or workspace.numel() < need:
+        workspace = torch.empty(need, dtype=torch.uint8, device=dev)
+    _lib.check(lib.mbrl_trajectory(ctypes_ref(prob.shape), _lib.ptr(prob.packed), ctypes_ref(prob.norm), _lib.ptr(s0),
+                                   _lib.ptr(actions), H, _lib.ptr(states), _lib.ptr(member_states),
+                                   _lib.ptr(workspace), workspace.numel(), _lib.stream_handle(dev)),
+               "mbrl_trajectory")
+    return states
+
+
 def sample_actions(sampler, H, a, N, n_offset, out):
     lib = _lib.load()
     _lib.check(lib.mbrl_sample_actions(ctypes_ref(sampler), H, a, N, n_offset, _lib.ptr(out),

@@ -232,41 +232,44 @@ def _cem_fused_single(prob, s0, st):
     return out
 
 
-def _cem_fused_sharded(prob, s0, st, world):
-    """Candidates [r*N/G, (r+1)*N/G) on rank r; per iteration: local rollout -> RCCL all-gather of
-    the [E, N/G] costs -> replicated selection + refit (identical on every rank)."""
-    import torch.distributed as dist
-    dev = prob.device
-    md = prob.mdesc
-    N, K, H, I = st["N"], st["K"], st["H"], st["I"]
-    a, s, E = md["a"], md["s"], md["E"]
-    rank = dist.get_rank()
+def cem_sharded_protocol(ops, st, world, rank):
+    """Host protocol of the sharded CEM plan, independent of where the math runs.
+
+    Rank r of G owns global candidates [r*N/G, (r+1)*N/G). Per iteration: local proposal draw +
+    rollout (proposals keyed by the GLOBAL candidate index) -> one all-gather of the [E, N/G] local
+    costs -> every rank runs the same deterministic select + refit on the full [E, N] costs. The
+    refit regenerates the elites' actions from the counter RNG, so no moment collective is needed
+    and mu / sigma are bit-identical on every rank and for every G.
+
+    ops: .device; .rollout(it, mu, sigma, n_offset, n_local, costs_out[E, n_local]);
+    .all_gather(out_flat[G*E*n_local], local[E, n_local]); .select(costs[E, N], K, returns_out) -> elites;
+    .refit(it, mu, sigma, elites, mu_out, sigma_out); .trajectory(actions[H, a]) -> states[H, s].
+    The fused path binds them to the HIP extension + RCCL; tests bind them to the CPU oracle + gloo."""
+    N, K, H, I, E, a = st["N"], st["K"], st["H"], st["I"], st["E"], st["a"]
     if N % world:
         raise ValueError(f"num_candidates {N} must divide evenly over {world} ranks")
     Nl = N // world
+    dev = ops.device
     mu = torch.zeros((H, a), dtype=torch.float32, device=dev)
     sigma = torch.full((H, a), st["init_std"], dtype=torch.float32, device=dev)
     mu_n, sigma_n = torch.empty_like(mu), torch.empty_like(sigma)
     local = torch.empty((E, Nl), dtype=torch.float32, device=dev)
-    acts = torch.empty((H, Nl, a), dtype=torch.float32, device=dev)
-    gathered = torch.empty((world, E, Nl), dtype=torch.float32, device=dev)
+    gathered = torch.empty(world * E * Nl, dtype=torch.float32, device=dev)
     rec = st["record"]
     hist = dict(costs=[], returns=[], elites=[])
     events = st["events"]
     for it in range(I):
-        sp = fused.make_sampler(st["seed"], it, mu, sigma, st["lo"], st["hi"])
         if events is not None:
             events[it][0].record()
-        fused.rollout(prob, s0, Nl, H, sampler=sp, n_offset=rank * Nl, costs=local, actions_out=acts)
+        ops.rollout(it, mu, sigma, rank * Nl, Nl, local)
         if events is not None:
             events[it][1].record()
-        dist.all_gather_into_tensor(gathered, local)
-        costs = gathered.permute(1, 0, 2).reshape(E, N) if E > 1 else gathered.reshape(1, N)
+        ops.all_gather(gathered, local)
+        # candidate r*Nl + j lives at gathered[r, :, j]
+        costs = gathered.view(world, E, Nl).permute(1, 0, 2).reshape(E, N) if world > 1 else gathered.view(E, N)
         rets = torch.empty(N, dtype=torch.float32, device=dev) if rec else None
-        elites = fused.select(costs, K, returns_out=rets,
-                              workspace=_workspace(("sel", str(dev)), _lib.load().mbrl_select_workspace_bytes(N), dev))
-        fused.refit(sp, H, a, elites, st["alpha"], mu_n, sigma_n,
-                    workspace=_workspace(("refit", str(dev)), _lib.load().mbrl_refit_workspace_bytes(H, a, K), dev))
+        elites = ops.select(costs, K, rets)
+        ops.refit(it, mu, sigma, elites, mu_n, sigma_n)
         mu, mu_n = mu_n, mu
         sigma, sigma_n = sigma_n, sigma
         if rec:
@@ -274,13 +277,55 @@ def _cem_fused_sharded(prob, s0, st, world):
             hist["returns"].append(rets)
             hist["elites"].append(elites)
     actions = mu.clamp(st["lo"], st["hi"]).contiguous()
-    states_e = torch.empty((E, H, 1, s), dtype=torch.float32, device=dev)
-    fused.rollout(prob, s0, 1, H, actions=actions.view(H, 1, a), states_out=states_e)
-    states = states_e[:, :, 0, :].mean(0) if E > 1 else states_e[0, :, 0, :]
+    states = ops.trajectory(actions)
     out = dict(states=states, actions=actions, mu=mu, sigma=sigma)
     if rec:
         out.update({k: torch.stack(v) for k, v in hist.items()})
     return out
+
+
+class _FusedShardOps:
+    """cem_sharded_protocol bound to the HIP extension (C ABI) and torch.distributed (RCCL)."""
+
+    def __init__(self, prob, s0, st):
+        self.prob, self.s0, self.st, self.device = prob, s0, st, prob.device
+        H, a, N, K = st["H"], prob.mdesc["a"], st["N"], st["K"]
+        lib = _lib.load()
+        self._acts = None
+        self._sel_ws = _workspace(("sel", str(self.device)), lib.mbrl_select_workspace_bytes(N), self.device)
+        self._refit_ws = _workspace(("refit", str(self.device)), lib.mbrl_refit_workspace_bytes(H, a, K), self.device)
+        self._traj_ws = _workspace(("traj", str(self.device)),
+                                   lib.mbrl_trajectory_workspace_bytes(fused.ctypes_ref(prob.shape), H), self.device)
+
+    def _sampler(self, it, mu, sigma):
+        return fused.make_sampler(self.st["seed"], it, mu, sigma, self.st["lo"], self.st["hi"])
+
+    def rollout(self, it, mu, sigma, n_offset, n_local, costs_out):
+        H, a = self.st["H"], self.prob.mdesc["a"]
+        if self._acts is None or self._acts.shape[1] != n_local:
+            self._acts = torch.empty((H, n_local, a), dtype=torch.float32, device=self.device)
+        fused.rollout(self.prob, self.s0, n_local, H, sampler=self._sampler(it, mu, sigma), n_offset=n_offset,
+                      costs=costs_out, actions_out=self._acts)
+
+    def all_gather(self, out_flat, local):
+        import torch.distributed as dist
+        dist.all_gather_into_tensor(out_flat, local.reshape(-1))
+
+    def select(self, costs, K, returns_out):
+        return fused.select(costs, K, returns_out=returns_out, workspace=self._sel_ws)
+
+    def refit(self, it, mu, sigma, elites, mu_out, sigma_out):
+        fused.refit(self._sampler(it, mu, sigma), self.st["H"], self.prob.mdesc["a"], elites, self.st["alpha"],
+                    mu_out, sigma_out, workspace=self._refit_ws)
+
+    def trajectory(self, actions):
+        return fused.trajectory(self.prob, self.s0, actions, self.st["H"], workspace=self._traj_ws)
+
+
+def _cem_fused_sharded(prob, s0, st, world):
+    import torch.distributed as dist
+    st = dict(st, E=prob.mdesc["E"], a=prob.mdesc["a"])
+    return cem_sharded_protocol(_FusedShardOps(prob, s0, st), st, world, dist.get_rank())
 
 
 def _cem_generic(model, cost, s0, st, a, dev):

@@ -274,3 +274,58 @@ def test_full_size_plan_sampled_candidates(cid):
         mu, sg = ocem.refit(mu, sg, np.ascontiguousarray(Ael.transpose(1, 0, 2)), 0.1)
     assert np.array_equal(res["mu"].cpu().numpy(), mu)
     assert np.array_equal(res["sigma"].cpu().numpy(), sg)
+
+
+# ------------------------------------------------------------------------------------------------ trajectory / sharding
+@pytest.mark.parametrize("cid,H", [(2, 20), (3, 30), (4, 7), (5, 50)])
+def test_trajectory_states_match_oracle(cid, H):
+    """mbrl_trajectory (cooperative kernel) vs the oracle's N=1 rollout, per member and member mean."""
+    from mbrl_amd import fused
+    p = ocem.synth_problem(cid, N=1, H=H)
+    a, s, E = p["cfg"]["a"], p["cfg"]["s"], p["cfg"]["E"]
+    acts = np.random.default_rng(cid).uniform(-1, 1, size=(H, a)).astype(np.float32)
+    prob = device_problem(p)
+    members = torch.empty((E, H, s), dtype=torch.float32, device=DEV)
+    st = fused.trajectory(prob, torch.from_numpy(p["s0"]).to(DEV), torch.from_numpy(acts).to(DEV), H,
+                          member_states=members)
+    torch.cuda.synchronize()
+    _, ref = ocem.rollout(p["model"], p["norm"], p["cost"], p["s0"], acts[:, None, :], store_states=True)
+    assert np.allclose(members.cpu().numpy(), ref[:, :, 0, :], rtol=1e-4, atol=1e-4)
+    assert np.allclose(st.cpu().numpy(), np.mean(ref[:, :, 0, :], axis=0, dtype=np.float32), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("cid,N,H,world", [(3, 2048, 10, 2), (5, 512, 6, 4)])
+def test_sharded_protocol_with_fused_ops_matches_single_gpu_plan(cid, N, H, world):
+    """The multi-GPU protocol with its math on the HIP extension: every rank's shard computed here on
+    one GPU (the all-gather stitches the shards' rollouts), against the single-call mbrl_cem_plan.
+    Elites, mu and sigma must be bit-identical (no floating-point reduction crosses ranks)."""
+    from mbrl_amd import CEMPlanner, fused, planners
+    p = ocem.synth_problem(cid, N=N, H=H)
+    _, model_fn, cost_fn, sample_action = build(p)
+    I, K = 3, N // 10
+    single = CEMPlanner.plan_detailed(torch.from_numpy(p["s0"]), model_fn, cost_fn, sample_action, H,
+                                      num_candidates=N, num_elites=K, num_iterations=I, seed=p["rng_seed"],
+                                      record=True, return_device=True)
+    prob = device_problem(p)
+    s0 = torch.from_numpy(p["s0"]).to(DEV)
+    st = dict(N=N, K=K, H=H, I=I, E=p["cfg"]["E"], a=p["cfg"]["a"], alpha=0.1, lo=-1.0, hi=1.0, init_std=0.5,
+              seed=p["rng_seed"], record=True, events=None)
+
+    class AllShardsOps(planners._FusedShardOps):
+        def rollout(self, it, mu, sigma, n_offset, n_local, costs_out):
+            self._it_args = (it, mu, sigma)
+            super().rollout(it, mu, sigma, n_offset, n_local, costs_out)
+
+        def all_gather(self, out_flat, local):
+            it, mu, sigma = self._it_args
+            E, Nl = local.shape
+            view = out_flat.view(world, E, Nl)
+            for r in range(world):
+                super().rollout(it, mu, sigma, r * Nl, Nl, view[r])
+
+    res = planners.cem_sharded_protocol(AllShardsOps(prob, s0, st), st, world, 0)
+    assert torch.equal(res["elites"], single["elites"])
+    assert torch.equal(res["returns"], single["returns"])
+    assert torch.equal(res["mu"], single["mu"]) and torch.equal(res["sigma"], single["sigma"])
+    assert torch.allclose(res["states"], single["states"], rtol=1e-5, atol=1e-5)
+    assert fused is not None

@@ -1,0 +1,101 @@
+"""CPU, world_size 2 (gloo): the sharded CEM protocol (planners.cem_sharded_protocol).
+
+The protocol -- candidate ranges per rank, proposals keyed by the global index, the all-gather
+layout, replicated select + refit -- runs here with its math bound to the CPU oracle (the checker)
+and its collective to gloo. The fused path binds the same protocol to the HIP extension and RCCL.
+Bar: elites of every iteration and the final mu, sigma and actions bit-identical to a
+single-process oracle CEM plan, on every rank."""
+import os
+import sys
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+class OracleShardOps:
+    device = torch.device("cpu")
+
+    def __init__(self, p, st):
+        from oracle import cem as ocem
+        from oracle.philox import cem_actions
+        self.ocem, self.cem_actions, self.p, self.st = ocem, cem_actions, p, st
+
+    def _draw(self, it, mu, sigma, idx):
+        st = self.st
+        return self.cem_actions(mu.numpy(), sigma.numpy(), st["lo"], st["hi"], st["seed"], it, idx)
+
+    def rollout(self, it, mu, sigma, n_offset, n_local, costs_out):
+        A = self._draw(it, mu, sigma, np.arange(n_offset, n_offset + n_local))
+        p = self.p
+        costs_out.copy_(torch.from_numpy(self.ocem.rollout(p["model"], p["norm"], p["cost"], p["s0"], A)))
+
+    def all_gather(self, out_flat, local):
+        dist.all_gather_into_tensor(out_flat, local.reshape(-1).contiguous())
+
+    def select(self, costs, K, returns_out):
+        r = self.ocem.ensemble_returns(costs.numpy())
+        if returns_out is not None:
+            returns_out.copy_(torch.from_numpy(r))
+        return torch.from_numpy(self.ocem.select_elites(r, K))
+
+    def refit(self, it, mu, sigma, elites, mu_out, sigma_out):
+        A = self._draw(it, mu, sigma, elites.numpy())           # regenerated, [H, K, a]
+        m, s = self.ocem.refit(mu.numpy(), sigma.numpy(), np.ascontiguousarray(A.transpose(1, 0, 2)),
+                               self.st["alpha"])
+        mu_out.copy_(torch.from_numpy(m))
+        sigma_out.copy_(torch.from_numpy(s))
+
+    def trajectory(self, actions):
+        p = self.p
+        _, states = self.ocem.rollout(p["model"], p["norm"], p["cost"], p["s0"], actions.numpy()[:, None, :],
+                                      store_states=True)
+        return torch.from_numpy(np.mean(states[:, :, 0, :], axis=0, dtype=np.float32))
+
+
+def _settings(p, N, H, K, I):
+    from oracle import cem as ocem
+    cfg = p["cfg"]
+    return dict(N=N, K=K, H=H, I=I, E=cfg["E"], a=cfg["a"], alpha=ocem.CEM_DEFAULTS["alpha"], lo=-1.0, hi=1.0,
+                init_std=0.5, seed=p["rng_seed"], record=True, events=None)
+
+
+def _worker(rank, world, init_file, case, out_dir):
+    sys.path[:0] = [REPO, os.path.join(REPO, "mujoco-mbrl_amd")]
+    torch.set_num_threads(1)
+    from mbrl_amd.planners import cem_sharded_protocol
+    from oracle import cem as ocem
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    try:
+        cid, N, H, K, I = case
+        p = ocem.synth_problem(cid, N=N, H=H)
+        st = _settings(p, N, H, K, I)
+        res = cem_sharded_protocol(OracleShardOps(p, st), st, world, rank)
+        np.savez(os.path.join(out_dir, f"r{rank}.npz"), **{k: v.numpy() for k, v in res.items()})
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case", [(3, 64, 4, 6, 3), (5, 32, 3, 4, 2)])   # (config, N, H, K, I); config 5: E=5
+def test_sharded_protocol_bit_identical_to_single_process(case):
+    from oracle import cem as ocem
+    cid, N, H, K, I = case
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_worker, args=(world, os.path.join(d, "pg"), case, d), nprocs=world, join=True,
+                           start_method="spawn")
+        got = [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
+    ref = ocem.cem_plan(ocem.synth_problem(cid, N=N, H=H), N=N, H=H, K=K, num_iterations=I)
+    for g in got:
+        assert np.array_equal(g["elites"], np.stack(ref["elites"]))
+        # the oracle's own matmul rounding depends on its batch size (BLAS blocking): costs and
+        # states to 1e-5; the GPU rollout is per-candidate and has no such dependence
+        assert np.allclose(g["costs"], np.stack(ref["costs"]), rtol=1e-5, atol=0)
+        assert np.array_equal(g["mu"], ref["mu"][-1]) and np.array_equal(g["sigma"], ref["sigma"][-1])
+        assert np.array_equal(g["actions"], ref["final_actions"])
+        assert np.allclose(g["states"], ref["final_states"], rtol=1e-5, atol=1e-5)
