@@ -187,10 +187,33 @@ __device__ __forceinline__ void fetch_actions(const RolloutArgs& A, int tile, in
     }
 }
 
+// Per-lane copies of the step-invariant epilogue operands (this lane's feature slots d = (l&15) +
+// 16k), loaded once so the per-step epilogue issues no LDS parameter reads.
+template <int SS>
+struct EpiParams {
+    float om[SS], os[SS], goal[SS], cw[SS], bo[SS];   // state slots
+    float am[MAX_A_PER_LANE], as[MAX_A_PER_LANE];    // action slots
+};
+
+template <int SS>
+__device__ __forceinline__ void load_epi_params(const RolloutArgs& A, const LdsMap& L, int lane, EpiParams<SS>& P) {
+    const float* bout = L.hbias + A.L * A.Wpad;
+#pragma unroll
+    for (int k = 0; k < SS; ++k) {
+        const int d = min((lane & 15) + 16 * k, A.s - 1);
+        P.om[k] = L.obs_mean[d]; P.os[k] = L.obs_std[d]; P.goal[k] = L.goal[d]; P.cw[k] = L.cw[d]; P.bo[k] = bout[d];
+    }
+#pragma unroll
+    for (int k = 0; k < MAX_A_PER_LANE; ++k) {
+        const int d = min((lane & 15) + 16 * k, A.a - 1);
+        P.am[k] = L.act_mean[d]; P.as[k] = L.act_std[d];
+    }
+}
+
 // a_t -> normalised MLP input columns [s, s+a); returns this lane's share of sum_d (cosh(a_d/alpha)-1).
-template <int R>
-__device__ __forceinline__ void stage_actions(const RolloutArgs& A, const LdsMap& L, float* act, int wave, int lane,
-                                              const float (&av)[R][MAX_A_PER_LANE], float (&acp)[R]) {
+template <int R, int SS>
+__device__ __forceinline__ void stage_actions(const RolloutArgs& A, const EpiParams<SS>& P, float* act, int wave,
+                                              int lane, const float (&av)[R][MAX_A_PER_LANE], float (&acp)[R]) {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int m = epi_row(r, wave, lane);
@@ -200,7 +223,7 @@ __device__ __forceinline__ void stage_actions(const RolloutArgs& A, const LdsMap
             const int d = (lane & 15) + 16 * k;
             if (d < A.a) {
                 const float x = av[r][k];
-                act[m * A.lda + A.s + d] = A.norm_a ? (x - L.act_mean[d]) / L.act_std[d] : x;
+                act[m * A.lda + A.s + d] = A.norm_a ? (x - P.am[k]) / P.as[k] : x;
                 if (A.has_ac) c += coshf(x / A.alpha_a) - 1.0f;
             }
         }
@@ -216,6 +239,7 @@ __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
     constexpr int M = 16 * R;
     constexpr bool RING = K0C_T > 0;
     constexpr int NB = RING ? 4 : 2;
+    constexpr int SS = RING ? NOT_T : 1;    // register state slots per lane (ceil(s / 16) <= NOT); generic: LDS
     static_assert(!RING || ((K0C_T + NOT_T) % NB == 0 && K0C_T % 2 == 0 && NOT_T % 2 == 0), "ring layout");
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const LdsMap L = lds_map(A, smem, M);
@@ -252,7 +276,9 @@ __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
         const int m = i / A.k0pad_extra, j = i - (i / A.k0pad_extra) * A.k0pad_extra;
         actX[m * A.lda + A.s + A.a + j] = 0.f;
     }
-    stage_actions<R>(A, L, actX, wave, lane, av, acp);
+    EpiParams<SS> P;
+    load_epi_params<SS>(A, L, lane, P);
+    stage_actions<R, SS>(A, P, actX, wave, lane, av, acp);
     __syncthreads();
 
     // ---- weight stream: this wave's slice of chunk g is at wb + g * cs (f32x4 units)
@@ -369,24 +395,32 @@ __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
                 const int m = epi_row(r, wave, lane);
                 const int n = tile * M + m;
                 float sc = 0.f;
-                for (int d = j; d < A.s; d += 16) {
+                auto slot = [&](int d, float om, float os, float goal, float cw, float bo) {
                     const int ro = m * A.pw + d;
-                    const float o = L.part[ro] + L.part[ws + ro] + L.part[2 * ws + ro] + L.part[3 * ws + ro] + bout[d];
-                    const float sn = A.unnorm_s ? o * L.obs_std[d] + L.obs_mean[d] : o;
+                    const float o = L.part[ro] + L.part[ws + ro] + L.part[2 * ws + ro] + L.part[3 * ws + ro] + bo;
+                    const float sn = A.unnorm_s ? o * os + om : o;
                     if (A.has_sc) {
-                        const float x = (sn - L.goal[d]) * L.cw[d];
+                        const float x = (sn - goal) * cw;
                         sc += sqrtf(x * x + A.alpha_s2) - A.alpha_s;
                     }
-                    actX[m * A.lda + d] = A.norm_s ? (sn - L.obs_mean[d]) / L.obs_std[d] : sn;
+                    actX[m * A.lda + d] = A.norm_s ? (sn - om) / os : sn;
                     if (A.states_out != nullptr && n < A.N)
                         A.states_out[(((size_t)e * A.H + t) * A.N + n) * A.s + d] = sn;
+                };
+                if constexpr (RING) {
+#pragma unroll
+                    for (int k = 0; k < SS; ++k)
+                        if (j + 16 * k < A.s) slot(j + 16 * k, P.om[k], P.os[k], P.goal[k], P.cw[k], P.bo[k]);
+                } else {
+                    for (int d = j; d < A.s; d += 16)
+                        slot(d, L.obs_mean[d], L.obs_std[d], L.goal[d], L.cw[d], bout[d]);
                 }
                 for (int d = A.s + A.a + j; d < A.s + A.a + A.k0pad_extra; d += 16) actX[m * A.lda + d] = 0.f;
                 sc = rowsum16(sc);
                 const float ac = rowsum16(acp[r]);
                 total[r] += sc + A.alpha_a2 * (ac / (float)A.a);
             }
-            if (t + 1 < A.H) stage_actions<R>(A, L, actX, wave, lane, av, acp);
+            if (t + 1 < A.H) stage_actions<R, SS>(A, P, actX, wave, lane, av, acp);
         }
         __syncthreads();
         STAMP(6);
