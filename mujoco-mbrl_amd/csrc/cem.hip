@@ -324,6 +324,81 @@ __global__ void refit_kernel(const float* __restrict__ aelite, int a, int K, flo
     }
 }
 
+// Fused gather + refit for one timestep per workgroup: the K elites' a_t are regenerated from the
+// counter RNG straight into LDS ([K][a], when it fits), then the canonical chunked sums run out of
+// LDS. Same operation order as gather_elites_kernel + refit_kernel (bit-identical). With `final`
+// set it also writes the plan outputs: mu / sigma copies and actions = clip(mu', lo, hi).
+constexpr int REFIT_THREADS = 256;
+constexpr size_t REFIT_LDS_MAX = 96 * 1024;
+
+__global__ void __launch_bounds__(REFIT_THREADS) refit_fused_kernel(
+    uint64_t seed, int iteration, const float* __restrict__ mu, const float* __restrict__ sigma, float lo, float hi,
+    int a, const int64_t* __restrict__ elite_idx, int K, float alpha, float oma, float* __restrict__ mu_out,
+    float* __restrict__ sigma_out, float* __restrict__ fin_mu, float* __restrict__ fin_sigma,
+    float* __restrict__ fin_actions) {
+#pragma clang fp contract(off)
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int t = blockIdx.x;
+    const int G = (a + 3) >> 2;
+    const int nch = (K + ELITE_CHUNK - 1) / ELITE_CHUNK;
+    float* ael = smem;                                   // [K][a]
+    float* part = smem + (((size_t)K * a + 3) & ~(size_t)3);   // [nch][a]
+    float* mean = part + (((size_t)nch * a + 3) & ~(size_t)3);  // [a]
+    for (int idx = threadIdx.x; idx < K * G; idx += REFIT_THREADS) {
+        const int e = idx / G, g = idx - (idx / G) * G;
+        float z[4];
+        cem_normal4(seed, (uint32_t)elite_idx[e], (uint32_t)t, (uint32_t)iteration, (uint32_t)g, z);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int d = 4 * g + j;
+            if (d < a) ael[(size_t)e * a + d] = cem_action(mu[t * a + d], sigma[t * a + d], z[j], lo, hi);
+        }
+    }
+    __syncthreads();
+    for (int pass = 0; pass < 2; ++pass) {
+        for (int idx = threadIdx.x; idx < nch * a; idx += REFIT_THREADS) {
+            const int c = idx / a, d = idx - (idx / a) * a;
+            const int e0 = c * ELITE_CHUNK, e1 = min(K, e0 + ELITE_CHUNK);
+            const float md = pass == 1 ? mean[d] : 0.f;
+            float acc = 0.f;
+            for (int e = e0; e < e1; ++e) {
+                float v = ael[(size_t)e * a + d];
+                if (pass == 1) { const float df = __fadd_rn(v, -md); v = __fmul_rn(df, df); }
+                acc = (e == e0) ? v : __fadd_rn(acc, v);
+            }
+            part[c * a + d] = acc;
+        }
+        __syncthreads();
+        if ((int)threadIdx.x < a) {
+            const int d = threadIdx.x;
+            float tot = part[d];
+            for (int c = 1; c < nch; ++c) tot = __fadd_rn(tot, part[c * a + d]);
+            const float m = __fdiv_rn(tot, (float)K);
+            if (pass == 0) {
+                mean[d] = m;
+            } else {
+                const float mu0 = mu[t * a + d], s0 = sigma[t * a + d];
+                const float mn = __fadd_rn(__fmul_rn(alpha, mu0), __fmul_rn(oma, mean[d]));
+                const float v = __fadd_rn(__fmul_rn(alpha, __fmul_rn(s0, s0)), __fmul_rn(oma, m));
+                const float sn = exact_sqrt(v);
+                mu_out[t * a + d] = mn;
+                sigma_out[t * a + d] = sn;
+                if (fin_actions) {
+                    if (fin_mu) fin_mu[t * a + d] = mn;
+                    if (fin_sigma) fin_sigma[t * a + d] = sn;
+                    fin_actions[t * a + d] = fminf(fmaxf(mn, lo), hi);
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+static size_t refit_fused_lds(int a, int K) {
+    const size_t nch = (size_t)(K + ELITE_CHUNK - 1) / ELITE_CHUNK;
+    return ((((size_t)K * a + 3) & ~(size_t)3) + ((nch * a + 3) & ~(size_t)3) + ((size_t)a + 3)) * sizeof(float);
+}
+
 __global__ void sample_kernel(uint64_t seed, int iteration, const float* __restrict__ mu,
                               const float* __restrict__ sigma, float lo, float hi, int H, int a, int N,
                               int n_offset, float* __restrict__ out) {
@@ -488,19 +563,39 @@ static int select_impl(const float* costs, int E, int N, int K, int nan_policy, 
 }
 
 static int refit_impl(const mbrl_sampler* sp, int H, int a, const int64_t* elite_idx, int K, float alpha,
-                      float* aelite, float* mu_out, float* sigma_out, hipStream_t stream) {
-    if (!sp || !sp->mu || !sp->sigma || !elite_idx || !mu_out || !sigma_out || !aelite)
+                      float* aelite, float* mu_out, float* sigma_out, hipStream_t stream, float* fin_mu = nullptr,
+                      float* fin_sigma = nullptr, float* fin_actions = nullptr) {
+    if (!sp || !sp->mu || !sp->sigma || !elite_idx || !mu_out || !sigma_out)
         return fail(MBRL_EINVAL, "refit: NULL argument");
     if (H < 1 || a < 1 || a > 64 || K < 1) return fail(MBRL_EINVAL, "refit: H=%d a=%d K=%d", H, a, K);
+    const float oma = 1.0f - alpha;
+    const size_t lds = refit_fused_lds(a, K);
+    if (lds <= REFIT_LDS_MAX) {
+        static bool attr_set = false;
+        if (!attr_set) {
+            hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(&refit_fused_kernel),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)REFIT_LDS_MAX);
+            if (err != hipSuccess) return hip_check(err, "refit attribute");
+            attr_set = true;
+        }
+        hipLaunchKernelGGL(refit_fused_kernel, dim3(H), dim3(REFIT_THREADS), lds, stream, sp->seed, sp->iteration,
+                           sp->mu, sp->sigma, sp->lo, sp->hi, a, elite_idx, K, alpha, oma, mu_out, sigma_out, fin_mu,
+                           fin_sigma, fin_actions);
+        return hip_check(hipGetLastError(), "refit launch");
+    }
+    // large K x a: elite actions staged through HBM
+    if (!aelite) return fail(MBRL_EINVAL, "refit: NULL workspace");
     if ((size_t)((K + ELITE_CHUNK - 1) / ELITE_CHUNK) * a * sizeof(float) > 64 * 1024)
         return fail(MBRL_EUNSUPPORTED, "refit: K=%d x a=%d exceeds the refit kernel's LDS", K, a);
     const int G = (a + 3) / 4;
     hipLaunchKernelGGL(gather_elites_kernel, dim3((K * G + 255) / 256, H), dim3(256), 0, stream, sp->seed,
                        sp->iteration, sp->mu, sp->sigma, sp->lo, sp->hi, a, elite_idx, K, aelite);
     const int nch = (K + ELITE_CHUNK - 1) / ELITE_CHUNK;
-    const float oma = 1.0f - alpha;
     hipLaunchKernelGGL(refit_kernel, dim3(H), dim3(256), (size_t)nch * a * sizeof(float), stream, aelite, a, K,
                        alpha, oma, sp->mu, sp->sigma, mu_out, sigma_out);
+    if (fin_actions)
+        hipLaunchKernelGGL(finalize_kernel, dim3((H * a + 255) / 256), dim3(256), 0, stream, mu_out, sigma_out,
+                           sp->lo, sp->hi, H * a, fin_mu, fin_sigma, fin_actions);
     return hip_check(hipGetLastError(), "refit launch");
 }
 
@@ -637,11 +732,14 @@ int mbrl_trajectory(const mbrl_mlp_shape* shape, const void* packed, const mbrl_
     if (!packed || !s0 || !actions || !states_out || !workspace) return fail(MBRL_EINVAL, "trajectory: NULL argument");
     TrajWs w = traj_ws(g, H, workspace);
     if (ws_bytes < w.bytes) return fail(MBRL_EWORKSPACE, "trajectory workspace %zu < %zu", ws_bytes, w.bytes);
-    float* per_member = member_states_out ? member_states_out : w.states;
+    float* per_member = member_states_out ? member_states_out : (g.E == 1 ? states_out : w.states);
     rc = traj_impl(g, packed, norm, s0, actions, H, per_member, w.xchg, w.xchg_bytes, w.status, stream);
     if (rc) return rc;
-    const int Hs = H * g.s;
-    hipLaunchKernelGGL(member_mean_kernel, dim3((Hs + 255) / 256), dim3(256), 0, stream, per_member, g.E, Hs, states_out);
+    if (per_member != states_out) {
+        const int Hs = H * g.s;
+        hipLaunchKernelGGL(member_mean_kernel, dim3((Hs + 255) / 256), dim3(256), 0, stream, per_member, g.E, Hs,
+                           states_out);
+    }
     return hip_check(hipGetLastError(), "trajectory launch");
 }
 
@@ -720,17 +818,21 @@ int mbrl_cem_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_no
         }
         rc = select_impl(costs, g.E, p->N, p->K, MBRL_NAN_LAST, elites, rets, w.keys, align256((size_t)p->N * 4), stream);
         if (rc) return rc;
-        rc = refit_impl(&sp, p->H, g.a, elites, p->K, p->alpha, w.aelite, w.mu[cur ^ 1], w.sigma[cur ^ 1], stream);
+        const bool last = it + 1 == p->iterations;   // the last refit also writes mu / sigma / clip(mu)
+        rc = refit_impl(&sp, p->H, g.a, elites, p->K, p->alpha, w.aelite, w.mu[cur ^ 1], w.sigma[cur ^ 1], stream,
+                        last ? mu : nullptr, last ? sigma : nullptr, last ? actions_out : nullptr);
         if (rc) return rc;
         cur ^= 1;
     }
-    hipLaunchKernelGGL(finalize_kernel, dim3((Ha + 255) / 256), dim3(256), 0, stream, w.mu[cur], w.sigma[cur], p->lo,
-                       p->hi, Ha, mu, sigma, actions_out);
-    // final mean's rollout -> predicted states [E][H][s], then the member mean
-    rc = traj_impl(g, packed, norm, s0, actions_out, p->H, w.states, w.xchg, w.xchg_bytes, w.status, stream);
+    // final mean's rollout -> predicted states [E][H][s] (E == 1: straight into states_out), member mean
+    float* per_member = g.E == 1 ? states_out : w.states;
+    rc = traj_impl(g, packed, norm, s0, actions_out, p->H, per_member, w.xchg, w.xchg_bytes, w.status, stream);
     if (rc) return rc;
-    const int Hs = p->H * g.s;
-    hipLaunchKernelGGL(member_mean_kernel, dim3((Hs + 255) / 256), dim3(256), 0, stream, w.states, g.E, Hs, states_out);
+    if (g.E > 1) {
+        const int Hs = p->H * g.s;
+        hipLaunchKernelGGL(member_mean_kernel, dim3((Hs + 255) / 256), dim3(256), 0, stream, w.states, g.E, Hs,
+                           states_out);
+    }
     return hip_check(hipGetLastError(), "plan launch");
 }
 
