@@ -197,7 +197,7 @@ template <int KPT>
 __global__ void __launch_bounds__(1024) select_reg_kernel(const float* __restrict__ costs, int E, int N, int K,
                                                           int nan_policy, int64_t* __restrict__ elite_idx,
                                                           float* __restrict__ returns_out) {
-    __shared__ uint32_t hist[16][256];
+    __shared__ uint32_t hist[2][16][256];
     __shared__ uint32_t scan_ws[16];
     __shared__ uint32_t sel[2];
     const int tid = threadIdx.x, wave = tid >> 6;
@@ -217,26 +217,40 @@ __global__ void __launch_bounds__(1024) select_reg_kernel(const float* __restric
             key[k] = order_key(r, nan_policy);
         }
     }
+    // 4 radix passes over 8-bit digits; the histogram buffer of pass p+1 is cleared during pass p,
+    // and the bucket search is a 256-entry scan by waves 0-3 only: 3 barriers per pass
     uint32_t prefix = 0, mask = 0, kk = (uint32_t)K;
-    for (int shift = 24; shift >= 0; shift -= 8) {
-        for (int i = tid; i < 16 * 256; i += 1024) (&hist[0][0])[i] = 0;
-        __syncthreads();
+    for (int i = tid; i < 16 * 256; i += 1024) (&hist[0][0][0])[i] = 0;
+    __syncthreads();
+    int buf = 0;
+    for (int shift = 24; shift >= 0; shift -= 8, buf ^= 1) {
 #pragma unroll
         for (int k = 0; k < KPT; ++k)
-            if (n0 + k < N && (key[k] & mask) == prefix) atomicAdd(&hist[wave][(key[k] >> shift) & 255u], 1u);
+            if (n0 + k < N && (key[k] & mask) == prefix) atomicAdd(&hist[buf][wave][(key[k] >> shift) & 255u], 1u);
+        for (int i = tid; i < 16 * 256; i += 1024) (&hist[buf ^ 1][0][0])[i] = 0;
         __syncthreads();
-        uint32_t h = 0;
-        if (tid < 256)
+        uint32_t h = 0, incl = 0;
+        if (tid < 256) {
 #pragma unroll
-            for (int w = 0; w < 16; ++w) h += hist[w][tid];
-        uint32_t tot;
-        const uint32_t before = block_exclusive_scan(h, scan_ws, &tot);
-        if (tid < 256 && before < kk && before + h >= kk) { sel[0] = (uint32_t)tid; sel[1] = before; }
+            for (int w = 0; w < 16; ++w) h += hist[buf][w][tid];
+            incl = h;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o, 64);
+                if ((tid & 63) >= o) incl += y;
+            }
+            if ((tid & 63) == 63) scan_ws[wave] = incl;
+        }
+        __syncthreads();
+        if (tid < 256) {
+            uint32_t before = incl - h;
+            for (int w = 0; w < wave; ++w) before += scan_ws[w];
+            if (before < kk && before + h >= kk) { sel[0] = (uint32_t)tid; sel[1] = before; }
+        }
         __syncthreads();
         prefix |= sel[0] << shift;
         mask |= 0xFFu << shift;
         kk -= sel[1];
-        __syncthreads();
     }
     uint32_t eq = 0;
 #pragma unroll
@@ -344,27 +358,42 @@ __global__ void __launch_bounds__(REFIT_THREADS) refit_fused_kernel(
     float* ael = smem;                                   // [K][a]
     float* part = smem + (((size_t)K * a + 3) & ~(size_t)3);   // [nch][a]
     float* mean = part + (((size_t)nch * a + 3) & ~(size_t)3);  // [a]
+    float* musg = mean + ((a + 3) & ~3);                         // [2][a]: this step's mu, sigma
+    uint32_t* eidx = reinterpret_cast<uint32_t*>(musg + 2 * ((a + 3) & ~3));  // [K]
+    // stage every global operand first (all loads in flight together), then compute from LDS
+    for (int e = threadIdx.x; e < K; e += REFIT_THREADS) eidx[e] = (uint32_t)elite_idx[e];
+    for (int d = threadIdx.x; d < a; d += REFIT_THREADS) {
+        musg[d] = mu[t * a + d];
+        musg[((a + 3) & ~3) + d] = sigma[t * a + d];
+    }
+    __syncthreads();
+    const float* smu = musg;
+    const float* ssg = musg + ((a + 3) & ~3);
     for (int idx = threadIdx.x; idx < K * G; idx += REFIT_THREADS) {
         const int e = idx / G, g = idx - (idx / G) * G;
         float z[4];
-        cem_normal4(seed, (uint32_t)elite_idx[e], (uint32_t)t, (uint32_t)iteration, (uint32_t)g, z);
+        cem_normal4(seed, eidx[e], (uint32_t)t, (uint32_t)iteration, (uint32_t)g, z);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int d = 4 * g + j;
-            if (d < a) ael[(size_t)e * a + d] = cem_action(mu[t * a + d], sigma[t * a + d], z[j], lo, hi);
+            if (d < a) ael[(size_t)e * a + d] = cem_action(smu[d], ssg[d], z[j], lo, hi);
         }
     }
     __syncthreads();
     for (int pass = 0; pass < 2; ++pass) {
         for (int idx = threadIdx.x; idx < nch * a; idx += REFIT_THREADS) {
             const int c = idx / a, d = idx - (idx / a) * a;
-            const int e0 = c * ELITE_CHUNK, e1 = min(K, e0 + ELITE_CHUNK);
+            const int e0 = c * ELITE_CHUNK, n = min(K - e0, ELITE_CHUNK);
             const float md = pass == 1 ? mean[d] : 0.f;
+            float v[ELITE_CHUNK];
+#pragma unroll
+            for (int q = 0; q < ELITE_CHUNK; ++q) v[q] = q < n ? ael[(size_t)(e0 + q) * a + d] : 0.f;
             float acc = 0.f;
-            for (int e = e0; e < e1; ++e) {
-                float v = ael[(size_t)e * a + d];
-                if (pass == 1) { const float df = __fadd_rn(v, -md); v = __fmul_rn(df, df); }
-                acc = (e == e0) ? v : __fadd_rn(acc, v);
+#pragma unroll
+            for (int q = 0; q < ELITE_CHUNK; ++q) {
+                float x = v[q];
+                if (pass == 1) { const float df = __fadd_rn(x, -md); x = __fmul_rn(df, df); }
+                if (q < n) acc = q == 0 ? x : __fadd_rn(acc, x);
             }
             part[c * a + d] = acc;
         }
@@ -377,7 +406,7 @@ __global__ void __launch_bounds__(REFIT_THREADS) refit_fused_kernel(
             if (pass == 0) {
                 mean[d] = m;
             } else {
-                const float mu0 = mu[t * a + d], s0 = sigma[t * a + d];
+                const float mu0 = smu[d], s0 = ssg[d];
                 const float mn = __fadd_rn(__fmul_rn(alpha, mu0), __fmul_rn(oma, mean[d]));
                 const float v = __fadd_rn(__fmul_rn(alpha, __fmul_rn(s0, s0)), __fmul_rn(oma, m));
                 const float sn = exact_sqrt(v);
@@ -396,7 +425,8 @@ __global__ void __launch_bounds__(REFIT_THREADS) refit_fused_kernel(
 
 static size_t refit_fused_lds(int a, int K) {
     const size_t nch = (size_t)(K + ELITE_CHUNK - 1) / ELITE_CHUNK;
-    return ((((size_t)K * a + 3) & ~(size_t)3) + ((nch * a + 3) & ~(size_t)3) + ((size_t)a + 3)) * sizeof(float);
+    const size_t a4 = ((size_t)a + 3) & ~(size_t)3;
+    return ((((size_t)K * a + 3) & ~(size_t)3) + ((nch * a + 3) & ~(size_t)3) + 3 * a4 + (size_t)K) * sizeof(float);
 }
 
 __global__ void sample_kernel(uint64_t seed, int iteration, const float* __restrict__ mu,
