@@ -197,7 +197,7 @@ template <int KPT>
 __global__ void __launch_bounds__(1024) select_reg_kernel(const float* __restrict__ costs, int E, int N, int K,
                                                           int nan_policy, int64_t* __restrict__ elite_idx,
                                                           float* __restrict__ returns_out) {
-    __shared__ uint32_t hist[2][16][256];
+    __shared__ uint32_t hist[2][16][257];
     __shared__ uint32_t scan_ws[16];
     __shared__ uint32_t sel[2];
     const int tid = threadIdx.x, wave = tid >> 6;
@@ -220,14 +220,31 @@ __global__ void __launch_bounds__(1024) select_reg_kernel(const float* __restric
     // 4 radix passes over 8-bit digits; the histogram buffer of pass p+1 is cleared during pass p,
     // and the bucket search is a 256-entry scan by waves 0-3 only: 3 barriers per pass
     uint32_t prefix = 0, mask = 0, kk = (uint32_t)K;
-    for (int i = tid; i < 16 * 256; i += 1024) (&hist[0][0][0])[i] = 0;
+    for (int i = tid; i < 16 * 257; i += 1024) (&hist[0][0][0])[i] = 0;
     __syncthreads();
     int buf = 0;
     for (int shift = 24; shift >= 0; shift -= 8, buf ^= 1) {
+        // wave-aggregated counting: returns cluster (most candidates share the leading digits), so
+        // up to 4 rounds elect the first remaining digit and add its lane count in one atomic; the
+        // rest (spread digits, no contention) add individually. Rows padded to 257: no cross-wave
+        // bank collisions on a shared digit.
 #pragma unroll
-        for (int k = 0; k < KPT; ++k)
-            if (n0 + k < N && (key[k] & mask) == prefix) atomicAdd(&hist[buf][wave][(key[k] >> shift) & 255u], 1u);
-        for (int i = tid; i < 16 * 256; i += 1024) (&hist[buf ^ 1][0][0])[i] = 0;
+        for (int k = 0; k < KPT; ++k) {
+            bool pending = n0 + k < N && (key[k] & mask) == prefix;
+            const uint32_t dig = (key[k] >> shift) & 255u;
+#pragma unroll
+            for (int round = 0; round < 4; ++round) {
+                const uint64_t act = __ballot(pending);
+                if (act == 0) break;
+                const int leader = __builtin_ctzll(act);
+                const uint32_t d0 = __shfl(dig, leader, 64);
+                const uint64_t same = __ballot(pending && dig == d0);
+                if ((int)(tid & 63) == leader) atomicAdd(&hist[buf][wave][d0], (uint32_t)__popcll(same));
+                pending = pending && dig != d0;
+            }
+            if (pending) atomicAdd(&hist[buf][wave][dig], 1u);
+        }
+        for (int i = tid; i < 16 * 257; i += 1024) (&hist[buf ^ 1][0][0])[i] = 0;
         __syncthreads();
         uint32_t h = 0, incl = 0;
         if (tid < 256) {
@@ -342,7 +359,7 @@ __global__ void refit_kernel(const float* __restrict__ aelite, int a, int K, flo
 // counter RNG straight into LDS ([K][a], when it fits), then the canonical chunked sums run out of
 // LDS. Same operation order as gather_elites_kernel + refit_kernel (bit-identical). With `final`
 // set it also writes the plan outputs: mu / sigma copies and actions = clip(mu', lo, hi).
-constexpr int REFIT_THREADS = 256;
+constexpr int REFIT_THREADS = 1024;
 constexpr size_t REFIT_LDS_MAX = 96 * 1024;
 
 __global__ void __launch_bounds__(REFIT_THREADS) refit_fused_kernel(
