@@ -123,6 +123,20 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* l
 // index -> compaction in ascending index order. One workgroup of 1024 threads (N is small:
 // 1e3..3e4 candidates; the pass is a few microseconds).
 // ------------------------------------------------------------------------------------------------
+// Diagnostic build only (-DMBRL_STAMPS): thread 0's s_memrealtime at fixed points of the select
+// kernel, written to a buffer set by mbrl_diag_set_cem_stamps() (tools/select_stamps.py).
+#ifdef MBRL_STAMPS
+__device__ unsigned long long* g_cem_stamps;
+#define CSTAMP(k)                                                                      \
+    do {                                                                               \
+        if (threadIdx.x == 0 && g_cem_stamps) g_cem_stamps[k] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define CSTAMP(k) \
+    do {          \
+    } while (0)
+#endif
+
 __device__ __forceinline__ uint32_t order_key(float v, int nan_policy) {
     if (v != v) return nan_policy == MBRL_NAN_LAST ? 0xFFFFFFFFu : 0u;
     if (v == 0.0f) v = 0.0f;  // -0.0 ties with +0.0, as in NumPy's comparisons
@@ -190,59 +204,66 @@ __global__ void __launch_bounds__(1024) select_kernel(const float* __restrict__ 
     }
 }
 
-// Register-resident variant for N <= 1024 * KPT: thread t owns candidates [t*KPT, t*KPT + KPT);
-// radix histograms are private per wave (16 x 256 counters) so clustered returns (every candidate
-// sharing the top key byte, the common case) do not serialise on one LDS counter.
+// Register-resident variant for N <= 1024 * KPT: thread t owns candidates [t*KPT, t*KPT + KPT)
+// (contiguous, so the compaction scan yields ascending indices). Returns are computed and stored
+// coalesced (candidate n by thread n % 1024) into LDS keys, then each thread takes its KPT keys from
+// LDS; the LDS key array is reused for the per-wave radix histograms afterwards.
+constexpr int SEL_HIST_WORDS = 2 * 16 * 257;
+
 template <int KPT>
 __global__ void __launch_bounds__(1024) select_reg_kernel(const float* __restrict__ costs, int E, int N, int K,
                                                           int nan_policy, int64_t* __restrict__ elite_idx,
                                                           float* __restrict__ returns_out) {
-    __shared__ uint32_t hist[2][16][257];
+    extern __shared__ __attribute__((aligned(16))) uint32_t sel_smem[];
+    uint32_t(*hist)[16][257] = reinterpret_cast<uint32_t(*)[16][257]>(sel_smem);  // [2][16][257], aliases keys
     __shared__ uint32_t scan_ws[16];
     __shared__ uint32_t sel[2];
+    CSTAMP(0);
     const int tid = threadIdx.x, wave = tid >> 6;
     const int n0 = tid * KPT;
+    for (int n = tid; n < N; n += 1024) {
+        float r = costs[n];
+        if (E > 1) {
+            for (int e = 1; e < E; ++e) r = __fadd_rn(r, costs[(size_t)e * N + n]);
+            r = __fdiv_rn(r, (float)E);
+        }
+        if (returns_out) returns_out[n] = r;
+        sel_smem[n] = order_key(r, nan_policy);
+    }
+    __syncthreads();
     uint32_t key[KPT];
 #pragma unroll
     for (int k = 0; k < KPT; ++k) {
-        const int n = n0 + k;
-        key[k] = 0xFFFFFFFFu;
-        if (n < N) {
-            float r = costs[n];
-            if (E > 1) {
-                for (int e = 1; e < E; ++e) r = __fadd_rn(r, costs[(size_t)e * N + n]);
-                r = __fdiv_rn(r, (float)E);
-            }
-            if (returns_out) returns_out[n] = r;
-            key[k] = order_key(r, nan_policy);
-        }
+        const int kr = (k + tid) & (KPT - 1);          // rotated: neighbouring threads hit different banks
+        const int n = n0 + kr;
+        key[kr] = n < N ? sel_smem[n] : 0xFFFFFFFFu;
     }
+    __syncthreads();
     // 4 radix passes over 8-bit digits; the histogram buffer of pass p+1 is cleared during pass p,
     // and the bucket search is a 256-entry scan by waves 0-3 only: 3 barriers per pass
+    CSTAMP(1);
     uint32_t prefix = 0, mask = 0, kk = (uint32_t)K;
     for (int i = tid; i < 16 * 257; i += 1024) (&hist[0][0][0])[i] = 0;
     __syncthreads();
     int buf = 0;
     for (int shift = 24; shift >= 0; shift -= 8, buf ^= 1) {
-        // wave-aggregated counting: returns cluster (most candidates share the leading digits), so
-        // up to 4 rounds elect the first remaining digit and add its lane count in one atomic; the
-        // rest (spread digits, no contention) add individually. Rows padded to 257: no cross-wave
-        // bank collisions on a shared digit.
+        // returns cluster (most candidates share the leading digits): when every pending lane of a
+        // wave has the same digit, one lane adds the count; otherwise plain per-lane atomics. Rows
+        // padded to 257: no cross-wave bank collisions on a shared digit.
 #pragma unroll
         for (int k = 0; k < KPT; ++k) {
-            bool pending = n0 + k < N && (key[k] & mask) == prefix;
+            const bool pending = n0 + k < N && (key[k] & mask) == prefix;
             const uint32_t dig = (key[k] >> shift) & 255u;
-#pragma unroll
-            for (int round = 0; round < 4; ++round) {
-                const uint64_t act = __ballot(pending);
-                if (act == 0) break;
+            const uint64_t act = __ballot(pending);
+            if (act != 0) {
                 const int leader = __builtin_ctzll(act);
                 const uint32_t d0 = __shfl(dig, leader, 64);
-                const uint64_t same = __ballot(pending && dig == d0);
-                if ((int)(tid & 63) == leader) atomicAdd(&hist[buf][wave][d0], (uint32_t)__popcll(same));
-                pending = pending && dig != d0;
+                if (__ballot(pending && dig == d0) == act) {
+                    if ((int)(tid & 63) == leader) atomicAdd(&hist[buf][wave][d0], (uint32_t)__popcll(act));
+                } else if (pending) {
+                    atomicAdd(&hist[buf][wave][dig], 1u);
+                }
             }
-            if (pending) atomicAdd(&hist[buf][wave][dig], 1u);
         }
         for (int i = tid; i < 16 * 257; i += 1024) (&hist[buf ^ 1][0][0])[i] = 0;
         __syncthreads();
@@ -268,6 +289,7 @@ __global__ void __launch_bounds__(1024) select_reg_kernel(const float* __restric
         prefix |= sel[0] << shift;
         mask |= 0xFFu << shift;
         kk -= sel[1];
+        CSTAMP(2 + (24 - shift) / 8);
     }
     uint32_t eq = 0;
 #pragma unroll
@@ -289,6 +311,7 @@ __global__ void __launch_bounds__(1024) select_reg_kernel(const float* __restric
 #pragma unroll
     for (int k = 0; k < KPT; ++k)
         if (take[k] && pos < (uint32_t)K) elite_idx[pos++] = n0 + k;
+    CSTAMP(6);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -598,7 +621,15 @@ static int select_impl(const float* costs, int E, int N, int K, int nan_policy, 
     if (ws_bytes < align256((size_t)N * 4)) return fail(MBRL_EWORKSPACE, "select workspace %zu < %zu", ws_bytes, align256((size_t)N * 4));
 #define MBRL_SEL(KPT)                                                                                       \
     if (N <= 1024 * (KPT)) {                                                                                \
-        hipLaunchKernelGGL(select_reg_kernel<KPT>, dim3(1), dim3(1024), 0, stream, costs, E, N, K, nan_policy, \
+        const size_t lds = 4 * (size_t)max(1024 * (KPT), SEL_HIST_WORDS);                                  \
+        static bool attr_set = false;                                                                       \
+        if (!attr_set) {                                                                                    \
+            hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(&select_reg_kernel<KPT>),     \
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);     \
+            if (err != hipSuccess) return hip_check(err, "select attribute");                               \
+            attr_set = true;                                                                                \
+        }                                                                                                   \
+        hipLaunchKernelGGL(select_reg_kernel<KPT>, dim3(1), dim3(1024), lds, stream, costs, E, N, K, nan_policy, \
                            elite_idx, returns_out);                                                         \
         return hip_check(hipGetLastError(), "select launch");                                               \
     }
@@ -882,5 +913,11 @@ int mbrl_cem_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_no
     }
     return hip_check(hipGetLastError(), "plan launch");
 }
+
+#ifdef MBRL_STAMPS
+int mbrl_diag_set_cem_stamps(void* buf) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(mbrl::g_cem_stamps), &buf, sizeof(buf));
+}
+#endif
 
 }  // extern "C"
