@@ -228,15 +228,14 @@ __global__ void __launch_bounds__(1024) select_reg_kernel(const float* __restric
             r = __fdiv_rn(r, (float)E);
         }
         if (returns_out) returns_out[n] = r;
-        sel_smem[n] = order_key(r, nan_policy);
+        sel_smem[n + (n >> 5)] = order_key(r, nan_policy);  // one pad word per 32: conflict-free reads below
     }
     __syncthreads();
     uint32_t key[KPT];
 #pragma unroll
     for (int k = 0; k < KPT; ++k) {
-        const int kr = (k + tid) & (KPT - 1);          // rotated: neighbouring threads hit different banks
-        const int n = n0 + kr;
-        key[kr] = n < N ? sel_smem[n] : 0xFFFFFFFFu;
+        const int n = n0 + k;
+        key[k] = n < N ? sel_smem[n + (n >> 5)] : 0xFFFFFFFFu;
     }
     __syncthreads();
     // 4 radix passes over 8-bit digits; the histogram buffer of pass p+1 is cleared during pass p,
@@ -621,7 +620,7 @@ static int select_impl(const float* costs, int E, int N, int K, int nan_policy, 
     if (ws_bytes < align256((size_t)N * 4)) return fail(MBRL_EWORKSPACE, "select workspace %zu < %zu", ws_bytes, align256((size_t)N * 4));
 #define MBRL_SEL(KPT)                                                                                       \
     if (N <= 1024 * (KPT)) {                                                                                \
-        const size_t lds = 4 * (size_t)max(1024 * (KPT), SEL_HIST_WORDS);                                  \
+        const size_t lds = 4 * (size_t)max(33 * 32 * (KPT), SEL_HIST_WORDS);                               \
         static bool attr_set = false;                                                                       \
         if (!attr_set) {                                                                                    \
             hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(&select_reg_kernel<KPT>),     \
