@@ -221,14 +221,28 @@ __global__ void __launch_bounds__(1024) select_reg_kernel(const float* __restric
     CSTAMP(0);
     const int tid = threadIdx.x, wave = tid >> 6;
     const int n0 = tid * KPT;
-    for (int n = tid; n < N; n += 1024) {
-        float r = costs[n];
-        if (E > 1) {
-            for (int e = 1; e < E; ++e) r = __fadd_rn(r, costs[(size_t)e * N + n]);
-            r = __fdiv_rn(r, (float)E);
+    {
+        float r[KPT];                                   // every load in flight before the first use
+#pragma unroll
+        for (int k = 0; k < KPT; ++k) {
+            const int n = tid + 1024 * k;
+            r[k] = n < N ? costs[n] : 0.f;
         }
-        if (returns_out) returns_out[n] = r;
-        sel_smem[n + (n >> 5)] = order_key(r, nan_policy);  // one pad word per 32: conflict-free reads below
+        for (int e = 1; e < E; ++e)
+#pragma unroll
+            for (int k = 0; k < KPT; ++k) {
+                const int n = tid + 1024 * k;
+                if (n < N) r[k] = __fadd_rn(r[k], costs[(size_t)e * N + n]);
+            }
+#pragma unroll
+        for (int k = 0; k < KPT; ++k) {
+            const int n = tid + 1024 * k;
+            if (n < N) {
+                const float v = E > 1 ? __fdiv_rn(r[k], (float)E) : r[k];
+                if (returns_out) returns_out[n] = v;
+                sel_smem[n + (n >> 5)] = order_key(v, nan_policy);  // one pad word per 32: conflict-free reads
+            }
+        }
     }
     __syncthreads();
     uint32_t key[KPT];
@@ -247,8 +261,9 @@ __global__ void __launch_bounds__(1024) select_reg_kernel(const float* __restric
     int buf = 0;
     for (int shift = 24; shift >= 0; shift -= 8, buf ^= 1) {
         // returns cluster (most candidates share the leading digits): when every pending lane of a
-        // wave has the same digit, one lane adds the count; otherwise plain per-lane atomics. Rows
-        // padded to 257: no cross-wave bank collisions on a shared digit.
+        // wave has the same digit, one lane adds the count; otherwise plain per-lane atomics (more
+        // aggregation rounds cost more VALU issue than the contention they save). Rows padded to
+        // 257: no cross-wave bank collisions on a shared digit.
 #pragma unroll
         for (int k = 0; k < KPT; ++k) {
             const bool pending = n0 + k < N && (key[k] & mask) == prefix;
