@@ -65,6 +65,7 @@ struct RolloutArgs {
     size_t member_stride;
     size_t stream_floats;
     int s, a, L, Wpad, K0C, NOT, E, chunks_per_step, lda, pw, k0pad_extra;
+    int nw;  // waves per workgroup (set by the launcher; sizes the output partials)
     int N, H, n_offset;
     const float *obs_mean, *obs_std, *act_mean, *act_std;
     int norm_s, unnorm_s, norm_a;
@@ -92,7 +93,7 @@ __host__ __device__ inline LdsMap lds_map(const RolloutArgs& A, float* base, int
     auto take = [&](size_t n) { float* p = base ? base + o : nullptr; o += lds_round4(n); return p; };
     L.act = take((size_t)M * A.lda);
     L.act2 = take((size_t)M * A.lda);
-    L.part = take((size_t)4 * M * A.pw);
+    L.part = take((size_t)(A.nw > 4 ? A.nw : 4) * M * A.pw);
     L.sterm = take((size_t)M * A.s);
     L.aterm = take((size_t)2 * M * A.a);
     L.obs_mean = take(A.s);

@@ -27,18 +27,25 @@
 
 #include "mbrl_internal.h"
 
+// Waves per workgroup for the rollout (4: one per SIMD; 8: two per SIMD, T/2 tiles each). Measured on
+// cheetah (tools/variants.sh): 8 waves gave no gain over 4, so 4 is the default.
+#ifndef MBRL_ROLLOUT_NW
+#define MBRL_ROLLOUT_NW 4
+#endif
+
 namespace mbrl {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 #define MBRL_PIN() __builtin_amdgcn_sched_barrier(0)
 
-// Spread a chunk's T weight loads (and the next A read) between its 4*T*R MFMAs: issued as one
-// burst they cost ~120 cycles of idle matrix pipe per chunk (stamps), issued in the MFMAs' shadow
-// they are free. Masks: 0x8 MFMA, 0x20 VMEM read, 0x100 DS read.
+// Optional (-DMBRL_INTERLEAVE): spread a chunk's T weight loads (and the next A read) between its
+// 4*T*R MFMAs with sched_group_barrier. Off by default: with the 4-deep ring the compiler's own
+// order (loads issued as one burst at the chunk head) is 2 % faster (tools/variants.sh, r01).
+// Masks: 0x8 MFMA, 0x20 VMEM read, 0x100 DS read.
 template <int T, int R>
 __device__ __forceinline__ void interleave_loads() {
-#ifdef MBRL_NO_INTERLEAVE
+#ifndef MBRL_INTERLEAVE
     return;
 #endif
     __builtin_amdgcn_sched_group_barrier(0x008, 2 * R, 0);
@@ -127,6 +134,7 @@ __device__ __forceinline__ void mma_out(const f32x4 (&aout)[R][T], const f32x4 (
 }
 
 // acc + bias -> ReLU -> next activation buffer (float4 row stores); one barrier (ping-pong buffers).
+// T here is the tiles per wave (TW): wave w owns columns [16 T w, 16 T (w + 1)).
 template <int T, int R>
 __device__ __forceinline__ void hidden_store(const f32x4 (&acc)[R][T], const f32x4 (&bias)[T], float* out,
                                              int lda, int wave, int lane) {
@@ -234,9 +242,16 @@ __device__ __forceinline__ void stage_actions(const RolloutArgs& A, const EpiPar
 // K0C / NOT > 0: compile-time layer-0 / output chunk counts, enabling a 4-deep weight ring with
 // static register slots (three chunks = ~3000 MFMA cycles of load cover). K0C == 0: runtime counts,
 // 2-deep ring (any shape).
-template <int T, int R, int K0C_T, int NOT_T>
-__global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
+// NW = 4 or 8 waves per workgroup; each wave owns TW = 4T/NW 16-column tiles of every layer. With
+// NW = 8 two waves share a SIMD: while one issues its weight loads the other keeps the matrix pipe
+// busy (a wave's own VMEM issue otherwise stalls its MFMA stream ~10 %: tools/ubench). The epilogue
+// (per-candidate VALU work) runs on waves 0-3.
+template <int T, int R, int K0C_T, int NOT_T, int NW>
+__global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A) {
     constexpr int M = 16 * R;
+    constexpr int TW = 4 * T / NW;
+    constexpr int NT = 64 * NW;
+    static_assert(TW >= 1 && TW * NW == 4 * T, "tiles per wave");
     constexpr bool RING = K0C_T > 0;
     constexpr int NB = RING ? 4 : 2;
     constexpr int SS = RING ? NOT_T : 1;    // register state slots per lane (ceil(s / 16) <= NOT); generic: LDS
@@ -249,50 +264,51 @@ __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
     float* const actX = L.act;   // step input (layer 0) and every even layer's input
     float* const actY = L.act2;
 
+    const bool epi = wave < 4;   // epilogue waves
     // ---- prologue: parameters into LDS, s0 and a_0 into the MLP input
     float av[R][MAX_A_PER_LANE];
     float acp[R];  // this lane's share of the current step's CoshLoss sum, per row
-    fetch_actions<R>(A, tile, 0, wave, lane, av);
-    for (int i = tid; i < A.s; i += 256) {
+    if (epi) fetch_actions<R>(A, tile, 0, wave, lane, av);
+    for (int i = tid; i < A.s; i += NT) {
         L.obs_mean[i] = A.obs_mean ? A.obs_mean[i] : 0.f;
         L.obs_std[i] = A.obs_std ? A.obs_std[i] : 1.f;
         L.goal[i] = A.goal ? A.goal[i] : 0.f;
         L.cw[i] = A.cw ? A.cw[i] : 0.f;
     }
-    for (int i = tid; i < A.a; i += 256) {
+    for (int i = tid; i < A.a; i += NT) {
         L.act_mean[i] = A.act_mean ? A.act_mean[i] : 0.f;
         L.act_std[i] = A.act_std ? A.act_std[i] : 1.f;
     }
     const float* bias_src = member + A.stream_floats;
-    for (int i = tid; i < A.L * A.Wpad + 16 * A.NOT; i += 256) L.hbias[i] = bias_src[i];
+    for (int i = tid; i < A.L * A.Wpad + 16 * A.NOT; i += NT) L.hbias[i] = bias_src[i];
     __syncthreads();
-    for (int i = tid; i < M * A.s; i += 256) {
+    for (int i = tid; i < M * A.s; i += NT) {
         const int m = i / A.s, d = i - (i / A.s) * A.s;
         const int n = min(tile * M + m, A.N - 1);
         const float sv = A.s0_per_cand ? A.s0[(size_t)n * A.s + d] : A.s0[d];
         actX[m * A.lda + d] = A.norm_s ? (sv - L.obs_mean[d]) / L.obs_std[d] : sv;
     }
-    for (int i = tid; i < M * A.k0pad_extra; i += 256) {
+    for (int i = tid; i < M * A.k0pad_extra; i += NT) {
         const int m = i / A.k0pad_extra, j = i - (i / A.k0pad_extra) * A.k0pad_extra;
         actX[m * A.lda + A.s + A.a + j] = 0.f;
     }
     EpiParams<SS> P;
     load_epi_params<SS>(A, L, lane, P);
-    stage_actions<R, SS>(A, P, actX, wave, lane, av, acp);
+    if (epi) stage_actions<R, SS>(A, P, actX, wave, lane, av, acp);
     __syncthreads();
 
     // ---- weight stream: this wave's slice of chunk g is at wb + g * cs (f32x4 units)
-    const f32x4* wb = reinterpret_cast<const f32x4*>(member) + wave * T * 64 + lane;
+    const f32x4* wb = reinterpret_cast<const f32x4*>(member) + wave * TW * 64 + lane;
     const int cs = 4 * T * 64;
     const int C = A.chunks_per_step;
     auto chunk_ptr = [&](int g) { return wb + (size_t)(g < C ? g : g - C) * cs; };
 
-    f32x4 ring[NB][T];
+    f32x4 ring[NB][TW];
     f32x4 aAB[2][R];  // A fragments of chunks with even / odd index within the layer
-    f32x4 acc[R][T];
-    f32x4 bias[T];
+    f32x4 acc[R][TW];
+    f32x4 bias[TW];
 #pragma unroll
-    for (int q = 0; q < NB - 1; ++q) load_chunk<T>(ring[q], chunk_ptr(q));
+    for (int q = 0; q < NB - 1; ++q) load_chunk<TW>(ring[q], chunk_ptr(q));
     float total[R];  // return of row epi_row(r, wave, lane), held by the 16 lanes of that row
 #pragma unroll
     for (int r = 0; r < R; ++r) total[r] = 0.f;
@@ -305,10 +321,10 @@ __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
 // next A fragment, then the MFMAs of chunk c. SLOT must fold to a constant (unrolled loops).
 #define MBRL_HIDDEN_CHUNK(SLOT, KC, NK, IN)                                          \
     do {                                                                             \
-        load_chunk<T>(ring[((SLOT) + NB - 1) % NB], chunk_ptr(g + NB - 1));          \
+        load_chunk<TW>(ring[((SLOT) + NB - 1) % NB], chunk_ptr(g + NB - 1));         \
         if ((KC) + 1 < (NK)) read_a<R>(aAB[((KC) + 1) & 1], IN, A.lda, (KC) + 1, lane); \
-        mma_hidden<T, R>(acc, aAB[(KC) & 1], ring[SLOT]);                            \
-        interleave_loads<T, R>();                                                    \
+        mma_hidden<TW, R>(acc, aAB[(KC) & 1], ring[SLOT]);                           \
+        interleave_loads<TW, R>();                                                   \
         MBRL_PIN();                                                                  \
         ++g;                                                                         \
     } while (0)
@@ -316,10 +332,10 @@ __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
     for (int t = 0; t < A.H; ++t) {
         int g = 0;
         // a_{t+1} from HBM now; consumed in this step's epilogue
-        if (t + 1 < A.H) fetch_actions<R>(A, tile, t + 1, wave, lane, av);
+        if (epi && t + 1 < A.H) fetch_actions<R>(A, tile, t + 1, wave, lane, av);
         // ---- layer 0: actX [s | a | 0-pad] -> actY (W)
-        zero_acc<T, R>(acc);
-        load_bias<T>(bias, L.hbias, wave, lane);
+        zero_acc<TW, R>(acc);
+        load_bias<TW>(bias, L.hbias, wave, lane);
         read_a<R>(aAB[0], actX, A.lda, 0, lane);
         if constexpr (RING) {
 #pragma unroll
@@ -332,39 +348,39 @@ __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
             }
         }
         STAMP(0);
-        hidden_store<T, R>(acc, bias, actY, A.lda, wave, lane);
+        hidden_store<TW, R>(acc, bias, actY, A.lda, wave, lane);
         STAMP(1);
         // ---- hidden layers 1..L-1 (W -> W), alternating Y->X->Y...
         float* in = actY;
         float* out = actX;
         for (int l = 1; l < A.L; ++l) {
-            zero_acc<T, R>(acc);
-            load_bias<T>(bias, L.hbias + l * A.Wpad, wave, lane);
+            zero_acc<TW, R>(acc);
+            load_bias<TW>(bias, L.hbias + l * A.Wpad, wave, lane);
             read_a<R>(aAB[0], in, A.lda, 0, lane);
             constexpr int KH = 4 * T;  // 4T % NB == 0: every hidden layer starts on the same slot
             constexpr int S0 = RING ? K0C_T % NB : 0;
 #pragma unroll
             for (int kc = 0; kc < KH; ++kc) MBRL_HIDDEN_CHUNK((S0 + kc) % NB, kc, KH, in);
             STAMP(2);
-            hidden_store<T, R>(acc, bias, out, A.lda, wave, lane);
+            hidden_store<TW, R>(acc, bias, out, A.lda, wave, lane);
             STAMP(3);
             float* tmp = in; in = out; out = tmp;
         }
         // ---- output layer: W -> s, K split over the 4 waves, partials through LDS
         {
-            f32x4 aout[R][T];
+            f32x4 aout[R][TW];
 #pragma unroll
             for (int r = 0; r < R; ++r)
 #pragma unroll
-                for (int kc = 0; kc < T; ++kc)
+                for (int kc = 0; kc < TW; ++kc)
                     aout[r][kc] = *reinterpret_cast<const f32x4*>(
-                        in + (16 * r + (lane & 15)) * A.lda + wave * 16 * T + 16 * kc + 4 * (lane >> 4));
+                        in + (16 * r + (lane & 15)) * A.lda + wave * 16 * TW + 16 * kc + 4 * (lane >> 4));
             float* part = L.part + wave * M * A.pw;
 #define MBRL_OUT_CHUNK(SLOT, J)                                                   \
     do {                                                                          \
-        load_chunk<T>(ring[((SLOT) + NB - 1) % NB], chunk_ptr(g + NB - 1));       \
+        load_chunk<TW>(ring[((SLOT) + NB - 1) % NB], chunk_ptr(g + NB - 1));      \
         MBRL_PIN();                                                               \
-        mma_out<T, R>(aout, ring[SLOT], part, A.pw, J, lane);                     \
+        mma_out<TW, R>(aout, ring[SLOT], part, A.pw, J, lane);                    \
         MBRL_PIN();                                                               \
         ++g;                                                                      \
     } while (0)
@@ -386,7 +402,7 @@ __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
 
         // ---- epilogue (one pass, no cross-wave traffic): s_{t+1} = unnormalize(out), goal cost of
         // (s_{t+1}, a_t), next MLP input [norm(s_{t+1}) | norm(a_{t+1}) | 0-pad] into actX
-        {
+        if (epi) {
             const float* bout = L.hbias + A.L * A.Wpad;
             const int ws = M * A.pw;
             const int j = lane & 15;
@@ -397,7 +413,10 @@ __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
                 float sc = 0.f;
                 auto slot = [&](int d, float om, float os, float goal, float cw, float bo) {
                     const int ro = m * A.pw + d;
-                    const float o = L.part[ro] + L.part[ws + ro] + L.part[2 * ws + ro] + L.part[3 * ws + ro] + bo;
+                    float o = L.part[ro] + L.part[ws + ro] + L.part[2 * ws + ro] + L.part[3 * ws + ro];
+                    if constexpr (NW == 8)
+                        o = o + ((L.part[4 * ws + ro] + L.part[5 * ws + ro]) + (L.part[6 * ws + ro] + L.part[7 * ws + ro]));
+                    o = o + bo;
                     const float sn = A.unnorm_s ? o * os + om : o;
                     if (A.has_sc) {
                         const float x = (sn - goal) * cw;
@@ -428,12 +447,12 @@ __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
 #undef MBRL_HIDDEN_CHUNK
 #ifdef MBRL_STAMPS
     if (lane == 0 && g_mbrl_stamps != nullptr) {
-        unsigned long long* dst = g_mbrl_stamps + (((size_t)e * gridDim.x + tile) * 4 + wave) * NSEG;
+        unsigned long long* dst = g_mbrl_stamps + (((size_t)e * gridDim.x + tile) * NW + wave) * NSEG;
 #pragma unroll
         for (int k = 0; k < NSEG; ++k) dst[k] = seg[k];
     }
 #endif
-    if ((lane & 15) == 0) {
+    if (epi && (lane & 15) == 0) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int n = tile * M + epi_row(r, wave, lane);
@@ -442,31 +461,35 @@ __global__ void __launch_bounds__(256, 1) rollout_kernel(const RolloutArgs A) {
     }
 }
 
-template <int T, int R, int K0C_T, int NOT_T>
-static hipError_t launch_rollout_tr(const RolloutArgs& A, hipStream_t stream) {
+template <int T, int R, int K0C_T, int NOT_T, int NW>
+static hipError_t launch_rollout_tr(const RolloutArgs& A_in, hipStream_t stream) {
+    RolloutArgs A = A_in;
+    A.nw = NW;
     const int M = 16 * R;
     dim3 grid((A.N + M - 1) / M, A.E);
     const size_t lds = rollout_lds_bytes(A, M);
     static bool attr_set = false;  // raise the dynamic-LDS cap once per instantiation
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&rollout_kernel<T, R, K0C_T, NOT_T>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&rollout_kernel<T, R, K0C_T, NOT_T, NW>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    hipLaunchKernelGGL((rollout_kernel<T, R, K0C_T, NOT_T>), grid, dim3(256), lds, stream, A);
+    hipLaunchKernelGGL((rollout_kernel<T, R, K0C_T, NOT_T, NW>), grid, dim3(64 * NW), lds, stream, A);
     return hipGetLastError();
 }
 
 template <int T, int R>
 static hipError_t launch_rollout_t(const RolloutArgs& A, hipStream_t stream) {
-    if constexpr (T <= 8) {  // the 4-deep ring needs 4*T*4 VGPRs
-        if (A.K0C == 2 && A.NOT == 2) return launch_rollout_tr<T, R, 2, 2>(A, stream);
-        if (A.K0C == 6 && A.NOT == 6) return launch_rollout_tr<T, R, 6, 6>(A, stream);
-        if (A.K0C == 2 && A.NOT == 6) return launch_rollout_tr<T, R, 2, 6>(A, stream);
-        if (A.K0C == 6 && A.NOT == 2) return launch_rollout_tr<T, R, 6, 2>(A, stream);
+    // two waves per SIMD (8 waves, T/2 tiles each) where the tile count allows it
+    constexpr int NW = (T >= 2 && MBRL_ROLLOUT_NW == 8) ? 8 : 4;
+    if constexpr (4 * T / NW <= 8) {  // the 4-deep ring needs 4*TW*4 VGPRs
+        if (A.K0C == 2 && A.NOT == 2) return launch_rollout_tr<T, R, 2, 2, NW>(A, stream);
+        if (A.K0C == 6 && A.NOT == 6) return launch_rollout_tr<T, R, 6, 6, NW>(A, stream);
+        if (A.K0C == 2 && A.NOT == 6) return launch_rollout_tr<T, R, 2, 6, NW>(A, stream);
+        if (A.K0C == 6 && A.NOT == 2) return launch_rollout_tr<T, R, 6, 2, NW>(A, stream);
     }
-    return launch_rollout_tr<T, R, 0, 0>(A, stream);
+    return launch_rollout_tr<T, R, 0, 0, NW>(A, stream);
 }
 
 hipError_t launch_rollout(const RolloutArgs& A, int T, int R, hipStream_t stream) {
