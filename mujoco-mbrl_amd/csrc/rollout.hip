@@ -27,10 +27,16 @@
 
 #include "mbrl_internal.h"
 
-// Waves per workgroup for the rollout (4: one per SIMD; 8: two per SIMD, T/2 tiles each). Measured on
-// cheetah (tools/variants.sh): 8 waves gave no gain over 4, so 4 is the default.
+// Waves per workgroup for the rollout: 8 (two per SIMD, T/2 tiles each) for R = 1, 4 for R = 2 (the
+// 8-wave output partials would push R = 2 past 160 KiB of LDS). -DMBRL_ROLLOUT_NW=4 forces 4.
+// Weight stream through buffer_load (SGPR descriptor + 32-bit offsets); -DMBRL_GLOBAL_LOAD for the
+// global_load form. Measured on cheetah, rollout ms (tools/variants.sh, r01):
+//   global 4 waves 1.083 | buffer 4 waves 1.044 | global 8 waves 1.171 | buffer 8 waves 1.035
 #ifndef MBRL_ROLLOUT_NW
-#define MBRL_ROLLOUT_NW 4
+#define MBRL_ROLLOUT_NW 8
+#endif
+#ifndef MBRL_GLOBAL_LOAD
+#define MBRL_BUFFER_LOAD 1
 #endif
 
 namespace mbrl {
@@ -87,6 +93,15 @@ __device__ __forceinline__ void load_chunk(f32x4 (&b)[T], const f32x4* __restric
 #pragma unroll
     for (int j = 0; j < T; ++j) b[j] = p[j * 64];
 #endif
+}
+
+// -DMBRL_BUFFER_LOAD variant: the same stream through buffer_load_dwordx4 (SGPR descriptor, 32-bit
+// per-lane offsets: one VGPR of address per load instead of two).
+template <int T>
+__device__ __forceinline__ void load_chunk_buf(f32x4 (&b)[T], __amdgpu_buffer_rsrc_t rsrc, unsigned voff) {
+#pragma unroll
+    for (int j = 0; j < T; ++j)
+        b[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + (unsigned)(j * 64 * 16), 0, 0));
 }
 
 template <int R>
@@ -301,14 +316,24 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
     const f32x4* wb = reinterpret_cast<const f32x4*>(member) + wave * TW * 64 + lane;
     const int cs = 4 * T * 64;
     const int C = A.chunks_per_step;
+#ifdef MBRL_BUFFER_LOAD
+    (void)wb;
+    const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(member), 0, (int)(A.stream_floats * sizeof(float)), 0x00020000);
+    const unsigned lane_off = (unsigned)((wave * TW * 64 + lane) * 16);
+#define MBRL_LOAD_CHUNK(DST, G) \
+    load_chunk_buf<TW>(DST, wrsrc, lane_off + (unsigned)(((G) < C ? (G) : (G) - C) * cs * 16))
+#else
     auto chunk_ptr = [&](int g) { return wb + (size_t)(g < C ? g : g - C) * cs; };
+#define MBRL_LOAD_CHUNK(DST, G) load_chunk<TW>(DST, chunk_ptr(G))
+#endif
 
     f32x4 ring[NB][TW];
     f32x4 aAB[2][R];  // A fragments of chunks with even / odd index within the layer
     f32x4 acc[R][TW];
     f32x4 bias[TW];
 #pragma unroll
-    for (int q = 0; q < NB - 1; ++q) load_chunk<TW>(ring[q], chunk_ptr(q));
+    for (int q = 0; q < NB - 1; ++q) MBRL_LOAD_CHUNK(ring[q], q);
     float total[R];  // return of row epi_row(r, wave, lane), held by the 16 lanes of that row
 #pragma unroll
     for (int r = 0; r < R; ++r) total[r] = 0.f;
@@ -321,7 +346,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
 // next A fragment, then the MFMAs of chunk c. SLOT must fold to a constant (unrolled loops).
 #define MBRL_HIDDEN_CHUNK(SLOT, KC, NK, IN)                                          \
     do {                                                                             \
-        load_chunk<TW>(ring[((SLOT) + NB - 1) % NB], chunk_ptr(g + NB - 1));         \
+        MBRL_LOAD_CHUNK(ring[((SLOT) + NB - 1) % NB], g + NB - 1);                   \
         if ((KC) + 1 < (NK)) read_a<R>(aAB[((KC) + 1) & 1], IN, A.lda, (KC) + 1, lane); \
         mma_hidden<TW, R>(acc, aAB[(KC) & 1], ring[SLOT]);                           \
         interleave_loads<TW, R>();                                                   \
@@ -378,7 +403,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
             float* part = L.part + wave * M * A.pw;
 #define MBRL_OUT_CHUNK(SLOT, J)                                                   \
     do {                                                                          \
-        load_chunk<TW>(ring[((SLOT) + NB - 1) % NB], chunk_ptr(g + NB - 1));      \
+        MBRL_LOAD_CHUNK(ring[((SLOT) + NB - 1) % NB], g + NB - 1);                \
         MBRL_PIN();                                                               \
         mma_out<TW, R>(aout, ring[SLOT], part, A.pw, J, lane);                    \
         MBRL_PIN();                                                               \
@@ -445,6 +470,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
         STAMP(6);
     }
 #undef MBRL_HIDDEN_CHUNK
+#undef MBRL_LOAD_CHUNK
 #ifdef MBRL_STAMPS
     if (lane == 0 && g_mbrl_stamps != nullptr) {
         unsigned long long* dst = g_mbrl_stamps + (((size_t)e * gridDim.x + tile) * NW + wave) * NSEG;
@@ -481,8 +507,8 @@ static hipError_t launch_rollout_tr(const RolloutArgs& A_in, hipStream_t stream)
 
 template <int T, int R>
 static hipError_t launch_rollout_t(const RolloutArgs& A, hipStream_t stream) {
-    // two waves per SIMD (8 waves, T/2 tiles each) where the tile count allows it
-    constexpr int NW = (T >= 2 && MBRL_ROLLOUT_NW == 8) ? 8 : 4;
+    // two waves per SIMD (8 waves, T/2 tiles each) where the tile count and LDS allow it
+    constexpr int NW = (T >= 2 && R == 1 && MBRL_ROLLOUT_NW == 8) ? 8 : 4;
     if constexpr (4 * T / NW <= 8) {  // the 4-deep ring needs 4*TW*4 VGPRs
         if (A.K0C == 2 && A.NOT == 2) return launch_rollout_tr<T, R, 2, 2, NW>(A, stream);
         if (A.K0C == 6 && A.NOT == 6) return launch_rollout_tr<T, R, 6, 6, NW>(A, stream);
