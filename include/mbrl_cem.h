@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MBRL_ABI_VERSION 1
+#define MBRL_ABI_VERSION 2
 
 typedef struct ihipStream_t* mbrl_stream_t; /* == hipStream_t */
 typedef struct ihipEvent_t* mbrl_event_t;   /* == hipEvent_t  */
@@ -41,8 +41,13 @@ enum {
     MBRL_EWORKSPACE = -4     /* workspace too small */
 };
 
-/* Cost kinds. GOAL_STATE = state_action_cost(SmoothAbsLoss, CoshLoss), agents.py:182-183,231. */
-enum { MBRL_COST_GOAL_STATE = 0 };
+/* Cost kinds.
+ * GOAL_STATE   = state_action_cost(SmoothAbsLoss, CoshLoss) on (s_{t+1}, a_t), agents.py:182-183,231.
+ * MODEL_REWARD = the reward head of the dynamics model itself, evaluated at (s_{t+1}, a_t) and
+ *                unnormalised: RewardAgent's compose(partial(model, ...), itemgetter(1)) cost
+ *                (agents.py:342-362, models.py:143-163). Needs mbrl_mlp_shape.reward_head = 1; every
+ *                step then runs the MLP twice (the state pass, then the reward pass). */
+enum { MBRL_COST_GOAL_STATE = 0, MBRL_COST_MODEL_REWARD = 1 };
 
 /* Ordering of NaN returns in elite selection. */
 enum {
@@ -51,13 +56,16 @@ enum {
 };
 
 /* Dynamics MLP shape: Linear(s+a -> W), ReLU, [Linear(W -> W), ReLU] x (L-1), Linear(W -> s).
- * models.py:96-110 (Model, L = 2) generalised to L hidden layers; E ensemble members. */
+ * models.py:96-110 (Model, L = 2) generalised to L hidden layers; E ensemble members.
+ * reward_head = 1: ModelWithReward (models.py:125-141): the same trunk plus a reward head
+ * Linear(W -> 1) beside the state head. */
 typedef struct {
-    int32_t state_dim;  /* s  (observation dim, env_wrappers.py:86 flat 'observations') */
-    int32_t action_dim; /* a */
-    int32_t hidden;     /* W  (any >= 1; zero-padded inside the packed stream) */
-    int32_t n_hidden;   /* L >= 1 */
-    int32_t ensemble;   /* E >= 1 */
+    int32_t state_dim;   /* s  (observation dim, env_wrappers.py:86 flat 'observations') */
+    int32_t action_dim;  /* a */
+    int32_t hidden;      /* W  (any >= 1; zero-padded inside the packed stream) */
+    int32_t n_hidden;    /* L >= 1 */
+    int32_t ensemble;    /* E >= 1 */
+    int32_t reward_head; /* 0 or 1 */
 } mbrl_mlp_shape;
 
 /* Normalisation affine, TransitionsDataset.normalize_field / unnormalize_field (data.py:255-260),
@@ -67,15 +75,17 @@ typedef struct {
     const float* obs_std;   /* [s] */
     const float* act_mean;  /* [a] */
     const float* act_std;   /* [a] */
+    const float* rew_mean;  /* [1] "rewards" statistics (agents.py:340), reward_head models only */
+    const float* rew_std;   /* [1] */
     int32_t normalize_state;
     int32_t unnormalize_state;
     int32_t normalize_action;
-    int32_t _pad;
+    int32_t unnormalize_reward;
 } mbrl_norm;
 
 /* Per-step cost on the (s_{t+1}, a_t) pair (planners.py:210). */
 typedef struct {
-    int32_t kind;             /* MBRL_COST_GOAL_STATE */
+    int32_t kind;             /* MBRL_COST_GOAL_STATE or MBRL_COST_MODEL_REWARD */
     int32_t has_state_cost;   /* SmoothAbsLoss term present (models.py:244-259) */
     int32_t has_action_cost;  /* CoshLoss term present (models.py:262-272) */
     int32_t _pad;
@@ -116,8 +126,9 @@ const char* mbrl_last_error(void);
 
 /* ---- model upload: replaces the per-call nn.Linear weight reads of Model._forward (models.py:106-110) */
 size_t mbrl_mlp_packed_bytes(const mbrl_mlp_shape* shape);
-/* weights[e*(L+1)+l] / biases[...]: DEVICE pointers to nn.Linear weight [out][in] and bias [out],
- * passed in a HOST array. Writes the fragment-ordered weight stream the rollout kernel reads. */
+/* weights[e*NL+l] / biases[...], NL = L + 1 + reward_head: DEVICE pointers to nn.Linear weight
+ * [out][in] and bias [out] (trunk layers, the state head, then the reward head), passed in a HOST
+ * array. Writes the fragment-ordered weight stream the rollout kernel reads. */
 int mbrl_mlp_pack(const mbrl_mlp_shape* shape, const float* const* weights, const float* const* biases,
                   void* packed, mbrl_stream_t stream);
 

@@ -52,8 +52,9 @@ __global__ void pack_hidden_kernel(const float* __restrict__ w, int in_real, int
 }
 
 // Output layer: chunk j = output tile j; fragment kc covers this wave's K rows w*16T + 16kc + ...
-__global__ void pack_out_kernel(const float* __restrict__ w, int in_real, int out_real, int NOT, int T,
-                                float* __restrict__ dst) {
+// Rows [0, out_real) come from w; with a reward head, row out_real comes from w_r ([1][in]).
+__global__ void pack_out_kernel(const float* __restrict__ w, const float* __restrict__ w_r, int in_real,
+                                int out_real, int NOT, int T, float* __restrict__ dst) {
     const size_t total = (size_t)NOT * 4 * T * 64 * 4;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
         const int s = (int)(i & 3);
@@ -64,7 +65,12 @@ __global__ void pack_out_kernel(const float* __restrict__ w, int in_real, int ou
         const int j = (int)(frag / T / 4);
         const int n = 16 * j + (lane & 15);
         const int k = wave * 16 * T + 16 * kc + 4 * (lane >> 4) + s;
-        dst[i] = (n < out_real && k < in_real) ? w[(size_t)n * in_real + k] : 0.0f;
+        float v = 0.0f;
+        if (k < in_real) {
+            if (n < out_real) v = w[(size_t)n * in_real + k];
+            else if (w_r && n == out_real) v = w_r[k];
+        }
+        dst[i] = v;
     }
 }
 
@@ -533,9 +539,10 @@ __global__ void member_mean_kernel(const float* __restrict__ src, int E, int n, 
 // ------------------------------------------------------------------------------------------------
 static int shape_geometry(const mbrl_mlp_shape* sh, Geometry* g) {
     if (!sh) return fail(MBRL_EINVAL, "shape is NULL");
-    if (!make_geometry(sh->state_dim, sh->action_dim, sh->hidden, sh->n_hidden, sh->ensemble, g))
-        return fail(MBRL_EUNSUPPORTED, "unsupported MLP shape s=%d a=%d W=%d L=%d E=%d (need all >= 1, W <= 1024)",
-                    sh->state_dim, sh->action_dim, sh->hidden, sh->n_hidden, sh->ensemble);
+    if (!make_geometry(sh->state_dim, sh->action_dim, sh->hidden, sh->n_hidden, sh->ensemble, sh->reward_head, g))
+        return fail(MBRL_EUNSUPPORTED,
+                    "unsupported MLP shape s=%d a=%d W=%d L=%d E=%d reward_head=%d (need all >= 1, W <= 1024, L <= %d)",
+                    sh->state_dim, sh->action_dim, sh->hidden, sh->n_hidden, sh->ensemble, sh->reward_head, MAX_LAYERS);
     return MBRL_OK;
 }
 
@@ -568,12 +575,18 @@ static int rollout_impl(const Geometry& g, const void* packed, const mbrl_norm* 
         A.obs_mean = norm->obs_mean; A.obs_std = norm->obs_std;
         A.act_mean = norm->act_mean; A.act_std = norm->act_std;
         A.norm_s = norm->normalize_state; A.unnorm_s = norm->unnormalize_state; A.norm_a = norm->normalize_action;
+        A.unnorm_r = norm->unnormalize_reward; A.rew_mean = norm->rew_mean; A.rew_std = norm->rew_std;
+        if (A.unnorm_r && (!A.rew_mean || !A.rew_std))
+            return fail(MBRL_EINVAL, "reward unnormalisation requested without rew_mean/rew_std");
         if ((A.norm_s || A.unnorm_s) && (!A.obs_mean || !A.obs_std))
             return fail(MBRL_EINVAL, "state normalisation requested without obs_mean/obs_std");
         if (A.norm_a && (!A.act_mean || !A.act_std))
             return fail(MBRL_EINVAL, "action normalisation requested without act_mean/act_std");
     }
-    if (cost) {
+    if (cost && cost->kind == MBRL_COST_MODEL_REWARD) {
+        if (!g.reward) return fail(MBRL_EINVAL, "MODEL_REWARD cost needs a reward_head model");
+        A.reward = 1;
+    } else if (cost) {
         if (cost->kind != MBRL_COST_GOAL_STATE) return fail(MBRL_EUNSUPPORTED, "cost kind %d", cost->kind);
         A.has_sc = cost->has_state_cost; A.has_ac = cost->has_action_cost;
         A.cw = cost->weights; A.goal = cost->goal;
@@ -599,8 +612,11 @@ static int rollout_impl(const Geometry& g, const void* packed, const mbrl_norm* 
     (void)G;
     if (16 * R * g.a > 768) R = 1;
     if (16 * g.a > 768) return fail(MBRL_EUNSUPPORTED, "action_dim %d too large (max 48)", g.a);
+    // waves per workgroup as launch_rollout_t picks them: 8 for R = 1 (T >= 2), else 4
+    A.nw = (R == 1 && g.T >= 2) ? 8 : 4;
     if (rollout_lds_bytes(A, 16 * R) > 160 * 1024) {
         R = 1;
+        A.nw = g.T >= 2 ? 8 : 4;
         if (rollout_lds_bytes(A, 16) > 160 * 1024)
             return fail(MBRL_EUNSUPPORTED, "LDS footprint %zu B exceeds 160 KiB", rollout_lds_bytes(A, 16));
     }
@@ -717,12 +733,12 @@ int mbrl_mlp_pack(const mbrl_mlp_shape* shape, const float* const* weights, cons
     int rc = shape_geometry(shape, &g);
     if (rc) return rc;
     if (!weights || !biases || !packed) return fail(MBRL_EINVAL, "pack: NULL argument");
-    const int nl = g.L + 1;
+    const int nl = g.L + 1 + g.reward;   // trunk, state head, [reward head]
     for (int e = 0; e < g.E; ++e) {
         float* base = static_cast<float*>(packed) + (size_t)e * g.member_stride;
         float* bias_base = base + g.stream_floats;
         size_t chunk = 0;
-        for (int l = 0; l < nl; ++l) {
+        for (int l = 0; l <= g.L; ++l) {
             const float* w = weights[e * nl + l];
             const float* b = biases[e * nl + l];
             if (!w || !b) return fail(MBRL_EINVAL, "pack: NULL weight/bias for member %d layer %d", e, l);
@@ -736,10 +752,18 @@ int mbrl_mlp_pack(const mbrl_mlp_shape* shape, const float* const* weights, cons
                 hipLaunchKernelGGL(pack_transposed_kernel, dim3(256), dim3(256), 0, stream, w, in_real, g.W, g.Wpad, plain);
                 chunk += nkc;
             } else {
-                hipLaunchKernelGGL(pack_out_kernel, dim3(256), dim3(256), 0, stream, w, g.W, g.s, g.NOT, g.T, dst);
-                hipLaunchKernelGGL(pack_bias_kernel, dim3(1), dim3(256), 0, stream, b, g.s, 16 * g.NOT,
-                                   bias_base + (size_t)g.L * g.Wpad);
+                const float* wr = g.reward ? weights[e * nl + g.L + 1] : nullptr;
+                const float* br = g.reward ? biases[e * nl + g.L + 1] : nullptr;
+                if (g.reward && (!wr || !br)) return fail(MBRL_EINVAL, "pack: NULL reward head for member %d", e);
+                hipLaunchKernelGGL(pack_out_kernel, dim3(256), dim3(256), 0, stream, w, wr, g.W, g.s, g.NOT, g.T, dst);
+                float* ob = bias_base + (size_t)g.L * g.Wpad;
+                hipLaunchKernelGGL(pack_bias_kernel, dim3(1), dim3(256), 0, stream, b, g.s, 16 * g.NOT, ob);
                 hipLaunchKernelGGL(copy_kernel, dim3(64), dim3(256), 0, stream, w, (size_t)g.s * g.W, plain);
+                if (g.reward) {   // row s of the output block: the reward head (after the zero padding)
+                    hipLaunchKernelGGL(copy_kernel, dim3(1), dim3(64), 0, stream, br, (size_t)1, ob + g.s);
+                    hipLaunchKernelGGL(copy_kernel, dim3(4), dim3(256), 0, stream, wr, (size_t)g.W,
+                                       plain + (size_t)g.s * g.W);
+                }
                 chunk += g.NOT;
             }
         }

@@ -12,17 +12,19 @@ constexpr int MAX_LAYERS = 4;  // hidden layers
 // Packed-stream geometry for one MLP shape (DESIGN.md §2 "weight stream").
 struct Geometry {
     int s, a, W, L, E;
+    int reward;     // 1: reward head (output rows = s + 1)
+    int so;         // output rows: s + reward
     int T;          // 16-column tiles per wave per hidden layer; Wpad = 64 * T
     int Wpad;
     int K0C;        // layer-0 K chunks of 16 (even)
-    int NOT;        // output tiles of 16 (even)
+    int NOT;        // output tiles of 16 (even), covering so rows
     int C;          // chunks per step = K0C + (L-1)*4T + NOT
     int lda;        // LDS activation row stride (floats)
     int pw;         // LDS output-partial row stride (floats)
     size_t stream_floats;  // C * 1024 * T
     size_t bias_floats;    // L * Wpad + 16 * NOT
     // plain copies for the single-trajectory kernel (traj.hip): layer 0 and hidden layers
-    // transposed W^T [in][Wpad]; the output layer row-major [s][W]
+    // transposed W^T [in][Wpad]; the output layer row-major [so][W] (state rows, then reward)
     int Opad;
     size_t tw_off[MAX_LAYERS + 1];  // offsets inside the plain region
     size_t tw_floats;
@@ -31,16 +33,18 @@ struct Geometry {
 
 inline int round_even(int x) { return (x + 1) & ~1; }
 
-inline bool make_geometry(int s, int a, int W, int L, int E, Geometry* g) {
-    if (s < 1 || a < 1 || W < 1 || L < 1 || L > MAX_LAYERS || E < 1) return false;
+inline bool make_geometry(int s, int a, int W, int L, int E, int reward, Geometry* g) {
+    if (s < 1 || a < 1 || W < 1 || L < 1 || L > MAX_LAYERS || E < 1 || reward < 0 || reward > 1) return false;
     int T = 1;
     while (64 * T < W) T *= 2;
     if (T > 16) return false;
     g->s = s; g->a = a; g->W = W; g->L = L; g->E = E;
+    g->reward = reward;
+    g->so = s + reward;
     g->T = T;
     g->Wpad = 64 * T;
     g->K0C = round_even((s + a + 15) / 16);
-    g->NOT = round_even((s + 15) / 16);
+    g->NOT = round_even((g->so + 15) / 16);
     if (g->NOT > 2 * 4 * T * 4) return false;
     g->C = g->K0C + (L - 1) * 4 * T + g->NOT;
     const int k0 = 16 * g->K0C;
@@ -48,13 +52,13 @@ inline bool make_geometry(int s, int a, int W, int L, int E, Geometry* g) {
     g->pw = 16 * g->NOT + 4;
     g->stream_floats = (size_t)g->C * 1024 * T;
     g->bias_floats = (size_t)L * g->Wpad + 16 * (size_t)g->NOT;
-    g->Opad = (s + 3) & ~3;
+    g->Opad = (g->so + 3) & ~3;
     size_t o = 0;
     g->tw_off[0] = o;
     o += (size_t)(s + a) * g->Wpad;
     for (int l = 1; l < L; ++l) { g->tw_off[l] = o; o += (size_t)W * g->Wpad; }
     g->tw_off[L] = o;
-    o += (size_t)s * W;
+    o += (size_t)g->so * W;
     g->tw_floats = o;
     g->member_stride = (g->stream_floats + g->bias_floats + g->tw_floats + 63) / 64 * 64;
     return true;
@@ -69,6 +73,9 @@ struct RolloutArgs {
     int N, H, n_offset;
     const float *obs_mean, *obs_std, *act_mean, *act_std;
     int norm_s, unnorm_s, norm_a;
+    int reward;                        // cost = unnormalised reward head at (s_{t+1}, a_t), 2 passes/step
+    int unnorm_r;
+    const float *rew_mean, *rew_std;   // [1] each (device), read once in the prologue
     const float *cw, *goal;
     float alpha_s, alpha_s2, alpha_a, alpha_a2;
     int has_sc, has_ac;

@@ -235,8 +235,9 @@ __device__ __forceinline__ void load_epi_params(const RolloutArgs& A, const LdsM
 
 // a_t -> normalised MLP input columns [s, s+a); returns this lane's share of sum_d (cosh(a_d/alpha)-1).
 template <int R, int SS>
-__device__ __forceinline__ void stage_actions(const RolloutArgs& A, const EpiParams<SS>& P, float* act, int wave,
-                                              int lane, const float (&av)[R][MAX_A_PER_LANE], float (&acp)[R]) {
+__device__ __forceinline__ void stage_actions(const RolloutArgs& A, const EpiParams<SS>& P, float* act, float* asave,
+                                              int wave, int lane, const float (&av)[R][MAX_A_PER_LANE],
+                                              float (&acp)[R]) {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int m = epi_row(r, wave, lane);
@@ -246,7 +247,9 @@ __device__ __forceinline__ void stage_actions(const RolloutArgs& A, const EpiPar
             const int d = (lane & 15) + 16 * k;
             if (d < A.a) {
                 const float x = av[r][k];
-                act[m * A.lda + A.s + d] = A.norm_a ? (x - P.am[k]) / P.as[k] : x;
+                const float xn = A.norm_a ? (x - P.am[k]) / P.as[k] : x;
+                act[m * A.lda + A.s + d] = xn;
+                if (A.reward) asave[m * A.a + d] = xn;   // the state pass re-reads a_t
                 if (A.has_ac) c += coshf(x / A.alpha_a) - 1.0f;
             }
         }
@@ -309,7 +312,12 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
     }
     EpiParams<SS> P;
     load_epi_params<SS>(A, L, lane, P);
-    if (epi) stage_actions<R, SS>(A, P, actX, wave, lane, av, acp);
+    if (epi) stage_actions<R, SS>(A, P, actX, L.aterm, wave, lane, av, acp);
+    // reward-head models: two MLP passes per step (state pass on (s_t, a_t), reward pass on
+    // (s_{t+1}, a_t)); the normalised s_{t+1} and a_t are kept in LDS across the passes
+    const int npass = A.reward ? 2 : 1;
+    const float rmean = (A.reward && A.unnorm_r) ? A.rew_mean[0] : 0.f;
+    const float rstd = (A.reward && A.unnorm_r) ? A.rew_std[0] : 1.f;
     __syncthreads();
 
     // ---- weight stream: this wave's slice of chunk g is at wb + g * cs (f32x4 units)
@@ -354,10 +362,12 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
         ++g;                                                                         \
     } while (0)
 
-    for (int t = 0; t < A.H; ++t) {
+    for (int tp = 0; tp < A.H * npass; ++tp) {
+        const int t = A.reward ? (tp >> 1) : tp;
+        const int pass = A.reward ? (tp & 1) : 0;
         int g = 0;
-        // a_{t+1} from HBM now; consumed in this step's epilogue
-        if (epi && t + 1 < A.H) fetch_actions<R>(A, tile, t + 1, wave, lane, av);
+        // a_{t+1} from HBM now; consumed in this step's (last) epilogue
+        if (epi && pass == 0 && t + 1 < A.H) fetch_actions<R>(A, tile, t + 1, wave, lane, av);
         // ---- layer 0: actX [s | a | 0-pad] -> actY (W)
         zero_acc<TW, R>(acc);
         load_bias<TW>(bias, L.hbias, wave, lane);
@@ -427,7 +437,49 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
 
         // ---- epilogue (one pass, no cross-wave traffic): s_{t+1} = unnormalize(out), goal cost of
         // (s_{t+1}, a_t), next MLP input [norm(s_{t+1}) | norm(a_{t+1}) | 0-pad] into actX
-        if (epi) {
+        if (epi && A.reward) {
+            // reward-head model. State pass: s_{t+1} -> states_out, next input [norm(s_{t+1}) | norm(a_t)].
+            // Reward pass: cost_t = unnormalize_reward(reward head), next input [norm(s_{t+1}) | norm(a_{t+1})].
+            const float* bout = L.hbias + A.L * A.Wpad;
+            const int ws = M * A.pw;
+            const int j = lane & 15;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int m = epi_row(r, wave, lane);
+                const int n = tile * M + m;
+                float rc = 0.f;
+                for (int d = j; d <= A.s; d += 16) {
+                    const int ro = m * A.pw + d;
+                    float o = 0.f;
+                    if (pass == 0 || d == A.s) {
+                        for (int q = 0; q < NW; ++q) o = q == 0 ? L.part[ro] : o + L.part[q * ws + ro];
+                        o = o + bout[d];
+                    }
+                    if (d < A.s) {
+                        float xn;
+                        if (pass == 0) {
+                            const float sn = A.unnorm_s ? o * L.obs_std[d] + L.obs_mean[d] : o;
+                            if (A.states_out != nullptr && n < A.N)
+                                A.states_out[(((size_t)e * A.H + t) * A.N + n) * A.s + d] = sn;
+                            xn = A.norm_s ? (sn - L.obs_mean[d]) / L.obs_std[d] : sn;
+                            L.sterm[m * A.s + d] = xn;
+                        } else {
+                            xn = L.sterm[m * A.s + d];
+                        }
+                        actX[m * A.lda + d] = xn;
+                    } else if (pass == 1) {
+                        rc = A.unnorm_r ? o * rstd + rmean : o;
+                    }
+                }
+                for (int d = A.s + A.a + j; d < A.s + A.a + A.k0pad_extra; d += 16) actX[m * A.lda + d] = 0.f;
+                if (pass == 0) {
+                    for (int d = j; d < A.a; d += 16) actX[m * A.lda + A.s + d] = L.aterm[m * A.a + d];
+                } else {
+                    total[r] += rowsum16(rc);
+                }
+            }
+            if (pass == 1 && t + 1 < A.H) stage_actions<R, SS>(A, P, actX, L.aterm, wave, lane, av, acp);
+        } else if (epi) {
             const float* bout = L.hbias + A.L * A.Wpad;
             const int ws = M * A.pw;
             const int j = lane & 15;
@@ -464,7 +516,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
                 const float ac = rowsum16(acp[r]);
                 total[r] += sc + A.alpha_a2 * (ac / (float)A.a);
             }
-            if (t + 1 < A.H) stage_actions<R, SS>(A, P, actX, wave, lane, av, acp);
+            if (t + 1 < A.H) stage_actions<R, SS>(A, P, actX, L.aterm, wave, lane, av, acp);
         }
         __syncthreads();
         STAMP(6);

@@ -19,6 +19,8 @@ LIB_PATH = os.environ.get("MBRL_AMD_LIB") or os.path.join(os.path.dirname(os.pat
 
 MBRL_OK = 0
 MBRL_COST_GOAL_STATE = 0
+MBRL_COST_MODEL_REWARD = 1
+ABI_VERSION = 2
 MBRL_NAN_LAST = 0
 MBRL_NAN_FIRST = 1
 
@@ -33,13 +35,14 @@ EXPORTED = (
 
 class MlpShape(ctypes.Structure):
     _fields_ = [("state_dim", c_int32), ("action_dim", c_int32), ("hidden", c_int32),
-                ("n_hidden", c_int32), ("ensemble", c_int32)]
+                ("n_hidden", c_int32), ("ensemble", c_int32), ("reward_head", c_int32)]
 
 
 class Norm(ctypes.Structure):
     _fields_ = [("obs_mean", c_void_p), ("obs_std", c_void_p), ("act_mean", c_void_p),
-                ("act_std", c_void_p), ("normalize_state", c_int32), ("unnormalize_state", c_int32),
-                ("normalize_action", c_int32), ("_pad", c_int32)]
+                ("act_std", c_void_p), ("rew_mean", c_void_p), ("rew_std", c_void_p),
+                ("normalize_state", c_int32), ("unnormalize_state", c_int32),
+                ("normalize_action", c_int32), ("unnormalize_reward", c_int32)]
 
 
 class Cost(ctypes.Structure):
@@ -96,8 +99,8 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.mbrl_abi_version() != 1:
-        raise ImportError(f"mbrl_amd ABI version mismatch: {lib.mbrl_abi_version()} != 1")
+    if lib.mbrl_abi_version() != ABI_VERSION:
+        raise ImportError(f"mbrl_amd ABI version mismatch: {lib.mbrl_abi_version()} != {ABI_VERSION}")
     _lib = lib
     return lib
 
@@ -123,4 +126,5 @@ def require_gpu(t):
 
 
 __all__ = ["load", "check", "ptr", "stream_handle", "MlpShape", "Norm", "Cost", "Sampler", "CemParams",
-           "EXPORTED", "MBRL_NAN_LAST", "MBRL_NAN_FIRST", "MBRL_COST_GOAL_STATE", "c_int64"]
+           "EXPORTED", "MBRL_NAN_LAST", "MBRL_NAN_FIRST", "MBRL_COST_GOAL_STATE", "MBRL_COST_MODEL_REWARD",
+           "ABI_VERSION", "c_int64"]

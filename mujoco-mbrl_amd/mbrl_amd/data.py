@@ -38,11 +38,15 @@ class TransitionsDataset:
         if rewards is not None:
             self.statistics["rewards"] = self._get_stats(rewards)
 
-    def normalizers(self):
-        """The three partials GoalStateAgent builds (agents.py:219-221)."""
+    def normalizers(self, reward=False):
+        """The three partials GoalStateAgent builds (agents.py:219-221); with reward=True also
+        RewardAgent's unnormalize_reward (agents.py:340)."""
         st = self.statistics
-        return dict(
+        out = dict(
             normalize_state=functools.partial(self.normalize_field, field_name="observations", stats=st),
             unnormalize_state=functools.partial(self.unnormalize_field, field_name="observations", stats=st),
             normalize_action=functools.partial(self.normalize_field, field_name="actions", stats=st),
         )
+        if reward:
+            out["unnormalize_reward"] = functools.partial(self.unnormalize_field, field_name="rewards", stats=st)
+        return out

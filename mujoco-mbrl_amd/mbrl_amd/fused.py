@@ -14,13 +14,14 @@ Device state is cached per module: packed weights are re-packed only when a para
 (torch's in-place version counter moves on every optimizer.step()).
 """
 import functools
+import operator
 import weakref
 
 import numpy as np
 import torch
 
 from . import _lib
-from .models import CoshLoss, EnsembleModel, Model, SmoothAbsLoss
+from .models import CoshLoss, EnsembleModel, Model, ModelWithReward, SmoothAbsLoss
 
 
 # ------------------------------------------------------------------------------------------------
@@ -32,6 +33,43 @@ def _unpartial(f):
         kw = {**f.keywords, **kw}
         f = f.func
     return f, kw
+
+
+def _uncompose(f):
+    """compose(a, b) closure (agents.py:300-304, models.compose) -> (a, b), else None."""
+    code, cells = getattr(f, "__code__", None), getattr(f, "__closure__", None)
+    if code is None or cells is None or set(code.co_freevars) != {"a", "b"}:
+        return None
+    env = dict(zip(code.co_freevars, (c.cell_contents for c in cells)))
+    return env["a"], env["b"]
+
+
+def _getter_index(g):
+    """operator.itemgetter(i) -> i for a single int index, else None."""
+    if not isinstance(g, operator.itemgetter):
+        return None
+    try:
+        _, args = g.__reduce__()
+    except Exception:  # pragma: no cover
+        return None
+    return args[0] if len(args) == 1 and isinstance(args[0], int) else None
+
+
+def _reward_layers(module):
+    """(members, L, W, s, a) for a reward-head model: this package's ModelWithReward, or the
+    reference's (duck-typed: linear1..linear4, ReLU, linear3 -> s, linear4 -> 1)."""
+    if isinstance(module, ModelWithReward):
+        return [module.linears()], module.n_hidden, module.hidden_units, module.state_dim, module.action_dim
+    lins = [getattr(module, f"linear{i}", None) for i in range(1, 5)]
+    if (type(module).__name__ == "ModelWithReward" and all(isinstance(l, torch.nn.Linear) for l in lins)
+            and isinstance(getattr(module, "activation_fn", None), torch.nn.ReLU) and not hasattr(module, "linear5")):
+        W = lins[0].out_features
+        s = lins[2].out_features
+        a = lins[0].in_features - s
+        if (lins[1].in_features == W and lins[1].out_features == W and lins[2].in_features == W
+                and lins[3].in_features == W and lins[3].out_features == 1 and a >= 1):
+            return [lins], 2, W, s, a
+    return None
 
 
 def _linear_layers(module):
@@ -88,26 +126,65 @@ def describe_norm(normalize_state, normalize_action, unnormalize_state, s, a):
         return None
     return dict(obs_mean=obs[1] if obs else None, obs_std=obs[2] if obs else None,
                 act_mean=na[1] if na else None, act_std=na[2] if na else None,
-                normalize_state=bool(ns), unnormalize_state=bool(us), normalize_action=bool(na))
+                normalize_state=bool(ns), unnormalize_state=bool(us), normalize_action=bool(na),
+                rew_mean=None, rew_std=None, unnormalize_reward=False)
 
 
-def describe_model(model):
-    """Model callable -> dict(module, layers, L, W, s, a, norm) or None."""
-    f, kw = _unpartial(model)
-    if set(kw) - {"normalize_state", "normalize_action", "unnormalize_state"}:
+def _describe_partial(fn, reward):
+    """partial(module, <normaliser keywords>) -> model description, else None."""
+    f, kw = _unpartial(fn)
+    allowed = {"normalize_state", "normalize_action", "unnormalize_state"} | ({"unnormalize_reward"} if reward else set())
+    if set(kw) - allowed or not isinstance(f, torch.nn.Module):
         return None
-    layers = _linear_layers(f) if isinstance(f, torch.nn.Module) else None
+    layers = _reward_layers(f) if reward else _linear_layers(f)
     if layers is None:
         return None
     members, L, W, s, a = layers
     norm = describe_norm(kw.get("normalize_state"), kw.get("normalize_action"), kw.get("unnormalize_state"), s, a)
     if norm is None:
         return None
-    return dict(module=f, members=members, L=L, W=W, s=s, a=a, E=len(members), norm=norm)
+    if reward:
+        rn = _field_stats(kw.get("unnormalize_reward"), "unnormalize_field")
+        if rn is False or (rn and (rn[1].numel() != 1 or rn[2].numel() != 1)):
+            return None
+        if rn:
+            norm.update(rew_mean=rn[1].reshape(1), rew_std=rn[2].reshape(1), unnormalize_reward=True)
+    return dict(module=f, members=members, L=L, W=W, s=s, a=a, E=len(members), norm=norm, reward=reward)
 
 
-def describe_cost(cost, s):
-    """partial(state_action_cost, state_cost=SmoothAbsLoss, action_cost=CoshLoss) -> dict or None."""
+def _norms_equal(n1, n2):
+    for k in ("obs_mean", "obs_std", "act_mean", "act_std", "rew_mean", "rew_std"):
+        x, y = n1[k], n2[k]
+        if (x is None) != (y is None) or (x is not None and not torch.equal(x.float(), y.float())):
+            return False
+    return all(n1[k] == n2[k] for k in ("normalize_state", "unnormalize_state", "normalize_action",
+                                         "unnormalize_reward"))
+
+
+def describe_model(model):
+    """Model callable -> dict(module, members, L, W, s, a, E, norm, reward) or None. Accepts
+    partial(Model|EnsembleModel, ...) (agents.py:224-230) and RewardAgent's
+    compose(partial(ModelWithReward, ...), itemgetter(0)) (agents.py:342-352)."""
+    uc = _uncompose(model)
+    if uc is not None:
+        if _getter_index(uc[1]) != 0:
+            return None
+        return _describe_partial(uc[0], reward=True)
+    return _describe_partial(model, reward=False)
+
+
+def describe_cost(cost, s, mdesc=None):
+    """partial(state_action_cost, state_cost=SmoothAbsLoss, action_cost=CoshLoss) -> goal-state dict;
+    compose(partial(<the model's module>, <the same normalisers>), itemgetter(1)) (agents.py:353-362)
+    -> reward dict when `mdesc` is that reward model; else None."""
+    uc = _uncompose(cost)
+    if uc is not None:
+        if _getter_index(uc[1]) != 1 or mdesc is None or not mdesc.get("reward"):
+            return None
+        cd = _describe_partial(uc[0], reward=True)
+        if cd is None or cd["module"] is not mdesc["module"] or not _norms_equal(cd["norm"], mdesc["norm"]):
+            return None
+        return dict(kind=_lib.MBRL_COST_MODEL_REWARD, key=("reward", id(mdesc["module"])))
     f, kw = _unpartial(cost)
     if getattr(f, "__name__", "") != "state_action_cost" or set(kw) != {"state_cost", "action_cost"}:
         return None
@@ -128,7 +205,8 @@ def describe_cost(cost, s):
         return None
     def raw_key(x):
         return _tensor_key(x) if torch.is_tensor(x) else ("v", float(np.asarray(x).ravel()[0]), np.size(x))
-    return dict(weights=w.contiguous(), goal=goal.contiguous(), alpha_state=float(sc.alpha),
+    return dict(kind=_lib.MBRL_COST_GOAL_STATE, weights=w.contiguous(), goal=goal.contiguous(),
+                alpha_state=float(sc.alpha),
                 alpha_action=float(ac.alpha), key=(raw_key(sc.weights), raw_key(sc.goal_state),
                                                    float(sc.alpha), float(ac.alpha)))
 
@@ -156,7 +234,7 @@ def _param_key(members, device):
 
 
 def mlp_shape(desc):
-    return _lib.MlpShape(desc["s"], desc["a"], desc["W"], desc["L"], desc["E"])
+    return _lib.MlpShape(desc["s"], desc["a"], desc["W"], desc["L"], desc["E"], int(desc.get("reward", False)))
 
 
 def packed_weights(desc, device):
@@ -209,10 +287,14 @@ class DeviceProblem:
         self.shape = mlp_shape(mdesc)
         self.packed = packed_weights(mdesc, device)
         n = mdesc["norm"]
-        self._norm_t = [_dev(n[k], device) for k in ("obs_mean", "obs_std", "act_mean", "act_std")]
+        self._norm_t = [_dev(n[k], device) for k in ("obs_mean", "obs_std", "act_mean", "act_std", "rew_mean",
+                                                     "rew_std")]
         self.norm = _lib.Norm(*[_lib.ptr(t) for t in self._norm_t], int(n["normalize_state"]),
-                              int(n["unnormalize_state"]), int(n["normalize_action"]), 0)
-        if cdesc is not None:
+                              int(n["unnormalize_state"]), int(n["normalize_action"]), int(n["unnormalize_reward"]))
+        if cdesc is not None and cdesc["kind"] == _lib.MBRL_COST_MODEL_REWARD:
+            self._cost_t = []
+            self.cost = _lib.Cost(_lib.MBRL_COST_MODEL_REWARD, 0, 0, 0, None, None, 0.0, 0.0)
+        elif cdesc is not None:
             self._cost_t = [_dev(cdesc["weights"], device), _dev(cdesc["goal"], device)]
             self.cost = _lib.Cost(_lib.MBRL_COST_GOAL_STATE, 1, 1, 0, _lib.ptr(self._cost_t[0]),
                                   _lib.ptr(self._cost_t[1]), cdesc["alpha_state"], cdesc["alpha_action"])
@@ -232,8 +314,8 @@ def device_problem(mdesc, cdesc, device):
     """Cached DeviceProblem: rebuilt only when weights, statistics or cost parameters change."""
     n = mdesc["norm"]
     key = (id(mdesc["module"]), _param_key(mdesc["members"], device),
-           tuple(_tensor_key(n[k]) for k in ("obs_mean", "obs_std", "act_mean", "act_std")),
-           (n["normalize_state"], n["unnormalize_state"], n["normalize_action"]),
+           tuple(_tensor_key(n[k]) for k in ("obs_mean", "obs_std", "act_mean", "act_std", "rew_mean", "rew_std")),
+           (n["normalize_state"], n["unnormalize_state"], n["normalize_action"], n["unnormalize_reward"]),
            None if cdesc is None else cdesc["key"])
     hit = _PROBLEMS.get(key)
     if hit is not None and hit[0]() is mdesc["module"]:
@@ -331,7 +413,7 @@ def try_forward(module, state, action, normalize_action, normalize_state, unnorm
     norm = describe_norm(normalize_state, normalize_action, unnormalize_state, s, a)
     if norm is None:
         return None
-    desc = dict(module=module, members=members, L=L, W=W, s=s, a=a, E=1, norm=norm)
+    desc = dict(module=module, members=members, L=L, W=W, s=s, a=a, E=1, norm=norm, reward=False)
     dev = state.device
     prob = device_problem(desc, None, dev)
     B = state.shape[0]

@@ -86,22 +86,36 @@ class EnsembleModel(DynamicsModel):
 
 
 class ModelWithReward(nn.Module):
-    """models.py:125-163 (shared trunk, state head linear3, reward head linear4). The planners run
-    it through the generic callable path (RewardAgent's reward-as-cost wiring, agents.py:342-366)."""
+    """models.py:125-163: a shared Linear-ReLU trunk, state head and reward head. `n_hidden`
+    generalises the reference's 2-layer trunk. Layers are linear1..linear{n_hidden} (trunk),
+    linear{n_hidden+1} (state head) and linear{n_hidden+2} (reward head). n_hidden=2 gives the
+    reference's names, so state_dicts load both ways.
 
-    def __init__(self, state_dim, action_dim, hidden_units=200):
+    The planners take RewardAgent's wiring (agents.py:342-362) on the fused path: the model closure
+    compose(partial(model, ...), itemgetter(0)) and the cost closure compose(partial(model, ...),
+    itemgetter(1)). The cost is the unnormalised reward head at (s_{t+1}, a_t)."""
+
+    def __init__(self, state_dim, action_dim, hidden_units=200, n_hidden=2):
         super().__init__()
         self.train_iterations = 0
-        self.linear1 = nn.Linear(state_dim + action_dim, hidden_units)
-        self.linear2 = nn.Linear(hidden_units, hidden_units)
-        self.linear3 = nn.Linear(hidden_units, state_dim)
-        self.linear4 = nn.Linear(hidden_units, 1)
+        self.state_dim, self.action_dim = state_dim, action_dim
+        self.hidden_units, self.n_hidden = hidden_units, n_hidden
+        dims = [state_dim + action_dim] + [hidden_units] * n_hidden
+        for i, (fi, fo) in enumerate(zip(dims[:-1], dims[1:])):
+            setattr(self, f"linear{i + 1}", nn.Linear(fi, fo))
+        setattr(self, f"linear{n_hidden + 1}", nn.Linear(hidden_units, state_dim))
+        setattr(self, f"linear{n_hidden + 2}", nn.Linear(hidden_units, 1))
         self.activation_fn = nn.ReLU()
 
+    def linears(self):
+        """Trunk layers, state head, reward head (the packing order of mbrl_mlp_pack)."""
+        return [getattr(self, f"linear{i + 1}") for i in range(self.n_hidden + 2)]
+
     def _forward(self, x):
-        x = self.activation_fn(self.linear1(x))
-        x = self.activation_fn(self.linear2(x))
-        return self.linear3(x), self.linear4(x)
+        lins = self.linears()
+        for lin in lins[:self.n_hidden]:
+            x = self.activation_fn(lin(x))
+        return lins[-2](x), lins[-1](x)
 
     def forward(self, state, action, normalize_state=None, unnormalize_state=None, normalize_action=None,
                 unnormalize_reward=None):

@@ -101,7 +101,7 @@ class RandomShootingPlanner(ModelPlanner):
             acts = action_list.to(device=dev, dtype=torch.float32).reshape(H, N, a).contiguous()
             s0 = initial_state.to(device=dev, dtype=torch.float32).contiguous()
             mdesc = fused.describe_model(model)
-            cdesc = fused.describe_cost(cost, mdesc["s"]) if mdesc is not None else None
+            cdesc = fused.describe_cost(cost, mdesc["s"], mdesc) if mdesc is not None else None
             if mdesc is not None and cdesc is not None and mdesc["E"] == 1 and mdesc["a"] == a:
                 prob = fused.device_problem(mdesc, cdesc, dev)
                 states = torch.empty((1, H, N, mdesc["s"]), dtype=torch.float32, device=dev)
@@ -166,7 +166,7 @@ class CEMPlanner(ModelPlanner):
         with torch.cuda.device(dev):
             s0 = initial_state.to(device=dev, dtype=torch.float32).contiguous()
             mdesc = fused.describe_model(model)
-            cdesc = fused.describe_cost(cost, mdesc["s"]) if mdesc is not None else None
+            cdesc = fused.describe_cost(cost, mdesc["s"], mdesc) if mdesc is not None else None
             ws = None
             if st["distributed"] and torch.distributed.is_available() and torch.distributed.is_initialized() \
                     and torch.distributed.get_world_size() > 1:

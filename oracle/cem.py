@@ -43,6 +43,8 @@ CONFIGS = {
     3: dict(name="cheetah-run-cem", s=17, a=6, W=512, L=3, N=4096, H=30, E=1, planner="cem"),
     4: dict(name="walker-walk-cem", s=24, a=6, W=512, L=3, N=16384, H=30, E=1, planner="cem"),
     5: dict(name="humanoid-stand-cem-ens5", s=67, a=21, W=512, L=3, N=32768, H=50, E=5, planner="cem"),
+    # reward-head variant: ModelWithReward's 2-layer trunk, RewardAgent cost
+    6: dict(name="cheetah-run-reward-cem", s=17, a=6, W=512, L=2, N=4096, H=30, E=1, planner="cem", reward=True),
 }
 
 CEM_DEFAULTS = dict(num_iterations=5, elite_frac=0.1, alpha=0.1, lo=-1.0, hi=1.0)
@@ -64,6 +66,25 @@ def synth_model(seed, s, a, W, L, E=1):
             b = rng.uniform(-bound, bound, size=(fan_out,)).astype(F32)
             layers.append((w, b))
         members.append(layers)
+    return members
+
+
+def synth_reward_model(seed, s, a, W, L, E=1):
+    """E ModelWithReward members (models.py:125-141, trunk generalised to L layers): trunk layers,
+    state head [s, W] and reward head [1, W] drawn in that order with the nn.Linear law. The head is
+    stored combined: the last layer is [s + 1, W] (state rows, then the reward row)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    dims = [s + a] + [W] * L
+    members = []
+    for _ in range(E):
+        layers = []
+        for fan_in, fan_out in list(zip(dims[:-1], dims[1:])) + [(W, s), (W, 1)]:
+            bound = 1.0 / np.sqrt(fan_in)
+            w = rng.uniform(-bound, bound, size=(fan_out, fan_in)).astype(F32)
+            b = rng.uniform(-bound, bound, size=(fan_out,)).astype(F32)
+            layers.append((w, b))
+        (ws, bs), (wr, br) = layers[-2], layers[-1]
+        members.append(layers[:-2] + [(np.vstack([ws, wr]), np.concatenate([bs, br]))])
     return members
 
 
@@ -90,11 +111,17 @@ def synth_problem(config_id, **overrides):
     cfg.update(overrides)
     seed = 1000 + config_id
     s, a = cfg["s"], cfg["a"]
-    model = synth_model(seed, s, a, cfg["W"], cfg["L"], cfg["E"])
     norm = synth_norm(seed, s, a)
     s0, goal = synth_state_goal(seed, s)
-    cost = dict(weights=np.ones(s, dtype=F32), goal=goal, alpha_state=SMOOTH_ABS_ALPHA,
-                alpha_action=COSH_ALPHA)
+    if cfg.get("reward"):
+        model = synth_reward_model(seed, s, a, cfg["W"], cfg["L"], cfg["E"])
+        rr = np.random.Generator(np.random.PCG64(seed + 4))
+        norm.update(rew_mean=rr.uniform(-0.5, 0.5, size=1).astype(F32), rew_std=rr.uniform(0.5, 2.0, size=1).astype(F32))
+        cost = dict(kind="reward")
+    else:
+        model = synth_model(seed, s, a, cfg["W"], cfg["L"], cfg["E"])
+        cost = dict(weights=np.ones(s, dtype=F32), goal=goal, alpha_state=SMOOTH_ABS_ALPHA,
+                    alpha_action=COSH_ALPHA)
     return dict(cfg=cfg, seed=seed, rng_seed=seed + 3, model=model, norm=norm, s0=s0, cost=cost)
 
 
@@ -118,18 +145,33 @@ def mlp_forward(layers, x):
     return (x @ w.T + b).astype(F32)
 
 
-def dynamics_step(layers, norm, s, a):
-    """DynamicsModel.forward (models.py:13-29) with the GoalStateAgent normalisers (agents.py:219-230)."""
+def _model_out(layers, norm, s, a):
+    """normalize_action, normalize_state, cat (state first), the MLP (models.py:13-29 / 143-163)."""
     if norm is not None:
         a = ((a - norm["act_mean"]) / norm["act_std"]).astype(F32)        # normalize_action first
         sn = ((s - norm["obs_mean"]) / norm["obs_std"]).astype(F32)       # then normalize_state
     else:
         sn = s
     x = np.concatenate([sn, a], axis=1).astype(F32)                        # state first
-    out = mlp_forward(layers, x)
+    return mlp_forward(layers, x)
+
+
+def dynamics_step(layers, norm, s, a):
+    """DynamicsModel.forward (models.py:13-29) with the GoalStateAgent normalisers (agents.py:219-230);
+    for a reward-head model, the state head of ModelWithReward.forward (models.py:143-163)."""
+    out = _model_out(layers, norm, s, a)[:, :s.shape[1]]
     if norm is not None:
         out = (out * norm["obs_std"] + norm["obs_mean"]).astype(F32)       # unnormalize_state
     return out
+
+
+def reward_cost(layers, norm, s_next, a):
+    """RewardAgent's cost (agents.py:353-362): compose(partial(model, ...), itemgetter(1)) evaluated on
+    (s_{t+1}, a_t) (planners.py:210) = the reward head, unnormalised (models.py:157-158)."""
+    r = _model_out(layers, norm, s_next, a)[:, s_next.shape[1]]
+    if norm is not None and norm.get("rew_mean") is not None:
+        r = (r * norm["rew_std"][0] + norm["rew_mean"][0]).astype(F32)      # unnormalize_reward
+    return r.astype(F32)
 
 
 def goal_state_cost(s, a, cost):
@@ -161,7 +203,9 @@ def rollout(model, norm, cost, s0, actions, store_states=False):
         total = np.zeros(N, dtype=F32)
         for t in range(H):
             st = dynamics_step(layers, norm, st, actions[t])
-            total = (total + goal_state_cost(st, actions[t], cost)).astype(F32)
+            c = reward_cost(layers, norm, st, actions[t]) if cost.get("kind") == "reward" \
+                else goal_state_cost(st, actions[t], cost)
+            total = (total + c).astype(F32)
             if store_states:
                 member_states.append(st)
         costs[e] = total

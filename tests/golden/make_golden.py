@@ -10,7 +10,9 @@ What runs from the reference (imported read-only from /root/reference, no byteco
     -- for L = 3 a DynamicsModel subclass whose _forward follows Model._forward's pattern
   * models.SmoothAbsLoss / models.CoshLoss                          (src/mbrl/models.py:244-272)
   * data.TransitionsDataset.normalize_field / unnormalize_field     (src/mbrl/data.py:255-260)
-Wired exactly as GoalStateAgent does (src/mbrl/agents.py:219-233). Two small pieces that live in
+  * models.ModelWithReward (config 6)                                (src/mbrl/models.py:125-163)
+Wired exactly as GoalStateAgent does (src/mbrl/agents.py:219-233), or, for config 6, as RewardAgent
+does (agents.py:336-362; compose, agents.py:300-304, restated). Two small pieces that live in
 modules that cannot import here (dm_control / tensorboardX missing) are restated verbatim in
 behaviour: state_action_cost (agents.py:182-183) and EnvWrapper._sample_action
 (env_wrappers.py:50-62).
@@ -97,8 +99,43 @@ def build_reference_model(models, layers, s, a, W):
     return m
 
 
+def compose(a, b):
+    # agents.py:300-304 (agents.py does not import here)
+    def ab(*args, **kwargs):
+        return b(a(*args, **kwargs))
+    return ab
+
+
+def wire_reward(data, models, problem, layers):
+    """RewardAgent's model / cost closures (agents.py:336-362) around the reference ModelWithReward."""
+    import operator
+    cfg = problem["cfg"]
+    norm = problem["norm"]
+    s, a, W = cfg["s"], cfg["a"], cfg["W"]
+    assert cfg["L"] == 2, "the reference ModelWithReward has a 2-layer trunk"
+    stats = {"observations": {"mean": torch.from_numpy(norm["obs_mean"]), "std": torch.from_numpy(norm["obs_std"])},
+             "actions": {"mean": torch.from_numpy(norm["act_mean"]), "std": torch.from_numpy(norm["act_std"])},
+             "rewards": {"mean": torch.from_numpy(norm["rew_mean"]), "std": torch.from_numpy(norm["rew_std"])}}
+    TD = data.TransitionsDataset
+    m = models.ModelWithReward(s, a, hidden_units=W)
+    head_w, head_b = layers[-1]
+    with torch.no_grad():
+        for lin, (w, b) in zip([m.linear1, m.linear2, m.linear3, m.linear4],
+                               list(layers[:-1]) + [(head_w[:s], head_b[:s]), (head_w[s:], head_b[s:])]):
+            lin.weight.copy_(torch.from_numpy(np.ascontiguousarray(w)))
+            lin.bias.copy_(torch.from_numpy(np.ascontiguousarray(b)))
+    kw = dict(normalize_state=functools.partial(TD.normalize_field, field_name="observations", stats=stats),
+              normalize_action=functools.partial(TD.normalize_field, field_name="actions", stats=stats),
+              unnormalize_state=functools.partial(TD.unnormalize_field, field_name="observations", stats=stats),
+              unnormalize_reward=functools.partial(TD.unnormalize_field, field_name="rewards", stats=stats))
+    return compose(functools.partial(m, **kw), operator.itemgetter(0)), \
+        compose(functools.partial(m, **kw), operator.itemgetter(1))
+
+
 def wire(data, models, problem, layers):
     cfg = problem["cfg"]
+    if cfg.get("reward"):
+        return wire_reward(data, models, problem, layers)
     norm = problem["norm"]
     stats = {"observations": {"mean": torch.from_numpy(norm["obs_mean"]),
                               "std": torch.from_numpy(norm["obs_std"])},
@@ -237,12 +274,16 @@ def main():
     out_dir = HERE
     data, models, planners = _import_reference()
     torch.set_num_threads(min(8, os.cpu_count() or 1))
+    if len(sys.argv) > 1 and sys.argv[1] == "6":           # regenerate only the reward-head fixture
+        make_cem(data, models, planners, out_dir, 6, N=512, H=10)
+        return
     make_toy(planners, out_dir)
     make_rs(data, models, planners, out_dir)
     make_cem(data, models, planners, out_dir, 2)
     make_cem(data, models, planners, out_dir, 3)
     make_cem(data, models, planners, out_dir, 4, N=2048)
     make_cem(data, models, planners, out_dir, 5, N=256, H=20)
+    make_cem(data, models, planners, out_dir, 6, N=512, H=10)
 
 
 if __name__ == "__main__":

@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     assert decl == sorted(_lib.EXPORTED)
     for name in decl:
         assert hasattr(lib, name), name
-    assert lib.mbrl_abi_version() == 1
+    assert lib.mbrl_abi_version() == _lib.ABI_VERSION == 2
 
 
 def test_no_gpu_needed_for_sizing_calls():
@@ -43,6 +43,11 @@ def test_no_gpu_needed_for_sizing_calls():
     assert lib.mbrl_refit_workspace_bytes(30, 6, 409) >= 30 * 6 * 409 * 4
     p = _lib.CemParams(4096, 30, 409, 5, 0.1, -1.0, 1.0, 0.0, 0.5, 0, 1)
     assert lib.mbrl_cem_workspace_bytes(ctypes.byref(sh), ctypes.byref(p)) > 4096 * 4
+    # reward head: one more output row (17 + 1 still fits two 16-row tiles) and its plain copy
+    shr = _lib.MlpShape(17, 6, 512, 2, 1, 1)
+    plain_r = 23 * 512 + 512 * 512 + 18 * 512
+    assert lib.mbrl_mlp_packed_bytes(ctypes.byref(shr)) == ((36 * 8192 + 2 * 512 + 32 + plain_r + 63) // 64 * 64) * 4
+    assert lib.mbrl_mlp_packed_bytes(ctypes.byref(_lib.MlpShape(17, 6, 512, 2, 1, 2))) == 0
 
 
 def test_errors_are_reported_not_crashing():
@@ -57,9 +62,9 @@ def test_errors_are_reported_not_crashing():
 
 
 STRUCTS = {
-    "MlpShape": ("mbrl_mlp_shape", ["state_dim", "action_dim", "hidden", "n_hidden", "ensemble"]),
-    "Norm": ("mbrl_norm", ["obs_mean", "obs_std", "act_mean", "act_std", "normalize_state", "unnormalize_state",
-                           "normalize_action"]),
+    "MlpShape": ("mbrl_mlp_shape", ["state_dim", "action_dim", "hidden", "n_hidden", "ensemble", "reward_head"]),
+    "Norm": ("mbrl_norm", ["obs_mean", "obs_std", "act_mean", "act_std", "rew_mean", "rew_std", "normalize_state",
+                           "unnormalize_state", "normalize_action", "unnormalize_reward"]),
     "Cost": ("mbrl_cost", ["kind", "has_state_cost", "has_action_cost", "weights", "goal", "alpha_state",
                            "alpha_action"]),
     "Sampler": ("mbrl_sampler", ["seed", "iteration", "mu", "sigma", "lo", "hi"]),

@@ -21,10 +21,26 @@ def rel_err(x, ref):
 
 
 def build(problem):
-    """mbrl_amd model / cost / sampler closures wired exactly as GoalStateAgent (agents.py:219-233)."""
+    """mbrl_amd model / cost / sampler closures wired exactly as GoalStateAgent (agents.py:219-233),
+    or as RewardAgent (agents.py:336-362) for a reward-head problem."""
     from mbrl_amd import data, env, models
     cfg = problem["cfg"]
     s, a, W, L = cfg["s"], cfg["a"], cfg["W"], cfg["L"]
+    if cfg.get("reward"):
+        import operator
+        m = models.ModelWithReward(s, a, hidden_units=W, n_hidden=L)
+        (*trunk, (hw, hb)) = problem["model"][0]
+        with torch.no_grad():
+            for lin, (w, b) in zip(m.linears(), trunk + [(hw[:s], hb[:s]), (hw[s:], hb[s:])]):
+                lin.weight.copy_(torch.from_numpy(np.ascontiguousarray(w)))
+                lin.bias.copy_(torch.from_numpy(np.ascontiguousarray(b)))
+        nm = problem["norm"]
+        ds = data.TransitionsDataset({k: {"mean": torch.from_numpy(nm[p + "_mean"]), "std": torch.from_numpy(nm[p + "_std"])}
+                                      for k, p in (("observations", "obs"), ("actions", "act"), ("rewards", "rew"))})
+        kw = ds.normalizers(reward=True)
+        model_fn = models.compose(functools.partial(m, **kw), operator.itemgetter(0))
+        cost_fn = models.compose(functools.partial(m, **kw), operator.itemgetter(1))
+        return m, model_fn, cost_fn, env.sample_action_fn(env.BoundedActionSpec(a, -1.0, 1.0))
     members = []
     for layers in problem["model"]:
         m = models.Model(s, a, hidden_units=W, n_hidden=L)
@@ -51,7 +67,7 @@ def device_problem(problem):
     from mbrl_amd import fused
     _, model_fn, cost_fn, _ = build(problem)
     md = fused.describe_model(model_fn)
-    cd = fused.describe_cost(cost_fn, md["s"])
+    cd = fused.describe_cost(cost_fn, md["s"], md)
     assert md is not None and cd is not None, "closures not recognised by the fused path"
     return fused.device_problem(md, cd, torch.device(DEV))
 
@@ -74,7 +90,8 @@ def test_proposal_draw_bit_exact(a, N, H, it, offset):
 
 # ------------------------------------------------------------------------------------------------ rollout
 @pytest.mark.parametrize("cid,over", [(2, dict(N=1000, H=20)), (3, dict(N=300, H=30)), (4, dict(N=200, H=7)),
-                                      (5, dict(N=40, H=6)), (2, dict(N=1, H=3)), (3, dict(N=17, H=2))])
+                                      (5, dict(N=40, H=6)), (2, dict(N=1, H=3)), (3, dict(N=17, H=2)),
+                                      (6, dict(N=300, H=12)), (6, dict(N=5000, H=4)), (6, dict(N=9000, H=3))])
 def test_rollout_costs_and_states_given_actions(cid, over):
     from mbrl_amd import fused
     p = ocem.synth_problem(cid, **over)
@@ -172,7 +189,7 @@ def test_refit_bit_exact(H, a, N, K):
 
 # ------------------------------------------------------------------------------------------------ whole planners
 CEM_CASES = [("config2_cem", 2, {}), ("config3_cem", 3, {}), ("config4_cem_N2048", 4, dict(N=2048)),
-             ("config5_cem_N256_H20", 5, dict(N=256, H=20))]
+             ("config5_cem_N256_H20", 5, dict(N=256, H=20)), ("config6_cem_N512_H10", 6, dict(N=512, H=10))]
 
 
 @pytest.mark.parametrize("name,cid,over", CEM_CASES, ids=[c[0] for c in CEM_CASES])
@@ -244,7 +261,7 @@ def test_cem_generic_path_matches_fused():
 
 
 # ------------------------------------------------------------------------------------------------ full sizes
-@pytest.mark.parametrize("cid", [3, 4, 5])
+@pytest.mark.parametrize("cid", [3, 4, 5, 6])
 def test_full_size_plan_sampled_candidates(cid):
     """BASELINE configs at full N/H/E: every iteration's returns for 48 random candidates are
     recomputed by the oracle from the counter RNG (size-independent check), elites are exactly the
@@ -329,3 +346,21 @@ def test_sharded_protocol_with_fused_ops_matches_single_gpu_plan(cid, N, H, worl
     assert torch.equal(res["mu"], single["mu"]) and torch.equal(res["sigma"], single["sigma"])
     assert torch.allclose(res["states"], single["states"], rtol=1e-5, atol=1e-5)
     assert fused is not None
+
+
+def test_random_shooting_with_reward_model():
+    """RewardAgent wiring through RandomShootingPlanner (agents.py:336-362 + planners.py:140-187): the
+    fused path rolls out with the reward head as the cost and takes the first argmin."""
+    from mbrl_amd import RandomShootingPlanner
+    p = ocem.synth_problem(6, N=700, H=8)
+    _, model_fn, cost_fn, sample_action = build(p)
+    np.random.seed(3)
+    states, actions = RandomShootingPlanner.plan(torch.from_numpy(p["s0"]), model_fn, cost_fn, sample_action, 8,
+                                                 num_trajectories=700)
+    np.random.seed(3)
+    flat = sample_action(batch_size=700 * 8).numpy()
+    A = flat.reshape(8, 700, 6)
+    costs, st = ocem.rollout(p["model"], p["norm"], p["cost"], p["s0"], A, store_states=True)
+    idx = ocem.rs_argmin(costs[0])
+    assert np.array_equal(actions.numpy(), A[:, idx])
+    assert np.allclose(states.numpy(), st[0, :, idx], rtol=1e-4, atol=1e-4)

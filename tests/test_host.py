@@ -96,3 +96,69 @@ def test_model_state_dict_compatible_with_reference_layout():
     assert sorted(m.state_dict()) == sorted(
         [f"linear{i}.{p}" for i in (1, 2, 3) for p in ("weight", "bias")])
     assert isinstance(functools.partial(m), functools.partial)
+
+
+def _reward_layers_combined(m):
+    lay = [(l.weight.detach().numpy(), l.bias.detach().numpy()) for l in m.linears()]
+    (ws, bs), (wr, br) = lay[-2], lay[-1]
+    return lay[:-2] + [(np.vstack([ws, wr]), np.concatenate([bs, br]))]
+
+
+def test_reward_problem_matches_oracle_and_reference_semantics():
+    """Config 6: synthetic ModelWithReward == oracle draw; the RewardAgent
+    closures (compose + itemgetter, agents.py:342-362) compute the oracle's next state and reward."""
+    from mbrl_amd import synthetic
+    prob = synthetic.make_problem(6, N=16, H=3)
+    p = ocem.synth_problem(6, N=16, H=3)
+    assert ocem.weights_sha256([_reward_layers_combined(prob["module"])]) == ocem.weights_sha256(p["model"])
+    assert np.array_equal(prob["stats"]["rewards"]["mean"].numpy(), p["norm"]["rew_mean"])
+    rng = np.random.default_rng(6)
+    s = rng.standard_normal((32, 17)).astype(np.float32)
+    a = rng.uniform(-1, 1, (32, 6)).astype(np.float32)
+    with torch.no_grad():
+        ns = prob["model"](torch.from_numpy(s), torch.from_numpy(a))
+        r = prob["cost"](ns, torch.from_numpy(a))
+    ref_ns = ocem.dynamics_step(p["model"][0], p["norm"], s, a)
+    assert np.allclose(ns.numpy(), ref_ns, rtol=1e-5, atol=1e-5)
+    assert r.shape == (32, 1)
+    assert np.allclose(r.numpy()[:, 0], ocem.reward_cost(p["model"][0], p["norm"], ref_ns, a), rtol=1e-5, atol=1e-5)
+
+
+def test_reward_closure_recognition():
+    import operator
+    from mbrl_amd import _lib, fused, models, synthetic
+    prob = synthetic.make_problem(6, N=16, H=3)
+    md = fused.describe_model(prob["model"])
+    assert md is not None and md["reward"] and (md["s"], md["a"], md["W"], md["L"]) == (17, 6, 512, 2)
+    assert md["norm"]["unnormalize_reward"] and md["norm"]["rew_std"].numel() == 1
+    assert fused.mlp_shape(md).reward_head == 1
+    cd = fused.describe_cost(prob["cost"], 17, md)
+    assert cd is not None and cd["kind"] == _lib.MBRL_COST_MODEL_REWARD
+    # the reward cost needs the model description of the same module
+    assert fused.describe_cost(prob["cost"], 17) is None
+    other = synthetic.make_problem(6, N=16, H=3)
+    assert fused.describe_cost(other["cost"], 17, md) is None
+    # itemgetter(1) as the model, or a goal-state model with a reward cost -> generic path
+    f = prob["cost"].__closure__
+    swapped = models.compose(functools.partial(prob["module"]), operator.itemgetter(1))
+    assert fused.describe_model(swapped) is None
+    assert f is not None
+    plain = synthetic.make_problem(3, N=8, H=2)
+    assert fused.describe_cost(prob["cost"], 17, fused.describe_model(plain["model"])) is None
+
+
+def test_reference_style_reward_model_duck_typed():
+    """The reference's ModelWithReward (linear1..4, models.py:125-141) is recognised by duck typing."""
+    import operator
+    from mbrl_amd import fused, models
+
+    class ModelWithReward(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.linear1 = torch.nn.Linear(9, 40)
+            self.linear2 = torch.nn.Linear(40, 40)
+            self.linear3 = torch.nn.Linear(40, 6)
+            self.linear4 = torch.nn.Linear(40, 1)
+            self.activation_fn = torch.nn.ReLU()
+    md = fused.describe_model(models.compose(functools.partial(ModelWithReward()), operator.itemgetter(0)))
+    assert md is not None and md["reward"] and (md["s"], md["a"], md["W"], md["L"]) == (6, 3, 40, 2)

@@ -44,7 +44,8 @@ def test_config1_random_shooting(golden):
 
 
 CEM_CASES = [("config2_cem", 2, {}), ("config3_cem", 3, {}), ("config4_cem_N2048", 4, dict(N=2048)),
-             ("config5_cem_N256_H20", 5, dict(N=256, H=20))]
+             ("config5_cem_N256_H20", 5, dict(N=256, H=20)),
+             ("config6_cem_N512_H10", 6, dict(N=512, H=10))]   # reward head: ModelWithReward + RewardAgent cost
 
 
 @pytest.mark.parametrize("name,cid,over", CEM_CASES, ids=[c[0] for c in CEM_CASES])

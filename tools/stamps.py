@@ -31,7 +31,7 @@ def main():
     lib.mbrl_diag_set_stamps.argtypes = [ctypes.c_void_p]
     dev = torch.device("cuda", 0)
     md = fused.describe_model(prob["model"])
-    cd = fused.describe_cost(prob["cost"], md["s"])
+    cd = fused.describe_cost(prob["cost"], md["s"], md)
     p = fused.device_problem(md, cd, dev)
     R = 2 if (N >= 2 * 16 * 256 and md["W"] <= 512) else 1
     tiles = (N + 16 * R - 1) // (16 * R)
