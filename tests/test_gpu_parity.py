@@ -364,3 +364,18 @@ def test_random_shooting_with_reward_model():
     idx = ocem.rs_argmin(costs[0])
     assert np.array_equal(actions.numpy(), A[:, idx])
     assert np.allclose(states.numpy(), st[0, :, idx], rtol=1e-4, atol=1e-4)
+
+
+def test_mpc_policy_drives_the_planner_like_the_reference_agent():
+    """agents.py:29-56: plan per step, act with actions[0], reset at timestep 0."""
+    from mbrl_amd import CEMPlanner, MPCPolicy
+    p = ocem.synth_problem(3, N=512, H=6)
+    _, model_fn, cost_fn, sample_action = build(p)
+    pol = MPCPolicy(model_fn, cost_fn, CEMPlanner, sample_action, 6, num_candidates=512, seed=p["rng_seed"])
+    obs = torch.from_numpy(p["s0"])
+    a0 = pol.get_action({"timestep": 0, "observation": obs})
+    ref = ocem.cem_plan(p, N=512, H=6)
+    assert a0.shape == (6,) and np.array_equal(a0.numpy(), ref["final_actions"][0])
+    assert pol.last_trajectory[0].shape == (6, 17)
+    a1 = pol.get_action({"timestep": 1, "observation": pol.last_trajectory[0][0]})
+    assert a1.shape == (6,) and torch.isfinite(a1).all()

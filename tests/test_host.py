@@ -162,3 +162,26 @@ def test_reference_style_reward_model_duck_typed():
             self.activation_fn = torch.nn.ReLU()
     md = fused.describe_model(models.compose(functools.partial(ModelWithReward()), operator.itemgetter(0)))
     assert md is not None and md["reward"] and (md["s"], md["a"], md["W"], md["L"]) == (6, 3, 40, 2)
+
+
+def test_mpc_policy_host_logic():
+    """agents.py:37-56: reset at timestep 0, (states[1:], actions[0:]) as initial_trajectory, act with
+    actions[0]; kwargs are forwarded to the planner."""
+    from mbrl_amd import MPCPolicy
+    calls = []
+
+    class FakePlanner:
+        @staticmethod
+        def plan(initial_state, model, cost, sample_action, horizon, initial_trajectory=None, **kw):
+            calls.append((initial_trajectory, kw))
+            k = len(calls)
+            return torch.full((horizon, 2), float(k)), torch.full((horizon, 1), 10.0 * k)
+
+    pol = MPCPolicy(None, None, FakePlanner, None, 4, num_candidates=64)
+    a = pol.get_action({"timestep": 0, "observation": torch.zeros(2)})
+    assert a.tolist() == [10.0] and calls[0][0] is None and calls[0][1] == {"num_candidates": 64}
+    pol.get_action({"timestep": 1, "observation": torch.zeros(2)})
+    it = calls[1][0]
+    assert it[0].shape == (3, 2) and it[1].shape == (4, 1) and float(it[1][0, 0]) == 10.0
+    pol.get_action({"timestep": 0, "observation": torch.zeros(2)})
+    assert calls[2][0] is None
