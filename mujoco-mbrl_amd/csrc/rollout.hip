@@ -383,7 +383,10 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
             }
         }
         STAMP(0);
-        hidden_store<TW, R>(acc, bias, actY, A.lda, wave, lane);
+        // The last hidden layer's activations stay in registers: the output layer splits K by wave,
+        // so wave w only needs the columns it produced itself, in exactly the accumulator layout
+        // (lane: 4 consecutive units of candidate lane & 15). No LDS store, barrier or re-read.
+        if (A.L > 1) hidden_store<TW, R>(acc, bias, actY, A.lda, wave, lane);
         STAMP(1);
         // ---- hidden layers 1..L-1 (W -> W), alternating Y->X->Y...
         float* in = actY;
@@ -397,19 +400,18 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
 #pragma unroll
             for (int kc = 0; kc < KH; ++kc) MBRL_HIDDEN_CHUNK((S0 + kc) % NB, kc, KH, in);
             STAMP(2);
-            hidden_store<TW, R>(acc, bias, out, A.lda, wave, lane);
+            if (l + 1 < A.L) hidden_store<TW, R>(acc, bias, out, A.lda, wave, lane);
             STAMP(3);
             float* tmp = in; in = out; out = tmp;
         }
         // ---- output layer: W -> s, K split over the 4 waves, partials through LDS
         {
             f32x4 aout[R][TW];
+            const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int r = 0; r < R; ++r)
 #pragma unroll
-                for (int kc = 0; kc < TW; ++kc)
-                    aout[r][kc] = *reinterpret_cast<const f32x4*>(
-                        in + (16 * r + (lane & 15)) * A.lda + wave * 16 * TW + 16 * kc + 4 * (lane >> 4));
+                for (int kc = 0; kc < TW; ++kc) aout[r][kc] = __builtin_elementwise_max(acc[r][kc] + bias[kc], zero4);
             float* part = L.part + wave * M * A.pw;
 #define MBRL_OUT_CHUNK(SLOT, J)                                                   \
     do {                                                                          \
