@@ -283,10 +283,17 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
     float* const actY = L.act2;
 
     const bool epi = wave < 4;   // epilogue waves
+    // 8 waves, goal-state cost: waves 4-7 own the actions (fetch, normalise, CoshLoss) for the rows
+    // of wave w-4, in parallel with waves 0-3's state epilogue; the per-row action cost crosses
+    // through LDS (acs[t & 1][m]), so the return still accumulates sc_t + ac_t in t order.
+    const bool split = NW == 8 && !A.reward;
+    const bool actw = split ? wave >= 4 : epi;    // waves holding the action registers
+    const int awave = split ? wave - 4 : wave;     // their row mapping (epi_row of wave w - 4)
+    float* acs = L.aterm;                          // [2][M] per-row action cost (split mode)
     // ---- prologue: parameters into LDS, s0 and a_0 into the MLP input
     float av[R][MAX_A_PER_LANE];
     float acp[R];  // this lane's share of the current step's CoshLoss sum, per row
-    if (epi) fetch_actions<R>(A, tile, 0, wave, lane, av);
+    if (actw) fetch_actions<R>(A, tile, 0, awave, lane, av);
     for (int i = tid; i < A.s; i += NT) {
         L.obs_mean[i] = A.obs_mean ? A.obs_mean[i] : 0.f;
         L.obs_std[i] = A.obs_std ? A.obs_std[i] : 1.f;
@@ -312,7 +319,15 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
     }
     EpiParams<SS> P;
     load_epi_params<SS>(A, L, lane, P);
-    if (epi) stage_actions<R, SS>(A, P, actX, L.aterm, wave, lane, av, acp);
+    if (actw) {
+        stage_actions<R, SS>(A, P, actX, L.aterm, awave, lane, av, acp);
+        if (split)
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const float v = rowsum16(acp[r]);      // all 16 lanes of the row take part in the DPP sum
+                if ((lane & 15) == 0) acs[epi_row(r, awave, lane)] = v;
+            }
+    }
     // reward-head models: two MLP passes per step (state pass on (s_t, a_t), reward pass on
     // (s_{t+1}, a_t)); the normalised s_{t+1} and a_t are kept in LDS across the passes
     const int npass = A.reward ? 2 : 1;
@@ -367,7 +382,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
         const int pass = A.reward ? (tp & 1) : 0;
         int g = 0;
         // a_{t+1} from HBM now; consumed in this step's (last) epilogue
-        if (epi && pass == 0 && t + 1 < A.H) fetch_actions<R>(A, tile, t + 1, wave, lane, av);
+        if (actw && pass == 0 && t + 1 < A.H) fetch_actions<R>(A, tile, t + 1, awave, lane, av);
         // ---- layer 0: actX [s | a | 0-pad] -> actY (W)
         zero_acc<TW, R>(acc);
         load_bias<TW>(bias, L.hbias, wave, lane);
@@ -515,10 +530,18 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
                 }
                 for (int d = A.s + A.a + j; d < A.s + A.a + A.k0pad_extra; d += 16) actX[m * A.lda + d] = 0.f;
                 sc = rowsum16(sc);
-                const float ac = rowsum16(acp[r]);
+                const float ac = split ? acs[(t & 1) * M + m] : rowsum16(acp[r]);
                 total[r] += sc + A.alpha_a2 * (ac / (float)A.a);
             }
-            if (t + 1 < A.H) stage_actions<R, SS>(A, P, actX, L.aterm, wave, lane, av, acp);
+            if (!split && t + 1 < A.H) stage_actions<R, SS>(A, P, actX, L.aterm, wave, lane, av, acp);
+        } else if (split && actw && t + 1 < A.H) {
+            // waves 4-7, concurrently: a_{t+1} into the next MLP input, its CoshLoss row sum into LDS
+            stage_actions<R, SS>(A, P, actX, L.aterm, awave, lane, av, acp);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const float v = rowsum16(acp[r]);
+                if ((lane & 15) == 0) acs[((t + 1) & 1) * M + epi_row(r, awave, lane)] = v;
+            }
         }
         __syncthreads();
         STAMP(6);
