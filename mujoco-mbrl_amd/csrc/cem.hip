@@ -153,10 +153,10 @@ __device__ __forceinline__ uint32_t order_key(float v, int nan_policy) {
 __global__ void __launch_bounds__(1024) select_kernel(const float* __restrict__ costs, int E, int N, int K,
                                                       int nan_policy, int64_t* __restrict__ elite_idx,
                                                       float* __restrict__ returns_out, uint32_t* __restrict__ keys) {
-    __shared__ uint32_t hist[256];
+    __shared__ uint32_t hist[16][257];   // per-wave rows, padded (no cross-wave bank collisions)
     __shared__ uint32_t scan_ws[16];
     __shared__ uint32_t sel[3];  // prefix, bucket, remaining k
-    const int tid = threadIdx.x, nt = blockDim.x;
+    const int tid = threadIdx.x, nt = blockDim.x, wave = tid >> 6;
     for (int n = tid; n < N; n += nt) {
         float r = costs[n];
         if (E > 1) {
@@ -169,15 +169,29 @@ __global__ void __launch_bounds__(1024) select_kernel(const float* __restrict__ 
     uint32_t prefix = 0, mask = 0, kk = (uint32_t)K;
     __syncthreads();
     for (int shift = 24; shift >= 0; shift -= 8) {
-        if (tid < 256) hist[tid] = 0;
+        for (int i = tid; i < 16 * 257; i += nt) (&hist[0][0])[i] = 0;
         __syncthreads();
-        for (int n = tid; n < N; n += nt) {
-            const uint32_t k = keys[n];
-            if ((k & mask) == prefix) atomicAdd(&hist[(k >> shift) & 255u], 1u);
+        for (int n0 = 0; n0 < N; n0 += nt) {        // wave-uniform trip count (ballots below)
+            const int n = n0 + tid;
+            const uint32_t k = n < N ? keys[n] : 0u;
+            const bool pending = n < N && (k & mask) == prefix;
+            const uint32_t dig = (k >> shift) & 255u;
+            const uint64_t act = __ballot(pending);
+            if (act != 0) {
+                const int leader = __builtin_ctzll(act);
+                const uint32_t d0 = __shfl(dig, leader, 64);
+                if (__ballot(pending && dig == d0) == act) {   // clustered: one add per wave
+                    if ((tid & 63) == leader) atomicAdd(&hist[wave][d0], (uint32_t)__popcll(act));
+                } else if (pending) {
+                    atomicAdd(&hist[wave][dig], 1u);
+                }
+            }
         }
         __syncthreads();
         uint32_t tot;
-        const uint32_t h = tid < 256 ? hist[tid] : 0u;
+        uint32_t h = 0;
+        if (tid < 256)
+            for (int w = 0; w < nt / 64; ++w) h += hist[w][tid];
         const uint32_t before = block_exclusive_scan(h, scan_ws, &tot);
         if (tid < 256 && before < kk && before + h >= kk) { sel[0] = (uint32_t)tid; sel[1] = before; }
         __syncthreads();

@@ -146,7 +146,8 @@ def test_dynamics_forward_matches_oracle_step():
 def test_select_matches_stable_argsort_with_ties_nan_and_signed_zero():
     from mbrl_amd import _lib, fused
     rng = np.random.default_rng(0)
-    for N, K in [(1, 1), (10, 3), (1000, 100), (4096, 409), (32768, 3276), (5000, 5000), (70001, 7000)]:
+    for N, K in [(1, 1), (10, 3), (1000, 100), (4096, 409), (32768, 3276), (5000, 5000), (70001, 7000),
+                 (250000, 25000)]:
         r = rng.integers(0, 50, size=N).astype(np.float32)      # heavy ties
         if N >= 10:
             r[rng.integers(0, N, size=N // 10 + 1)] = np.nan
@@ -379,3 +380,20 @@ def test_mpc_policy_drives_the_planner_like_the_reference_agent():
     assert pol.last_trajectory[0].shape == (6, 17)
     a1 = pol.get_action({"timestep": 1, "observation": pol.last_trajectory[0][0]})
     assert a1.shape == (6,) and torch.isfinite(a1).all()
+
+
+@pytest.mark.parametrize("cid,W,L", [(3, 50, 2), (6, 200, 2), (2, 100, 1), (3, 200, 3)])
+def test_reference_default_widths(cid, W, L):
+    """The reference's default widths (Model hidden_units=50, ModelWithReward 200; models.py:97,126)
+    are not multiples of 64: the packed stream zero-pads them. CEM plan vs the oracle, elites exact."""
+    from mbrl_amd import CEMPlanner
+    p = ocem.synth_problem(cid, N=640, H=7, W=W, L=L)
+    _, model_fn, cost_fn, sample_action = build(p)
+    res = CEMPlanner.plan_detailed(torch.from_numpy(p["s0"]), model_fn, cost_fn, sample_action, 7,
+                                   num_candidates=640, num_iterations=3, seed=p["rng_seed"], record=True)
+    ref = ocem.cem_plan(p, N=640, H=7, num_iterations=3)
+    for it in range(3):
+        assert rel_err(res["returns"][it], ref["returns"][it]) < RTOL, it
+        assert np.array_equal(res["elites"][it].cpu().numpy(), ref["elites"][it]), it
+    assert np.array_equal(res["mu"].cpu().numpy(), ref["mu"][-1])
+    assert np.allclose(res["states"].numpy(), ref["final_states"], rtol=1e-4, atol=1e-4)
