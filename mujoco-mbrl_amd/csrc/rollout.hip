@@ -287,7 +287,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
     // of wave w-4, in parallel with waves 0-3's state epilogue; the per-row action cost crosses
     // through LDS (acs[t & 1][m]), so the return still accumulates sc_t + ac_t in t order.
     const bool split = NW == 8 && !A.reward;
-    const bool actw = split ? wave >= 4 : epi;    // waves holding the action registers
+    const bool actw = split ? (wave >= 4 && wave < 8) : epi;    // waves holding the action registers
     const int awave = split ? wave - 4 : wave;     // their row mapping (epi_row of wave w - 4)
     float* acs = L.aterm;                          // [2][M] per-row action cost (split mode)
     // ---- prologue: parameters into LDS, s0 and a_0 into the MLP input
@@ -510,6 +510,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
                     float o = L.part[ro] + L.part[ws + ro] + L.part[2 * ws + ro] + L.part[3 * ws + ro];
                     if constexpr (NW == 8)
                         o = o + ((L.part[4 * ws + ro] + L.part[5 * ws + ro]) + (L.part[6 * ws + ro] + L.part[7 * ws + ro]));
+
                     o = o + bo;
                     const float sn = A.unnorm_s ? o * os + om : o;
                     if (A.has_sc) {
@@ -585,7 +586,8 @@ static hipError_t launch_rollout_tr(const RolloutArgs& A_in, hipStream_t stream)
 template <int T, int R>
 static hipError_t launch_rollout_t(const RolloutArgs& A, hipStream_t stream) {
     // two waves per SIMD (8 waves, T/2 tiles each) where the tile count and LDS allow it
-    constexpr int NW = (T >= 2 && R == 1 && MBRL_ROLLOUT_NW == 8) ? 8 : 4;
+    // (16 waves, T/4 tiles each, measured 8 % slower than 8: the 128-VGPR budget spills)
+    constexpr int NW = (T >= 2 && R == 1 && MBRL_ROLLOUT_NW >= 8) ? 8 : 4;
     if constexpr (4 * T / NW <= 8) {  // the 4-deep ring needs 4*TW*4 VGPRs
         if (A.K0C == 2 && A.NOT == 2) return launch_rollout_tr<T, R, 2, 2, NW>(A, stream);
         if (A.K0C == 6 && A.NOT == 6) return launch_rollout_tr<T, R, 6, 6, NW>(A, stream);

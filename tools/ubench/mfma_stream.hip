@@ -224,14 +224,14 @@ void run_spec(const f32x4* w, float* out, unsigned long long* cyc, const char* n
 // Two waves per SIMD, each with half the tiles (T = 4) and its own weight loads (8 waves / CU):
 // per-SIMD MFMA rate when another wave can issue MFMAs while one issues its loads.
 template <int NT>
-__global__ void __launch_bounds__(512) dual(const f32x4* __restrict__ w, int chunks, float* out,
+__global__ void __launch_bounds__(64 * 32 / NT) dual(const f32x4* __restrict__ w, int chunks, float* out,
                                             unsigned long long* cyc) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     f32x4 acc[NT];
     for (int j = 0; j < NT; ++j) acc[j] = f32x4{0, 0, 0, 0};
     f32x4 ring[4][NT];
     const f32x4* p = w + wave * NT * 64 + lane;
-    const int cs = 8 * NT * 64;
+    const int cs = 32 * 64;   // one chunk = 32 tiles x 1 KiB, whatever the waves-per-tile split
     const int wrap = 68;
     auto ld = [&](f32x4 (&b)[NT], int g) {
         g = g % wrap;
@@ -258,23 +258,24 @@ __global__ void __launch_bounds__(512) dual(const f32x4* __restrict__ w, int chu
     float sacc = 0;
     for (int j = 0; j < NT; ++j) sacc += acc[j].x + acc[j].y;
     if (sacc == 1234.5f) out[threadIdx.x] = sacc;
-    if (lane == 0) cyc[blockIdx.x * 8 + wave] = t1 - t0;
+    if (lane == 0) cyc[blockIdx.x * (32 / NT) + wave] = t1 - t0;
 }
 
 template <int NT>
 void run_dual(const f32x4* w, float* out, unsigned long long* cyc, const char* name) {
     const int chunks = 68 * 30;
+    const int nw = 32 / NT;                 // waves per workgroup; nw / 4 share each SIMD
     for (int rep = 0; rep < 2; ++rep) {
-        hipLaunchKernelGGL((dual<NT>), dim3(256), dim3(512), 0, 0, w, chunks, out, cyc);
+        hipLaunchKernelGGL((dual<NT>), dim3(256), dim3(64 * nw), 0, 0, w, chunks, out, cyc);
         hipDeviceSynchronize();
     }
-    unsigned long long h[2048];
-    hipMemcpy(h, cyc, sizeof(h), hipMemcpyDeviceToHost);
+    static unsigned long long h[256 * 16];
+    hipMemcpy(h, cyc, sizeof(unsigned long long) * 256 * nw, hipMemcpyDeviceToHost);
     double s = 0;
-    for (int i = 0; i < 2048; ++i) s += h[i];
-    s /= 2048;
-    // two waves share a SIMD: per-SIMD cycles per MFMA = wave time / (2 * chunks * 4 * NT)
-    printf("%-44s cycles/MFMA per SIMD %.2f  (ideal 32)\n", name, s / (2.0 * chunks * 4 * NT));
+    for (int i = 0; i < 256 * nw; ++i) s += h[i];
+    s /= 256 * nw;
+    // nw/4 waves share a SIMD: per-SIMD cycles per MFMA = wave time / ((nw/4) * chunks * 4 * NT)
+    printf("%-44s cycles/MFMA per SIMD %.2f  (ideal 32)\n", name, s / ((nw / 4.0) * chunks * 4 * NT));
 }
 
 int main() {
@@ -299,6 +300,8 @@ int main() {
     run_spec<1, 4>(w, out, cyc, "spec: + streamer global_load sink, sleep 4");
     run_spec<2, 0>(w, out, cyc, "spec: + streamer LDS-DMA, ds_read, sleep 0");
     run_spec<2, 4>(w, out, cyc, "spec: + streamer LDS-DMA, ds_read, sleep 4");
+    run_dual<8>(w, out, cyc, "dual: 1 wave/SIMD x 8 tiles, own loads");
     run_dual<4>(w, out, cyc, "dual: 2 waves/SIMD x 4 tiles, own loads");
+    run_dual<2>(w, out, cyc, "dual: 4 waves/SIMD x 2 tiles, own loads");
     return 0;
 }
