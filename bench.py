@@ -96,12 +96,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # one GPU per rank; on a box with fewer GPUs than ranks (a gloo rehearsal, MBRL_DIST_BACKEND=gloo)
+    # ranks share devices round-robin
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local_rank % ndev)
+    torch.cuda.set_device(dev)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("MBRL_DIST_BACKEND", "nccl")     # nccl == RCCL over xGMI on ROCm
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from mbrl_amd import CEMPlanner, synthetic
     prob = synthetic.make_problem(args.config)

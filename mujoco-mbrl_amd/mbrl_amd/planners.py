@@ -309,7 +309,14 @@ class _FusedShardOps:
 
     def all_gather(self, out_flat, local):
         import torch.distributed as dist
-        dist.all_gather_into_tensor(out_flat, local.reshape(-1))
+        if dist.get_backend() == "gloo":
+            # host-staged for gloo (CPU rehearsals of the sharded path on a shared GPU); RCCL gathers
+            # device memory directly
+            host = torch.empty(out_flat.shape, dtype=out_flat.dtype)
+            dist.all_gather_into_tensor(host, local.reshape(-1).cpu())
+            out_flat.copy_(host)
+        else:
+            dist.all_gather_into_tensor(out_flat, local.reshape(-1))
 
     def select(self, costs, K, returns_out):
         return fused.select(costs, K, returns_out=returns_out, workspace=self._sel_ws)

@@ -2,6 +2,7 @@
 vectors. Bars: bit-exact for the RNG draw, elite index sets, argmin and the refit's mu / sigma;
 returns within 1e-5 relative (BASELINE.json north_star) against max(|ref|, 1)."""
 import functools
+import os
 
 import numpy as np
 import pytest
@@ -397,3 +398,46 @@ def test_reference_default_widths(cid, W, L):
         assert np.array_equal(res["elites"][it].cpu().numpy(), ref["elites"][it]), it
     assert np.array_equal(res["mu"].cpu().numpy(), ref["mu"][-1])
     assert np.allclose(res["states"].numpy(), ref["final_states"], rtol=1e-4, atol=1e-4)
+
+
+def _sharded_worker(rank, world, init_file, out_dir):
+    import os
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [repo, os.path.join(repo, "mujoco-mbrl_amd")]
+    import torch.distributed as dist
+    from mbrl_amd import CEMPlanner
+    from oracle import cem as oc
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    try:
+        p = oc.synth_problem(3, N=1024, H=8)
+        _, model_fn, cost_fn, sample_action = build(p)
+        res = CEMPlanner.plan_detailed(torch.from_numpy(p["s0"]), model_fn, cost_fn, sample_action, 8,
+                                       num_candidates=1024, num_iterations=3, seed=p["rng_seed"], record=True,
+                                       distributed=True, device="cuda:0")
+        np.savez(os.path.join(out_dir, f"r{rank}.npz"), mu=res["mu"].cpu().numpy(), sigma=res["sigma"].cpu().numpy(),
+                 elites=res["elites"].cpu().numpy(), states=res["states"].numpy(), actions=res["actions"].numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_plan_two_processes_on_one_gpu():
+    """The real multi-process sharded path (CEMPlanner(distributed=True), fused ops, a process group)
+    with two ranks sharing this GPU over gloo: bit-identical to the single-process plan."""
+    import tempfile
+    import torch.multiprocessing as mp
+    from mbrl_amd import CEMPlanner
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_sharded_worker, args=(2, os.path.join(d, "pg"), d), nprocs=2, join=True,
+                           start_method="spawn")
+        got = [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(2)]
+    p = ocem.synth_problem(3, N=1024, H=8)
+    _, model_fn, cost_fn, sample_action = build(p)
+    ref = CEMPlanner.plan_detailed(torch.from_numpy(p["s0"]), model_fn, cost_fn, sample_action, 8,
+                                   num_candidates=1024, num_iterations=3, seed=p["rng_seed"], record=True)
+    for g in got:
+        assert np.array_equal(g["elites"], ref["elites"].cpu().numpy())
+        assert np.array_equal(g["mu"], ref["mu"].cpu().numpy()) and np.array_equal(g["sigma"], ref["sigma"].cpu().numpy())
+        assert np.array_equal(g["actions"], ref["actions"].numpy())
+        assert np.allclose(g["states"], ref["states"].numpy(), rtol=1e-5, atol=1e-5)
