@@ -241,7 +241,8 @@ def cem_sharded_protocol(ops, st, world, rank):
     refit regenerates the elites' actions from the counter RNG, so no moment collective is needed
     and mu / sigma are bit-identical on every rank and for every G.
 
-    ops: .device; .rollout(it, mu, sigma, n_offset, n_local, costs_out[E, n_local]);
+    ops: .device; .rollout(it, mu, sigma, n_offset, n_local, costs_out[E, n_local], events) (events: None
+    or a (start, end) pair to record around the rollout kernel alone);
     .all_gather(out_flat[G*E*n_local], local[E, n_local]); .select(costs[E, N], K, returns_out) -> elites;
     .refit(it, mu, sigma, elites, mu_out, sigma_out); .trajectory(actions[H, a]) -> states[H, s].
     The fused path binds them to the HIP extension + RCCL; tests bind them to the CPU oracle + gloo."""
@@ -259,11 +260,7 @@ def cem_sharded_protocol(ops, st, world, rank):
     hist = dict(costs=[], returns=[], elites=[])
     events = st["events"]
     for it in range(I):
-        if events is not None:
-            events[it][0].record()
-        ops.rollout(it, mu, sigma, rank * Nl, Nl, local)
-        if events is not None:
-            events[it][1].record()
+        ops.rollout(it, mu, sigma, rank * Nl, Nl, local, None if events is None else events[it])
         ops.all_gather(gathered, local)
         # candidate r*Nl + j lives at gathered[r, :, j]
         costs = gathered.view(world, E, Nl).permute(1, 0, 2).reshape(E, N) if world > 1 else gathered.view(E, N)
@@ -300,12 +297,17 @@ class _FusedShardOps:
     def _sampler(self, it, mu, sigma):
         return fused.make_sampler(self.st["seed"], it, mu, sigma, self.st["lo"], self.st["hi"])
 
-    def rollout(self, it, mu, sigma, n_offset, n_local, costs_out):
+    def rollout(self, it, mu, sigma, n_offset, n_local, costs_out, events=None):
         H, a = self.st["H"], self.prob.mdesc["a"]
         if self._acts is None or self._acts.shape[1] != n_local:
             self._acts = torch.empty((H, n_local, a), dtype=torch.float32, device=self.device)
-        fused.rollout(self.prob, self.s0, n_local, H, sampler=self._sampler(it, mu, sigma), n_offset=n_offset,
-                      costs=costs_out, actions_out=self._acts)
+        # proposal draw, then the rollout kernel alone between the events (bench.py's roofline)
+        fused.sample_actions(self._sampler(it, mu, sigma), H, a, n_local, n_offset, self._acts)
+        if events is not None:
+            events[0].record()
+        fused.rollout(self.prob, self.s0, n_local, H, actions=self._acts, costs=costs_out)
+        if events is not None:
+            events[1].record()
 
     def all_gather(self, out_flat, local):
         import torch.distributed as dist

@@ -331,9 +331,9 @@ def test_sharded_protocol_with_fused_ops_matches_single_gpu_plan(cid, N, H, worl
               seed=p["rng_seed"], record=True, events=None)
 
     class AllShardsOps(planners._FusedShardOps):
-        def rollout(self, it, mu, sigma, n_offset, n_local, costs_out):
+        def rollout(self, it, mu, sigma, n_offset, n_local, costs_out, events=None):
             self._it_args = (it, mu, sigma)
-            super().rollout(it, mu, sigma, n_offset, n_local, costs_out)
+            super().rollout(it, mu, sigma, n_offset, n_local, costs_out, events)
 
         def all_gather(self, out_flat, local):
             it, mu, sigma = self._it_args

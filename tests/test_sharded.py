@@ -30,7 +30,7 @@ class OracleShardOps:
         st = self.st
         return self.cem_actions(mu.numpy(), sigma.numpy(), st["lo"], st["hi"], st["seed"], it, idx)
 
-    def rollout(self, it, mu, sigma, n_offset, n_local, costs_out):
+    def rollout(self, it, mu, sigma, n_offset, n_local, costs_out, events=None):
         A = self._draw(it, mu, sigma, np.arange(n_offset, n_offset + n_local))
         p = self.p
         costs_out.copy_(torch.from_numpy(self.ocem.rollout(p["model"], p["norm"], p["cost"], p["s0"], A)))
