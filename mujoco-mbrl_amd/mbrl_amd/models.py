@@ -8,16 +8,88 @@ reference's arithmetic.
 """
 import functools
 
+import numpy as np
 import torch
 import torch.nn as nn
 
 
+def _epoch_batches(dataset, batch_size):
+    """The batches DataLoader(dataset, batch_size, sampler=TransitionsSampler(dataset)) yields
+    (models.py:61-63), as row indices into dataset.stacked(): same sampler, same NumPy RNG draw."""
+    from .data import TransitionsSampler
+    index = dataset.transition_index()
+    pos = {t: i for i, t in enumerate(index)}
+    order = [pos[t] for t in TransitionsSampler(dataset)]
+    return [order[i:i + batch_size] for i in range(0, len(order), batch_size)]
+
+
+def _device_of(module):
+    return next(module.parameters()).device
+
+
+def _train_loop(model, dataset, optimizer, batch_size, num_epochs, step_loss, writer, tags):
+    """models.py:53-93 / 165-217 on the model's device: per batch, the loss summed over the horizon
+    steps, zero_grad, backward, step -- the reference's order of operations. Batches are gathered
+    from device-resident transitions (TransitionsDataset.stacked) instead of per-sample collation."""
+    dev = _device_of(model)
+    _, ins, outs = dataset.stacked(dev)
+    num_iters = 0
+    for _ in range(num_epochs):
+        for rows in _epoch_batches(dataset, batch_size):
+            idx = torch.as_tensor(rows, device=dev)
+            bi = [x.index_select(0, idx) for x in ins]
+            bo = [x.index_select(0, idx) for x in outs]
+            loss, parts = 0, [0] * len(tags)
+            for h in range(dataset.horizon):
+                terms = step_loss([x[:, h] for x in bi], [x[:, h] for x in bo])
+                for k, term in enumerate(terms):
+                    parts[k] = parts[k] + term
+                    loss = loss + term
+            optimizer.zero_grad()
+            loss.backward(retain_graph=True)
+            optimizer.step()
+            num_iters += 1
+            if writer is not None:
+                for tag, val in zip(tags, parts if len(tags) > 1 else [loss]):
+                    writer.add_scalar(tag.format(model.train_iterations), val, num_iters)
+                if len(tags) > 1:
+                    writer.add_scalar("loss/total/{}".format(model.train_iterations), loss, num_iters)
+    model.train_iterations += 1
+
+
 class DynamicsModel(nn.Module):
-    """models.py:8-29."""
+    """models.py:8-93."""
 
     def __init__(self):
         super().__init__()
         self.train_iterations = 0
+
+    def train_model(self, dataset, optimizer, batch_size=512, num_epochs=50, criterion=None, writer=None):
+        """models.py:53-93 (state_only / obs_only data modes: inputs (s, a), outputs (r, s'))."""
+        criterion = criterion or torch.nn.MSELoss()
+
+        def step_loss(inp, out):
+            (states, actions), (_, next_states) = inp, out
+            return [criterion(self.forward(states, actions, normalize_action=None, normalize_state=None,
+                                           unnormalize_state=None), next_states)]
+        _train_loop(self, dataset, optimizer, batch_size, num_epochs, step_loss, writer, ["loss/state/{}"])
+
+    def evaluate_model(self, dataset, batch_size, criterion=None):
+        """models.py:30-51: one criterion value per batch and horizon step."""
+        criterion = criterion or torch.nn.MSELoss()
+        dev = _device_of(self)
+        _, ins, outs = dataset.stacked(dev)
+        evals = []
+        with torch.no_grad():
+            for rows in _epoch_batches(dataset, batch_size):
+                idx = torch.as_tensor(rows, device=dev)
+                bi = [x.index_select(0, idx) for x in ins]
+                bo = [x.index_select(0, idx) for x in outs]
+                for h in range(dataset.horizon):
+                    hat = self.forward(bi[0][:, h], bi[1][:, h], normalize_action=None, normalize_state=None,
+                                       unnormalize_state=None)
+                    evals.append(np.asarray(criterion(hat, bo[1][:, h]).cpu()))
+        return evals
 
     def forward(self, state, action, normalize_action=None, normalize_state=None, unnormalize_state=None):
         if state.is_cuda and not torch.is_grad_enabled() and getattr(self, "noise", None) is None:
@@ -116,6 +188,18 @@ class ModelWithReward(nn.Module):
         for lin in lins[:self.n_hidden]:
             x = self.activation_fn(lin(x))
         return lins[-2](x), lins[-1](x)
+
+    def train_model(self, dataset, optimizer, batch_size=512, num_epochs=50, criterion=None, writer=None):
+        """models.py:165-217: state loss + reward loss per horizon step."""
+        criterion = criterion or torch.nn.MSELoss()
+
+        def step_loss(inp, out):
+            (states, actions), (rewards, next_states) = inp, out
+            s_hat, r_hat = self.forward(states, actions, normalize_action=None, normalize_state=None,
+                                        unnormalize_state=None, unnormalize_reward=None)
+            return [criterion(s_hat, next_states), criterion(r_hat, rewards.reshape(-1, 1))]
+        _train_loop(self, dataset, optimizer, batch_size, num_epochs, step_loss, writer,
+                    ["loss/state/{}", "loss/reward/{}"])
 
     def forward(self, state, action, normalize_state=None, unnormalize_state=None, normalize_action=None,
                 unnormalize_reward=None):

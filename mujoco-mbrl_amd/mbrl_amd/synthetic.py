@@ -79,7 +79,7 @@ def make_problem(config_id, **overrides):
         rr = np.random.Generator(np.random.PCG64(seed + 4))
         stats["rewards"] = {"mean": torch.from_numpy(rr.uniform(-0.5, 0.5, size=1).astype(np.float32)),
                             "std": torch.from_numpy(rr.uniform(0.5, 2.0, size=1).astype(np.float32))}
-    ds = data.TransitionsDataset(stats)
+    ds = data.TransitionsDataset.from_statistics(stats)
     if reward:                                                                         # agents.py:342-362
         model_fn = models.compose(functools.partial(module, **ds.normalizers(reward=True)), operator.itemgetter(0))
         cost_fn = models.compose(functools.partial(module, **ds.normalizers(reward=True)), operator.itemgetter(1))

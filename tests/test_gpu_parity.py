@@ -36,7 +36,7 @@ def build(problem):
                 lin.weight.copy_(torch.from_numpy(np.ascontiguousarray(w)))
                 lin.bias.copy_(torch.from_numpy(np.ascontiguousarray(b)))
         nm = problem["norm"]
-        ds = data.TransitionsDataset({k: {"mean": torch.from_numpy(nm[p + "_mean"]), "std": torch.from_numpy(nm[p + "_std"])}
+        ds = data.TransitionsDataset.from_statistics({k: {"mean": torch.from_numpy(nm[p + "_mean"]), "std": torch.from_numpy(nm[p + "_std"])}
                                       for k, p in (("observations", "obs"), ("actions", "act"), ("rewards", "rew"))})
         kw = ds.normalizers(reward=True)
         model_fn = models.compose(functools.partial(m, **kw), operator.itemgetter(0))
@@ -52,7 +52,7 @@ def build(problem):
         members.append(m)
     module = members[0] if len(members) == 1 else models.EnsembleModel(members)
     nm = problem["norm"]
-    ds = data.TransitionsDataset({"observations": {"mean": torch.from_numpy(nm["obs_mean"]),
+    ds = data.TransitionsDataset.from_statistics({"observations": {"mean": torch.from_numpy(nm["obs_mean"]),
                                                    "std": torch.from_numpy(nm["obs_std"])},
                                   "actions": {"mean": torch.from_numpy(nm["act_mean"]),
                                               "std": torch.from_numpy(nm["act_std"])}})

@@ -1,0 +1,87 @@
+"""Model training: mbrl_amd's TransitionsDataset / train_model against the
+reference's own (golden fixtures from tests/golden/make_golden_train.py).
+
+CPU: bit-exact final weights (same batches in the same order, the same torch ops). GPU: the same
+loop on the MI355X within a float tolerance (different GEMM summation order)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "golden"))
+import make_golden_train as mg  # noqa: E402
+
+
+def build(name, device):
+    from mbrl_amd import data, models
+    kind, mode, horizon, batch, epochs, opt, lr = mg.CASES[name]
+    rolls = [data.Rollout(states=[torch.from_numpy(x) for x in s], observations=[torch.from_numpy(x) for x in o],
+                          actions=[torch.from_numpy(x) for x in a], rewards=[torch.tensor(x) for x in r])
+             for s, o, a, r in mg.synth_rollouts()]
+    ds = data.TransitionsDataset(rollouts=rolls, horizon=horizon)
+    ds.set_data_mode(mode)
+    m = (models.Model(mg.S, mg.A, hidden_units=mg.W) if kind == "model"
+         else models.ModelWithReward(mg.O, mg.A, hidden_units=mg.W))
+    with torch.no_grad():
+        for lin, (w, b) in zip(m.linears(), mg.synth_weights(kind)):
+            lin.weight.copy_(torch.from_numpy(w))
+            lin.bias.copy_(torch.from_numpy(b))
+    m = m.to(device)
+    optimizer = (torch.optim.Adam(m.parameters(), lr=lr) if opt == "adam"
+                 else torch.optim.SGD(m.parameters(), lr=lr))
+    return m, ds, optimizer, batch, epochs, kind
+
+
+def run(name, device, golden):
+    g = golden(name)
+    m, ds, optimizer, batch, epochs, kind = build(name, device)
+    seed = int(g["np_seed"])
+    before = after = None
+    if kind == "model":
+        np.random.seed(seed - 1)
+        before = np.mean(m.evaluate_model(ds, batch_size=batch))
+    np.random.seed(seed)
+    m.train_model(dataset=ds, optimizer=optimizer, batch_size=batch, num_epochs=epochs)
+    if kind == "model":
+        np.random.seed(seed + 1)
+        after = np.mean(m.evaluate_model(ds, batch_size=batch))
+    got = [(l.weight.detach().cpu().numpy(), l.bias.detach().cpu().numpy()) for l in m.linears()]
+    ref = [(g[f"w{i}"], g[f"b{i}"]) for i in range(len(got))]
+    return got, ref, before, after, g
+
+
+@pytest.mark.parametrize("name", list(mg.CASES))
+def test_train_model_cpu_bit_exact_to_reference(golden, name):
+    got, ref, before, after, g = run(name, "cpu", golden)
+    for (w, b), (rw, rb) in zip(got, ref):
+        assert np.array_equal(w, rw) and np.array_equal(b, rb)
+    if before is not None:
+        assert before == np.float32(g["eval_before"]) and after == np.float32(g["eval_after"])
+
+
+def test_dataset_semantics():
+    from mbrl_amd import data
+    rolls = [data.Rollout(states=[torch.full((2,), float(i)) for i in range(5)],
+                          observations=[torch.full((3,), 10.0 + i) for i in range(5)],
+                          actions=[torch.full((1,), -float(i)) for i in range(4)],
+                          rewards=[torch.tensor(100.0 + i) for i in range(4)])]
+    ds = data.TransitionsDataset(rollouts=rolls, horizon=2, normalise=False)
+    assert len(ds) == 3 and ds.transition_index() == [(0, 0), (0, 1)]
+    ds.set_data_mode("state_only")
+    inp, out = ds[(0, 1)]
+    assert [float(x[0][0]) for x in inp] == [1.0, 2.0] and [float(x[1][0]) for x in inp] == [-1.0, -2.0]
+    assert [float(x[0]) for x in out] == [101.0, 102.0] and [float(x[1][0]) for x in out] == [2.0, 3.0]
+    assert torch.allclose(ds.statistics["rewards"]["mean"], torch.tensor(101.5))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", list(mg.CASES))
+def test_train_model_on_gpu_matches_reference(golden, name):
+    got, ref, before, after, g = run(name, "cuda:0", golden)
+    for (w, b), (rw, rb) in zip(got, ref):
+        assert np.allclose(w, rw, rtol=1e-4, atol=1e-5) and np.allclose(b, rb, rtol=1e-4, atol=1e-5)
+    if before is not None:
+        assert abs(before - g["eval_before"]) < 1e-5 and abs(after - g["eval_after"]) < 1e-5
