@@ -27,33 +27,90 @@ def _device_of(module):
     return next(module.parameters()).device
 
 
+def _batch_loss(dataset, ins, outs, idx, step_loss, n_parts):
+    bi = [x.index_select(0, idx) for x in ins]
+    bo = [x.index_select(0, idx) for x in outs]
+    loss, parts = 0, [0] * n_parts
+    for h in range(dataset.horizon):
+        for k, term in enumerate(step_loss([x[:, h] for x in bi], [x[:, h] for x in bo])):
+            parts[k] = parts[k] + term
+            loss = loss + term
+    return loss, parts
+
+
+class _GraphStep:
+    """A full-size batch's gather + forward + loss + backward captured once in a HIP graph (through
+    torch.cuda.CUDAGraph) and replayed per batch; optimizer.step() stays eager so any optimizer
+    works unchanged. The warm-up before capture only touches .grad (zeroed after), never the
+    parameters, so training follows exactly the eager sequence of updates."""
+
+    def __init__(self, model, dataset, ins, outs, batch_size, step_loss, n_parts):
+        dev = _device_of(model)
+        self.params = [p for p in model.parameters() if p.requires_grad]
+        self.idx = torch.zeros(batch_size, dtype=torch.long, device=dev)
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                loss, _ = _batch_loss(dataset, ins, outs, self.idx, step_loss, n_parts)
+                loss.backward()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        self._zero()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.loss, self.parts = _batch_loss(dataset, ins, outs, self.idx, step_loss, n_parts)
+            self.loss.backward()
+
+    def _zero(self):
+        grads = [p.grad for p in self.params if p.grad is not None]
+        if grads:
+            torch._foreach_zero_(grads)
+
+    def run(self, rows):
+        self.idx.copy_(rows)
+        self._zero()                      # backward accumulates into the captured .grad buffers
+        self.graph.replay()
+        return self.loss, self.parts
+
+
 def _train_loop(model, dataset, optimizer, batch_size, num_epochs, step_loss, writer, tags):
     """models.py:53-93 / 165-217 on the model's device: per batch, the loss summed over the horizon
     steps, zero_grad, backward, step -- the reference's order of operations. Batches are gathered
-    from device-resident transitions (TransitionsDataset.stacked) instead of per-sample collation."""
+    from device-resident transitions (TransitionsDataset.stacked) instead of per-sample collation;
+    on a GPU the full-size batches replay one captured graph (_GraphStep)."""
     dev = _device_of(model)
     _, ins, outs = dataset.stacked(dev)
+    n_parts = len(tags)
+    graph = None
+    if dev.type == "cuda" and len(dataset.transition_index()) >= batch_size:
+        try:
+            graph = _GraphStep(model, dataset, ins, outs, batch_size, step_loss, n_parts)
+        except RuntimeError:           # capture unsupported for this model / criterion: stay eager
+            graph = None
+            for p in model.parameters():
+                p.grad = None
     num_iters = 0
     for _ in range(num_epochs):
-        for rows in _epoch_batches(dataset, batch_size):
-            idx = torch.as_tensor(rows, device=dev)
-            bi = [x.index_select(0, idx) for x in ins]
-            bo = [x.index_select(0, idx) for x in outs]
-            loss, parts = 0, [0] * len(tags)
-            for h in range(dataset.horizon):
-                terms = step_loss([x[:, h] for x in bi], [x[:, h] for x in bo])
-                for k, term in enumerate(terms):
-                    parts[k] = parts[k] + term
-                    loss = loss + term
-            optimizer.zero_grad()
-            loss.backward(retain_graph=True)
+        batches = _epoch_batches(dataset, batch_size)
+        order = torch.as_tensor([r for b in batches for r in b], device=dev)
+        for i, rows in enumerate(batches):
+            idx = order[i * batch_size:i * batch_size + len(rows)]
+            if graph is not None and len(rows) == batch_size:
+                loss, parts = graph.run(idx)
+            else:
+                optimizer.zero_grad()
+                loss, parts = _batch_loss(dataset, ins, outs, idx, step_loss, n_parts)
+                loss.backward(retain_graph=True)
             optimizer.step()
             num_iters += 1
             if writer is not None:
-                for tag, val in zip(tags, parts if len(tags) > 1 else [loss]):
+                for tag, val in zip(tags, parts if n_parts > 1 else [loss]):
                     writer.add_scalar(tag.format(model.train_iterations), val, num_iters)
-                if len(tags) > 1:
+                if n_parts > 1:
                     writer.add_scalar("loss/total/{}".format(model.train_iterations), loss, num_iters)
+    if graph is not None:
+        for p in model.parameters():      # release the graph-pool grads; the eager path re-allocates
+            p.grad = None
     model.train_iterations += 1
 
 
