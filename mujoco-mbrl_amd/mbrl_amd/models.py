@@ -54,12 +54,16 @@ class _GraphStep:
             for _ in range(2):
                 loss, _ = _batch_loss(dataset, ins, outs, self.idx, step_loss, n_parts)
                 loss.backward()
+            del loss                      # drop the warm-up autograd graph before capturing
         torch.cuda.current_stream(dev).wait_stream(side)
         self._zero()
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.loss, self.parts = _batch_loss(dataset, ins, outs, self.idx, step_loss, n_parts)
             self.loss.backward()
+        # the replay accumulates into exactly these tensors; an eager step in between (the last,
+        # partial batch: optimizer.zero_grad() sets .grad to None) must not orphan them
+        self.grads = [p.grad for p in self.params]
 
     def _zero(self):
         grads = [p.grad for p in self.params if p.grad is not None]
@@ -68,7 +72,9 @@ class _GraphStep:
 
     def run(self, rows):
         self.idx.copy_(rows)
-        self._zero()                      # backward accumulates into the captured .grad buffers
+        for p, g in zip(self.params, self.grads):
+            p.grad = g
+        torch._foreach_zero_(self.grads)
         self.graph.replay()
         return self.loss, self.parts
 
