@@ -79,6 +79,37 @@ def _generic_costs(model, cost, s0, actions, H, N):
     return total.reshape(1, N).contiguous(), states
 
 
+class GradientDescentPlanner(ModelPlanner):
+    """planners.py:28-137: Adam(lr=0.01) on one action sequence through the learned dynamics, on the
+    GPU for recognised closures (mbrl_amd/gd.py), else the reference's loop on the given callables.
+    Returns lists of H+1 states [1, s] and H actions [1, a], as the reference does."""
+    defaults = dict(num_iterations=40, stop_condition=0.002)
+
+    @staticmethod
+    def plan(initial_state, model, cost, sample_action, horizon, initial_trajectory=None, **kwargs):
+        from . import gd
+        num_iterations = int(kwargs.get("num_iterations", GradientDescentPlanner.defaults["num_iterations"]))
+        stop_condition = float(kwargs.get("stop_condition", GradientDescentPlanner.defaults["stop_condition"]))
+        H = int(horizon)
+        mdesc, cdesc = gd.describe(model, cost)
+        if mdesc is not None and torch.cuda.is_available():
+            dev = _device(kwargs)
+            if initial_trajectory is None:
+                # planners.py:94: the nominal sequence (its states are not used for a deterministic model)
+                action_list = list(sample_action(batch_size=H).split(1, dim=0))
+            else:
+                action_list = initial_trajectory[1]
+            with torch.cuda.device(dev):
+                states, actions = gd.plan_device(initial_state, mdesc, cdesc, action_list, H, num_iterations,
+                                                 stop_condition, dev)
+        else:
+            states, actions = gd.plan_generic(initial_state, model, cost, sample_action, H, initial_trajectory,
+                                              num_iterations, stop_condition)
+        keep = kwargs.get("return_device", False)
+        states, actions = _to_host(states, keep), _to_host(actions, keep)
+        return list(states.split(1, 0)), list(actions.split(1, 0))
+
+
 class RandomShootingPlanner(ModelPlanner):
     """planners.py:140-216 on the GPU."""
     defaults = dict(num_trajectories=1000)

@@ -1,0 +1,69 @@
+"""GradientDescentPlanner against the reference's own planner (golden fixtures
+from tests/golden/make_golden_gd.py): the device restatement on the GPU, and the host loop on the
+callables on CPU."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import cem as ocem
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "golden"))
+import make_golden_gd as mgd  # noqa: E402
+
+
+def closures(cid, over):
+    import test_gpu_parity as tg
+    p = ocem.synth_problem(cid, **over)
+    _, model_fn, cost_fn, sample_action = tg.build(p)
+    return p, model_fn, cost_fn
+
+
+def plan(name, golden, device=None):
+    from mbrl_amd import GradientDescentPlanner
+    cid, over, H, iters, stop = mgd.CASES[name]
+    g = golden(name)
+    p, model_fn, cost_fn = closures(cid, over)
+    assert ocem.weights_sha256(p["model"]) == str(g["weights_sha256"])
+    A0 = g["init_actions"]
+    init = ([], [torch.from_numpy(A0[i:i + 1].copy()) for i in range(H)])
+    kw = dict(num_iterations=iters, stop_condition=stop)
+    if device is not None:
+        kw["device"] = device
+    states, actions = GradientDescentPlanner.plan(torch.from_numpy(p["s0"]), model_fn, cost_fn, None, H, init, **kw)
+    assert len(states) == H + 1 and len(actions) == H and states[0].shape == (1, p["cfg"]["s"])
+    return torch.cat(states).numpy(), torch.cat(actions).numpy(), g
+
+
+@pytest.mark.parametrize("name", list(mgd.CASES))
+def test_gd_host_loop_matches_reference(golden, name, monkeypatch):
+    """Unrecognised closures (forced here) run the reference's loop on the given callables."""
+    from mbrl_amd import gd
+    monkeypatch.setattr(gd, "describe", lambda model, cost: (None, None))
+    st, ac, g = plan(name, golden)
+    assert np.allclose(ac, g["actions"], rtol=1e-5, atol=1e-6)
+    assert np.allclose(st, g["states"], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", list(mgd.CASES))
+def test_gd_device_matches_reference(golden, name):
+    st, ac, g = plan(name, golden, device="cuda:0")
+    assert np.allclose(ac, g["actions"], rtol=1e-4, atol=1e-5), np.max(np.abs(ac - g["actions"]))
+    assert np.allclose(st, g["states"], rtol=1e-4, atol=1e-4), np.max(np.abs(st - g["states"]))
+
+
+@pytest.mark.gpu
+def test_gd_graph_replay_equals_eager():
+    from mbrl_amd import gd
+    p, model_fn, cost_fn = closures(3, dict(W=50, L=2))
+    mdesc, cdesc = gd.describe(model_fn, cost_fn)
+    A0 = mgd.initial_actions(10, 6)
+    acts = [torch.from_numpy(A0[i:i + 1].copy()) for i in range(10)]
+    dev = torch.device("cuda:0")
+    s1, a1 = gd.plan_device(torch.from_numpy(p["s0"]), mdesc, cdesc, acts, 10, 20, 0.0, dev, use_graph=True)
+    s2, a2 = gd.plan_device(torch.from_numpy(p["s0"]), mdesc, cdesc, acts, 10, 20, 0.0, dev, use_graph=False)
+    assert torch.equal(a1, a2) and torch.equal(s1, s2)

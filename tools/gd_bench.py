@@ -1,0 +1,46 @@
+"""GradientDescentPlanner timing: one plan (40 Adam iterations, no early
+stop) on the cheetah model (3x512, H=30) -- GPU (graph-replayed iteration) vs the reference's loop on
+CPU (torch threads = this process's share). One JSON line."""
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "mujoco-mbrl_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from mbrl_amd import gd, synthetic  # noqa: E402
+
+
+def main():
+    cid = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    iters = 40
+    torch.set_num_threads(min(16, len(os.sched_getaffinity(0))))
+    prob = synthetic.make_problem(cid)
+    H, a = prob["cfg"]["H"], prob["cfg"]["a"]
+    A0 = np.random.Generator(np.random.PCG64(99)).uniform(-0.5, 0.5, (H, a)).astype(np.float32)
+    acts = [torch.from_numpy(A0[i:i + 1].copy()) for i in range(H)]
+    out = dict(workload=f"GD plan {prob['cfg']['name']} H={H}, {iters} Adam iterations")
+    t0 = time.perf_counter()
+    gd.plan_generic(prob["s0"], prob["model"], prob["cost"], None, H, ([], acts), iters, 0.0)
+    out["cpu_ms_per_plan"] = (time.perf_counter() - t0) * 1e3
+    if torch.cuda.is_available():
+        md, cd = gd.describe(prob["model"], prob["cost"])
+        dev = torch.device("cuda:0")
+        gd.plan_device(prob["s0"], md, cd, acts, H, iters, 0.0, dev)          # warm-up
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        reps = 5
+        for _ in range(reps):
+            gd.plan_device(prob["s0"], md, cd, acts, H, iters, 0.0, dev)
+        torch.cuda.synchronize()
+        out["gpu_ms_per_plan"] = (time.perf_counter() - t0) * 1e3 / reps
+        out["speedup"] = out["cpu_ms_per_plan"] / out["gpu_ms_per_plan"]
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
