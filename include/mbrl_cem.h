@@ -188,6 +188,19 @@ int mbrl_cem_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_no
                   mbrl_event_t* rollout_events, void* workspace, size_t ws_bytes,
                   mbrl_stream_t stream);
 
+/* ---- batched planning: B independent CEM plans, one per initial state s0[b] (parallel environments
+ * feeding one GPU planner), in shared launches: one proposal draw, one rollout
+ * of B*N candidates, one segmented selection, one batched refit per iteration. Problem b's candidate
+ * n is global candidate b*N + n for the proposal RNG, so problem b's plan equals a single-problem
+ * plan whose candidates are drawn with n_offset = b*N. params->N, ->K are PER problem.
+ * s0: [B][s]; mu / sigma (optional): [B][H][a]; actions_out: [B][H][a] = clip(mu);
+ * states_out: [B][H][s] (member mean). */
+size_t mbrl_cem_plan_batch_workspace_bytes(const mbrl_mlp_shape* shape, const mbrl_cem_params* params, int32_t B);
+int mbrl_cem_plan_batch(const mbrl_mlp_shape* shape, const void* packed, const mbrl_norm* norm,
+                        const mbrl_cost* cost, const float* s0, int32_t B, const mbrl_cem_params* params,
+                        float* mu, float* sigma, float* actions_out, float* states_out, void* workspace,
+                        size_t ws_bytes, mbrl_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

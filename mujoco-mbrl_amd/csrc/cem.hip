@@ -152,7 +152,12 @@ __device__ __forceinline__ uint32_t order_key(float v, int nan_policy) {
 
 __global__ void __launch_bounds__(1024) select_kernel(const float* __restrict__ costs, int E, int N, int K,
                                                       int nan_policy, int64_t* __restrict__ elite_idx,
-                                                      float* __restrict__ returns_out, uint32_t* __restrict__ keys) {
+                                                      float* __restrict__ returns_out, uint32_t* __restrict__ keys,
+                                                      int member_stride) {
+    costs += (size_t)blockIdx.x * N;                   // segment b (see select_reg_kernel)
+    elite_idx += (size_t)blockIdx.x * K;
+    if (returns_out) returns_out += (size_t)blockIdx.x * N;
+    keys += (size_t)blockIdx.x * N;
     __shared__ uint32_t hist[16][257];   // per-wave rows, padded (no cross-wave bank collisions)
     __shared__ uint32_t scan_ws[16];
     __shared__ uint32_t sel[3];  // prefix, bucket, remaining k
@@ -160,7 +165,7 @@ __global__ void __launch_bounds__(1024) select_kernel(const float* __restrict__ 
     for (int n = tid; n < N; n += nt) {
         float r = costs[n];
         if (E > 1) {
-            for (int e = 1; e < E; ++e) r = __fadd_rn(r, costs[(size_t)e * N + n]);
+            for (int e = 1; e < E; ++e) r = __fadd_rn(r, costs[(size_t)e * member_stride + n]);
             r = __fdiv_rn(r, (float)E);
         }
         if (returns_out) returns_out[n] = r;
@@ -230,11 +235,17 @@ __global__ void __launch_bounds__(1024) select_kernel(const float* __restrict__ 
 // LDS; the LDS key array is reused for the per-wave radix histograms afterwards.
 constexpr int SEL_HIST_WORDS = 2 * 16 * 257;
 
+// Segmented over blockIdx.x (independent problems of N candidates each, batched planning): segment
+// b reads costs[e * member_stride + b * N + n] and writes elite_idx[b * K ..] (local indices) and
+// returns_out[b * N ..].
 template <int KPT>
 __global__ void __launch_bounds__(1024) select_reg_kernel(const float* __restrict__ costs, int E, int N, int K,
                                                           int nan_policy, int64_t* __restrict__ elite_idx,
-                                                          float* __restrict__ returns_out) {
+                                                          float* __restrict__ returns_out, int member_stride) {
     extern __shared__ __attribute__((aligned(16))) uint32_t sel_smem[];
+    costs += (size_t)blockIdx.x * N;
+    elite_idx += (size_t)blockIdx.x * K;
+    if (returns_out) returns_out += (size_t)blockIdx.x * N;
     uint32_t(*hist)[16][257] = reinterpret_cast<uint32_t(*)[16][257]>(sel_smem);  // [2][16][257], aliases keys
     __shared__ uint32_t scan_ws[16];
     __shared__ uint32_t sel[2];
@@ -252,7 +263,7 @@ __global__ void __launch_bounds__(1024) select_reg_kernel(const float* __restric
 #pragma unroll
             for (int k = 0; k < KPT; ++k) {
                 const int n = tid + 1024 * k;
-                if (n < N) r[k] = __fadd_rn(r[k], costs[(size_t)e * N + n]);
+                if (n < N) r[k] = __fadd_rn(r[k], costs[(size_t)e * member_stride + n]);
             }
 #pragma unroll
         for (int k = 0; k < KPT; ++k) {
@@ -423,10 +434,21 @@ __global__ void __launch_bounds__(REFIT_THREADS) refit_fused_kernel(
     uint64_t seed, int iteration, const float* __restrict__ mu, const float* __restrict__ sigma, float lo, float hi,
     int a, const int64_t* __restrict__ elite_idx, int K, float alpha, float oma, float* __restrict__ mu_out,
     float* __restrict__ sigma_out, float* __restrict__ fin_mu, float* __restrict__ fin_sigma,
-    float* __restrict__ fin_actions) {
+    float* __restrict__ fin_actions, int n_env) {
 #pragma clang fp contract(off)
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int t = blockIdx.x;
+    // batched planning: blockIdx.y = problem b, whose [H][a] distribution rows sit at b*H*a, whose
+    // K elites (local indices) at b*K, and whose candidates are global n = b*n_env + local
+    const int t = blockIdx.x, H = gridDim.x;
+    {
+        const size_t eo = (size_t)blockIdx.y * H * a;
+        mu += eo; sigma += eo; mu_out += eo; sigma_out += eo;
+        if (fin_mu) fin_mu += eo;
+        if (fin_sigma) fin_sigma += eo;
+        if (fin_actions) fin_actions += eo;
+        elite_idx += (size_t)blockIdx.y * K;
+    }
+    const uint32_t nbase = (uint32_t)blockIdx.y * (uint32_t)n_env;
     const int G = (a + 3) >> 2;
     const int nch = (K + ELITE_CHUNK - 1) / ELITE_CHUNK;
     float* ael = smem;                                   // [K][a]
@@ -435,7 +457,7 @@ __global__ void __launch_bounds__(REFIT_THREADS) refit_fused_kernel(
     float* musg = mean + ((a + 3) & ~3);                         // [2][a]: this step's mu, sigma
     uint32_t* eidx = reinterpret_cast<uint32_t*>(musg + 2 * ((a + 3) & ~3));  // [K]
     // stage every global operand first (all loads in flight together), then compute from LDS
-    for (int e = threadIdx.x; e < K; e += REFIT_THREADS) eidx[e] = (uint32_t)elite_idx[e];
+    for (int e = threadIdx.x; e < K; e += REFIT_THREADS) eidx[e] = nbase + (uint32_t)elite_idx[e];
     for (int d = threadIdx.x; d < a; d += REFIT_THREADS) {
         musg[d] = mu[t * a + d];
         musg[((a + 3) & ~3) + d] = sigma[t * a + d];
@@ -503,9 +525,11 @@ static size_t refit_fused_lds(int a, int K) {
     return ((((size_t)K * a + 3) & ~(size_t)3) + ((nch * a + 3) & ~(size_t)3) + 3 * a4 + (size_t)K) * sizeof(float);
 }
 
+// Batched planning: local candidate n belongs to problem n / n_env, whose distribution rows sit at
+// mu + (n / n_env) * H * a (n_env = N for a single problem).
 __global__ void sample_kernel(uint64_t seed, int iteration, const float* __restrict__ mu,
                               const float* __restrict__ sigma, float lo, float hi, int H, int a, int N,
-                              int n_offset, float* __restrict__ out) {
+                              int n_offset, float* __restrict__ out, int n_env) {
     const int G = (a + 3) >> 2;
     const size_t total = (size_t)H * N * G;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
@@ -514,10 +538,11 @@ __global__ void sample_kernel(uint64_t seed, int iteration, const float* __restr
         const int t = (int)(i / G / N);
         float z[4];
         cem_normal4(seed, (uint32_t)(n_offset + n), (uint32_t)t, (uint32_t)iteration, (uint32_t)g, z);
+        const size_t mo = (size_t)(n / n_env) * H * a + (size_t)t * a;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int d = 4 * g + j;
-            if (d < a) out[((size_t)t * N + n) * a + d] = cem_action(mu[t * a + d], sigma[t * a + d], z[j], lo, hi);
+            if (d < a) out[((size_t)t * N + n) * a + d] = cem_action(mu[mo + d], sigma[mo + d], z[j], lo, hi);
         }
     }
 }
@@ -562,11 +587,20 @@ static int shape_geometry(const mbrl_mlp_shape* sh, Geometry* g) {
 
 static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-static int sample_impl(const mbrl_sampler* sp, int H, int a, int N, int n_offset, float* out, hipStream_t stream) {
+__global__ void expand_rows_kernel(const float* __restrict__ src, int B, int n_rep, int s, float* __restrict__ dst) {
+    const size_t total = (size_t)B * n_rep * s;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t row = i / s;
+        dst[i] = src[(row / n_rep) * s + (i - row * s)];
+    }
+}
+
+static int sample_impl(const mbrl_sampler* sp, int H, int a, int N, int n_offset, float* out, hipStream_t stream,
+                       int n_env = 0) {
     const size_t total = (size_t)H * N * ((a + 3) / 4);
     const int blocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
     hipLaunchKernelGGL(sample_kernel, dim3(blocks), dim3(256), 0, stream, sp->seed, sp->iteration, sp->mu, sp->sigma,
-                       sp->lo, sp->hi, H, a, N, n_offset, out);
+                       sp->lo, sp->hi, H, a, N, n_offset, out, n_env > 0 ? n_env : N);
     return hip_check(hipGetLastError(), "sample launch");
 }
 
@@ -659,10 +693,13 @@ static int traj_impl(const Geometry& g, const void* packed, const mbrl_norm* nor
 }
 
 static int select_impl(const float* costs, int E, int N, int K, int nan_policy, int64_t* elite_idx,
-                       float* returns_out, void* ws, size_t ws_bytes, hipStream_t stream) {
+                       float* returns_out, void* ws, size_t ws_bytes, hipStream_t stream, int segments = 1) {
     if (!costs || !elite_idx || !ws) return fail(MBRL_EINVAL, "costs, elite_idx and workspace must be non-NULL");
-    if (N < 1 || K < 1 || K > N || E < 1) return fail(MBRL_EINVAL, "need 1 <= K (%d) <= N (%d), E >= 1", K, N);
-    if (ws_bytes < align256((size_t)N * 4)) return fail(MBRL_EWORKSPACE, "select workspace %zu < %zu", ws_bytes, align256((size_t)N * 4));
+    if (N < 1 || K < 1 || K > N || E < 1 || segments < 1)
+        return fail(MBRL_EINVAL, "need 1 <= K (%d) <= N (%d), E >= 1, segments >= 1", K, N);
+    const size_t need = align256((size_t)N * segments * 4);
+    if (ws_bytes < need) return fail(MBRL_EWORKSPACE, "select workspace %zu < %zu", ws_bytes, need);
+    const int member_stride = N * segments;
 #define MBRL_SEL(KPT)                                                                                       \
     if (N <= 1024 * (KPT)) {                                                                                \
         const size_t lds = 4 * (size_t)max(33 * 32 * (KPT), SEL_HIST_WORDS);                               \
@@ -673,20 +710,20 @@ static int select_impl(const float* costs, int E, int N, int K, int nan_policy, 
             if (err != hipSuccess) return hip_check(err, "select attribute");                               \
             attr_set = true;                                                                                \
         }                                                                                                   \
-        hipLaunchKernelGGL(select_reg_kernel<KPT>, dim3(1), dim3(1024), lds, stream, costs, E, N, K, nan_policy, \
-                           elite_idx, returns_out);                                                         \
+        hipLaunchKernelGGL(select_reg_kernel<KPT>, dim3(segments), dim3(1024), lds, stream, costs, E, N, K,  \
+                           nan_policy, elite_idx, returns_out, member_stride);                              \
         return hip_check(hipGetLastError(), "select launch");                                               \
     }
     MBRL_SEL(1) MBRL_SEL(2) MBRL_SEL(4) MBRL_SEL(8) MBRL_SEL(16) MBRL_SEL(32)
 #undef MBRL_SEL
-    hipLaunchKernelGGL(select_kernel, dim3(1), dim3(1024), 0, stream, costs, E, N, K, nan_policy, elite_idx,
-                       returns_out, static_cast<uint32_t*>(ws));
+    hipLaunchKernelGGL(select_kernel, dim3(segments), dim3(1024), 0, stream, costs, E, N, K, nan_policy, elite_idx,
+                       returns_out, static_cast<uint32_t*>(ws), member_stride);
     return hip_check(hipGetLastError(), "select launch");
 }
 
 static int refit_impl(const mbrl_sampler* sp, int H, int a, const int64_t* elite_idx, int K, float alpha,
                       float* aelite, float* mu_out, float* sigma_out, hipStream_t stream, float* fin_mu = nullptr,
-                      float* fin_sigma = nullptr, float* fin_actions = nullptr) {
+                      float* fin_sigma = nullptr, float* fin_actions = nullptr, int B = 1, int n_env = 0) {
     if (!sp || !sp->mu || !sp->sigma || !elite_idx || !mu_out || !sigma_out)
         return fail(MBRL_EINVAL, "refit: NULL argument");
     if (H < 1 || a < 1 || a > 64 || K < 1) return fail(MBRL_EINVAL, "refit: H=%d a=%d K=%d", H, a, K);
@@ -700,12 +737,13 @@ static int refit_impl(const mbrl_sampler* sp, int H, int a, const int64_t* elite
             if (err != hipSuccess) return hip_check(err, "refit attribute");
             attr_set = true;
         }
-        hipLaunchKernelGGL(refit_fused_kernel, dim3(H), dim3(REFIT_THREADS), lds, stream, sp->seed, sp->iteration,
-                           sp->mu, sp->sigma, sp->lo, sp->hi, a, elite_idx, K, alpha, oma, mu_out, sigma_out, fin_mu,
-                           fin_sigma, fin_actions);
+        hipLaunchKernelGGL(refit_fused_kernel, dim3(H, B), dim3(REFIT_THREADS), lds, stream, sp->seed,
+                           sp->iteration, sp->mu, sp->sigma, sp->lo, sp->hi, a, elite_idx, K, alpha, oma, mu_out,
+                           sigma_out, fin_mu, fin_sigma, fin_actions, n_env);
         return hip_check(hipGetLastError(), "refit launch");
     }
     // large K x a: elite actions staged through HBM
+    if (B != 1) return fail(MBRL_EUNSUPPORTED, "batched refit: K=%d x a=%d exceeds the fused kernel's LDS", K, a);
     if (!aelite) return fail(MBRL_EINVAL, "refit: NULL workspace");
     if ((size_t)((K + ELITE_CHUNK - 1) / ELITE_CHUNK) * a * sizeof(float) > 64 * 1024)
         return fail(MBRL_EUNSUPPORTED, "refit: K=%d x a=%d exceeds the refit kernel's LDS", K, a);
@@ -971,5 +1009,94 @@ int mbrl_diag_set_cem_stamps(void* buf) {
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(mbrl::g_cem_stamps), &buf, sizeof(buf));
 }
 #endif
+
+// ---- batched planning: B independent CEM plans (one initial state each) in shared launches.
+struct BatchWs {
+    float *costs, *actions, *mu[2], *sigma[2], *s0x, *states;
+    unsigned long long* xchg;
+    unsigned* status;
+    size_t xchg_bytes;
+    int64_t* elites;
+    uint32_t* keys;
+    size_t bytes;
+};
+
+static BatchWs batch_ws(const Geometry& g, const mbrl_cem_params* p, int B, void* base) {
+    BatchWs w{};
+    char* b = static_cast<char*>(base);
+    size_t o = 0;
+    auto take = [&](size_t n) { void* r = b ? b + o : nullptr; o += align256(n); return r; };
+    const size_t BN = (size_t)B * p->N, BHa = (size_t)B * p->H * g.a;
+    w.xchg_bytes = (size_t)g.E * 2 * g.Wpad * 8;
+    w.xchg = (unsigned long long*)take(w.xchg_bytes);   // memset block first, status right behind (G16)
+    w.status = (unsigned*)take(16);
+    w.costs = (float*)take((size_t)g.E * BN * 4);
+    w.actions = (float*)take((size_t)p->H * BN * g.a * 4);
+    w.mu[0] = (float*)take(BHa * 4); w.mu[1] = (float*)take(BHa * 4);
+    w.sigma[0] = (float*)take(BHa * 4); w.sigma[1] = (float*)take(BHa * 4);
+    w.s0x = (float*)take(BN * g.s * 4);
+    w.states = (float*)take((size_t)g.E * p->H * g.s * 4);
+    w.elites = (int64_t*)take((size_t)B * p->K * 8);
+    w.keys = (uint32_t*)take(BN * 4);
+    w.bytes = o;
+    return w;
+}
+
+size_t mbrl_cem_plan_batch_workspace_bytes(const mbrl_mlp_shape* shape, const mbrl_cem_params* params, int32_t B) {
+    Geometry g;
+    if (shape_geometry(shape, &g) != MBRL_OK || !params || B < 1) return 0;
+    return batch_ws(g, params, B, nullptr).bytes;
+}
+
+int mbrl_cem_plan_batch(const mbrl_mlp_shape* shape, const void* packed, const mbrl_norm* norm, const mbrl_cost* cost,
+                        const float* s0, int32_t B, const mbrl_cem_params* p, float* mu, float* sigma,
+                        float* actions_out, float* states_out, void* workspace, size_t ws_bytes,
+                        mbrl_stream_t stream_) {
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
+    Geometry g;
+    int rc = shape_geometry(shape, &g);
+    if (rc) return rc;
+    if (!p || B < 1) return fail(MBRL_EINVAL, "params NULL or B=%d", B);
+    if (p->N < 1 || p->H < 1 || p->K < 1 || p->K > p->N || p->iterations < 1)
+        return fail(MBRL_EINVAL, "bad CEM params N=%d H=%d K=%d I=%d", p->N, p->H, p->K, p->iterations);
+    if ((int64_t)B * p->N > INT32_MAX / 2) return fail(MBRL_EUNSUPPORTED, "B*N too large");
+    if (!s0 || !actions_out || !states_out || !workspace) return fail(MBRL_EINVAL, "s0/actions_out/states_out/workspace NULL");
+    BatchWs w = batch_ws(g, p, B, workspace);
+    if (ws_bytes < w.bytes) return fail(MBRL_EWORKSPACE, "workspace %zu < %zu", ws_bytes, w.bytes);
+    const int BN = B * p->N, BHa = B * p->H * g.a;
+    hipLaunchKernelGGL(fill2_kernel, dim3((BHa + 255) / 256), dim3(256), 0, stream, w.mu[0], p->init_mu, w.sigma[0],
+                       p->init_sigma, BHa);
+    hipLaunchKernelGGL(expand_rows_kernel, dim3(256), dim3(256), 0, stream, s0, B, p->N, g.s, w.s0x);
+    int cur = 0;
+    for (int it = 0; it < p->iterations; ++it) {
+        mbrl_sampler sp{};
+        sp.seed = p->seed; sp.iteration = it; sp.mu = w.mu[cur]; sp.sigma = w.sigma[cur]; sp.lo = p->lo; sp.hi = p->hi;
+        // problem b's candidate n is global candidate b*N + n (its Philox counter)
+        rc = sample_impl(&sp, p->H, g.a, BN, 0, w.actions, stream, p->N);
+        if (rc) return rc;
+        rc = rollout_impl(g, packed, norm, cost, w.s0x, 1, w.actions, nullptr, BN, p->H, 0, w.costs, nullptr, nullptr,
+                          stream);
+        if (rc) return rc;
+        rc = select_impl(w.costs, g.E, p->N, p->K, MBRL_NAN_LAST, w.elites, nullptr, w.keys, align256((size_t)BN * 4),
+                         stream, B);
+        if (rc) return rc;
+        const bool last = it + 1 == p->iterations;
+        rc = refit_impl(&sp, p->H, g.a, w.elites, p->K, p->alpha, nullptr, w.mu[cur ^ 1], w.sigma[cur ^ 1], stream,
+                        last ? mu : nullptr, last ? sigma : nullptr, last ? actions_out : nullptr, B, p->N);
+        if (rc) return rc;
+        cur ^= 1;
+    }
+    const int Hs = p->H * g.s;
+    for (int b = 0; b < B; ++b) {   // each final mean's states (the cooperative trajectory kernel)
+        float* per_member = g.E == 1 ? states_out + (size_t)b * Hs : w.states;
+        rc = traj_impl(g, packed, norm, s0 + (size_t)b * g.s, actions_out + (size_t)b * p->H * g.a, p->H, per_member,
+                       w.xchg, w.xchg_bytes, w.status, stream);
+        if (rc) return rc;
+        if (g.E > 1)
+            hipLaunchKernelGGL(member_mean_kernel, dim3((Hs + 255) / 256), dim3(256), 0, stream, w.states, g.E, Hs,
+                               states_out + (size_t)b * Hs);
+    }
+    return hip_check(hipGetLastError(), "batched plan launch");
+}
 
 }  // extern "C"

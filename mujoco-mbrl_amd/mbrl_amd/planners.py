@@ -166,6 +166,11 @@ class CEMPlanner(ModelPlanner):
         return res["states"], res["actions"]
 
     @staticmethod
+    def plan_batch(initial_states, model, cost, sample_action, horizon, **kwargs):
+        """B plans at once, one per row of initial_states [B, s] (see cem_plan_batch)."""
+        return cem_plan_batch(initial_states, model, cost, sample_action, horizon, **kwargs)
+
+    @staticmethod
     def _settings(sample_action, horizon, kwargs):
         d = CEMPlanner.defaults
         g = lambda k: kwargs.get(k, d[k])  # noqa: E731
@@ -216,6 +221,45 @@ class CEMPlanner(ModelPlanner):
             res["states"] = _to_host(res["states"], st["keep"])
             res["actions"] = _to_host(res["actions"], st["keep"])
             return res
+
+
+def cem_plan_batch(initial_states, model, cost, sample_action, horizon, **kwargs):
+    """B independent CEM plans in shared launches (mbrl_cem_plan_batch): one per row of
+    initial_states [B, s], e.g. the observations of B parallel environments (parallel.py:20-52
+    runs one planner per worker process; here one GPU serves them all). kwargs as CEMPlanner.plan;
+    num_candidates / num_elites are per problem. Problem b draws its proposals as candidates
+    [b*N, (b+1)*N) of one Philox stream. Returns (states [B, H, s], actions [B, H, a]).
+
+    Closures the fused path does not recognise fall back to one CEMPlanner.plan per row."""
+    dev = _device(kwargs)
+    st = CEMPlanner._settings(sample_action, horizon, kwargs)
+    B = int(initial_states.shape[0])
+    with torch.cuda.device(dev):
+        mdesc = fused.describe_model(model)
+        cdesc = fused.describe_cost(cost, mdesc["s"], mdesc) if mdesc is not None else None
+        if mdesc is None or cdesc is None:
+            outs = [CEMPlanner.plan(initial_states[b], model, cost, sample_action, horizon,
+                                    **dict(kwargs, seed=st["seed"], return_device=True)) for b in range(B)]
+            states, actions = torch.stack([o[0] for o in outs]), torch.stack([o[1] for o in outs])
+        else:
+            lib = _lib.load()
+            prob = fused.device_problem(mdesc, cdesc, dev)
+            N, K, H, I = st["N"], st["K"], st["H"], st["I"]
+            a, s = mdesc["a"], mdesc["s"]
+            params = _lib.CemParams(N, H, K, I, st["alpha"], st["lo"], st["hi"], 0.0, st["init_std"], 0,
+                                    int(st["seed"]) & 0xFFFFFFFFFFFFFFFF)
+            need = lib.mbrl_cem_plan_batch_workspace_bytes(fused.ctypes_ref(prob.shape), fused.ctypes_ref(params), B)
+            ws = _workspace(("cem_batch", str(dev)), need, dev)
+            s0 = initial_states.to(device=dev, dtype=torch.float32).reshape(B, s).contiguous()
+            actions = torch.empty((B, H, a), dtype=torch.float32, device=dev)
+            states = torch.empty((B, H, s), dtype=torch.float32, device=dev)
+            _lib.check(lib.mbrl_cem_plan_batch(fused.ctypes_ref(prob.shape), _lib.ptr(prob.packed),
+                                               fused.ctypes_ref(prob.norm), fused.ctypes_ref(prob.cost), _lib.ptr(s0),
+                                               B, fused.ctypes_ref(params), None, None, _lib.ptr(actions),
+                                               _lib.ptr(states), _lib.ptr(ws), ws.numel(), _lib.stream_handle(dev)),
+                       "mbrl_cem_plan_batch")
+        keep = st["keep"]
+        return _to_host(states, keep), _to_host(actions, keep)
 
 
 _WS = {}

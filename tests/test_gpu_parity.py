@@ -441,3 +441,32 @@ def test_sharded_plan_two_processes_on_one_gpu():
         assert np.array_equal(g["mu"], ref["mu"].cpu().numpy()) and np.array_equal(g["sigma"], ref["sigma"].cpu().numpy())
         assert np.array_equal(g["actions"], ref["actions"].numpy())
         assert np.allclose(g["states"], ref["states"].numpy(), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("cid,N,H,B", [(2, 1024, 20, 4), (3, 512, 6, 3), (6, 256, 5, 2), (5, 128, 4, 2)])
+def test_batched_plans_match_per_problem_oracle(cid, N, H, B):
+    """mbrl_cem_plan_batch: problem b == a single CEM plan whose proposals are candidates
+    [b*N, (b+1)*N) of the Philox stream; elites, mu and the final actions bit-exact per problem."""
+    from mbrl_amd import CEMPlanner
+    p = ocem.synth_problem(cid, N=N, H=H)
+    _, model_fn, cost_fn, sample_action = build(p)
+    s = p["cfg"]["s"]
+    rng = np.random.default_rng(cid)
+    S0 = np.stack([p["s0"]] + [rng.standard_normal(s).astype(np.float32) for _ in range(B - 1)])
+    states, actions = CEMPlanner.plan_batch(torch.from_numpy(S0), model_fn, cost_fn, sample_action, H,
+                                            num_candidates=N, num_iterations=3, seed=p["rng_seed"])
+    assert states.shape == (B, H, s) and actions.shape == (B, H, p["cfg"]["a"])
+    a, K = p["cfg"]["a"], N // 10
+    for b in range(B):
+        mu = np.zeros((H, a), np.float32)
+        sg = np.full((H, a), 0.5, np.float32)
+        idx = np.arange(b * N, (b + 1) * N)
+        for it in range(3):
+            A = cem_actions(mu, sg, -1.0, 1.0, p["rng_seed"], it, idx)
+            r = ocem.ensemble_returns(ocem.rollout(p["model"], p["norm"], p["cost"], S0[b], A))
+            el = ocem.select_elites(r, K)
+            mu, sg = ocem.refit(mu, sg, np.ascontiguousarray(A[:, el].transpose(1, 0, 2)), 0.1)
+        fa = np.clip(mu, -1.0, 1.0).astype(np.float32)
+        assert np.array_equal(actions[b].numpy(), fa), b
+        _, st = ocem.rollout(p["model"], p["norm"], p["cost"], S0[b], fa[:, None, :], store_states=True)
+        assert np.allclose(states[b].numpy(), np.mean(st[:, :, 0, :], axis=0), rtol=1e-4, atol=1e-4), b
