@@ -5,7 +5,10 @@
 #include <stdarg.h>
 #include <stdio.h>
 
+#include <mutex>
+#include <set>
 #include <string>
+#include <tuple>
 
 #include "../../include/mbrl_cem.h"
 #include "mbrl_internal.h"
@@ -29,6 +32,19 @@ static int fail(int code, const char* fmt, ...) {
 static int hip_check(hipError_t e, const char* what) {
     if (e == hipSuccess) return MBRL_OK;
     return fail(MBRL_EHIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+hipError_t ensure_dynamic_lds(const void* fn, int bytes) {
+    static std::mutex mu;
+    static std::set<std::tuple<const void*, int, int>> done;
+    int dev = 0;
+    hipError_t err = hipGetDevice(&dev);
+    if (err != hipSuccess) return err;
+    std::lock_guard<std::mutex> lock(mu);
+    if (done.count({fn, dev, bytes})) return hipSuccess;
+    err = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (err == hipSuccess) done.insert({fn, dev, bytes});
+    return err;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -703,13 +719,8 @@ static int select_impl(const float* costs, int E, int N, int K, int nan_policy, 
 #define MBRL_SEL(KPT)                                                                                       \
     if (N <= 1024 * (KPT)) {                                                                                \
         const size_t lds = 4 * (size_t)max(33 * 32 * (KPT), SEL_HIST_WORDS);                               \
-        static bool attr_set = false;                                                                       \
-        if (!attr_set) {                                                                                    \
-            hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(&select_reg_kernel<KPT>),     \
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);     \
-            if (err != hipSuccess) return hip_check(err, "select attribute");                               \
-            attr_set = true;                                                                                \
-        }                                                                                                   \
+        hipError_t err = ensure_dynamic_lds(reinterpret_cast<const void*>(&select_reg_kernel<KPT>), (int)lds); \
+        if (err != hipSuccess) return hip_check(err, "select attribute");                                   \
         hipLaunchKernelGGL(select_reg_kernel<KPT>, dim3(segments), dim3(1024), lds, stream, costs, E, N, K,  \
                            nan_policy, elite_idx, returns_out, member_stride);                              \
         return hip_check(hipGetLastError(), "select launch");                                               \
@@ -730,13 +741,8 @@ static int refit_impl(const mbrl_sampler* sp, int H, int a, const int64_t* elite
     const float oma = 1.0f - alpha;
     const size_t lds = refit_fused_lds(a, K);
     if (lds <= REFIT_LDS_MAX) {
-        static bool attr_set = false;
-        if (!attr_set) {
-            hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(&refit_fused_kernel),
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)REFIT_LDS_MAX);
-            if (err != hipSuccess) return hip_check(err, "refit attribute");
-            attr_set = true;
-        }
+        hipError_t err = ensure_dynamic_lds(reinterpret_cast<const void*>(&refit_fused_kernel), (int)REFIT_LDS_MAX);
+        if (err != hipSuccess) return hip_check(err, "refit attribute");
         hipLaunchKernelGGL(refit_fused_kernel, dim3(H, B), dim3(REFIT_THREADS), lds, stream, sp->seed,
                            sp->iteration, sp->mu, sp->sigma, sp->lo, sp->hi, a, elite_idx, K, alpha, oma, mu_out,
                            sigma_out, fin_mu, fin_sigma, fin_actions, n_env);

@@ -122,6 +122,10 @@ inline size_t rollout_lds_bytes(const RolloutArgs& A, int M) {
     return need > floor_bytes ? need : floor_bytes;
 }
 
+// Raise `fn`'s dynamic-LDS limit to `bytes` on the current device, once per (kernel, device,
+// bytes); thread-safe (cem.hip).
+hipError_t ensure_dynamic_lds(const void* fn, int bytes);
+
 hipError_t launch_rollout(const RolloutArgs& A, int T, int R, hipStream_t stream);
 
 // Single-trajectory rollout (one candidate per ensemble member): the final CEM mean's predicted

@@ -572,13 +572,9 @@ static hipError_t launch_rollout_tr(const RolloutArgs& A_in, hipStream_t stream)
     const int M = 16 * R;
     dim3 grid((A.N + M - 1) / M, A.E);
     const size_t lds = rollout_lds_bytes(A, M);
-    static bool attr_set = false;  // raise the dynamic-LDS cap once per instantiation
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&rollout_kernel<T, R, K0C_T, NOT_T, NW>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
+    hipError_t e = ensure_dynamic_lds(reinterpret_cast<const void*>(&rollout_kernel<T, R, K0C_T, NOT_T, NW>),
+                                      160 * 1024);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL((rollout_kernel<T, R, K0C_T, NOT_T, NW>), grid, dim3(64 * NW), lds, stream, A);
     return hipGetLastError();
 }

@@ -373,13 +373,8 @@ size_t traj_coop_xchg_bytes(const TrajArgs& A, int E) { return (size_t)E * 2 * A
 
 template <int K0R, int SM, int WI>
 static hipError_t launch_coop_variant(const TrajArgs& A, int E, u64* xchg, unsigned* status, hipStream_t stream) {
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(&traj_coop_kernel<K0R, SM, WI>),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if (err != hipSuccess) return err;
-        attr_set = true;
-    }
+    hipError_t err = ensure_dynamic_lds(reinterpret_cast<const void*>(&traj_coop_kernel<K0R, SM, WI>), 160 * 1024);
+    if (err != hipSuccess) return err;
     const size_t lds = coop_lds(A.s, A.a, A.W, A.Wpad, A.L, A.H, K0R).total;
     hipLaunchKernelGGL((traj_coop_kernel<K0R, SM, WI>), dim3(A.Wpad / COOP_ROWS, E), dim3(COOP_THREADS), lds,
                        stream, A, xchg, status);
