@@ -18,7 +18,8 @@ def main():
     roll.sort()
     dur = [(e - s) / 1e6 for s, e in roll]
     timed = dur[-steps * 5:]
-    bench = json.loads(open(bench_log).read().strip().splitlines()[-1])
+    # the bench line is the last line that parses as a JSON object (rocprofv3 logs to the same file)
+    bench = [json.loads(l) for l in open(bench_log) if l.startswith('{"metric"')][-1]
     res = dict(kernel="rollout_kernel", dispatches=len(dur), all_mean_ms=sum(dur) / len(dur),
                timed_dispatches=len(timed), timed_mean_ms=sum(timed) / len(timed),
                bench_events_mean_ms=bench["roofline"]["avg_launch_ms"],
