@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=3, help="SURVEY.md §8d config id (default: cheetah-run CEM)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--precision", default="f32", choices=["f32", "f16x3"],
+                    help="rollout matmul precision (include/mbrl_cem.h MBRL_PRECISION_*)")
     ap.add_argument("--traffic-bytes", type=float, default=None,
                     help="HBM bytes per rollout launch from a rocprofv3 PMC pass (profiles/)")
     return ap.parse_args()
@@ -118,7 +120,7 @@ def main():
     N = n_local * world
     K = N // 10
     kw = dict(num_candidates=N, num_elites=K, num_iterations=ITERATIONS, alpha=0.1, seed=prob["rng_seed"],
-              distributed=world > 1, device=dev)
+              distributed=world > 1, device=dev, precision=args.precision)
 
     def barrier():
         if dist is not None:
@@ -173,12 +175,13 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "f32" if args.precision == "f32" else "f32 (f16x3 split MFMA: fp32 emulated, 22-bit operands)",
         "data": "synthetic (random nn.Linear-law weights, PCG64 seed 1000+config; Philox proposals)",
         "config": {"workload": f"{cfg['name']} CEM N={N} H={H} s={cfg['s']} a={cfg['a']} "
                                f"{cfg['L']}x{cfg['W']} MLP E={E} I={ITERATIONS} K={K}",
                    "candidates_per_gpu": n_local, "horizon": H, "iterations": ITERATIONS, "elites": K,
-                   "parallelism": f"candidates sharded x{world}" if world > 1 else "single GPU"},
+                   "parallelism": f"candidates sharded x{world}" if world > 1 else "single GPU",
+                   "precision": args.precision},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / PEAK_FP32_MFMA_TFLOPS, "traffic": traffic,
                      "kernel": "rollout_kernel", "avg_launch_ms": avg_rollout_s * 1e3,

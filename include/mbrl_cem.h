@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MBRL_ABI_VERSION 2
+#define MBRL_ABI_VERSION 3
 
 typedef struct ihipStream_t* mbrl_stream_t; /* == hipStream_t */
 typedef struct ihipEvent_t* mbrl_event_t;   /* == hipEvent_t  */
@@ -55,6 +55,19 @@ enum {
     MBRL_NAN_FIRST = 1  /* np.argmin order: the first NaN wins (RandomShootingPlanner, planners.py:184) */
 };
 
+/* Matrix-product precision of the rollout's MLP layers (mbrl_mlp_shape.precision).
+ * F32   = v_mfma_f32_16x16x4_f32: exact fp32 products, fp32 accumulation.
+ * F16X3 = fp32 emulated on the f16 matrix cores: each fp32 operand x is split into
+ *         hi = f16(x) and lo = f16((x - hi) * 2^12) (22 significant bits), and every product is
+ *         hi*hi + 2^-12 * (hi*lo + lo*hi) with fp32 accumulation (v_mfma_f32_16x16x32_f16,
+ *         16x the fp32 matrix rate, so the three products still run 5.3x faster). The dropped
+ *         lo*lo term and the two 11-bit residuals bound the per-product error by ~3 * 2^-22
+ *         relative, below the fp32 rounding of a W-long dot product. Operands with
+ *         |x| >= 32768 cannot be split; a workgroup that meets one redoes its candidates in F32
+ *         (on the device, in the same call), so results never depend on the operand range.
+ *         Used for goal-state costs with 256 <= W <= 512; every other case runs F32. */
+enum { MBRL_PRECISION_F32 = 0, MBRL_PRECISION_F16X3 = 1 };
+
 /* Dynamics MLP shape: Linear(s+a -> W), ReLU, [Linear(W -> W), ReLU] x (L-1), Linear(W -> s).
  * models.py:96-110 (Model, L = 2) generalised to L hidden layers; E ensemble members.
  * reward_head = 1: ModelWithReward (models.py:125-141): the same trunk plus a reward head
@@ -66,6 +79,8 @@ typedef struct {
     int32_t n_hidden;    /* L >= 1 */
     int32_t ensemble;    /* E >= 1 */
     int32_t reward_head; /* 0 or 1 */
+    int32_t precision;   /* MBRL_PRECISION_F32 or MBRL_PRECISION_F16X3 (rollout only; the packed
+                            buffer holds both weight streams, so one pack serves either) */
 } mbrl_mlp_shape;
 
 /* Normalisation affine, TransitionsDataset.normalize_field / unnormalize_field (data.py:255-260),

@@ -90,6 +90,66 @@ __global__ void pack_out_kernel(const float* __restrict__ w, const float* __rest
     }
 }
 
+// F16X3 split stream (rollout_f16x3.hip): chunk = 32 K rows; per chunk 8 waves x T fragments of
+// 64 lanes x 8 halves; fragment f of a hidden-type chunk = tile f >> 1, piece f & 1 (hi, lo).
+// Lane l, element q: row n = 16 (wave T/2 + tile) + (l & 15), k = 32 kc + 8 (l >> 4) + q.
+// A weight with |w| >= 32768 cannot be split: *bad becomes nonzero and the rollout falls back.
+__device__ __forceinline__ void split_weight(float v, _Float16* hi, _Float16* lo, unsigned* bad) {
+    const _Float16 h = (_Float16)v;
+    *hi = h;
+    *lo = (_Float16)((v - (float)h) * 4096.0f);
+    if (fabsf(v) >= 32768.0f) atomicOr(bad, 1u);
+}
+
+__global__ void pack_split_hidden_kernel(const float* __restrict__ w, int in_real, int out_real, int nkc, int T,
+                                         _Float16* __restrict__ dst, unsigned* __restrict__ bad) {
+    const int TW = T / 2;
+    const size_t total = (size_t)nkc * 8 * TW * 64 * 8;   // (kc, wave, tile, lane, q); both pieces per item
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const int q = (int)(i & 7);
+        const int lane = (int)((i >> 3) & 63);
+        const size_t r = i >> 9;               // (kc * 8 + wave) * TW + tile
+        const int tile = (int)(r % TW);
+        const int wave = (int)((r / TW) & 7);
+        const int kc = (int)(r / TW / 8);
+        const int n = 16 * (wave * TW + tile) + (lane & 15);
+        const int k = 32 * kc + 8 * (lane >> 4) + q;
+        const float v = (n < out_real && k < in_real) ? w[(size_t)n * in_real + k] : 0.0f;
+        const size_t frag = ((size_t)kc * 8 + wave) * T + 2 * tile;   // hi fragment; lo = frag + 1
+        const size_t o = (frag * 64 + lane) * 8 + q;
+        split_weight(v, dst + o, dst + o + 512, bad);
+    }
+}
+
+// Output layer: chunk c pairs output tiles 2c, 2c + 1; wave w's K range is units [16 w TW, 16 (w+1) TW)
+// taken as K-chunks kk of two tiles (2kk, 2kk+1) in the accumulator order: element q of lane group
+// g is unit 16 (w TW + 2kk + (q >> 2)) + 4g + (q & 3). Fragment f = u TW + 2 kk + piece.
+__global__ void pack_split_out_kernel(const float* __restrict__ w, const float* __restrict__ w_r, int in_real,
+                                      int out_real, int NOS, int T, _Float16* __restrict__ dst,
+                                      unsigned* __restrict__ bad) {
+    const int TW = T / 2, KK = TW / 2;
+    const size_t total = (size_t)NOS * 8 * 2 * KK * 64 * 8;   // (c, wave, u, kk, lane, q)
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const int q = (int)(i & 7);
+        const int lane = (int)((i >> 3) & 63);
+        size_t r = i >> 9;
+        const int kk = (int)(r % KK); r /= KK;
+        const int u = (int)(r % 2); r /= 2;
+        const int wave = (int)(r % 8);
+        const int c = (int)(r / 8);
+        const int n = 16 * (2 * c + u) + (lane & 15);
+        const int k = 16 * (wave * TW + 2 * kk + (q >> 2)) + 4 * (lane >> 4) + (q & 3);
+        float v = 0.0f;
+        if (k < in_real) {
+            if (n < out_real) v = w[(size_t)n * in_real + k];
+            else if (w_r && n == out_real) v = w_r[k];
+        }
+        const size_t frag = ((size_t)c * 8 + wave) * T + u * TW + 2 * kk;
+        const size_t o = (frag * 64 + lane) * 8 + q;
+        split_weight(v, dst + o, dst + o + 512, bad);
+    }
+}
+
 // Plain copies for traj.hip: transposed W^T [in][cols] (zero-padded columns) ...
 __global__ void pack_transposed_kernel(const float* __restrict__ w, int in_real, int out_real, int cols,
                                        float* __restrict__ dst) {
@@ -594,10 +654,13 @@ __global__ void member_mean_kernel(const float* __restrict__ src, int E, int n, 
 // ------------------------------------------------------------------------------------------------
 static int shape_geometry(const mbrl_mlp_shape* sh, Geometry* g) {
     if (!sh) return fail(MBRL_EINVAL, "shape is NULL");
+    if (sh->precision != MBRL_PRECISION_F32 && sh->precision != MBRL_PRECISION_F16X3)
+        return fail(MBRL_EINVAL, "precision %d is not an MBRL_PRECISION_* value", sh->precision);
     if (!make_geometry(sh->state_dim, sh->action_dim, sh->hidden, sh->n_hidden, sh->ensemble, sh->reward_head, g))
         return fail(MBRL_EUNSUPPORTED,
                     "unsupported MLP shape s=%d a=%d W=%d L=%d E=%d reward_head=%d (need all >= 1, W <= 1024, L <= %d)",
                     sh->state_dim, sh->action_dim, sh->hidden, sh->n_hidden, sh->ensemble, sh->reward_head, MAX_LAYERS);
+    g->precision = sh->precision;
     return MBRL_OK;
 }
 
@@ -678,6 +741,24 @@ static int rollout_impl(const Geometry& g, const void* packed, const mbrl_norm* 
     if (16 * g.a > 768) return fail(MBRL_EUNSUPPORTED, "action_dim %d too large (max 48)", g.a);
     // waves per workgroup as launch_rollout_t picks them: 8 for R = 1 (T >= 2), else 4
     A.nw = (R == 1 && g.T >= 2) ? 8 : 4;
+    if (g.precision == MBRL_PRECISION_F16X3 && g.split_ok && !A.reward) {
+        RolloutArgs S = A;
+        S.split_off = g.split_off;
+        S.K0S = g.K0S;
+        S.CS = g.CS;
+        S.sr = 2 * (g.Wpad > 32 * g.K0S ? g.Wpad : 32 * g.K0S) + 8;
+        S.nw = 8;
+        if (rollout_split_supported(S, g.T)) {
+            hipError_t err = launch_rollout_split(S, g.T, stream);
+            if (err != hipSuccess) return hip_check(err, "F16X3 rollout launch");
+            // fp32 redo of the workgroups that met an operand outside the split range (usually none:
+            // every workgroup reads its 16 costs and exits)
+            RolloutArgs X = A;
+            X.redo = 1;
+            X.nw = g.T >= 2 ? 8 : 4;
+            return hip_check(launch_rollout(X, g.T, 1, stream), "F16X3 redo launch");
+        }
+    }
     if (rollout_lds_bytes(A, 16 * R) > 160 * 1024) {
         R = 1;
         A.nw = g.T >= 2 ? 8 : 4;
@@ -796,6 +877,13 @@ int mbrl_mlp_pack(const mbrl_mlp_shape* shape, const float* const* weights, cons
         float* base = static_cast<float*>(packed) + (size_t)e * g.member_stride;
         float* bias_base = base + g.stream_floats;
         size_t chunk = 0;
+        _Float16* split_base = reinterpret_cast<_Float16*>(base + g.split_off);
+        unsigned* split_bad = reinterpret_cast<unsigned*>(base + g.split_off + (size_t)g.CS * 2048 * g.T);
+        size_t split_chunk = 0;
+        if (g.split_ok) {
+            hipError_t err = hipMemsetAsync(split_bad, 0, 4, stream);
+            if (err != hipSuccess) return hip_check(err, "pack flag reset");
+        }
         for (int l = 0; l <= g.L; ++l) {
             const float* w = weights[e * nl + l];
             const float* b = biases[e * nl + l];
@@ -808,12 +896,21 @@ int mbrl_mlp_pack(const mbrl_mlp_shape* shape, const float* const* weights, cons
                 hipLaunchKernelGGL(pack_hidden_kernel, dim3(256), dim3(256), 0, stream, w, in_real, g.W, nkc, g.T, dst);
                 hipLaunchKernelGGL(pack_bias_kernel, dim3(4), dim3(256), 0, stream, b, g.W, g.Wpad, bias_base + (size_t)l * g.Wpad);
                 hipLaunchKernelGGL(pack_transposed_kernel, dim3(256), dim3(256), 0, stream, w, in_real, g.W, g.Wpad, plain);
+                if (g.split_ok) {
+                    const int nks = l == 0 ? g.K0S : 2 * g.T;
+                    hipLaunchKernelGGL(pack_split_hidden_kernel, dim3(256), dim3(256), 0, stream, w, in_real, g.W, nks,
+                                       g.T, split_base + split_chunk * 4096 * (size_t)g.T, split_bad);
+                    split_chunk += nks;
+                }
                 chunk += nkc;
             } else {
                 const float* wr = g.reward ? weights[e * nl + g.L + 1] : nullptr;
                 const float* br = g.reward ? biases[e * nl + g.L + 1] : nullptr;
                 if (g.reward && (!wr || !br)) return fail(MBRL_EINVAL, "pack: NULL reward head for member %d", e);
                 hipLaunchKernelGGL(pack_out_kernel, dim3(256), dim3(256), 0, stream, w, wr, g.W, g.s, g.NOT, g.T, dst);
+                if (g.split_ok)
+                    hipLaunchKernelGGL(pack_split_out_kernel, dim3(256), dim3(256), 0, stream, w, wr, g.W, g.s, g.NOS,
+                                       g.T, split_base + split_chunk * 4096 * (size_t)g.T, split_bad);
                 float* ob = bias_base + (size_t)g.L * g.Wpad;
                 hipLaunchKernelGGL(pack_bias_kernel, dim3(1), dim3(256), 0, stream, b, g.s, 16 * g.NOT, ob);
                 hipLaunchKernelGGL(copy_kernel, dim3(64), dim3(256), 0, stream, w, (size_t)g.s * g.W, plain);

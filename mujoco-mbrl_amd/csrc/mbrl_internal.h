@@ -28,6 +28,15 @@ struct Geometry {
     int Opad;
     size_t tw_off[MAX_LAYERS + 1];  // offsets inside the plain region
     size_t tw_floats;
+    // F16X3 split stream (rollout_f16x3.hip): 32-deep K chunks of f16 (hi, lo) fragment pairs,
+    // 8 waves x T fragments of 1 KiB per chunk. Present when split_ok (256 <= Wpad <= 512).
+    int split_ok;
+    int precision;         // requested MBRL_PRECISION_* (set by the ABI layer, not by make_geometry)
+    int K0S;               // layer-0 chunks of 32 (K0S + NOS even)
+    int NOS;               // output chunks (pairs of 16-row output tiles) = NOT / 2
+    int CS;                // split chunks per step = K0S + (L-1)*2T + NOS
+    size_t split_off;      // floats from the member base
+    size_t split_floats;   // CS * 2048 * T, then one flag word (nonzero: a weight is out of split range)
     size_t member_stride;  // floats per ensemble member (64-float aligned)
 };
 
@@ -60,7 +69,17 @@ inline bool make_geometry(int s, int a, int W, int L, int E, int reward, Geometr
     g->tw_off[L] = o;
     o += (size_t)g->so * W;
     g->tw_floats = o;
-    g->member_stride = (g->stream_floats + g->bias_floats + g->tw_floats + 63) / 64 * 64;
+    size_t end = g->stream_floats + g->bias_floats + g->tw_floats;
+    g->split_ok = (T == 4 || T == 8) ? 1 : 0;
+    g->precision = 0;
+    g->K0S = (s + a + 31) / 32;
+    g->NOS = g->NOT / 2;
+    if ((g->K0S + g->NOS) & 1) g->K0S += 1;   // every step then starts on the same ring phase pair
+    g->CS = g->K0S + (L - 1) * 2 * T + g->NOS;
+    g->split_off = (end + 63) / 64 * 64;
+    g->split_floats = g->split_ok ? (size_t)g->CS * 2048 * T + 64 : 0;
+    if (g->split_ok) end = g->split_off + g->split_floats;
+    g->member_stride = (end + 63) / 64 * 64;
     return true;
 }
 
@@ -85,7 +104,15 @@ struct RolloutArgs {
     float* costs;
     float* actions_out;
     float* states_out;
+    // F16X3 (rollout_f16x3.hip) and its F32 redo pass
+    size_t split_off;
+    int K0S, CS, sr;       // sr: LDS activation row stride in halves
+    int redo;              // F32 kernel: only workgroups whose candidates carry MBRL_REDO_MARK run
 };
+
+// Cost bit pattern the F16X3 kernel leaves for candidates it could not evaluate (an operand out of
+// split range); the F32 redo pass recomputes exactly those workgroups. A quiet NaN payload.
+constexpr uint32_t MBRL_REDO_MARK = 0x7FC0DEADu;
 
 struct LdsMap {
     float *act, *act2, *part, *sterm, *aterm, *obs_mean, *obs_std, *act_mean, *act_std, *goal, *cw, *hbias;
@@ -127,6 +154,12 @@ inline size_t rollout_lds_bytes(const RolloutArgs& A, int M) {
 hipError_t ensure_dynamic_lds(const void* fn, int bytes);
 
 hipError_t launch_rollout(const RolloutArgs& A, int T, int R, hipStream_t stream);
+
+// F16X3 rollout (8 waves, 16 candidates per workgroup, goal-state cost). Supported for
+// geometry.split_ok; the caller follows it with launch_rollout(redo = 1, R = 1).
+bool rollout_split_supported(const RolloutArgs& A, int T);
+size_t rollout_split_lds_bytes(const RolloutArgs& A);
+hipError_t launch_rollout_split(const RolloutArgs& A, int T, hipStream_t stream);
 
 // Single-trajectory rollout (one candidate per ensemble member): the final CEM mean's predicted
 // states. Latency-bound, so VALU dot products over plain weight copies on one workgroup per member

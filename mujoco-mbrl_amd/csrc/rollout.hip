@@ -278,6 +278,15 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
     const LdsMap L = lds_map(A, smem, M);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int tile = blockIdx.x, e = blockIdx.y;
+    if (A.redo) {
+        // F16X3 redo pass (rollout_f16x3.hip): run only where the split kernel left MBRL_REDO_MARK
+        bool any = false;
+        for (int m = 0; m < M; ++m) {
+            const int n = tile * M + m;
+            if (n < A.N && __float_as_uint(A.costs[(size_t)e * A.N + n]) == MBRL_REDO_MARK) any = true;
+        }
+        if (!any) return;
+    }
     const float* member = A.packed + (size_t)e * A.member_stride;
     float* const actX = L.act;   // step input (layer 0) and every even layer's input
     float* const actY = L.act2;

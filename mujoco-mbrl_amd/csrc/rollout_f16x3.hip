@@ -1,0 +1,491 @@
+// F16X3 persistent rollout: the rollout_kernel (rollout.hip) schedule with every Linear emulating
+// fp32 on the f16 matrix cores (mbrl_cem.h, MBRL_PRECISION_F16X3).
+//
+// Why. The fp32 kernel is MFMA-bound: v_mfma_f32_16x16x4_f32 gives 32 MAC/clk/SIMD, and with
+// 16 candidates per CU (N = 4096 over 256 CUs) every step re-streams the whole weight set (2.2 MB
+// for 3x512) from L2 at ~65 GB/s per CU. v_mfma_f32_16x16x32_f16 gives 512 MAC/clk/SIMD, so
+// the three split products of each fp32 product cost 3/16 of the fp32 instruction, and the step
+// becomes bound by the L2 weight stream instead (~125 GB/s per CU, tools/ubench/l2stream.hip).
+// The split weights are two f16 (4 bytes per weight, as fp32), so the stream does not grow.
+//
+// Split. x = hi + 2^-12 lo + r, hi = f16(x), lo = f16((x - hi) * 2^12): x - hi is exact in fp32
+// and lo keeps 11 more bits, so |r| <= 2^-22 |x| (f16 normal range; smaller |x| lose only
+// absolute bits below 2^-36). A product is hi_w hi_x + 2^-12 (hi_w lo_x + lo_w hi_x); the dropped
+// lo_w lo_x is 2^-24 relative. Two accumulators per output tile (main, cross), fp32 accumulation,
+// combined as main + 2^-12 cross. Operands with |x| >= 32768 would overflow lo: the workgroup
+// then marks its candidates (MBRL_REDO_MARK) and the fp32 kernel's redo pass recomputes them.
+//
+// Operand layouts for v_mfma_f32_16x16x32_f16 (cdna_hip_programming.md §3): lane l holds
+// A[row l&15][k = 8(l>>4) + e] and B[k = 8(l>>4) + e][col l&15], e = 0..7; C as the f32 form.
+// Weights are A (Y^T = W X^T, as rollout.hip), activations are B, so the accumulator of tile j
+// holds units 16j + 4(l>>4) + v of candidate l&15.
+//   * hidden-type layers (layer 0, W -> W): B comes from LDS, rows [hi: kmax halves | lo: kmax]
+//     per candidate; chunk kc covers K rows 32kc .. 32kc + 31 in natural order.
+//   * output layer: K split over the 8 waves and fed from registers. A K-chunk pairs two of the
+//     wave's own tiles (2kk, 2kk+1): lane group g's eight k are units {4g..4g+3} of each, exactly
+//     what its accumulators hold; the weight pack uses the same permutation (cem.hip).
+// One workgroup = 8 waves = 16 candidates of one member for all H steps; wave w owns units
+// [w W/8, (w+1) W/8) of every hidden layer (TW = T/2 tiles). Per chunk a wave loads T fragments
+// (TW tiles x {hi, lo}) through a register ring of 4 slots of 4 fragments (a chunk is T/4 slots),
+// 3 slots (12 KiB per wave) ahead across layers and steps.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mbrl_internal.h"
+
+namespace mbrl {
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int SW = 8;       // waves per workgroup
+constexpr int SM = 16;      // candidates per workgroup
+constexpr int SNB = 4;      // weight ring depth (chunks)
+constexpr int SMAXA = 3;    // action slots per lane (a <= 48)
+constexpr float LO_SCALE = 4096.0f;
+constexpr float LO_INV = 1.0f / 4096.0f;
+constexpr float SPLIT_LIMIT = 32768.0f;
+
+#define SPIN() __builtin_amdgcn_sched_barrier(0)
+
+struct SplitLds {
+    _Float16 *x, *y;
+    float *part, *acs, *obs_mean, *obs_std, *act_mean, *act_std, *goal, *cw, *hbias;
+    int* flag;
+    size_t bytes;
+};
+
+__host__ __device__ inline int split_kmax(const RolloutArgs& A) {
+    const int k0 = 32 * A.K0S;
+    return A.Wpad > k0 ? A.Wpad : k0;
+}
+
+__host__ __device__ inline SplitLds split_lds(const RolloutArgs& A, void* base) {
+    SplitLds L;
+    size_t o = 0;
+    char* b = static_cast<char*>(base);
+    auto take = [&](size_t bytes) {
+        void* p = b ? b + o : nullptr;
+        o += (bytes + 15) & ~(size_t)15;
+        return p;
+    };
+    L.x = static_cast<_Float16*>(take((size_t)SM * A.sr * 2));
+    L.y = static_cast<_Float16*>(take((size_t)SM * A.sr * 2));
+    L.part = static_cast<float*>(take((size_t)SW * SM * A.pw * 4));
+    L.acs = static_cast<float*>(take(2 * SM * 4));
+    L.obs_mean = static_cast<float*>(take(A.s * 4));
+    L.obs_std = static_cast<float*>(take(A.s * 4));
+    L.act_mean = static_cast<float*>(take(A.a * 4));
+    L.act_std = static_cast<float*>(take(A.a * 4));
+    L.goal = static_cast<float*>(take(A.s * 4));
+    L.cw = static_cast<float*>(take(A.s * 4));
+    L.hbias = static_cast<float*>(take(((size_t)A.L * A.Wpad + 16 * (size_t)A.NOT) * 4));
+    L.flag = static_cast<int*>(take(16));
+    L.bytes = o;
+    return L;
+}
+
+__device__ __forceinline__ void split4(const f32x4 x, f16x4& hi, f16x4& lo, bool& ovf) {
+    hi = __builtin_convertvector(x, f16x4);
+    const f32x4 r = x - __builtin_convertvector(hi, f32x4);
+    lo = __builtin_convertvector(r * LO_SCALE, f16x4);
+    const f32x4 ax = __builtin_elementwise_abs(x);
+    ovf |= (ax.x >= SPLIT_LIMIT) | (ax.y >= SPLIT_LIMIT) | (ax.z >= SPLIT_LIMIT) | (ax.w >= SPLIT_LIMIT);
+}
+
+__device__ __forceinline__ void split_store1(float x, _Float16* row, int kmax, int d, bool& ovf) {
+    const _Float16 hi = (_Float16)x;
+    row[d] = hi;
+    row[kmax + d] = (_Float16)((x - (float)hi) * LO_SCALE);
+    ovf |= fabsf(x) >= SPLIT_LIMIT;
+}
+
+__device__ __forceinline__ f32x4 mfma16(const f32x4 a_raw, const f16x8 b, const f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a_raw), b, c, 0, 0, 0);
+}
+
+template <int FR>
+__device__ __forceinline__ void sload(f32x4 (&dst)[FR], __amdgpu_buffer_rsrc_t rsrc, unsigned voff, unsigned soff) {
+#pragma unroll
+    for (int f = 0; f < FR; ++f)
+        dst[f] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + (unsigned)(f * 1024), soff, 0));
+}
+
+__device__ __forceinline__ void read_b(f16x8& bh, f16x8& bl, const _Float16* act, int sr, int kmax, int kc, int lane) {
+    const _Float16* row = act + (lane & 15) * sr + 32 * kc + 8 * (lane >> 4);
+    bh = *reinterpret_cast<const f16x8*>(row);
+    bl = *reinterpret_cast<const f16x8*>(row + kmax);
+}
+
+// One hidden-type chunk: TW tiles x (hi*hi -> main; hi*lo, lo*hi -> cross).
+template <int TW>
+__device__ __forceinline__ void mma_chunk(f32x4 (&mn)[TW], f32x4 (&cr)[TW], const f32x4 (&w)[2 * TW], const f16x8 bh,
+                                          const f16x8 bl) {
+#pragma unroll
+    for (int j = 0; j < TW; ++j) mn[j] = mfma16(w[2 * j], bh, mn[j]);
+#pragma unroll
+    for (int j = 0; j < TW; ++j) cr[j] = mfma16(w[2 * j], bl, cr[j]);
+#pragma unroll
+    for (int j = 0; j < TW; ++j) cr[j] = mfma16(w[2 * j + 1], bh, cr[j]);
+}
+
+template <int TW>
+__device__ __forceinline__ f32x4 layer_out(const f32x4 (&mn)[TW], const f32x4 (&cr)[TW], const float* hb, int wave,
+                                           int j, int lane) {
+    const f32x4 bias = *reinterpret_cast<const f32x4*>(hb + wave * 16 * TW + 16 * j + 4 * (lane >> 4));
+    const f32x4 v = (mn[j] + cr[j] * LO_INV) + bias;
+    return __builtin_elementwise_max(v, f32x4{0.f, 0.f, 0.f, 0.f});
+}
+
+// bias + ReLU + split of this wave's tiles into the next layer's B rows; one barrier.
+template <int TW>
+__device__ __forceinline__ void produce(const f32x4 (&mn)[TW], const f32x4 (&cr)[TW], const float* hb, _Float16* out,
+                                        int sr, int kmax, int wave, int lane, bool& ovf) {
+#pragma unroll
+    for (int j = 0; j < TW; ++j) {
+        f16x4 h, l;
+        split4(layer_out<TW>(mn, cr, hb, wave, j, lane), h, l, ovf);
+        _Float16* row = out + (lane & 15) * sr + 16 * (wave * TW + j) + 4 * (lane >> 4);
+        *reinterpret_cast<f16x4*>(row) = h;
+        *reinterpret_cast<f16x4*>(row + kmax) = l;
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ float rowsum16(float v) {
+    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false));
+    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x124, 0xF, 0xF, false));
+    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x122, 0xF, 0xF, false));
+    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x121, 0xF, 0xF, false));
+    return v;
+}
+
+template <int T, int K0S, int NOS>
+struct SplitRollout {
+    static constexpr int TW = T / 2;        // tiles per wave per hidden layer
+    static constexpr int FR = T;            // fragments per wave per chunk (TW tiles x {hi, lo})
+    static constexpr int SUB = T / 4;       // ring slots (sub-chunks of 4 fragments) per chunk
+    static constexpr int FS = 4;            // fragments per ring slot
+    static constexpr int TS = TW / SUB;     // tiles per sub-chunk (2)
+    static constexpr int KH = 2 * T;        // chunks per hidden layer
+    static constexpr int SS = 2 * NOS;      // state slots per lane (ceil(s / 16) <= NOT)
+    static constexpr int SHIFT = ((K0S + NOS) * SUB) % SNB;
+    static_assert(TW % 2 == 0 && TS == 2 && (KH * SUB) % SNB == 0 && (SHIFT == 0 || 2 * SHIFT == SNB),
+                  "ring phases");
+
+    const RolloutArgs& A;
+    const SplitLds& L;
+    const int wave, lane, tile, e, kmax;
+    const bool epi, actw;
+    const int arow;                 // epilogue / action row of this lane: 4 (wave & 3) + (lane >> 4)
+    __amdgpu_buffer_rsrc_t rsrc;
+    unsigned voff;
+    f32x4 ring[SNB][FS];
+    f32x4 mn[TW], cr[TW];
+    float av[SMAXA];
+    float total = 0.f;
+    bool ovf = false;
+    int g = 0;                      // sub-chunk index within the step
+
+    __device__ SplitRollout(const RolloutArgs& A_, const SplitLds& L_, int wave_, int lane_, int tile_, int e_,
+                            const float* member)
+        : A(A_), L(L_), wave(wave_), lane(lane_), tile(tile_), e(e_), kmax(split_kmax(A_)), epi(wave_ < 4),
+          actw(wave_ >= 4), arow(4 * (wave_ & 3) + (lane_ >> 4)) {
+        rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(member + A.split_off), 0,
+                                                 (int)((size_t)A.CS * 8192 * T), 0x00020000);
+        voff = (unsigned)((wave * FR * 64 + lane) * 16);
+    }
+
+    // sub-chunk G of the step sequence (wrapping into the next step): chunk G / SUB, fragments
+    // [FS (G % SUB), FS (G % SUB + 1)) of this wave's slice
+    __device__ __forceinline__ void load_sub(f32x4 (&dst)[FS], int G) {
+        const int css = A.CS * SUB;
+        const int gp = G < css ? G : G - css;
+        const unsigned soff = (unsigned)(gp / SUB) * (unsigned)(8192 * T) + (unsigned)((gp % SUB) * FS * 1024);
+        sload<FS>(dst, rsrc, voff, soff);
+    }
+
+    __device__ __forceinline__ void fetch_actions(int t) {
+        const int n = min(tile * SM + arow, A.N - 1);
+        const float* src = A.actions + ((size_t)t * A.N + n) * A.a;
+#pragma unroll
+        for (int k = 0; k < SMAXA; ++k) av[k] = src[min((lane & 15) + 16 * k, A.a - 1)];
+    }
+
+    // a_t -> normalised, split MLP input columns [s, s + a) of row arow; CoshLoss row sum -> acs[slot]
+    __device__ __forceinline__ void stage_actions(int slot) {
+        _Float16* row = L.x + arow * A.sr;
+        float c = 0.f;
+#pragma unroll
+        for (int k = 0; k < SMAXA; ++k) {
+            const int d = (lane & 15) + 16 * k;
+            if (d < A.a) {
+                const float x = av[k];
+                split_store1(A.norm_a ? (x - L.act_mean[d]) / L.act_std[d] : x, row, kmax, A.s + d, ovf);
+                if (A.has_ac) c += coshf(x / A.alpha_a) - 1.0f;
+            }
+        }
+        c = rowsum16(c);
+        if ((lane & 15) == 0) L.acs[slot * SM + arow] = c;
+    }
+
+    __device__ __forceinline__ void zero_pad() {
+        const int k0 = A.s + A.a, k1 = 32 * A.K0S;
+        for (int i = threadIdx.x; i < SM * (k1 - k0); i += 64 * SW) {
+            const int m = i / (k1 - k0), d = k0 + i - (i / (k1 - k0)) * (k1 - k0);
+            L.x[m * A.sr + d] = (_Float16)0.f;
+            L.x[m * A.sr + kmax + d] = (_Float16)0.f;
+        }
+    }
+
+    __device__ void prologue() {
+        for (int i = threadIdx.x; i < A.s; i += 64 * SW) {
+            L.obs_mean[i] = A.obs_mean ? A.obs_mean[i] : 0.f;
+            L.obs_std[i] = A.obs_std ? A.obs_std[i] : 1.f;
+            L.goal[i] = A.goal ? A.goal[i] : 0.f;
+            L.cw[i] = A.cw ? A.cw[i] : 0.f;
+        }
+        for (int i = threadIdx.x; i < A.a; i += 64 * SW) {
+            L.act_mean[i] = A.act_mean ? A.act_mean[i] : 0.f;
+            L.act_std[i] = A.act_std ? A.act_std[i] : 1.f;
+        }
+        const float* bias_src = A.packed + (size_t)e * A.member_stride + A.stream_floats;
+        for (int i = threadIdx.x; i < A.L * A.Wpad + 16 * A.NOT; i += 64 * SW) L.hbias[i] = bias_src[i];
+        if (threadIdx.x == 0) L.flag[0] = 0;
+        if (actw) fetch_actions(0);
+        __syncthreads();
+        for (int i = threadIdx.x; i < SM * A.s; i += 64 * SW) {
+            const int m = i / A.s, d = i - (i / A.s) * A.s;
+            const int n = min(tile * SM + m, A.N - 1);
+            const float sv = A.s0_per_cand ? A.s0[(size_t)n * A.s + d] : A.s0[d];
+            split_store1(A.norm_s ? (sv - L.obs_mean[d]) / L.obs_std[d] : sv, L.x + m * A.sr, kmax, d, ovf);
+        }
+        zero_pad();
+        if (actw) stage_actions(0);
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < SNB - 1; ++q) load_sub(ring[q], q);
+    }
+
+    // refill the slot chunk g-1 vacated with chunk g+SNB-1; `slot` folds to a constant once the
+    // chunk loops are unrolled (the ring must stay in registers)
+    __device__ __forceinline__ void prefetch(int slot) {
+        load_sub(ring[(slot + SNB - 1) % SNB], g + SNB - 1);
+    }
+
+    __device__ __forceinline__ void zero_acc() {
+#pragma unroll
+        for (int j = 0; j < TW; ++j) { mn[j] = f32x4{0.f, 0.f, 0.f, 0.f}; cr[j] = mn[j]; }
+    }
+
+    // Hidden-type layer over NK chunks (NK * SUB ring slots from slot S0), B rows from `in`.
+    template <int S0, int NK>
+    __device__ __forceinline__ void hidden_layer(const _Float16* in) {
+        zero_acc();
+        f16x8 bh[2], bl[2];
+        read_b(bh[0], bl[0], in, A.sr, kmax, 0, lane);
+#pragma unroll
+        for (int kc = 0; kc < NK; ++kc) {
+#pragma unroll
+            for (int h = 0; h < SUB; ++h) {
+                const int slot = (S0 + kc * SUB + h) % SNB;
+                prefetch(slot);
+                if (h == 0 && kc + 1 < NK) read_b(bh[(kc + 1) & 1], bl[(kc + 1) & 1], in, A.sr, kmax, kc + 1, lane);
+                const f32x4(&w)[FS] = ring[slot];
+#pragma unroll
+                for (int j = 0; j < TS; ++j) mn[TS * h + j] = mfma16(w[2 * j], bh[kc & 1], mn[TS * h + j]);
+#pragma unroll
+                for (int j = 0; j < TS; ++j) cr[TS * h + j] = mfma16(w[2 * j], bl[kc & 1], cr[TS * h + j]);
+#pragma unroll
+                for (int j = 0; j < TS; ++j) cr[TS * h + j] = mfma16(w[2 * j + 1], bh[kc & 1], cr[TS * h + j]);
+                SPIN();
+                ++g;
+            }
+        }
+    }
+
+    // Output layer (K split over the waves, B from this wave's last hidden tiles) -> part[wave].
+    // Output chunk q pairs tiles 2q + u (u = 0, 1); fragment u TW + 2 kk + piece; the ring slot of
+    // fragment f is sub-chunk f / FS.
+    template <int S0>
+    __device__ __forceinline__ void output_layer(const float* hb) {
+        f16x8 oh[TW / 2], ol[TW / 2];
+#pragma unroll
+        for (int kk = 0; kk < TW / 2; ++kk) {
+            f16x4 h0, l0, h1, l1;
+            split4(layer_out<TW>(mn, cr, hb, wave, 2 * kk, lane), h0, l0, ovf);
+            split4(layer_out<TW>(mn, cr, hb, wave, 2 * kk + 1, lane), h1, l1, ovf);
+            oh[kk] = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
+            ol[kk] = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+        float* part = L.part + wave * SM * A.pw + (lane & 15) * A.pw + 4 * (lane >> 4);
+#pragma unroll
+        for (int q = 0; q < NOS; ++q) {
+#pragma unroll
+            for (int h = 0; h < SUB; ++h) {
+                const int slot = (S0 + q * SUB + h) % SNB;
+                prefetch(slot);
+                const f32x4(&w)[FS] = ring[slot];
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    if ((u * TW) / FS != h) continue;      // this tile's fragments live in sub-chunk h
+                    const int f0 = u * TW - h * FS;
+                    f32x4 o = {0.f, 0.f, 0.f, 0.f}, c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int kk = 0; kk < TW / 2; ++kk) o = mfma16(w[f0 + 2 * kk], oh[kk], o);
+#pragma unroll
+                    for (int kk = 0; kk < TW / 2; ++kk) c = mfma16(w[f0 + 2 * kk], ol[kk], c);
+#pragma unroll
+                    for (int kk = 0; kk < TW / 2; ++kk) c = mfma16(w[f0 + 2 * kk + 1], oh[kk], c);
+                    *reinterpret_cast<f32x4*>(part + 16 * (2 * q + u)) = o + c * LO_INV;
+                }
+                SPIN();
+                ++g;
+            }
+        }
+    }
+
+    // Goal-state epilogue of step t on waves 0-3 (one row per lane group), actions a_{t+1} on 4-7.
+    __device__ __forceinline__ void epilogue(int t) {
+        if (epi) {
+            const int m = arow;
+            const int n = tile * SM + m;
+            const int ws = SM * A.pw;
+            const int j = lane & 15;
+            _Float16* row = L.x + m * A.sr;
+            float sc = 0.f;
+#pragma unroll
+            for (int k = 0; k < SS; ++k) {
+                const int d = j + 16 * k;
+                if (d < A.s) {
+                    const int ro = m * A.pw + d;
+                    float o = L.part[ro] + L.part[ws + ro] + L.part[2 * ws + ro] + L.part[3 * ws + ro];
+                    o = o + ((L.part[4 * ws + ro] + L.part[5 * ws + ro]) + (L.part[6 * ws + ro] + L.part[7 * ws + ro]));
+                    const float om = L.obs_mean[d], os = L.obs_std[d];
+                    o = o + L.hbias[A.L * A.Wpad + d];
+                    const float sn = A.unnorm_s ? o * os + om : o;
+                    if (A.has_sc) {
+                        const float x = (sn - L.goal[d]) * L.cw[d];
+                        sc += sqrtf(x * x + A.alpha_s2) - A.alpha_s;
+                    }
+                    split_store1(A.norm_s ? (sn - om) / os : sn, row, kmax, d, ovf);
+                    if (A.states_out != nullptr && n < A.N)
+                        A.states_out[(((size_t)e * A.H + t) * A.N + n) * A.s + d] = sn;
+                }
+            }
+            sc = rowsum16(sc);
+            const float ac = L.acs[(t & 1) * SM + m];
+            total += sc + A.alpha_a2 * (ac / (float)A.a);
+        } else if (t + 1 < A.H) {
+            stage_actions((t + 1) & 1);
+        }
+        zero_pad();
+        __syncthreads();
+    }
+
+    template <int PH>
+    __device__ __forceinline__ void step(int t) {
+        g = 0;
+        if (actw && t + 1 < A.H) fetch_actions(t + 1);
+        this->template hidden_layer<PH, K0S>(L.x);
+        constexpr int SH = (PH + K0S * SUB) % SNB;
+        if (A.L > 1) {
+            produce<TW>(mn, cr, L.hbias, L.y, A.sr, kmax, wave, lane, ovf);
+            const _Float16* in = L.y;
+            _Float16* out = L.x;
+            for (int l = 1; l < A.L; ++l) {
+                this->template hidden_layer<SH, KH>(in);
+                if (l + 1 < A.L) {
+                    produce<TW>(mn, cr, L.hbias + l * A.Wpad, out, A.sr, kmax, wave, lane, ovf);
+                    const _Float16* tmp = in;
+                    in = out;
+                    out = const_cast<_Float16*>(tmp);
+                }
+            }
+        }
+        this->template output_layer<SH>(L.hbias + (A.L - 1) * A.Wpad);
+        __syncthreads();
+        epilogue(t);
+    }
+
+    __device__ void finish() {
+        if (__any(ovf) && lane == 0) L.flag[0] = 1;
+        __syncthreads();
+        const bool redo = L.flag[0] != 0;
+        if (epi && (lane & 15) == 0) {
+            const int n = tile * SM + arow;
+            if (n < A.N) A.costs[(size_t)e * A.N + n] = redo ? __uint_as_float(MBRL_REDO_MARK) : total;
+        }
+    }
+};
+
+template <int T, int K0S, int NOS>
+__global__ void __launch_bounds__(64 * SW, 1) rollout_split_kernel(const RolloutArgs A) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const SplitLds L = split_lds(A, smem);
+    const int tid = threadIdx.x;
+    const int tile = blockIdx.x, e = blockIdx.y;
+    const float* member = A.packed + (size_t)e * A.member_stride;
+    SplitRollout<T, K0S, NOS> R(A, L, tid >> 6, tid & 63, tile, e, member);
+    // a weight outside the split range (flag word written by the pack): leave it all to the redo pass
+    const unsigned bad = *reinterpret_cast<const unsigned*>(member + A.split_off + (size_t)A.CS * 2048 * T);
+    if (bad != 0u) {
+        if (tid < SM && tile * SM + tid < A.N) A.costs[(size_t)e * A.N + tile * SM + tid] = __uint_as_float(MBRL_REDO_MARK);
+        return;
+    }
+    R.prologue();
+    constexpr int SHIFT = SplitRollout<T, K0S, NOS>::SHIFT;
+    for (int t = 0; t < A.H; t += 2) {
+        R.template step<0>(t);
+        if (t + 1 < A.H) R.template step<SHIFT>(t + 1);
+    }
+    R.finish();
+}
+
+template <int T, int K0S, int NOS>
+hipError_t launch_split_t(const RolloutArgs& A, hipStream_t stream) {
+    const auto fn = &rollout_split_kernel<T, K0S, NOS>;
+    hipError_t err = ensure_dynamic_lds(reinterpret_cast<const void*>(fn), 160 * 1024);
+    if (err != hipSuccess) return err;
+    dim3 grid((A.N + SM - 1) / SM, A.E);
+    hipLaunchKernelGGL(fn, grid, dim3(64 * SW), rollout_split_lds_bytes(A), stream, A);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+size_t rollout_split_lds_bytes(const RolloutArgs& A) {
+    const size_t need = split_lds(A, nullptr).bytes;
+    const size_t floor_bytes = 82 * 1024;   // one workgroup per CU, as rollout_lds_bytes
+    return need > floor_bytes ? need : floor_bytes;
+}
+
+#define MBRL_SPLIT_SHAPES(X) X(1, 1) X(2, 2) X(3, 1) X(1, 3) X(3, 3)
+
+bool rollout_split_supported(const RolloutArgs& A, int T) {
+    if (A.reward || (T != 4 && T != 8) || A.a > 16 * SMAXA) return false;
+    if (A.s > 16 * (A.NOT) || A.NOT != 2 * (A.CS - A.K0S - (A.L - 1) * 2 * T)) return false;
+    if (rollout_split_lds_bytes(A) > 160 * 1024) return false;
+    const int nos = A.NOT / 2;
+#define MBRL_SPLIT_OK(K, N) if (A.K0S == K && nos == N) return true;
+    MBRL_SPLIT_SHAPES(MBRL_SPLIT_OK)
+#undef MBRL_SPLIT_OK
+    return false;
+}
+
+hipError_t launch_rollout_split(const RolloutArgs& A, int T, hipStream_t stream) {
+    const int nos = A.NOT / 2;
+#define MBRL_SPLIT_CASE(K, N)                                          \
+    if (A.K0S == K && nos == N) {                                      \
+        if (T == 4) return launch_split_t<4, K, N>(A, stream);         \
+        if (T == 8) return launch_split_t<8, K, N>(A, stream);         \
+    }
+    MBRL_SPLIT_SHAPES(MBRL_SPLIT_CASE)
+#undef MBRL_SPLIT_CASE
+    return hipErrorInvalidValue;
+}
+
+}  // namespace mbrl

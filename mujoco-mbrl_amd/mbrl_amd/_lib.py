@@ -20,9 +20,20 @@ LIB_PATH = os.environ.get("MBRL_AMD_LIB") or os.path.join(os.path.dirname(os.pat
 MBRL_OK = 0
 MBRL_COST_GOAL_STATE = 0
 MBRL_COST_MODEL_REWARD = 1
-ABI_VERSION = 2
+ABI_VERSION = 3
 MBRL_NAN_LAST = 0
 MBRL_NAN_FIRST = 1
+MBRL_PRECISION_F32 = 0
+MBRL_PRECISION_F16X3 = 1
+PRECISIONS = {"f32": MBRL_PRECISION_F32, "f16x3": MBRL_PRECISION_F16X3}
+
+
+def precision_code(name):
+    """'f32' (exact fp32 MFMA) or 'f16x3' (fp32 emulated on the f16 matrix cores; mbrl_cem.h)."""
+    try:
+        return PRECISIONS[str(name).lower()]
+    except KeyError:
+        raise ValueError(f"precision must be one of {sorted(PRECISIONS)}, got {name!r}") from None
 
 # Every symbol include/mbrl_cem.h declares (tests/test_abi.py checks the two lists agree).
 EXPORTED = (
@@ -36,7 +47,7 @@ EXPORTED = (
 
 class MlpShape(ctypes.Structure):
     _fields_ = [("state_dim", c_int32), ("action_dim", c_int32), ("hidden", c_int32),
-                ("n_hidden", c_int32), ("ensemble", c_int32), ("reward_head", c_int32)]
+                ("n_hidden", c_int32), ("ensemble", c_int32), ("reward_head", c_int32), ("precision", c_int32)]
 
 
 class Norm(ctypes.Structure):
@@ -131,4 +142,4 @@ def require_gpu(t):
 
 __all__ = ["load", "check", "ptr", "stream_handle", "MlpShape", "Norm", "Cost", "Sampler", "CemParams",
            "EXPORTED", "MBRL_NAN_LAST", "MBRL_NAN_FIRST", "MBRL_COST_GOAL_STATE", "MBRL_COST_MODEL_REWARD",
-           "ABI_VERSION", "c_int64"]
+           "ABI_VERSION", "c_int64", "MBRL_PRECISION_F32", "MBRL_PRECISION_F16X3", "precision_code"]

@@ -233,8 +233,9 @@ def _param_key(members, device):
                                   for p in (lin.weight, lin.bias))
 
 
-def mlp_shape(desc):
-    return _lib.MlpShape(desc["s"], desc["a"], desc["W"], desc["L"], desc["E"], int(desc.get("reward", False)))
+def mlp_shape(desc, precision=_lib.MBRL_PRECISION_F32):
+    return _lib.MlpShape(desc["s"], desc["a"], desc["W"], desc["L"], desc["E"], int(desc.get("reward", False)),
+                         int(precision))
 
 
 def packed_weights(desc, device):
@@ -282,9 +283,9 @@ def _dev(t, device):
 class DeviceProblem:
     """Device-resident descriptors for one (model, cost) pair; holds the tensors the POD structs point at."""
 
-    def __init__(self, mdesc, cdesc, device):
+    def __init__(self, mdesc, cdesc, device, precision=_lib.MBRL_PRECISION_F32):
         self.mdesc, self.cdesc, self.device = mdesc, cdesc, device
-        self.shape = mlp_shape(mdesc)
+        self.shape = mlp_shape(mdesc, precision)   # the packed buffer serves both precisions
         self.packed = packed_weights(mdesc, device)
         n = mdesc["norm"]
         self._norm_t = [_dev(n[k], device) for k in ("obs_mean", "obs_std", "act_mean", "act_std", "rew_mean",
@@ -310,17 +311,17 @@ def _tensor_key(t):
 _PROBLEMS = {}
 
 
-def device_problem(mdesc, cdesc, device):
+def device_problem(mdesc, cdesc, device, precision=_lib.MBRL_PRECISION_F32):
     """Cached DeviceProblem: rebuilt only when weights, statistics or cost parameters change."""
     n = mdesc["norm"]
     key = (id(mdesc["module"]), _param_key(mdesc["members"], device),
            tuple(_tensor_key(n[k]) for k in ("obs_mean", "obs_std", "act_mean", "act_std", "rew_mean", "rew_std")),
            (n["normalize_state"], n["unnormalize_state"], n["normalize_action"], n["unnormalize_reward"]),
-           None if cdesc is None else cdesc["key"])
+           None if cdesc is None else cdesc["key"], int(precision))
     hit = _PROBLEMS.get(key)
     if hit is not None and hit[0]() is mdesc["module"]:
         return hit[1]
-    prob = DeviceProblem(mdesc, cdesc, device)
+    prob = DeviceProblem(mdesc, cdesc, device, precision)
     if len(_PROBLEMS) > 64:
         _PROBLEMS.clear()
     _PROBLEMS[key] = (weakref.ref(mdesc["module"]), prob)

@@ -134,7 +134,7 @@ class RandomShootingPlanner(ModelPlanner):
             mdesc = fused.describe_model(model)
             cdesc = fused.describe_cost(cost, mdesc["s"], mdesc) if mdesc is not None else None
             if mdesc is not None and cdesc is not None and mdesc["E"] == 1 and mdesc["a"] == a:
-                prob = fused.device_problem(mdesc, cdesc, dev)
+                prob = fused.device_problem(mdesc, cdesc, dev, _lib.precision_code(kwargs.get("precision", "f32")))
                 states = torch.empty((1, H, N, mdesc["s"]), dtype=torch.float32, device=dev)
                 costs = fused.rollout(prob, s0, N, H, actions=acts, states_out=states)
                 states = states[0]
@@ -154,10 +154,12 @@ class CEMPlanner(ModelPlanner):
     kwargs (defaults): num_candidates (1000), num_elites (None -> num_candidates // 10),
     num_iterations (5), alpha (0.1), seed (None -> drawn from the global NumPy RNG, like the
     reference's sampler), init_std (None -> (hi - lo) / 4), action_bounds (None -> from
-    sample_action's action_spec, else (-1, 1)), distributed (False), return_device (False).
+    sample_action's action_spec, else (-1, 1)), distributed (False), return_device (False),
+    precision ("f32": exact fp32 MFMA; "f16x3": fp32 emulated on the f16 matrix cores, see
+    include/mbrl_cem.h).
     Returns the final Gaussian mean (clipped) and its predicted states (ensemble mean)."""
     defaults = dict(num_candidates=1000, num_elites=None, num_iterations=5, alpha=0.1, seed=None, init_std=None,
-                    action_bounds=None, distributed=False, return_device=False)
+                    action_bounds=None, distributed=False, return_device=False, precision="f32")
 
     @staticmethod
     def plan(initial_state, model, cost, sample_action, horizon, initial_trajectory=None, **kwargs):
@@ -192,7 +194,8 @@ class CEMPlanner(ModelPlanner):
         return dict(N=N, K=K, H=int(horizon), I=int(g("num_iterations")), alpha=float(g("alpha")), lo=lo, hi=hi,
                     init_std=init_std, seed=seed, distributed=bool(g("distributed")),
                     keep=bool(g("return_device")), record=bool(kwargs.get("record", False)),
-                    events=kwargs.get("rollout_events"), adim=sdesc[2] if sdesc else None)
+                    events=kwargs.get("rollout_events"), adim=sdesc[2] if sdesc else None,
+                    precision=_lib.precision_code(g("precision")))
 
     @staticmethod
     def plan_detailed(initial_state, model, cost, sample_action, horizon, initial_trajectory=None, **kwargs):
@@ -208,7 +211,7 @@ class CEMPlanner(ModelPlanner):
                     and torch.distributed.get_world_size() > 1:
                 ws = torch.distributed.get_world_size()
             if mdesc is not None and cdesc is not None:
-                prob = fused.device_problem(mdesc, cdesc, dev)
+                prob = fused.device_problem(mdesc, cdesc, dev, st["precision"])
                 if ws is None:
                     res = _cem_fused_single(prob, s0, st)
                 else:
@@ -243,7 +246,7 @@ def cem_plan_batch(initial_states, model, cost, sample_action, horizon, **kwargs
             states, actions = torch.stack([o[0] for o in outs]), torch.stack([o[1] for o in outs])
         else:
             lib = _lib.load()
-            prob = fused.device_problem(mdesc, cdesc, dev)
+            prob = fused.device_problem(mdesc, cdesc, dev, st["precision"])
             N, K, H, I = st["N"], st["K"], st["H"], st["I"]
             a, s = mdesc["a"], mdesc["s"]
             params = _lib.CemParams(N, H, K, I, st["alpha"], st["lo"], st["hi"], 0.0, st["init_std"], 0,

@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     assert decl == sorted(_lib.EXPORTED)
     for name in decl:
         assert hasattr(lib, name), name
-    assert lib.mbrl_abi_version() == _lib.ABI_VERSION == 2
+    assert lib.mbrl_abi_version() == _lib.ABI_VERSION == 3
 
 
 def test_no_gpu_needed_for_sizing_calls():
@@ -36,7 +36,14 @@ def test_no_gpu_needed_for_sizing_calls():
     # 68 chunks x 8 KiB per wave x 4 waves + biases (3*512 + 32) + plain copies for the trajectory
     # kernel (W^T of layer 0 and the two hidden layers, row-major output layer), 64-float aligned
     plain = 23 * 512 + 2 * 512 * 512 + 17 * 512
-    assert lib.mbrl_mlp_packed_bytes(ctypes.byref(sh)) == ((68 * 8192 + 3 * 512 + 32 + plain + 63) // 64 * 64) * 4
+    # then the F16X3 split stream: 34 chunks of 32 K rows (1 + 2 x 16 + 1) x 8 waves x 8 KiB, one flag word
+    a64 = lambda x: (x + 63) // 64 * 64   # noqa: E731
+    split = 34 * 2048 * 8 + 64
+    assert lib.mbrl_mlp_packed_bytes(ctypes.byref(sh)) == a64(a64(68 * 8192 + 3 * 512 + 32 + plain) + split) * 4
+    # precision does not change the packed layout; an unknown precision is rejected
+    assert lib.mbrl_mlp_packed_bytes(ctypes.byref(_lib.MlpShape(17, 6, 512, 3, 1, 0, 1))) == \
+        lib.mbrl_mlp_packed_bytes(ctypes.byref(sh))
+    assert lib.mbrl_mlp_packed_bytes(ctypes.byref(_lib.MlpShape(17, 6, 512, 3, 1, 0, 7))) == 0
     bad = _lib.MlpShape(17, 6, 4096, 3, 1)
     assert lib.mbrl_mlp_packed_bytes(ctypes.byref(bad)) == 0
     assert lib.mbrl_select_workspace_bytes(4096) >= 4096 * 4
@@ -46,7 +53,8 @@ def test_no_gpu_needed_for_sizing_calls():
     # reward head: one more output row (17 + 1 still fits two 16-row tiles) and its plain copy
     shr = _lib.MlpShape(17, 6, 512, 2, 1, 1)
     plain_r = 23 * 512 + 512 * 512 + 18 * 512
-    assert lib.mbrl_mlp_packed_bytes(ctypes.byref(shr)) == ((36 * 8192 + 2 * 512 + 32 + plain_r + 63) // 64 * 64) * 4
+    split_r = 18 * 2048 * 8 + 64
+    assert lib.mbrl_mlp_packed_bytes(ctypes.byref(shr)) == a64(a64(36 * 8192 + 2 * 512 + 32 + plain_r) + split_r) * 4
     assert lib.mbrl_mlp_packed_bytes(ctypes.byref(_lib.MlpShape(17, 6, 512, 2, 1, 2))) == 0
 
 
@@ -62,7 +70,8 @@ def test_errors_are_reported_not_crashing():
 
 
 STRUCTS = {
-    "MlpShape": ("mbrl_mlp_shape", ["state_dim", "action_dim", "hidden", "n_hidden", "ensemble", "reward_head"]),
+    "MlpShape": ("mbrl_mlp_shape", ["state_dim", "action_dim", "hidden", "n_hidden", "ensemble", "reward_head",
+                                    "precision"]),
     "Norm": ("mbrl_norm", ["obs_mean", "obs_std", "act_mean", "act_std", "rew_mean", "rew_std", "normalize_state",
                            "unnormalize_state", "normalize_action", "unnormalize_reward"]),
     "Cost": ("mbrl_cost", ["kind", "has_state_cost", "has_action_cost", "weights", "goal", "alpha_state",
