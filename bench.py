@@ -18,6 +18,8 @@ Extra objects on the JSON line:
   cpu_baseline -- the CPU oracle (NumPy restatement of the reference rollout + CEM refit), rank 0,
                   N=1 only, on a bounded sample; a reported baseline, not the target.
   parity       -- iteration-0 returns of 256 sampled candidates re-computed by the CPU oracle.
+  variants     -- the same workload timed with the other rollout precision (default headline: exact
+                  fp32; variant: f16x3, fp32 emulated on the f16 matrix cores).
 """
 import argparse
 import json
@@ -45,6 +47,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--precision", default="f32", choices=["f32", "f16x3"],
                     help="rollout matmul precision (include/mbrl_cem.h MBRL_PRECISION_*)")
+    ap.add_argument("--no-variants", action="store_true",
+                    help="skip the second-precision measurement (rocprof runs: only the headline launches)")
     ap.add_argument("--traffic-bytes", type=float, default=None,
                     help="HBM bytes per rollout launch from a rocprofv3 PMC pass (profiles/)")
     return ap.parse_args()
@@ -127,31 +131,35 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(dev)
 
-    def plan(**extra):
-        return CEMPlanner.plan_detailed(prob["s0"], prob["model"], prob["cost"], prob["sample_action"], H, **kw, **extra)
+    def timed(precision):
+        """W warm-up plans, then K timed plans between barriers; (max-over-ranks seconds, mean rollout
+        launch seconds from HIP events on the launch stream, the first plan's record)."""
+        def plan(**extra):
+            return CEMPlanner.plan_detailed(prob["s0"], prob["model"], prob["cost"], prob["sample_action"], H,
+                                            **dict(kw, precision=precision), **extra)
+        first = plan(record=True)           # also warms the weight pack / workspaces
+        for _ in range(max(0, args.warmup - 1)):
+            plan()
+        events = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                   for _ in range(ITERATIONS)] for _ in range(args.steps)]
+        for ev in events:          # torch creates events lazily: record once so the C ABI gets live handles
+            for s_, e_ in ev:
+                s_.record()
+                e_.record()
+        barrier()
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            plan(rollout_events=events[k])
+        barrier()
+        elapsed = time.perf_counter() - t0
+        if dist is not None:
+            t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        rollout_ms = [s_.elapsed_time(e_) for ev in events for (s_, e_) in ev]
+        return elapsed, float(np.mean(rollout_ms)) / 1e3, first
 
-    first = plan(record=True)           # also warms the weight pack / workspaces
-    for _ in range(max(0, args.warmup - 1)):
-        plan()
-    events = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-               for _ in range(ITERATIONS)] for _ in range(args.steps)]
-    for ev in events:          # torch creates events lazily: record once so the C ABI gets live handles
-        for s_, e_ in ev:
-            s_.record()
-            e_.record()
-    barrier()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        plan(rollout_events=events[k])
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    rollout_ms = [s.elapsed_time(e) for ev in events for (s, e) in ev]
-    avg_rollout_s = float(np.mean(rollout_ms)) / 1e3
-
+    elapsed, avg_rollout_s, first = timed(args.precision)
     cand_steps = ITERATIONS * N * H * args.steps
     value = cand_steps / elapsed
     flop_launch = n_local * H * synthetic.flop_per_candidate_step(cfg)
@@ -189,6 +197,21 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["parity"] = parity_sample(prob, first)
+    if not args.no_variants:
+        # the same workload with the other matmul precision (include/mbrl_cem.h MBRL_PRECISION_*)
+        other = "f16x3" if args.precision == "f32" else "f32"
+        v_elapsed, v_rollout_s, v_first = timed(other)
+        var = dict(precision=other, value=cand_steps / v_elapsed, ms_per_step=v_elapsed / args.steps * 1e3,
+                   rollout_avg_launch_ms=v_rollout_s * 1e3,
+                   rollout_tflops_fp32_equivalent=flop_launch / v_rollout_s / 1e12,
+                   note="fp32 emulated on the f16 matrix cores: operands split into two f16 pieces (22 "
+                        "significant bits), 3 products per fp32 product, fp32 accumulation; same parity bars "
+                        "(tests/test_gpu_f16x3.py); bound by the L2 weight stream, not by MFMA"
+                        if other == "f16x3" else "exact fp32 MFMA")
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            var["parity"] = parity_sample(prob, v_first)
+        out["variants"] = [var]
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.config)
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -1,6 +1,7 @@
 // Weight packing, elite selection, CEM refit, proposal sampling and the extern "C" ABI
 // (include/mbrl_cem.h).
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <stdint.h>
 #include <stdarg.h>
 #include <stdio.h>
@@ -93,12 +94,15 @@ __global__ void pack_out_kernel(const float* __restrict__ w, const float* __rest
 // F16X3 split stream (rollout_f16x3.hip): chunk = 32 K rows; per chunk 8 waves x T fragments of
 // 64 lanes x 8 halves; fragment f of a hidden-type chunk = tile f >> 1, piece f & 1 (hi, lo).
 // Lane l, element q: row n = 16 (wave T/2 + tile) + (l & 15), k = 32 kc + 8 (l >> 4) + q.
-// A weight with |w| >= 32768 cannot be split: *bad becomes nonzero and the rollout falls back.
-__device__ __forceinline__ void split_weight(float v, _Float16* hi, _Float16* lo, unsigned* bad) {
+// Weights are scaled by MBRL_SPLIT_W_SCALE (exact) and split as hi = f16(w), lo = f16(w - hi). A
+// scaled weight >= 32768 (|w| >= 128) cannot be split: *bad becomes nonzero and every workgroup of
+// the rollout leaves its candidates to the fp32 redo pass.
+__device__ __forceinline__ void split_weight(float v0, _Float16* hi, _Float16* lo, unsigned* bad) {
+    const float v = v0 * MBRL_SPLIT_W_SCALE;
     const _Float16 h = (_Float16)v;
     *hi = h;
-    *lo = (_Float16)((v - (float)h) * 4096.0f);
-    if (fabsf(v) >= 32768.0f) atomicOr(bad, 1u);
+    *lo = (_Float16)(v - (float)h);
+    if (!(fabsf(v) < 32768.0f)) atomicOr(bad, 1u);
 }
 
 __global__ void pack_split_hidden_kernel(const float* __restrict__ w, int in_real, int out_real, int nkc, int T,
@@ -748,15 +752,24 @@ static int rollout_impl(const Geometry& g, const void* packed, const mbrl_norm* 
         S.CS = g.CS;
         S.sr = 2 * (g.Wpad > 32 * g.K0S ? g.Wpad : 32 * g.K0S) + 8;
         S.nw = 8;
-        if (rollout_split_supported(S, g.T)) {
-            hipError_t err = launch_rollout_split(S, g.T, stream);
+        // 32 candidates per workgroup once that still gives every CU a workgroup (N >= 8192): the
+        // split kernel is bound by the L2 weight stream, which R = 2 halves per candidate. At
+        // N = 4096 R = 2 would idle half the CUs: 0.607 vs 0.571 ms per rollout (cheetah, r01).
+        int RS = N >= 256 * 32 ? 2 : 1;
+        if (const char* env = getenv("MBRL_SPLIT_R")) RS = atoi(env) == 2 ? 2 : 1;   // tuning override
+        RolloutArgs X = A;                 // the fp32 redo pass at the same tile height
+        X.redo = 1;
+        X.nw = RS == 1 && g.T >= 2 ? 8 : 4;
+        if (RS == 2 && (!rollout_split_supported(S, g.T, 2) || rollout_lds_bytes(X, 32) > 160 * 1024)) {
+            RS = 1;
+            X.nw = g.T >= 2 ? 8 : 4;
+        }
+        if (rollout_split_supported(S, g.T, RS)) {
+            hipError_t err = launch_rollout_split(S, g.T, RS, stream);
             if (err != hipSuccess) return hip_check(err, "F16X3 rollout launch");
             // fp32 redo of the workgroups that met an operand outside the split range (usually none:
-            // every workgroup reads its 16 costs and exits)
-            RolloutArgs X = A;
-            X.redo = 1;
-            X.nw = g.T >= 2 ? 8 : 4;
-            return hip_check(launch_rollout(X, g.T, 1, stream), "F16X3 redo launch");
+            // every workgroup reads its candidates' costs and exits)
+            return hip_check(launch_rollout(X, g.T, RS, stream), "F16X3 redo launch");
         }
     }
     if (rollout_lds_bytes(A, 16 * R) > 160 * 1024) {

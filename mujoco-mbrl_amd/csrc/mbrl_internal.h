@@ -110,6 +110,11 @@ struct RolloutArgs {
     int redo;              // F32 kernel: only workgroups whose candidates carry MBRL_REDO_MARK run
 };
 
+// F16X3 operand scales (exact powers of two): activations and weights are scaled before the f16
+// split so that their residual pieces stay normal; products carry X_SCALE * W_SCALE.
+#define MBRL_SPLIT_X_SCALE 16.0f
+#define MBRL_SPLIT_W_SCALE 256.0f
+
 // Cost bit pattern the F16X3 kernel leaves for candidates it could not evaluate (an operand out of
 // split range); the F32 redo pass recomputes exactly those workgroups. A quiet NaN payload.
 constexpr uint32_t MBRL_REDO_MARK = 0x7FC0DEADu;
@@ -155,11 +160,11 @@ hipError_t ensure_dynamic_lds(const void* fn, int bytes);
 
 hipError_t launch_rollout(const RolloutArgs& A, int T, int R, hipStream_t stream);
 
-// F16X3 rollout (8 waves, 16 candidates per workgroup, goal-state cost). Supported for
-// geometry.split_ok; the caller follows it with launch_rollout(redo = 1, R = 1).
-bool rollout_split_supported(const RolloutArgs& A, int T);
-size_t rollout_split_lds_bytes(const RolloutArgs& A);
-hipError_t launch_rollout_split(const RolloutArgs& A, int T, hipStream_t stream);
+// F16X3 rollout (8 waves, 16 R candidates per workgroup, goal-state cost). Supported for
+// geometry.split_ok; the caller follows it with launch_rollout(redo = 1) at the same R.
+bool rollout_split_supported(const RolloutArgs& A, int T, int R);
+size_t rollout_split_lds_bytes(const RolloutArgs& A, int R);
+hipError_t launch_rollout_split(const RolloutArgs& A, int T, int R, hipStream_t stream);
 
 // Single-trajectory rollout (one candidate per ensemble member): the final CEM mean's predicted
 // states. Latency-bound, so VALU dot products over plain weight copies on one workgroup per member

@@ -8,12 +8,14 @@
 // becomes bound by the L2 weight stream instead (~125 GB/s per CU, tools/ubench/l2stream.hip).
 // The split weights are two f16 (4 bytes per weight, as fp32), so the stream does not grow.
 //
-// Split. x = hi + 2^-12 lo + r, hi = f16(x), lo = f16((x - hi) * 2^12): x - hi is exact in fp32
-// and lo keeps 11 more bits, so |r| <= 2^-22 |x| (f16 normal range; smaller |x| lose only
-// absolute bits below 2^-36). A product is hi_w hi_x + 2^-12 (hi_w lo_x + lo_w hi_x); the dropped
-// lo_w lo_x is 2^-24 relative. Two accumulators per output tile (main, cross), fp32 accumulation,
-// combined as main + 2^-12 cross. Operands with |x| >= 32768 would overflow lo: the workgroup
-// then marks its candidates (MBRL_REDO_MARK) and the fp32 kernel's redo pass recomputes them.
+// Split. An operand is scaled by an exact power of two (activations 2^4, weights 2^8) and split as
+// x = hi + lo + r, hi = f16(x), lo = f16(x - hi): x - hi is exact in fp32 and lo keeps 11 more
+// bits, so |r| <= 2^-22 |x| while lo is a normal f16 (|x| >= 2^-6 activations, 2^-10 weights;
+// below that the error is absolute, under 2^-29 and 2^-33). A product is hi_w hi_x + hi_w lo_x +
+// lo_w hi_x, all three into ONE fp32 accumulator (every product is at scale 2^12); the dropped
+// lo_w lo_x is 2^-22 relative. The layer output is acc * 2^-12 (exact). Scaled operands with
+// |x| >= 32768 (activations >= 2048, weights >= 128) would not split: the workgroup then marks its
+// candidates (MBRL_REDO_MARK) and the fp32 kernel's redo pass recomputes them.
 //
 // Operand layouts for v_mfma_f32_16x16x32_f16 (cdna_hip_programming.md §3): lane l holds
 // A[row l&15][k = 8(l>>4) + e] and B[k = 8(l>>4) + e][col l&15], e = 0..7; C as the f32 form.
@@ -42,17 +44,19 @@ typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int SW = 8;       // waves per workgroup
-constexpr int SM = 16;      // candidates per workgroup
 constexpr int SNB = 4;      // weight ring depth (chunks)
 constexpr int SMAXA = 3;    // action slots per lane (a <= 48)
-constexpr float LO_SCALE = 4096.0f;
-constexpr float LO_INV = 1.0f / 4096.0f;
-constexpr float SPLIT_LIMIT = 32768.0f;
+// Operand scaling (exact powers of two, mbrl_internal.h): activations x 2^4, weights x 2^8, so the
+// residual pieces stay normal f16 for |x| >= 2^-6 and |w| >= 2^-10 (smaller operands keep an
+// absolute error below 2^-29 and 2^-33); every product lands at 2^12 and is unscaled once.
+constexpr float X_SCALE = MBRL_SPLIT_X_SCALE;
+constexpr float OUT_UNSCALE = 1.0f / (MBRL_SPLIT_X_SCALE * MBRL_SPLIT_W_SCALE);
+constexpr float SPLIT_LIMIT = 32768.0f;     // |scaled operand| past this: redo in fp32
 
 #define SPIN() __builtin_amdgcn_sched_barrier(0)
 
 struct SplitLds {
-    _Float16 *x, *y;
+    _Float16 *x, *y;   // activation rows [hi: kmax | lo: kmax]; y == x without ping-pong (R = 2)
     float *part, *acs, *obs_mean, *obs_std, *act_mean, *act_std, *goal, *cw, *hbias;
     int* flag;
     size_t bytes;
@@ -63,7 +67,9 @@ __host__ __device__ inline int split_kmax(const RolloutArgs& A) {
     return A.Wpad > k0 ? A.Wpad : k0;
 }
 
-__host__ __device__ inline SplitLds split_lds(const RolloutArgs& A, void* base) {
+// R = 1: ping-pong activation buffers (one barrier per layer); R = 2: one buffer, written after a
+// second barrier, so that 32 candidates fit the 160 KiB
+__host__ __device__ inline SplitLds split_lds(const RolloutArgs& A, int R, void* base) {
     SplitLds L;
     size_t o = 0;
     char* b = static_cast<char*>(base);
@@ -72,10 +78,11 @@ __host__ __device__ inline SplitLds split_lds(const RolloutArgs& A, void* base) 
         o += (bytes + 15) & ~(size_t)15;
         return p;
     };
-    L.x = static_cast<_Float16*>(take((size_t)SM * A.sr * 2));
-    L.y = static_cast<_Float16*>(take((size_t)SM * A.sr * 2));
-    L.part = static_cast<float*>(take((size_t)SW * SM * A.pw * 4));
-    L.acs = static_cast<float*>(take(2 * SM * 4));
+    const size_t M = 16 * (size_t)R;
+    L.x = static_cast<_Float16*>(take(M * A.sr * 2));
+    L.y = R == 1 ? static_cast<_Float16*>(take(M * A.sr * 2)) : L.x;
+    L.part = static_cast<float*>(take((size_t)SW * M * A.pw * 4));
+    L.acs = static_cast<float*>(take(2 * M * 4));
     L.obs_mean = static_cast<float*>(take(A.s * 4));
     L.obs_std = static_cast<float*>(take(A.s * 4));
     L.act_mean = static_cast<float*>(take(A.a * 4));
@@ -88,18 +95,19 @@ __host__ __device__ inline SplitLds split_lds(const RolloutArgs& A, void* base) 
     return L;
 }
 
-__device__ __forceinline__ void split4(const f32x4 x, f16x4& hi, f16x4& lo, bool& ovf) {
+__device__ __forceinline__ void split4(const f32x4 x0, f16x4& hi, f16x4& lo, bool& ovf) {
+    const f32x4 x = x0 * X_SCALE;
     hi = __builtin_convertvector(x, f16x4);
-    const f32x4 r = x - __builtin_convertvector(hi, f32x4);
-    lo = __builtin_convertvector(r * LO_SCALE, f16x4);
+    lo = __builtin_convertvector(x - __builtin_convertvector(hi, f32x4), f16x4);
     const f32x4 ax = __builtin_elementwise_abs(x);
     ovf |= (ax.x >= SPLIT_LIMIT) | (ax.y >= SPLIT_LIMIT) | (ax.z >= SPLIT_LIMIT) | (ax.w >= SPLIT_LIMIT);
 }
 
-__device__ __forceinline__ void split_store1(float x, _Float16* row, int kmax, int d, bool& ovf) {
+__device__ __forceinline__ void split_store1(float x0, _Float16* row, int kmax, int d, bool& ovf) {
+    const float x = x0 * X_SCALE;
     const _Float16 hi = (_Float16)x;
     row[d] = hi;
-    row[kmax + d] = (_Float16)((x - (float)hi) * LO_SCALE);
+    row[kmax + d] = (_Float16)(x - (float)hi);
     ovf |= fabsf(x) >= SPLIT_LIMIT;
 }
 
@@ -114,45 +122,18 @@ __device__ __forceinline__ void sload(f32x4 (&dst)[FR], __amdgpu_buffer_rsrc_t r
         dst[f] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + (unsigned)(f * 1024), soff, 0));
 }
 
-__device__ __forceinline__ void read_b(f16x8& bh, f16x8& bl, const _Float16* act, int sr, int kmax, int kc, int lane) {
-    const _Float16* row = act + (lane & 15) * sr + 32 * kc + 8 * (lane >> 4);
+__device__ __forceinline__ void read_b(f16x8& bh, f16x8& bl, const _Float16* act, int sr, int kmax, int kc, int lane,
+                                       int r) {
+    const _Float16* row = act + (16 * r + (lane & 15)) * sr + 32 * kc + 8 * (lane >> 4);
     bh = *reinterpret_cast<const f16x8*>(row);
     bl = *reinterpret_cast<const f16x8*>(row + kmax);
 }
 
-// One hidden-type chunk: TW tiles x (hi*hi -> main; hi*lo, lo*hi -> cross).
 template <int TW>
-__device__ __forceinline__ void mma_chunk(f32x4 (&mn)[TW], f32x4 (&cr)[TW], const f32x4 (&w)[2 * TW], const f16x8 bh,
-                                          const f16x8 bl) {
-#pragma unroll
-    for (int j = 0; j < TW; ++j) mn[j] = mfma16(w[2 * j], bh, mn[j]);
-#pragma unroll
-    for (int j = 0; j < TW; ++j) cr[j] = mfma16(w[2 * j], bl, cr[j]);
-#pragma unroll
-    for (int j = 0; j < TW; ++j) cr[j] = mfma16(w[2 * j + 1], bh, cr[j]);
-}
-
-template <int TW>
-__device__ __forceinline__ f32x4 layer_out(const f32x4 (&mn)[TW], const f32x4 (&cr)[TW], const float* hb, int wave,
-                                           int j, int lane) {
+__device__ __forceinline__ f32x4 layer_out(const f32x4 (&acc)[TW], const float* hb, int wave, int j, int lane) {
     const f32x4 bias = *reinterpret_cast<const f32x4*>(hb + wave * 16 * TW + 16 * j + 4 * (lane >> 4));
-    const f32x4 v = (mn[j] + cr[j] * LO_INV) + bias;
+    const f32x4 v = acc[j] * OUT_UNSCALE + bias;
     return __builtin_elementwise_max(v, f32x4{0.f, 0.f, 0.f, 0.f});
-}
-
-// bias + ReLU + split of this wave's tiles into the next layer's B rows; one barrier.
-template <int TW>
-__device__ __forceinline__ void produce(const f32x4 (&mn)[TW], const f32x4 (&cr)[TW], const float* hb, _Float16* out,
-                                        int sr, int kmax, int wave, int lane, bool& ovf) {
-#pragma unroll
-    for (int j = 0; j < TW; ++j) {
-        f16x4 h, l;
-        split4(layer_out<TW>(mn, cr, hb, wave, j, lane), h, l, ovf);
-        _Float16* row = out + (lane & 15) * sr + 16 * (wave * TW + j) + 4 * (lane >> 4);
-        *reinterpret_cast<f16x4*>(row) = h;
-        *reinterpret_cast<f16x4*>(row + kmax) = l;
-    }
-    __syncthreads();
 }
 
 __device__ __forceinline__ float rowsum16(float v) {
@@ -163,8 +144,10 @@ __device__ __forceinline__ float rowsum16(float v) {
     return v;
 }
 
-template <int T, int K0S, int NOS>
+template <int T, int R, int K0S, int NOS>
 struct SplitRollout {
+    static constexpr int M = 16 * R;        // candidates per workgroup (R 16-column B tiles)
+    static constexpr bool PP = R == 1;      // ping-pong activation buffers (split_lds)
     static constexpr int TW = T / 2;        // tiles per wave per hidden layer
     static constexpr int FR = T;            // fragments per wave per chunk (TW tiles x {hi, lo})
     static constexpr int SUB = T / 4;       // ring slots (sub-chunks of 4 fragments) per chunk
@@ -180,24 +163,28 @@ struct SplitRollout {
     const SplitLds& L;
     const int wave, lane, tile, e, kmax;
     const bool epi, actw;
-    const int arow;                 // epilogue / action row of this lane: 4 (wave & 3) + (lane >> 4)
     __amdgpu_buffer_rsrc_t rsrc;
     unsigned voff;
     f32x4 ring[SNB][FS];
-    f32x4 mn[TW], cr[TW];
-    float av[SMAXA];
-    float total = 0.f;
+    f32x4 acc[R][TW];
+    float av[R][SMAXA];
+    float total[R];
     bool ovf = false;
     int g = 0;                      // sub-chunk index within the step
 
     __device__ SplitRollout(const RolloutArgs& A_, const SplitLds& L_, int wave_, int lane_, int tile_, int e_,
                             const float* member)
         : A(A_), L(L_), wave(wave_), lane(lane_), tile(tile_), e(e_), kmax(split_kmax(A_)), epi(wave_ < 4),
-          actw(wave_ >= 4), arow(4 * (wave_ & 3) + (lane_ >> 4)) {
+          actw(wave_ >= 4) {
         rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(member + A.split_off), 0,
                                                  (int)((size_t)A.CS * 8192 * T), 0x00020000);
         voff = (unsigned)((wave * FR * 64 + lane) * 16);
+#pragma unroll
+        for (int r = 0; r < R; ++r) total[r] = 0.f;
     }
+
+    // epilogue / action row of this lane in candidate tile r: 16 r + 4 (wave & 3) + (lane >> 4)
+    __device__ __forceinline__ int row_of(int r) const { return 16 * r + 4 * (wave & 3) + (lane >> 4); }
 
     // sub-chunk G of the step sequence (wrapping into the next step): chunk G / SUB, fragments
     // [FS (G % SUB), FS (G % SUB + 1)) of this wave's slice
@@ -209,32 +196,39 @@ struct SplitRollout {
     }
 
     __device__ __forceinline__ void fetch_actions(int t) {
-        const int n = min(tile * SM + arow, A.N - 1);
-        const float* src = A.actions + ((size_t)t * A.N + n) * A.a;
 #pragma unroll
-        for (int k = 0; k < SMAXA; ++k) av[k] = src[min((lane & 15) + 16 * k, A.a - 1)];
+        for (int r = 0; r < R; ++r) {
+            const int n = min(tile * M + row_of(r), A.N - 1);
+            const float* src = A.actions + ((size_t)t * A.N + n) * A.a;
+#pragma unroll
+            for (int k = 0; k < SMAXA; ++k) av[r][k] = src[min((lane & 15) + 16 * k, A.a - 1)];
+        }
     }
 
-    // a_t -> normalised, split MLP input columns [s, s + a) of row arow; CoshLoss row sum -> acs[slot]
+    // a_t -> normalised, split MLP input columns [s, s + a); CoshLoss row sums -> acs[slot]
     __device__ __forceinline__ void stage_actions(int slot) {
-        _Float16* row = L.x + arow * A.sr;
-        float c = 0.f;
 #pragma unroll
-        for (int k = 0; k < SMAXA; ++k) {
-            const int d = (lane & 15) + 16 * k;
-            if (d < A.a) {
-                const float x = av[k];
-                split_store1(A.norm_a ? (x - L.act_mean[d]) / L.act_std[d] : x, row, kmax, A.s + d, ovf);
-                if (A.has_ac) c += coshf(x / A.alpha_a) - 1.0f;
+        for (int r = 0; r < R; ++r) {
+            const int m = row_of(r);
+            _Float16* row = L.x + m * A.sr;
+            float c = 0.f;
+#pragma unroll
+            for (int k = 0; k < SMAXA; ++k) {
+                const int d = (lane & 15) + 16 * k;
+                if (d < A.a) {
+                    const float x = av[r][k];
+                    split_store1(A.norm_a ? (x - L.act_mean[d]) / L.act_std[d] : x, row, kmax, A.s + d, ovf);
+                    if (A.has_ac) c += coshf(x / A.alpha_a) - 1.0f;
+                }
             }
+            c = rowsum16(c);
+            if ((lane & 15) == 0) L.acs[slot * M + m] = c;
         }
-        c = rowsum16(c);
-        if ((lane & 15) == 0) L.acs[slot * SM + arow] = c;
     }
 
     __device__ __forceinline__ void zero_pad() {
         const int k0 = A.s + A.a, k1 = 32 * A.K0S;
-        for (int i = threadIdx.x; i < SM * (k1 - k0); i += 64 * SW) {
+        for (int i = threadIdx.x; i < M * (k1 - k0); i += 64 * SW) {
             const int m = i / (k1 - k0), d = k0 + i - (i / (k1 - k0)) * (k1 - k0);
             L.x[m * A.sr + d] = (_Float16)0.f;
             L.x[m * A.sr + kmax + d] = (_Float16)0.f;
@@ -257,9 +251,9 @@ struct SplitRollout {
         if (threadIdx.x == 0) L.flag[0] = 0;
         if (actw) fetch_actions(0);
         __syncthreads();
-        for (int i = threadIdx.x; i < SM * A.s; i += 64 * SW) {
+        for (int i = threadIdx.x; i < M * A.s; i += 64 * SW) {
             const int m = i / A.s, d = i - (i / A.s) * A.s;
-            const int n = min(tile * SM + m, A.N - 1);
+            const int n = min(tile * M + m, A.N - 1);
             const float sv = A.s0_per_cand ? A.s0[(size_t)n * A.s + d] : A.s0[d];
             split_store1(A.norm_s ? (sv - L.obs_mean[d]) / L.obs_std[d] : sv, L.x + m * A.sr, kmax, d, ovf);
         }
@@ -278,33 +272,75 @@ struct SplitRollout {
 
     __device__ __forceinline__ void zero_acc() {
 #pragma unroll
-        for (int j = 0; j < TW; ++j) { mn[j] = f32x4{0.f, 0.f, 0.f, 0.f}; cr[j] = mn[j]; }
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int j = 0; j < TW; ++j) acc[r][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
 
-    // Hidden-type layer over NK chunks (NK * SUB ring slots from slot S0), B rows from `in`.
+    // Hidden-type layer over NK chunks (NK * SUB ring slots from slot S0), B rows from `in`. The B
+    // fragments of chunk kc + 1 are read one chunk ahead when R = 1; at R = 2 (twice the B and
+    // accumulator registers) they are read at the head of their own chunk, behind its first
+    // sub-chunk's weight prefetch.
     template <int S0, int NK>
     __device__ __forceinline__ void hidden_layer(const _Float16* in) {
+        constexpr int NBB = R == 1 ? 2 : 1;
         zero_acc();
-        f16x8 bh[2], bl[2];
-        read_b(bh[0], bl[0], in, A.sr, kmax, 0, lane);
+        f16x8 bh[NBB][R], bl[NBB][R];
+        if (NBB == 2)
+#pragma unroll
+            for (int r = 0; r < R; ++r) read_b(bh[0][r], bl[0][r], in, A.sr, kmax, 0, lane, r);
 #pragma unroll
         for (int kc = 0; kc < NK; ++kc) {
 #pragma unroll
             for (int h = 0; h < SUB; ++h) {
                 const int slot = (S0 + kc * SUB + h) % SNB;
                 prefetch(slot);
-                if (h == 0 && kc + 1 < NK) read_b(bh[(kc + 1) & 1], bl[(kc + 1) & 1], in, A.sr, kmax, kc + 1, lane);
+                const int b = NBB == 2 ? (kc & 1) : 0;
+                if (h == 0) {
+                    if (NBB == 2) {
+                        if (kc + 1 < NK)
+#pragma unroll
+                            for (int r = 0; r < R; ++r)
+                                read_b(bh[(kc + 1) & 1][r], bl[(kc + 1) & 1][r], in, A.sr, kmax, kc + 1, lane, r);
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < R; ++r) read_b(bh[0][r], bl[0][r], in, A.sr, kmax, kc, lane, r);
+                    }
+                }
                 const f32x4(&w)[FS] = ring[slot];
 #pragma unroll
-                for (int j = 0; j < TS; ++j) mn[TS * h + j] = mfma16(w[2 * j], bh[kc & 1], mn[TS * h + j]);
+                for (int j = 0; j < TS; ++j)
 #pragma unroll
-                for (int j = 0; j < TS; ++j) cr[TS * h + j] = mfma16(w[2 * j], bl[kc & 1], cr[TS * h + j]);
+                    for (int r = 0; r < R; ++r) acc[r][TS * h + j] = mfma16(w[2 * j], bh[b][r], acc[r][TS * h + j]);
 #pragma unroll
-                for (int j = 0; j < TS; ++j) cr[TS * h + j] = mfma16(w[2 * j + 1], bh[kc & 1], cr[TS * h + j]);
+                for (int j = 0; j < TS; ++j)
+#pragma unroll
+                    for (int r = 0; r < R; ++r) acc[r][TS * h + j] = mfma16(w[2 * j], bl[b][r], acc[r][TS * h + j]);
+#pragma unroll
+                for (int j = 0; j < TS; ++j)
+#pragma unroll
+                    for (int r = 0; r < R; ++r) acc[r][TS * h + j] = mfma16(w[2 * j + 1], bh[b][r], acc[r][TS * h + j]);
                 SPIN();
                 ++g;
             }
         }
+    }
+
+    // bias + ReLU + split of this wave's tiles into the next layer's B rows. Without ping-pong the
+    // input rows are overwritten, so every wave must be done reading them first.
+    __device__ __forceinline__ void produce(const float* hb, _Float16* out) {
+        if (!PP) __syncthreads();
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int j = 0; j < TW; ++j) {
+                f16x4 h, l;
+                split4(layer_out<TW>(acc[r], hb, wave, j, lane), h, l, ovf);
+                _Float16* row = out + (16 * r + (lane & 15)) * A.sr + 16 * (wave * TW + j) + 4 * (lane >> 4);
+                *reinterpret_cast<f16x4*>(row) = h;
+                *reinterpret_cast<f16x4*>(row + kmax) = l;
+            }
+        __syncthreads();
     }
 
     // Output layer (K split over the waves, B from this wave's last hidden tiles) -> part[wave].
@@ -312,16 +348,18 @@ struct SplitRollout {
     // fragment f is sub-chunk f / FS.
     template <int S0>
     __device__ __forceinline__ void output_layer(const float* hb) {
-        f16x8 oh[TW / 2], ol[TW / 2];
+        f16x8 oh[R][TW / 2], ol[R][TW / 2];
 #pragma unroll
-        for (int kk = 0; kk < TW / 2; ++kk) {
-            f16x4 h0, l0, h1, l1;
-            split4(layer_out<TW>(mn, cr, hb, wave, 2 * kk, lane), h0, l0, ovf);
-            split4(layer_out<TW>(mn, cr, hb, wave, 2 * kk + 1, lane), h1, l1, ovf);
-            oh[kk] = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
-            ol[kk] = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
-        }
-        float* part = L.part + wave * SM * A.pw + (lane & 15) * A.pw + 4 * (lane >> 4);
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int kk = 0; kk < TW / 2; ++kk) {
+                f16x4 h0, l0, h1, l1;
+                split4(layer_out<TW>(acc[r], hb, wave, 2 * kk, lane), h0, l0, ovf);
+                split4(layer_out<TW>(acc[r], hb, wave, 2 * kk + 1, lane), h1, l1, ovf);
+                oh[r][kk] = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
+                ol[r][kk] = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
+            }
+        float* part = L.part + wave * M * A.pw + (lane & 15) * A.pw + 4 * (lane >> 4);
 #pragma unroll
         for (int q = 0; q < NOS; ++q) {
 #pragma unroll
@@ -333,14 +371,24 @@ struct SplitRollout {
                 for (int u = 0; u < 2; ++u) {
                     if ((u * TW) / FS != h) continue;      // this tile's fragments live in sub-chunk h
                     const int f0 = u * TW - h * FS;
-                    f32x4 o = {0.f, 0.f, 0.f, 0.f}, c = {0.f, 0.f, 0.f, 0.f};
+                    f32x4 o[R];
 #pragma unroll
-                    for (int kk = 0; kk < TW / 2; ++kk) o = mfma16(w[f0 + 2 * kk], oh[kk], o);
+                    for (int r = 0; r < R; ++r) o[r] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                    for (int kk = 0; kk < TW / 2; ++kk) c = mfma16(w[f0 + 2 * kk], ol[kk], c);
+                    for (int kk = 0; kk < TW / 2; ++kk)
 #pragma unroll
-                    for (int kk = 0; kk < TW / 2; ++kk) c = mfma16(w[f0 + 2 * kk + 1], oh[kk], c);
-                    *reinterpret_cast<f32x4*>(part + 16 * (2 * q + u)) = o + c * LO_INV;
+                        for (int r = 0; r < R; ++r) o[r] = mfma16(w[f0 + 2 * kk], oh[r][kk], o[r]);
+#pragma unroll
+                    for (int kk = 0; kk < TW / 2; ++kk)
+#pragma unroll
+                        for (int r = 0; r < R; ++r) o[r] = mfma16(w[f0 + 2 * kk], ol[r][kk], o[r]);
+#pragma unroll
+                    for (int kk = 0; kk < TW / 2; ++kk)
+#pragma unroll
+                        for (int r = 0; r < R; ++r) o[r] = mfma16(w[f0 + 2 * kk + 1], oh[r][kk], o[r]);
+#pragma unroll
+                    for (int r = 0; r < R; ++r)
+                        *reinterpret_cast<f32x4*>(part + 16 * r * A.pw + 16 * (2 * q + u)) = o[r] * OUT_UNSCALE;
                 }
                 SPIN();
                 ++g;
@@ -348,37 +396,40 @@ struct SplitRollout {
         }
     }
 
-    // Goal-state epilogue of step t on waves 0-3 (one row per lane group), actions a_{t+1} on 4-7.
+    // Goal-state epilogue of step t on waves 0-3 (R rows per lane group), actions a_{t+1} on 4-7.
     __device__ __forceinline__ void epilogue(int t) {
         if (epi) {
-            const int m = arow;
-            const int n = tile * SM + m;
-            const int ws = SM * A.pw;
+            const int ws = M * A.pw;
             const int j = lane & 15;
-            _Float16* row = L.x + m * A.sr;
-            float sc = 0.f;
 #pragma unroll
-            for (int k = 0; k < SS; ++k) {
-                const int d = j + 16 * k;
-                if (d < A.s) {
-                    const int ro = m * A.pw + d;
-                    float o = L.part[ro] + L.part[ws + ro] + L.part[2 * ws + ro] + L.part[3 * ws + ro];
-                    o = o + ((L.part[4 * ws + ro] + L.part[5 * ws + ro]) + (L.part[6 * ws + ro] + L.part[7 * ws + ro]));
-                    const float om = L.obs_mean[d], os = L.obs_std[d];
-                    o = o + L.hbias[A.L * A.Wpad + d];
-                    const float sn = A.unnorm_s ? o * os + om : o;
-                    if (A.has_sc) {
-                        const float x = (sn - L.goal[d]) * L.cw[d];
-                        sc += sqrtf(x * x + A.alpha_s2) - A.alpha_s;
+            for (int r = 0; r < R; ++r) {
+                const int m = row_of(r);
+                const int n = tile * M + m;
+                _Float16* row = L.x + m * A.sr;
+                float sc = 0.f;
+#pragma unroll
+                for (int k = 0; k < SS; ++k) {
+                    const int d = j + 16 * k;
+                    if (d < A.s) {
+                        const int ro = m * A.pw + d;
+                        float o = L.part[ro] + L.part[ws + ro] + L.part[2 * ws + ro] + L.part[3 * ws + ro];
+                        o = o + ((L.part[4 * ws + ro] + L.part[5 * ws + ro]) + (L.part[6 * ws + ro] + L.part[7 * ws + ro]));
+                        const float om = L.obs_mean[d], os = L.obs_std[d];
+                        o = o + L.hbias[A.L * A.Wpad + d];
+                        const float sn = A.unnorm_s ? o * os + om : o;
+                        if (A.has_sc) {
+                            const float x = (sn - L.goal[d]) * L.cw[d];
+                            sc += sqrtf(x * x + A.alpha_s2) - A.alpha_s;
+                        }
+                        split_store1(A.norm_s ? (sn - om) / os : sn, row, kmax, d, ovf);
+                        if (A.states_out != nullptr && n < A.N)
+                            A.states_out[(((size_t)e * A.H + t) * A.N + n) * A.s + d] = sn;
                     }
-                    split_store1(A.norm_s ? (sn - om) / os : sn, row, kmax, d, ovf);
-                    if (A.states_out != nullptr && n < A.N)
-                        A.states_out[(((size_t)e * A.H + t) * A.N + n) * A.s + d] = sn;
                 }
+                sc = rowsum16(sc);
+                const float ac = L.acs[(t & 1) * M + m];
+                total[r] += sc + A.alpha_a2 * (ac / (float)A.a);
             }
-            sc = rowsum16(sc);
-            const float ac = L.acs[(t & 1) * SM + m];
-            total += sc + A.alpha_a2 * (ac / (float)A.a);
         } else if (t + 1 < A.H) {
             stage_actions((t + 1) & 1);
         }
@@ -393,13 +444,13 @@ struct SplitRollout {
         this->template hidden_layer<PH, K0S>(L.x);
         constexpr int SH = (PH + K0S * SUB) % SNB;
         if (A.L > 1) {
-            produce<TW>(mn, cr, L.hbias, L.y, A.sr, kmax, wave, lane, ovf);
+            produce(L.hbias, L.y);
             const _Float16* in = L.y;
             _Float16* out = L.x;
             for (int l = 1; l < A.L; ++l) {
                 this->template hidden_layer<SH, KH>(in);
                 if (l + 1 < A.L) {
-                    produce<TW>(mn, cr, L.hbias + l * A.Wpad, out, A.sr, kmax, wave, lane, ovf);
+                    produce(L.hbias + l * A.Wpad, out);
                     const _Float16* tmp = in;
                     in = out;
                     out = const_cast<_Float16*>(tmp);
@@ -416,59 +467,64 @@ struct SplitRollout {
         __syncthreads();
         const bool redo = L.flag[0] != 0;
         if (epi && (lane & 15) == 0) {
-            const int n = tile * SM + arow;
-            if (n < A.N) A.costs[(size_t)e * A.N + n] = redo ? __uint_as_float(MBRL_REDO_MARK) : total;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int n = tile * M + row_of(r);
+                if (n < A.N) A.costs[(size_t)e * A.N + n] = redo ? __uint_as_float(MBRL_REDO_MARK) : total[r];
+            }
         }
     }
 };
 
-template <int T, int K0S, int NOS>
+template <int T, int R, int K0S, int NOS>
 __global__ void __launch_bounds__(64 * SW, 1) rollout_split_kernel(const RolloutArgs A) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const SplitLds L = split_lds(A, smem);
+    constexpr int M = 16 * R;
+    const SplitLds L = split_lds(A, R, smem);
     const int tid = threadIdx.x;
     const int tile = blockIdx.x, e = blockIdx.y;
     const float* member = A.packed + (size_t)e * A.member_stride;
-    SplitRollout<T, K0S, NOS> R(A, L, tid >> 6, tid & 63, tile, e, member);
     // a weight outside the split range (flag word written by the pack): leave it all to the redo pass
     const unsigned bad = *reinterpret_cast<const unsigned*>(member + A.split_off + (size_t)A.CS * 2048 * T);
     if (bad != 0u) {
-        if (tid < SM && tile * SM + tid < A.N) A.costs[(size_t)e * A.N + tile * SM + tid] = __uint_as_float(MBRL_REDO_MARK);
+        if (tid < M && tile * M + tid < A.N) A.costs[(size_t)e * A.N + tile * M + tid] = __uint_as_float(MBRL_REDO_MARK);
         return;
     }
-    R.prologue();
-    constexpr int SHIFT = SplitRollout<T, K0S, NOS>::SHIFT;
+    SplitRollout<T, R, K0S, NOS> S(A, L, tid >> 6, tid & 63, tile, e, member);
+    S.prologue();
+    constexpr int SHIFT = SplitRollout<T, R, K0S, NOS>::SHIFT;
     for (int t = 0; t < A.H; t += 2) {
-        R.template step<0>(t);
-        if (t + 1 < A.H) R.template step<SHIFT>(t + 1);
+        S.template step<0>(t);
+        if (t + 1 < A.H) S.template step<SHIFT>(t + 1);
     }
-    R.finish();
+    S.finish();
 }
 
-template <int T, int K0S, int NOS>
+template <int T, int R, int K0S, int NOS>
 hipError_t launch_split_t(const RolloutArgs& A, hipStream_t stream) {
-    const auto fn = &rollout_split_kernel<T, K0S, NOS>;
+    const auto fn = &rollout_split_kernel<T, R, K0S, NOS>;
     hipError_t err = ensure_dynamic_lds(reinterpret_cast<const void*>(fn), 160 * 1024);
     if (err != hipSuccess) return err;
-    dim3 grid((A.N + SM - 1) / SM, A.E);
-    hipLaunchKernelGGL(fn, grid, dim3(64 * SW), rollout_split_lds_bytes(A), stream, A);
+    dim3 grid((A.N + 16 * R - 1) / (16 * R), A.E);
+    hipLaunchKernelGGL(fn, grid, dim3(64 * SW), rollout_split_lds_bytes(A, R), stream, A);
     return hipGetLastError();
 }
 
 }  // namespace
 
-size_t rollout_split_lds_bytes(const RolloutArgs& A) {
-    const size_t need = split_lds(A, nullptr).bytes;
+size_t rollout_split_lds_bytes(const RolloutArgs& A, int R) {
+    const size_t need = split_lds(A, R, nullptr).bytes;
     const size_t floor_bytes = 82 * 1024;   // one workgroup per CU, as rollout_lds_bytes
     return need > floor_bytes ? need : floor_bytes;
 }
 
 #define MBRL_SPLIT_SHAPES(X) X(1, 1) X(2, 2) X(3, 1) X(1, 3) X(3, 3)
 
-bool rollout_split_supported(const RolloutArgs& A, int T) {
+bool rollout_split_supported(const RolloutArgs& A, int T, int R) {
+    if (R != 1 && !(R == 2 && A.NOT == 2)) return false;
     if (A.reward || (T != 4 && T != 8) || A.a > 16 * SMAXA) return false;
     if (A.s > 16 * (A.NOT) || A.NOT != 2 * (A.CS - A.K0S - (A.L - 1) * 2 * T)) return false;
-    if (rollout_split_lds_bytes(A) > 160 * 1024) return false;
+    if (rollout_split_lds_bytes(A, R) > 160 * 1024) return false;
     const int nos = A.NOT / 2;
 #define MBRL_SPLIT_OK(K, N) if (A.K0S == K && nos == N) return true;
     MBRL_SPLIT_SHAPES(MBRL_SPLIT_OK)
@@ -476,12 +532,17 @@ bool rollout_split_supported(const RolloutArgs& A, int T) {
     return false;
 }
 
-hipError_t launch_rollout_split(const RolloutArgs& A, int T, hipStream_t stream) {
+hipError_t launch_rollout_split(const RolloutArgs& A, int T, int R, hipStream_t stream) {
     const int nos = A.NOT / 2;
-#define MBRL_SPLIT_CASE(K, N)                                          \
-    if (A.K0S == K && nos == N) {                                      \
-        if (T == 4) return launch_split_t<4, K, N>(A, stream);         \
-        if (T == 8) return launch_split_t<8, K, N>(A, stream);         \
+    // R = 2 only where its registers fit without spilling (one output chunk: NOS == 1)
+#define MBRL_SPLIT_CASE(K, N)                                                                  \
+    if (A.K0S == K && nos == N) {                                                              \
+        if (T == 4 && R == 1) return launch_split_t<4, 1, K, N>(A, stream);                    \
+        if (T == 8 && R == 1) return launch_split_t<8, 1, K, N>(A, stream);                    \
+        if constexpr (N == 1) {                                                                \
+            if (T == 4 && R == 2) return launch_split_t<4, 2, K, N>(A, stream);                \
+            if (T == 8 && R == 2) return launch_split_t<8, 2, K, N>(A, stream);                \
+        }                                                                                      \
     }
     MBRL_SPLIT_SHAPES(MBRL_SPLIT_CASE)
 #undef MBRL_SPLIT_CASE

@@ -26,7 +26,8 @@ def problems(p):
 
 
 @pytest.mark.parametrize("cid,over", [(2, dict(N=1000, H=20)), (3, dict(N=300, H=30)), (4, dict(N=200, H=7)),
-                                      (5, dict(N=40, H=6)), (3, dict(N=17, H=2)), (3, dict(N=4096, H=30))])
+                                      (5, dict(N=40, H=6)), (3, dict(N=17, H=2)), (3, dict(N=4096, H=30)),
+                                      (4, dict(N=8200, H=5))])
 def test_f16x3_rollout_costs_and_states(cid, over):
     from mbrl_amd import fused
     p = ocem.synth_problem(cid, **over)
@@ -96,16 +97,18 @@ def test_f16x3_full_size_plan_sampled_candidates(cid):
     assert np.array_equal(res["sigma"].cpu().numpy(), sg)
 
 
-def test_f16x3_activation_overflow_redone_in_f32():
-    """Candidates whose start state normalises past the split range (|x| >= 32768) are redone by the
-    F32 kernel: their 16-candidate workgroups match the F32 path bit for bit, the rest of the batch
-    stays F16X3 (within the return bar of the F32 path)."""
+@pytest.mark.parametrize("N,tile", [(256, 16), (8192, 32)])
+def test_f16x3_activation_overflow_redone_in_f32(N, tile):
+    """Candidates whose start state normalises past the split range (|x| >= 2048) are redone by the
+    F32 kernel: their workgroups (16 candidates, or 32 once N >= 8192) carry fp32 results (equal to
+    the F32 path's up to its summation order: the redo runs at the split kernel's tile height), the
+    rest of the batch stays F16X3 (within the return bar of the F32 path)."""
     from mbrl_amd import fused
-    p = ocem.synth_problem(3, N=256, H=6)
-    N, H, a, s = 256, 6, p["cfg"]["a"], p["cfg"]["s"]
+    p = ocem.synth_problem(3, N=N, H=6)
+    H, a, s = 6, p["cfg"]["a"], p["cfg"]["s"]
     f32, f16 = problems(p)
     s0 = np.tile(p["s0"], (N, 1)).astype(np.float32)
-    hot = [5, 40, 41, 200]                          # workgroups 0, 2, 12
+    hot = [5, 40, 41, 200]
     s0[hot, 3] = 1.0e6
     A = torch.from_numpy(cem_actions(np.zeros((H, a), np.float32), np.full((H, a), 0.5, np.float32), -1, 1, 3, 0,
                                      np.arange(N))).to(DEV)
@@ -117,17 +120,20 @@ def test_f16x3_activation_overflow_redone_in_f32():
     torch.cuda.synchronize()
     redone = np.zeros(N, bool)
     for n in hot:
-        redone[16 * (n // 16):16 * (n // 16) + 16] = True
+        redone[tile * (n // tile):tile * (n // tile) + tile] = True
     c32n, c16n = c32.cpu().numpy()[0], c16.cpu().numpy()[0]
-    bits = lambda x: x.view(np.int32)                # noqa: E731  (bitwise, NaN-safe)
-    assert np.array_equal(bits(c16n[redone]), bits(c32n[redone]))
+    # no redo mark survives, and the redone workgroups hold fp32 results
+    assert not np.any(c16n.view(np.uint32) == 0x7FC0DEAD)
+    assert np.allclose(c16n[redone], c32n[redone], rtol=1e-6, atol=0, equal_nan=True)
     m = torch.from_numpy(redone).to(DEV)
-    assert torch.equal(st16[:, :, m].view(torch.int32), st32[:, :, m].view(torch.int32))
+    assert torch.allclose(st16[:, :, m], st32[:, :, m], rtol=1e-4, atol=1e-4, equal_nan=True)
+    if tile == 16:   # same tile height and waves as the F32 path at this N: bit for bit
+        assert np.array_equal(c16n[redone].view(np.int32), c32n[redone].view(np.int32))
     assert rel_err(c16n[~redone], c32n[~redone].astype(np.float64)) < RTOL
 
 
 def test_f16x3_weight_out_of_range_falls_back_to_f32():
-    """A weight with |w| >= 32768 cannot be split: the pack flags it and every workgroup is redone in
+    """A weight with |w| >= 128 cannot be split: the pack flags it and every workgroup is redone in
     F32, so the F16X3 call returns the F32 costs exactly."""
     from mbrl_amd import fused
     p = ocem.synth_problem(2, N=300, H=5)

@@ -27,7 +27,7 @@ __global__ void __launch_bounds__(NW * 64) stream_kernel(const f32x4* __restrict
 }
 
 template <int NW, int DEPTH>
-void run(const f32x4* w, size_t bytes, float* out) {
+void run(const f32x4* w, size_t bytes, float* out, int grid = 256) {
     const size_t frags = bytes / 1024 / NW;  // per wave per step
     const int steps = 30;
     hipFuncSetAttribute((const void*)&stream_kernel<NW, DEPTH>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -35,15 +35,15 @@ void run(const f32x4* w, size_t bytes, float* out) {
     hipEventCreate(&a); hipEventCreate(&b);
     for (int rep = 0; rep < 3; ++rep) {
         hipEventRecord(a);
-        hipLaunchKernelGGL((stream_kernel<NW, DEPTH>), dim3(256), dim3(NW * 64), 96 * 1024, 0, w, frags, steps, out);
+        hipLaunchKernelGGL((stream_kernel<NW, DEPTH>), dim3(grid), dim3(NW * 64), 96 * 1024, 0, w, frags, steps, out);
         hipEventRecord(b);
         hipEventSynchronize(b);
     }
     float ms;
     hipEventElapsedTime(&ms, a, b);
     const double per_cu = (double)bytes * steps / (ms * 1e-3) / 1e9;
-    printf("waves/CU %2d  loads-in-flight/wave %2d : %.3f ms  per-CU %.1f GB/s  chip %.2f TB/s\n", NW, DEPTH, ms,
-           per_cu, per_cu * 256 / 1e3);
+    printf("workgroups %3d  waves/CU %2d  loads-in-flight/wave %2d : %.3f ms  per-CU %.1f GB/s  chip %.2f TB/s\n", grid,
+           NW, DEPTH, ms, per_cu, per_cu * grid / 1e3);
 }
 
 int main() {
@@ -60,5 +60,11 @@ int main() {
     run<8, 16>(w, bytes, out);
     run<16, 8>(w, bytes, out);
     run<16, 4>(w, bytes, out);
+    // half the CUs streaming (32 candidates per workgroup at N = 4096): per-CU rate when the
+    // aggregate L2 bandwidth is not shared by every CU
+    run<8, 8>(w, bytes, out, 128);
+    run<8, 16>(w, bytes, out, 128);
+    run<16, 8>(w, bytes, out, 128);
+    run<8, 8>(w, bytes, out, 64);
     return 0;
 }
