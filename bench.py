@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=3, help="SURVEY.md §8d config id (default: cheetah-run CEM)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--precision", default="f32", choices=["f32", "f16x3"],
+    ap.add_argument("--precision", default="f32", choices=["f32", "f16x3", "f16x6"],
                     help="rollout matmul precision (include/mbrl_cem.h MBRL_PRECISION_*)")
     ap.add_argument("--no-variants", action="store_true",
                     help="skip the second-precision measurement (rocprof runs: only the headline launches)")
@@ -183,7 +183,8 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32" if args.precision == "f32" else "f32 (f16x3 split MFMA: fp32 emulated, 22-bit operands)",
+        "dtype": {"f32": "f32", "f16x3": "f32 (f16x3 split MFMA: fp32 emulated, 22-bit operands)",
+                  "f16x6": "f32 (f16x6 split MFMA: fp32 emulated, 33-bit operands, fp32 accumulation)"}[args.precision],
         "data": "synthetic (random nn.Linear-law weights, PCG64 seed 1000+config; Philox proposals)",
         "config": {"workload": f"{cfg['name']} CEM N={N} H={H} s={cfg['s']} a={cfg['a']} "
                                f"{cfg['L']}x{cfg['W']} MLP E={E} I={ITERATIONS} K={K}",
@@ -198,19 +199,23 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["parity"] = parity_sample(prob, first)
     if not args.no_variants:
-        # the same workload with the other matmul precision (include/mbrl_cem.h MBRL_PRECISION_*)
-        other = "f16x3" if args.precision == "f32" else "f32"
-        v_elapsed, v_rollout_s, v_first = timed(other)
-        var = dict(precision=other, value=cand_steps / v_elapsed, ms_per_step=v_elapsed / args.steps * 1e3,
-                   rollout_avg_launch_ms=v_rollout_s * 1e3,
-                   rollout_tflops_fp32_equivalent=flop_launch / v_rollout_s / 1e12,
-                   note="fp32 emulated on the f16 matrix cores: operands split into two f16 pieces (22 "
-                        "significant bits), 3 products per fp32 product, fp32 accumulation; same parity bars "
-                        "(tests/test_gpu_f16x3.py); bound by the L2 weight stream, not by MFMA"
-                        if other == "f16x3" else "exact fp32 MFMA")
-        if rank == 0 and world == 1 and not args.no_cpu_baseline:
-            var["parity"] = parity_sample(prob, v_first)
-        out["variants"] = [var]
+        # the same workload with the other matmul precisions (include/mbrl_cem.h MBRL_PRECISION_*)
+        notes = {"f32": "exact fp32 MFMA",
+                 "f16x3": "fp32 emulated on the f16 matrix cores: operands split into two f16 pieces (22 "
+                          "significant bits), 3 partial products, fp32 accumulation; same parity bars "
+                          "(tests/test_gpu_f16x3.py); bound by the L2 weight stream",
+                 "f16x6": "fp32 emulated on the f16 matrix cores: operands split into three f16 pieces (33 "
+                          "significant bits), the 6 partial products x_i w_j with i + j < 3 (exact), fp32 "
+                          "accumulation; same parity bars (tests/test_gpu_f16x3.py)"}
+        out["variants"] = []
+        for other in [p for p in ("f32", "f16x6", "f16x3") if p != args.precision]:
+            v_elapsed, v_rollout_s, v_first = timed(other)
+            var = dict(precision=other, value=cand_steps / v_elapsed, ms_per_step=v_elapsed / args.steps * 1e3,
+                       rollout_avg_launch_ms=v_rollout_s * 1e3,
+                       rollout_tflops_fp32_equivalent=flop_launch / v_rollout_s / 1e12, note=notes[other])
+            if rank == 0 and world == 1 and not args.no_cpu_baseline:
+                var["parity"] = parity_sample(prob, v_first)
+            out["variants"].append(var)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.config)
     if rank == 0:

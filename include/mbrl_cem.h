@@ -57,16 +57,19 @@ enum {
 
 /* Matrix-product precision of the rollout's MLP layers (mbrl_mlp_shape.precision).
  * F32   = v_mfma_f32_16x16x4_f32: exact fp32 products, fp32 accumulation.
- * F16X3 = fp32 emulated on the f16 matrix cores: each fp32 operand x is split into
- *         hi = f16(x) and lo = f16((x - hi) * 2^12) (22 significant bits), and every product is
- *         hi*hi + 2^-12 * (hi*lo + lo*hi) with fp32 accumulation (v_mfma_f32_16x16x32_f16,
- *         16x the fp32 matrix rate, so the three products still run 5.3x faster). The dropped
- *         lo*lo term and the two 11-bit residuals bound the per-product error by ~3 * 2^-22
- *         relative, below the fp32 rounding of a W-long dot product. Operands with
- *         |x| >= 32768 cannot be split; a workgroup that meets one redoes its candidates in F32
- *         (on the device, in the same call), so results never depend on the operand range.
- *         Used for goal-state costs with 256 <= W <= 512; every other case runs F32. */
-enum { MBRL_PRECISION_F32 = 0, MBRL_PRECISION_F16X3 = 1 };
+ * F16X3 / F16X6 = fp32 emulated on the f16 matrix cores (v_mfma_f32_16x16x32_f16, 16x the fp32
+ *         matrix rate). Each operand is scaled by an exact power of two and split into P f16
+ *         pieces x0 = f16(x), x1 = f16(x - x0) (, x2 = f16(x - x0 - x1)); the products x_i w_j with
+ *         i + j < P accumulate in fp32.
+ *         F16X3: P = 2, 3 products, operands to 22 significant bits (fp32: 24); the dropped
+ *                term is 2^-22 relative.
+ *         F16X6: P = 3, 6 products, operands to 33 significant bits, dropped terms <= 2^-33
+ *                relative: at least fp32's operand precision with exact partial products.
+ *         Operands past the split range (activations >= 2048, weights >= 128) cannot be split;
+ *         a workgroup that meets one redoes its candidates in F32 (on the device, in the same
+ *         call), so results never depend on the operand range. Used for goal-state costs with
+ *         256 <= W <= 512; every other case runs F32. */
+enum { MBRL_PRECISION_F32 = 0, MBRL_PRECISION_F16X3 = 1, MBRL_PRECISION_F16X6 = 2 };
 
 /* Dynamics MLP shape: Linear(s+a -> W), ReLU, [Linear(W -> W), ReLU] x (L-1), Linear(W -> s).
  * models.py:96-110 (Model, L = 2) generalised to L hidden layers; E ensemble members.
@@ -79,8 +82,8 @@ typedef struct {
     int32_t n_hidden;    /* L >= 1 */
     int32_t ensemble;    /* E >= 1 */
     int32_t reward_head; /* 0 or 1 */
-    int32_t precision;   /* MBRL_PRECISION_F32 or MBRL_PRECISION_F16X3 (rollout only; the packed
-                            buffer holds both weight streams, so one pack serves either) */
+    int32_t precision;   /* MBRL_PRECISION_* (rollout only; the packed buffer holds every weight
+                            stream, so one pack serves each precision) */
 } mbrl_mlp_shape;
 
 /* Normalisation affine, TransitionsDataset.normalize_field / unnormalize_field (data.py:255-260),

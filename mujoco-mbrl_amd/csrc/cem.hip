@@ -91,24 +91,26 @@ __global__ void pack_out_kernel(const float* __restrict__ w, const float* __rest
     }
 }
 
-// F16X3 split stream (rollout_f16x3.hip): chunk = 32 K rows; per chunk 8 waves x T fragments of
-// 64 lanes x 8 halves; fragment f of a hidden-type chunk = tile f >> 1, piece f & 1 (hi, lo).
+// Split streams (rollout_f16x3.hip): chunk = 32 K rows; per chunk 8 waves x (T/2 tiles x P pieces)
+// fragments of 64 lanes x 8 halves. Fragment f of a hidden-type chunk = tile f / P, piece f % P.
 // Lane l, element q: row n = 16 (wave T/2 + tile) + (l & 15), k = 32 kc + 8 (l >> 4) + q.
-// Weights are scaled by MBRL_SPLIT_W_SCALE (exact) and split as hi = f16(w), lo = f16(w - hi). A
-// scaled weight >= 32768 (|w| >= 128) cannot be split: *bad becomes nonzero and every workgroup of
-// the rollout leaves its candidates to the fp32 redo pass.
-__device__ __forceinline__ void split_weight(float v0, _Float16* hi, _Float16* lo, unsigned* bad) {
-    const float v = v0 * MBRL_SPLIT_W_SCALE;
-    const _Float16 h = (_Float16)v;
-    *hi = h;
-    *lo = (_Float16)(v - (float)h);
+// Weights are scaled by MBRL_SPLIT_W_SCALE (exact) and split as w0 = f16(w), w1 = f16(w - w0),
+// w2 = f16(w - w0 - w1). A scaled weight >= 32768 (|w| >= 128) cannot be split: *bad becomes
+// nonzero and every workgroup of the rollout leaves its candidates to the fp32 redo pass.
+__device__ __forceinline__ void split_weight(float v0, int P, _Float16* dst, unsigned* bad) {
+    float v = v0 * MBRL_SPLIT_W_SCALE;
     if (!(fabsf(v) < 32768.0f)) atomicOr(bad, 1u);
+    for (int q = 0; q < P; ++q) {
+        const _Float16 h = (_Float16)v;
+        dst[q * 512] = h;                 // piece q is fragment f + q: 64 lanes x 8 halves further
+        v = v - (float)h;
+    }
 }
 
 __global__ void pack_split_hidden_kernel(const float* __restrict__ w, int in_real, int out_real, int nkc, int T,
-                                         _Float16* __restrict__ dst, unsigned* __restrict__ bad) {
+                                         int P, _Float16* __restrict__ dst, unsigned* __restrict__ bad) {
     const int TW = T / 2;
-    const size_t total = (size_t)nkc * 8 * TW * 64 * 8;   // (kc, wave, tile, lane, q); both pieces per item
+    const size_t total = (size_t)nkc * 8 * TW * 64 * 8;   // (kc, wave, tile, lane, q); all pieces per item
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
         const int q = (int)(i & 7);
         const int lane = (int)((i >> 3) & 63);
@@ -119,17 +121,16 @@ __global__ void pack_split_hidden_kernel(const float* __restrict__ w, int in_rea
         const int n = 16 * (wave * TW + tile) + (lane & 15);
         const int k = 32 * kc + 8 * (lane >> 4) + q;
         const float v = (n < out_real && k < in_real) ? w[(size_t)n * in_real + k] : 0.0f;
-        const size_t frag = ((size_t)kc * 8 + wave) * T + 2 * tile;   // hi fragment; lo = frag + 1
-        const size_t o = (frag * 64 + lane) * 8 + q;
-        split_weight(v, dst + o, dst + o + 512, bad);
+        const size_t frag = ((size_t)kc * 8 + wave) * TW * P + (size_t)tile * P;   // piece 0
+        split_weight(v, P, dst + (frag * 64 + lane) * 8 + q, bad);
     }
 }
 
 // Output layer: chunk c pairs output tiles 2c, 2c + 1; wave w's K range is units [16 w TW, 16 (w+1) TW)
 // taken as K-chunks kk of two tiles (2kk, 2kk+1) in the accumulator order: element q of lane group
-// g is unit 16 (w TW + 2kk + (q >> 2)) + 4g + (q & 3). Fragment f = u TW + 2 kk + piece.
+// g is unit 16 (w TW + 2kk + (q >> 2)) + 4g + (q & 3). Fragment f = (u TW/2 + kk) P + piece.
 __global__ void pack_split_out_kernel(const float* __restrict__ w, const float* __restrict__ w_r, int in_real,
-                                      int out_real, int NOS, int T, _Float16* __restrict__ dst,
+                                      int out_real, int NOS, int T, int P, _Float16* __restrict__ dst,
                                       unsigned* __restrict__ bad) {
     const int TW = T / 2, KK = TW / 2;
     const size_t total = (size_t)NOS * 8 * 2 * KK * 64 * 8;   // (c, wave, u, kk, lane, q)
@@ -148,9 +149,8 @@ __global__ void pack_split_out_kernel(const float* __restrict__ w, const float* 
             if (n < out_real) v = w[(size_t)n * in_real + k];
             else if (w_r && n == out_real) v = w_r[k];
         }
-        const size_t frag = ((size_t)c * 8 + wave) * T + u * TW + 2 * kk;
-        const size_t o = (frag * 64 + lane) * 8 + q;
-        split_weight(v, dst + o, dst + o + 512, bad);
+        const size_t frag = ((size_t)c * 8 + wave) * TW * P + (size_t)(u * KK + kk) * P;
+        split_weight(v, P, dst + (frag * 64 + lane) * 8 + q, bad);
     }
 }
 
@@ -658,7 +658,8 @@ __global__ void member_mean_kernel(const float* __restrict__ src, int E, int n, 
 // ------------------------------------------------------------------------------------------------
 static int shape_geometry(const mbrl_mlp_shape* sh, Geometry* g) {
     if (!sh) return fail(MBRL_EINVAL, "shape is NULL");
-    if (sh->precision != MBRL_PRECISION_F32 && sh->precision != MBRL_PRECISION_F16X3)
+    if (sh->precision != MBRL_PRECISION_F32 && sh->precision != MBRL_PRECISION_F16X3 &&
+        sh->precision != MBRL_PRECISION_F16X6)
         return fail(MBRL_EINVAL, "precision %d is not an MBRL_PRECISION_* value", sh->precision);
     if (!make_geometry(sh->state_dim, sh->action_dim, sh->hidden, sh->n_hidden, sh->ensemble, sh->reward_head, g))
         return fail(MBRL_EUNSUPPORTED,
@@ -745,31 +746,32 @@ static int rollout_impl(const Geometry& g, const void* packed, const mbrl_norm* 
     if (16 * g.a > 768) return fail(MBRL_EUNSUPPORTED, "action_dim %d too large (max 48)", g.a);
     // waves per workgroup as launch_rollout_t picks them: 8 for R = 1 (T >= 2), else 4
     A.nw = (R == 1 && g.T >= 2) ? 8 : 4;
-    if (g.precision == MBRL_PRECISION_F16X3 && g.split_ok && !A.reward) {
+    if ((g.precision == MBRL_PRECISION_F16X3 || g.precision == MBRL_PRECISION_F16X6) && g.split_ok && !A.reward) {
+        const int P = g.precision == MBRL_PRECISION_F16X6 ? 3 : 2;
         RolloutArgs S = A;
-        S.split_off = g.split_off;
+        S.split_off = P == 3 ? g.split3_off : g.split_off;
         S.K0S = g.K0S;
         S.CS = g.CS;
-        S.sr = 2 * (g.Wpad > 32 * g.K0S ? g.Wpad : 32 * g.K0S) + 8;
+        S.sr = P * (g.Wpad > 32 * g.K0S ? g.Wpad : 32 * g.K0S) + 8;
         S.nw = 8;
         // 32 candidates per workgroup once that still gives every CU a workgroup (N >= 8192): the
         // split kernel is bound by the L2 weight stream, which R = 2 halves per candidate. At
-        // N = 4096 R = 2 would idle half the CUs: 0.607 vs 0.571 ms per rollout (cheetah, r01).
+        // N = 4096 R = 2 would idle half the CUs: 0.607 vs 0.571 ms per F16X3 rollout (cheetah, r01).
         int RS = N >= 256 * 32 ? 2 : 1;
         if (const char* env = getenv("MBRL_SPLIT_R")) RS = atoi(env) == 2 ? 2 : 1;   // tuning override
         RolloutArgs X = A;                 // the fp32 redo pass at the same tile height
         X.redo = 1;
         X.nw = RS == 1 && g.T >= 2 ? 8 : 4;
-        if (RS == 2 && (!rollout_split_supported(S, g.T, 2) || rollout_lds_bytes(X, 32) > 160 * 1024)) {
+        if (RS == 2 && (!rollout_split_supported(S, g.T, 2, P) || rollout_lds_bytes(X, 32) > 160 * 1024)) {
             RS = 1;
             X.nw = g.T >= 2 ? 8 : 4;
         }
-        if (rollout_split_supported(S, g.T, RS)) {
-            hipError_t err = launch_rollout_split(S, g.T, RS, stream);
-            if (err != hipSuccess) return hip_check(err, "F16X3 rollout launch");
+        if (rollout_split_supported(S, g.T, RS, P)) {
+            hipError_t err = launch_rollout_split(S, g.T, RS, P, stream);
+            if (err != hipSuccess) return hip_check(err, "split rollout launch");
             // fp32 redo of the workgroups that met an operand outside the split range (usually none:
             // every workgroup reads its candidates' costs and exits)
-            return hip_check(launch_rollout(X, g.T, RS, stream), "F16X3 redo launch");
+            return hip_check(launch_rollout(X, g.T, RS, stream), "split redo launch");
         }
     }
     if (rollout_lds_bytes(A, 16 * R) > 160 * 1024) {
@@ -890,13 +892,17 @@ int mbrl_mlp_pack(const mbrl_mlp_shape* shape, const float* const* weights, cons
         float* base = static_cast<float*>(packed) + (size_t)e * g.member_stride;
         float* bias_base = base + g.stream_floats;
         size_t chunk = 0;
-        _Float16* split_base = reinterpret_cast<_Float16*>(base + g.split_off);
-        unsigned* split_bad = reinterpret_cast<unsigned*>(base + g.split_off + (size_t)g.CS * 2048 * g.T);
+        // the 2-piece (F16X3) and 3-piece (F16X6) split streams, each followed by its flag word
+        _Float16* split_base[2] = {reinterpret_cast<_Float16*>(base + g.split_off),
+                                   reinterpret_cast<_Float16*>(base + g.split3_off)};
+        unsigned* split_bad[2] = {reinterpret_cast<unsigned*>(base + g.split_off + (size_t)g.CS * 2048 * g.T),
+                                  reinterpret_cast<unsigned*>(base + g.split3_off + (size_t)g.CS * 3072 * g.T)};
         size_t split_chunk = 0;
-        if (g.split_ok) {
-            hipError_t err = hipMemsetAsync(split_bad, 0, 4, stream);
-            if (err != hipSuccess) return hip_check(err, "pack flag reset");
-        }
+        if (g.split_ok)
+            for (int q = 0; q < 2; ++q) {
+                hipError_t err = hipMemsetAsync(split_bad[q], 0, 4, stream);
+                if (err != hipSuccess) return hip_check(err, "pack flag reset");
+            }
         for (int l = 0; l <= g.L; ++l) {
             const float* w = weights[e * nl + l];
             const float* b = biases[e * nl + l];
@@ -911,8 +917,10 @@ int mbrl_mlp_pack(const mbrl_mlp_shape* shape, const float* const* weights, cons
                 hipLaunchKernelGGL(pack_transposed_kernel, dim3(256), dim3(256), 0, stream, w, in_real, g.W, g.Wpad, plain);
                 if (g.split_ok) {
                     const int nks = l == 0 ? g.K0S : 2 * g.T;
-                    hipLaunchKernelGGL(pack_split_hidden_kernel, dim3(256), dim3(256), 0, stream, w, in_real, g.W, nks,
-                                       g.T, split_base + split_chunk * 4096 * (size_t)g.T, split_bad);
+                    for (int P = 2; P <= 3; ++P)
+                        hipLaunchKernelGGL(pack_split_hidden_kernel, dim3(256), dim3(256), 0, stream, w, in_real, g.W,
+                                           nks, g.T, P, split_base[P - 2] + split_chunk * 2048 * (size_t)g.T * P,
+                                           split_bad[P - 2]);
                     split_chunk += nks;
                 }
                 chunk += nkc;
@@ -922,8 +930,10 @@ int mbrl_mlp_pack(const mbrl_mlp_shape* shape, const float* const* weights, cons
                 if (g.reward && (!wr || !br)) return fail(MBRL_EINVAL, "pack: NULL reward head for member %d", e);
                 hipLaunchKernelGGL(pack_out_kernel, dim3(256), dim3(256), 0, stream, w, wr, g.W, g.s, g.NOT, g.T, dst);
                 if (g.split_ok)
-                    hipLaunchKernelGGL(pack_split_out_kernel, dim3(256), dim3(256), 0, stream, w, wr, g.W, g.s, g.NOS,
-                                       g.T, split_base + split_chunk * 4096 * (size_t)g.T, split_bad);
+                    for (int P = 2; P <= 3; ++P)
+                        hipLaunchKernelGGL(pack_split_out_kernel, dim3(256), dim3(256), 0, stream, w, wr, g.W, g.s,
+                                           g.NOS, g.T, P, split_base[P - 2] + split_chunk * 2048 * (size_t)g.T * P,
+                                           split_bad[P - 2]);
                 float* ob = bias_base + (size_t)g.L * g.Wpad;
                 hipLaunchKernelGGL(pack_bias_kernel, dim3(1), dim3(256), 0, stream, b, g.s, 16 * g.NOT, ob);
                 hipLaunchKernelGGL(copy_kernel, dim3(64), dim3(256), 0, stream, w, (size_t)g.s * g.W, plain);

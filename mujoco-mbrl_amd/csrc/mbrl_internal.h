@@ -35,8 +35,10 @@ struct Geometry {
     int K0S;               // layer-0 chunks of 32 (K0S + NOS even)
     int NOS;               // output chunks (pairs of 16-row output tiles) = NOT / 2
     int CS;                // split chunks per step = K0S + (L-1)*2T + NOS
-    size_t split_off;      // floats from the member base
+    size_t split_off;      // floats from the member base: the 2-piece stream (F16X3)
     size_t split_floats;   // CS * 2048 * T, then one flag word (nonzero: a weight is out of split range)
+    size_t split3_off;     // the 3-piece stream (F16X6): CS * 3072 * T floats, then its flag word
+    size_t split3_floats;
     size_t member_stride;  // floats per ensemble member (64-float aligned)
 };
 
@@ -78,7 +80,9 @@ inline bool make_geometry(int s, int a, int W, int L, int E, int reward, Geometr
     g->CS = g->K0S + (L - 1) * 2 * T + g->NOS;
     g->split_off = (end + 63) / 64 * 64;
     g->split_floats = g->split_ok ? (size_t)g->CS * 2048 * T + 64 : 0;
-    if (g->split_ok) end = g->split_off + g->split_floats;
+    g->split3_off = g->split_off + g->split_floats;
+    g->split3_floats = g->split_ok ? (size_t)g->CS * 3072 * T + 64 : 0;
+    if (g->split_ok) end = g->split3_off + g->split3_floats;
     g->member_stride = (end + 63) / 64 * 64;
     return true;
 }
@@ -104,7 +108,7 @@ struct RolloutArgs {
     float* costs;
     float* actions_out;
     float* states_out;
-    // F16X3 (rollout_f16x3.hip) and its F32 redo pass
+    // F16X3 / F16X6 (rollout_f16x3.hip) and the F32 redo pass
     size_t split_off;
     int K0S, CS, sr;       // sr: LDS activation row stride in halves
     int redo;              // F32 kernel: only workgroups whose candidates carry MBRL_REDO_MARK run
@@ -162,9 +166,10 @@ hipError_t launch_rollout(const RolloutArgs& A, int T, int R, hipStream_t stream
 
 // F16X3 rollout (8 waves, 16 R candidates per workgroup, goal-state cost). Supported for
 // geometry.split_ok; the caller follows it with launch_rollout(redo = 1) at the same R.
-bool rollout_split_supported(const RolloutArgs& A, int T, int R);
+// P = 2 (F16X3) or 3 (F16X6) operand pieces; A.split_off / A.sr must describe that stream.
+bool rollout_split_supported(const RolloutArgs& A, int T, int R, int P);
 size_t rollout_split_lds_bytes(const RolloutArgs& A, int R);
-hipError_t launch_rollout_split(const RolloutArgs& A, int T, int R, hipStream_t stream);
+hipError_t launch_rollout_split(const RolloutArgs& A, int T, int R, int P, hipStream_t stream);
 
 // Single-trajectory rollout (one candidate per ensemble member): the final CEM mean's predicted
 // states. Latency-bound, so VALU dot products over plain weight copies on one workgroup per member

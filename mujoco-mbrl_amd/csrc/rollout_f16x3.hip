@@ -1,35 +1,40 @@
-// F16X3 persistent rollout: the rollout_kernel (rollout.hip) schedule with every Linear emulating
-// fp32 on the f16 matrix cores (mbrl_cem.h, MBRL_PRECISION_F16X3).
+// Split-operand persistent rollout: the rollout_kernel (rollout.hip) schedule with every Linear
+// emulating fp32 on the f16 matrix cores (mbrl_cem.h, MBRL_PRECISION_F16X3 / MBRL_PRECISION_F16X6).
 //
 // Why. The fp32 kernel is MFMA-bound: v_mfma_f32_16x16x4_f32 gives 32 MAC/clk/SIMD, and with
 // 16 candidates per CU (N = 4096 over 256 CUs) every step re-streams the whole weight set (2.2 MB
 // for 3x512) from L2 at ~65 GB/s per CU. v_mfma_f32_16x16x32_f16 gives 512 MAC/clk/SIMD, so
-// the three split products of each fp32 product cost 3/16 of the fp32 instruction, and the step
-// becomes bound by the L2 weight stream instead (~125 GB/s per CU, tools/ubench/l2stream.hip).
-// The split weights are two f16 (4 bytes per weight, as fp32), so the stream does not grow.
+// the split products of each fp32 product cost 3/16 (F16X3) or 6/16 (F16X6) of the fp32
+// instruction, and the step becomes bound by the L2 weight stream instead (~125 GB/s per CU when
+// every CU streams, ~153 GB/s when half do: tools/ubench/l2stream.hip).
 //
-// Split. An operand is scaled by an exact power of two (activations 2^4, weights 2^8) and split as
-// x = hi + lo + r, hi = f16(x), lo = f16(x - hi): x - hi is exact in fp32 and lo keeps 11 more
-// bits, so |r| <= 2^-22 |x| while lo is a normal f16 (|x| >= 2^-6 activations, 2^-10 weights;
-// below that the error is absolute, under 2^-29 and 2^-33). A product is hi_w hi_x + hi_w lo_x +
-// lo_w hi_x, all three into ONE fp32 accumulator (every product is at scale 2^12); the dropped
-// lo_w lo_x is 2^-22 relative. The layer output is acc * 2^-12 (exact). Scaled operands with
-// |x| >= 32768 (activations >= 2048, weights >= 128) would not split: the workgroup then marks its
-// candidates (MBRL_REDO_MARK) and the fp32 kernel's redo pass recomputes them.
+// Split into P pieces. An operand is scaled by an exact power of two (activations 2^4, weights
+// 2^8) and split as x = x0 + x1 (+ x2) + r, x0 = f16(x), x1 = f16(x - x0), x2 = f16(x - x0 - x1):
+// every difference is exact in fp32 and each piece keeps 11 more bits, so |r| <= 2^-22 |x| (P = 2)
+// or 2^-33 |x| (P = 3) while the last piece is a normal f16 (P = 2: |x| >= 2^-6 activations,
+// 2^-10 weights; P = 3: |x| >= 2^4 and 2^0); below that the error is absolute, under 2^-29
+// (activations) and 2^-33 (weights). The kept products are every x_i w_j with i + j < P:
+//   P = 2 (F16X3): x0w0 + x0w1 + x1w0; the dropped x1w1 is 2^-22 relative;
+//   P = 3 (F16X6): x0w0 + x0w1 + x1w0 + x0w2 + x1w1 + x2w0; dropped terms <= 2^-33 relative.
+// All into ONE fp32 accumulator (every product is at scale 2^12); the layer output is acc * 2^-12
+// (exact). F16X6 thus carries operands to 33 significant bits (fp32: 24), forms the partial products
+// exactly and accumulates in fp32. Scaled operands with |x| >= 32768 (activations >= 2048, weights
+// >= 128) would not split: the workgroup then marks its candidates (MBRL_REDO_MARK) and the fp32
+// kernel's redo pass recomputes them.
 //
 // Operand layouts for v_mfma_f32_16x16x32_f16 (cdna_hip_programming.md §3): lane l holds
 // A[row l&15][k = 8(l>>4) + e] and B[k = 8(l>>4) + e][col l&15], e = 0..7; C as the f32 form.
 // Weights are A (Y^T = W X^T, as rollout.hip), activations are B, so the accumulator of tile j
 // holds units 16j + 4(l>>4) + v of candidate l&15.
-//   * hidden-type layers (layer 0, W -> W): B comes from LDS, rows [hi: kmax halves | lo: kmax]
+//   * hidden-type layers (layer 0, W -> W): B comes from LDS, rows [x0: kmax | x1: kmax (| x2)]
 //     per candidate; chunk kc covers K rows 32kc .. 32kc + 31 in natural order.
 //   * output layer: K split over the 8 waves and fed from registers. A K-chunk pairs two of the
 //     wave's own tiles (2kk, 2kk+1): lane group g's eight k are units {4g..4g+3} of each, exactly
 //     what its accumulators hold; the weight pack uses the same permutation (cem.hip).
-// One workgroup = 8 waves = 16 candidates of one member for all H steps; wave w owns units
-// [w W/8, (w+1) W/8) of every hidden layer (TW = T/2 tiles). Per chunk a wave loads T fragments
-// (TW tiles x {hi, lo}) through a register ring of 4 slots of 4 fragments (a chunk is T/4 slots),
-// 3 slots (12 KiB per wave) ahead across layers and steps.
+// One workgroup = 8 waves = 16 R candidates of one member for all H steps; wave w owns units
+// [w W/8, (w+1) W/8) of every hidden layer (TW = T/2 tiles). Per chunk a wave loads TW P fragments
+// (TW tiles x P pieces, 1 KiB each) through a register ring of 4 slots of TS tiles (TS P fragments),
+// 3 slots ahead across layers and steps.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -56,7 +61,7 @@ constexpr float SPLIT_LIMIT = 32768.0f;     // |scaled operand| past this: redo 
 #define SPIN() __builtin_amdgcn_sched_barrier(0)
 
 struct SplitLds {
-    _Float16 *x, *y;   // activation rows [hi: kmax | lo: kmax]; y == x without ping-pong (R = 2)
+    _Float16 *x, *y;   // activation rows [x0: kmax | x1: kmax (| x2)]; y == x without ping-pong (R = 2)
     float *part, *acs, *obs_mean, *obs_std, *act_mean, *act_std, *goal, *cw, *hbias;
     int* flag;
     size_t bytes;
@@ -95,20 +100,29 @@ __host__ __device__ inline SplitLds split_lds(const RolloutArgs& A, int R, void*
     return L;
 }
 
-__device__ __forceinline__ void split4(const f32x4 x0, f16x4& hi, f16x4& lo, bool& ovf) {
-    const f32x4 x = x0 * X_SCALE;
-    hi = __builtin_convertvector(x, f16x4);
-    lo = __builtin_convertvector(x - __builtin_convertvector(hi, f32x4), f16x4);
+// x -> P f16 pieces (scaled by X_SCALE); flags an operand outside the split range
+template <int P>
+__device__ __forceinline__ void split4(const f32x4 x0, f16x4 (&pc)[P], bool& ovf) {
+    f32x4 x = x0 * X_SCALE;
     const f32x4 ax = __builtin_elementwise_abs(x);
     ovf |= (ax.x >= SPLIT_LIMIT) | (ax.y >= SPLIT_LIMIT) | (ax.z >= SPLIT_LIMIT) | (ax.w >= SPLIT_LIMIT);
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+        pc[q] = __builtin_convertvector(x, f16x4);
+        if (q + 1 < P) x = x - __builtin_convertvector(pc[q], f32x4);
+    }
 }
 
+template <int P>
 __device__ __forceinline__ void split_store1(float x0, _Float16* row, int kmax, int d, bool& ovf) {
-    const float x = x0 * X_SCALE;
-    const _Float16 hi = (_Float16)x;
-    row[d] = hi;
-    row[kmax + d] = (_Float16)(x - (float)hi);
+    float x = x0 * X_SCALE;
     ovf |= fabsf(x) >= SPLIT_LIMIT;
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+        const _Float16 h = (_Float16)x;
+        row[q * kmax + d] = h;
+        if (q + 1 < P) x = x - (float)h;
+    }
 }
 
 __device__ __forceinline__ f32x4 mfma16(const f32x4 a_raw, const f16x8 b, const f32x4 c) {
@@ -122,11 +136,21 @@ __device__ __forceinline__ void sload(f32x4 (&dst)[FR], __amdgpu_buffer_rsrc_t r
         dst[f] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + (unsigned)(f * 1024), soff, 0));
 }
 
-__device__ __forceinline__ void read_b(f16x8& bh, f16x8& bl, const _Float16* act, int sr, int kmax, int kc, int lane,
-                                       int r) {
+template <int P>
+__device__ __forceinline__ void read_b(f16x8 (&b)[P], const _Float16* act, int sr, int kmax, int kc, int lane, int r) {
     const _Float16* row = act + (16 * r + (lane & 15)) * sr + 32 * kc + 8 * (lane >> 4);
-    bh = *reinterpret_cast<const f16x8*>(row);
-    bl = *reinterpret_cast<const f16x8*>(row + kmax);
+#pragma unroll
+    for (int q = 0; q < P; ++q) b[q] = *reinterpret_cast<const f16x8*>(row + q * kmax);
+}
+
+// acc += sum over i + j < P of x_i w_j (w: this tile's P fragments)
+template <int P>
+__device__ __forceinline__ f32x4 split_mma(const f32x4* w, const f16x8 (&x)[P], f32x4 acc) {
+#pragma unroll
+    for (int d = 0; d < P; ++d)          // order: by significance, x0w0 first
+#pragma unroll
+        for (int i = 0; i <= d; ++i) acc = mfma16(w[d - i], x[i], acc);
+    return acc;
 }
 
 template <int TW>
@@ -144,19 +168,18 @@ __device__ __forceinline__ float rowsum16(float v) {
     return v;
 }
 
-template <int T, int R, int K0S, int NOS>
+template <int T, int R, int P, int TS, int K0S, int NOS>
 struct SplitRollout {
     static constexpr int M = 16 * R;        // candidates per workgroup (R 16-column B tiles)
     static constexpr bool PP = R == 1;      // ping-pong activation buffers (split_lds)
     static constexpr int TW = T / 2;        // tiles per wave per hidden layer
-    static constexpr int FR = T;            // fragments per wave per chunk (TW tiles x {hi, lo})
-    static constexpr int SUB = T / 4;       // ring slots (sub-chunks of 4 fragments) per chunk
-    static constexpr int FS = 4;            // fragments per ring slot
-    static constexpr int TS = TW / SUB;     // tiles per sub-chunk (2)
+    static constexpr int FR = TW * P;       // fragments per wave per chunk (TW tiles x P pieces)
+    static constexpr int FS = TS * P;       // fragments per ring slot
+    static constexpr int SUB = TW / TS;     // ring slots per chunk
     static constexpr int KH = 2 * T;        // chunks per hidden layer
     static constexpr int SS = 2 * NOS;      // state slots per lane (ceil(s / 16) <= NOT)
     static constexpr int SHIFT = ((K0S + NOS) * SUB) % SNB;
-    static_assert(TW % 2 == 0 && TS == 2 && (KH * SUB) % SNB == 0 && (SHIFT == 0 || 2 * SHIFT == SNB),
+    static_assert(TW % 2 == 0 && TW % TS == 0 && (KH * SUB) % SNB == 0 && (SHIFT == 0 || 2 * SHIFT == SNB),
                   "ring phases");
 
     const RolloutArgs& A;
@@ -170,14 +193,14 @@ struct SplitRollout {
     float av[R][SMAXA];
     float total[R];
     bool ovf = false;
-    int g = 0;                      // sub-chunk index within the step
+    int g = 0;                      // ring-slot index within the step
 
     __device__ SplitRollout(const RolloutArgs& A_, const SplitLds& L_, int wave_, int lane_, int tile_, int e_,
                             const float* member)
         : A(A_), L(L_), wave(wave_), lane(lane_), tile(tile_), e(e_), kmax(split_kmax(A_)), epi(wave_ < 4),
           actw(wave_ >= 4) {
         rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(member + A.split_off), 0,
-                                                 (int)((size_t)A.CS * 8192 * T), 0x00020000);
+                                                 (int)((size_t)A.CS * SW * FR * 1024), 0x00020000);
         voff = (unsigned)((wave * FR * 64 + lane) * 16);
 #pragma unroll
         for (int r = 0; r < R; ++r) total[r] = 0.f;
@@ -186,12 +209,12 @@ struct SplitRollout {
     // epilogue / action row of this lane in candidate tile r: 16 r + 4 (wave & 3) + (lane >> 4)
     __device__ __forceinline__ int row_of(int r) const { return 16 * r + 4 * (wave & 3) + (lane >> 4); }
 
-    // sub-chunk G of the step sequence (wrapping into the next step): chunk G / SUB, fragments
+    // ring slot G of the step sequence (wrapping into the next step): chunk G / SUB, fragments
     // [FS (G % SUB), FS (G % SUB + 1)) of this wave's slice
-    __device__ __forceinline__ void load_sub(f32x4 (&dst)[FS], int G) {
+    __device__ __forceinline__ void load_slot(f32x4 (&dst)[FS], int G) {
         const int css = A.CS * SUB;
         const int gp = G < css ? G : G - css;
-        const unsigned soff = (unsigned)(gp / SUB) * (unsigned)(8192 * T) + (unsigned)((gp % SUB) * FS * 1024);
+        const unsigned soff = (unsigned)(gp / SUB) * (unsigned)(SW * FR * 1024) + (unsigned)((gp % SUB) * FS * 1024);
         sload<FS>(dst, rsrc, voff, soff);
     }
 
@@ -217,7 +240,7 @@ struct SplitRollout {
                 const int d = (lane & 15) + 16 * k;
                 if (d < A.a) {
                     const float x = av[r][k];
-                    split_store1(A.norm_a ? (x - L.act_mean[d]) / L.act_std[d] : x, row, kmax, A.s + d, ovf);
+                    split_store1<P>(A.norm_a ? (x - L.act_mean[d]) / L.act_std[d] : x, row, kmax, A.s + d, ovf);
                     if (A.has_ac) c += coshf(x / A.alpha_a) - 1.0f;
                 }
             }
@@ -230,8 +253,8 @@ struct SplitRollout {
         const int k0 = A.s + A.a, k1 = 32 * A.K0S;
         for (int i = threadIdx.x; i < M * (k1 - k0); i += 64 * SW) {
             const int m = i / (k1 - k0), d = k0 + i - (i / (k1 - k0)) * (k1 - k0);
-            L.x[m * A.sr + d] = (_Float16)0.f;
-            L.x[m * A.sr + kmax + d] = (_Float16)0.f;
+#pragma unroll
+            for (int q = 0; q < P; ++q) L.x[m * A.sr + q * kmax + d] = (_Float16)0.f;
         }
     }
 
@@ -255,19 +278,19 @@ struct SplitRollout {
             const int m = i / A.s, d = i - (i / A.s) * A.s;
             const int n = min(tile * M + m, A.N - 1);
             const float sv = A.s0_per_cand ? A.s0[(size_t)n * A.s + d] : A.s0[d];
-            split_store1(A.norm_s ? (sv - L.obs_mean[d]) / L.obs_std[d] : sv, L.x + m * A.sr, kmax, d, ovf);
+            split_store1<P>(A.norm_s ? (sv - L.obs_mean[d]) / L.obs_std[d] : sv, L.x + m * A.sr, kmax, d, ovf);
         }
         zero_pad();
         if (actw) stage_actions(0);
         __syncthreads();
 #pragma unroll
-        for (int q = 0; q < SNB - 1; ++q) load_sub(ring[q], q);
+        for (int q = 0; q < SNB - 1; ++q) load_slot(ring[q], q);
     }
 
-    // refill the slot chunk g-1 vacated with chunk g+SNB-1; `slot` folds to a constant once the
+    // refill the slot that slot g-1 vacated with slot g+SNB-1; `slot` folds to a constant once the
     // chunk loops are unrolled (the ring must stay in registers)
     __device__ __forceinline__ void prefetch(int slot) {
-        load_sub(ring[(slot + SNB - 1) % SNB], g + SNB - 1);
+        load_slot(ring[(slot + SNB - 1) % SNB], g + SNB - 1);
     }
 
     __device__ __forceinline__ void zero_acc() {
@@ -280,15 +303,15 @@ struct SplitRollout {
     // Hidden-type layer over NK chunks (NK * SUB ring slots from slot S0), B rows from `in`. The B
     // fragments of chunk kc + 1 are read one chunk ahead when R = 1; at R = 2 (twice the B and
     // accumulator registers) they are read at the head of their own chunk, behind its first
-    // sub-chunk's weight prefetch.
+    // slot's weight prefetch.
     template <int S0, int NK>
     __device__ __forceinline__ void hidden_layer(const _Float16* in) {
         constexpr int NBB = R == 1 ? 2 : 1;
         zero_acc();
-        f16x8 bh[NBB][R], bl[NBB][R];
+        f16x8 bx[NBB][R][P];
         if (NBB == 2)
 #pragma unroll
-            for (int r = 0; r < R; ++r) read_b(bh[0][r], bl[0][r], in, A.sr, kmax, 0, lane, r);
+            for (int r = 0; r < R; ++r) read_b<P>(bx[0][r], in, A.sr, kmax, 0, lane, r);
 #pragma unroll
         for (int kc = 0; kc < NK; ++kc) {
 #pragma unroll
@@ -300,26 +323,23 @@ struct SplitRollout {
                     if (NBB == 2) {
                         if (kc + 1 < NK)
 #pragma unroll
-                            for (int r = 0; r < R; ++r)
-                                read_b(bh[(kc + 1) & 1][r], bl[(kc + 1) & 1][r], in, A.sr, kmax, kc + 1, lane, r);
+                            for (int r = 0; r < R; ++r) read_b<P>(bx[(kc + 1) & 1][r], in, A.sr, kmax, kc + 1, lane, r);
                     } else {
 #pragma unroll
-                        for (int r = 0; r < R; ++r) read_b(bh[0][r], bl[0][r], in, A.sr, kmax, kc, lane, r);
+                        for (int r = 0; r < R; ++r) read_b<P>(bx[0][r], in, A.sr, kmax, kc, lane, r);
                     }
                 }
                 const f32x4(&w)[FS] = ring[slot];
+                // significance-ordered products, interleaved over this slot's tiles and the R tiles
 #pragma unroll
-                for (int j = 0; j < TS; ++j)
+                for (int d = 0; d < P; ++d)
 #pragma unroll
-                    for (int r = 0; r < R; ++r) acc[r][TS * h + j] = mfma16(w[2 * j], bh[b][r], acc[r][TS * h + j]);
+                    for (int i = 0; i <= d; ++i)
 #pragma unroll
-                for (int j = 0; j < TS; ++j)
+                        for (int j = 0; j < TS; ++j)
 #pragma unroll
-                    for (int r = 0; r < R; ++r) acc[r][TS * h + j] = mfma16(w[2 * j], bl[b][r], acc[r][TS * h + j]);
-#pragma unroll
-                for (int j = 0; j < TS; ++j)
-#pragma unroll
-                    for (int r = 0; r < R; ++r) acc[r][TS * h + j] = mfma16(w[2 * j + 1], bh[b][r], acc[r][TS * h + j]);
+                            for (int r = 0; r < R; ++r)
+                                acc[r][TS * h + j] = mfma16(w[P * j + d - i], bx[b][r][i], acc[r][TS * h + j]);
                 SPIN();
                 ++g;
             }
@@ -334,65 +354,63 @@ struct SplitRollout {
         for (int r = 0; r < R; ++r)
 #pragma unroll
             for (int j = 0; j < TW; ++j) {
-                f16x4 h, l;
-                split4(layer_out<TW>(acc[r], hb, wave, j, lane), h, l, ovf);
+                f16x4 pc[P];
+                split4<P>(layer_out<TW>(acc[r], hb, wave, j, lane), pc, ovf);
                 _Float16* row = out + (16 * r + (lane & 15)) * A.sr + 16 * (wave * TW + j) + 4 * (lane >> 4);
-                *reinterpret_cast<f16x4*>(row) = h;
-                *reinterpret_cast<f16x4*>(row + kmax) = l;
+#pragma unroll
+                for (int q = 0; q < P; ++q) *reinterpret_cast<f16x4*>(row + q * kmax) = pc[q];
             }
         __syncthreads();
     }
 
     // Output layer (K split over the waves, B from this wave's last hidden tiles) -> part[wave].
-    // Output chunk q pairs tiles 2q + u (u = 0, 1); fragment u TW + 2 kk + piece; the ring slot of
-    // fragment f is sub-chunk f / FS.
+    // Output chunk q pairs tiles 2q + u (u = 0, 1); its fragments are (u TW/2 + kk) P + piece, so
+    // ring slot h of the chunk holds the (u, kk) pairs [h TS, (h + 1) TS).
     template <int S0>
     __device__ __forceinline__ void output_layer(const float* hb) {
-        f16x8 oh[R][TW / 2], ol[R][TW / 2];
+        constexpr int KK = TW / 2;
+        f16x8 ox[R][KK][P];
 #pragma unroll
         for (int r = 0; r < R; ++r)
 #pragma unroll
-            for (int kk = 0; kk < TW / 2; ++kk) {
-                f16x4 h0, l0, h1, l1;
-                split4(layer_out<TW>(acc[r], hb, wave, 2 * kk, lane), h0, l0, ovf);
-                split4(layer_out<TW>(acc[r], hb, wave, 2 * kk + 1, lane), h1, l1, ovf);
-                oh[r][kk] = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
-                ol[r][kk] = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
+            for (int kk = 0; kk < KK; ++kk) {
+                f16x4 p0[P], p1[P];
+                split4<P>(layer_out<TW>(acc[r], hb, wave, 2 * kk, lane), p0, ovf);
+                split4<P>(layer_out<TW>(acc[r], hb, wave, 2 * kk + 1, lane), p1, ovf);
+#pragma unroll
+                for (int q = 0; q < P; ++q) ox[r][kk][q] = __builtin_shufflevector(p0[q], p1[q], 0, 1, 2, 3, 4, 5, 6, 7);
             }
         float* part = L.part + wave * M * A.pw + (lane & 15) * A.pw + 4 * (lane >> 4);
 #pragma unroll
         for (int q = 0; q < NOS; ++q) {
+            f32x4 o[2][R];
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int r = 0; r < R; ++r) o[u][r] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int h = 0; h < SUB; ++h) {
                 const int slot = (S0 + q * SUB + h) % SNB;
                 prefetch(slot);
                 const f32x4(&w)[FS] = ring[slot];
 #pragma unroll
-                for (int u = 0; u < 2; ++u) {
-                    if ((u * TW) / FS != h) continue;      // this tile's fragments live in sub-chunk h
-                    const int f0 = u * TW - h * FS;
-                    f32x4 o[R];
+                for (int d = 0; d < P; ++d)
 #pragma unroll
-                    for (int r = 0; r < R; ++r) o[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    for (int i = 0; i <= d; ++i)
 #pragma unroll
-                    for (int kk = 0; kk < TW / 2; ++kk)
+                        for (int jj = 0; jj < TS; ++jj) {
+                            const int pair = TS * h + jj, u = pair / KK, kk = pair % KK;
 #pragma unroll
-                        for (int r = 0; r < R; ++r) o[r] = mfma16(w[f0 + 2 * kk], oh[r][kk], o[r]);
-#pragma unroll
-                    for (int kk = 0; kk < TW / 2; ++kk)
-#pragma unroll
-                        for (int r = 0; r < R; ++r) o[r] = mfma16(w[f0 + 2 * kk], ol[r][kk], o[r]);
-#pragma unroll
-                    for (int kk = 0; kk < TW / 2; ++kk)
-#pragma unroll
-                        for (int r = 0; r < R; ++r) o[r] = mfma16(w[f0 + 2 * kk + 1], oh[r][kk], o[r]);
-#pragma unroll
-                    for (int r = 0; r < R; ++r)
-                        *reinterpret_cast<f32x4*>(part + 16 * r * A.pw + 16 * (2 * q + u)) = o[r] * OUT_UNSCALE;
-                }
+                            for (int r = 0; r < R; ++r) o[u][r] = mfma16(w[P * jj + d - i], ox[r][kk][i], o[u][r]);
+                        }
                 SPIN();
                 ++g;
             }
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+                    *reinterpret_cast<f32x4*>(part + 16 * r * A.pw + 16 * (2 * q + u)) = o[u][r] * OUT_UNSCALE;
         }
     }
 
@@ -421,7 +439,7 @@ struct SplitRollout {
                             const float x = (sn - L.goal[d]) * L.cw[d];
                             sc += sqrtf(x * x + A.alpha_s2) - A.alpha_s;
                         }
-                        split_store1(A.norm_s ? (sn - om) / os : sn, row, kmax, d, ovf);
+                        split_store1<P>(A.norm_s ? (sn - om) / os : sn, row, kmax, d, ovf);
                         if (A.states_out != nullptr && n < A.N)
                             A.states_out[(((size_t)e * A.H + t) * A.N + n) * A.s + d] = sn;
                     }
@@ -476,7 +494,7 @@ struct SplitRollout {
     }
 };
 
-template <int T, int R, int K0S, int NOS>
+template <int T, int R, int P, int TS, int K0S, int NOS>
 __global__ void __launch_bounds__(64 * SW, 1) rollout_split_kernel(const RolloutArgs A) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int M = 16 * R;
@@ -485,14 +503,14 @@ __global__ void __launch_bounds__(64 * SW, 1) rollout_split_kernel(const Rollout
     const int tile = blockIdx.x, e = blockIdx.y;
     const float* member = A.packed + (size_t)e * A.member_stride;
     // a weight outside the split range (flag word written by the pack): leave it all to the redo pass
-    const unsigned bad = *reinterpret_cast<const unsigned*>(member + A.split_off + (size_t)A.CS * 2048 * T);
+    const unsigned bad = *reinterpret_cast<const unsigned*>(member + A.split_off + (size_t)A.CS * 2048 * T * P / 2);
     if (bad != 0u) {
         if (tid < M && tile * M + tid < A.N) A.costs[(size_t)e * A.N + tile * M + tid] = __uint_as_float(MBRL_REDO_MARK);
         return;
     }
-    SplitRollout<T, R, K0S, NOS> S(A, L, tid >> 6, tid & 63, tile, e, member);
+    SplitRollout<T, R, P, TS, K0S, NOS> S(A, L, tid >> 6, tid & 63, tile, e, member);
     S.prologue();
-    constexpr int SHIFT = SplitRollout<T, R, K0S, NOS>::SHIFT;
+    constexpr int SHIFT = SplitRollout<T, R, P, TS, K0S, NOS>::SHIFT;
     for (int t = 0; t < A.H; t += 2) {
         S.template step<0>(t);
         if (t + 1 < A.H) S.template step<SHIFT>(t + 1);
@@ -500,9 +518,14 @@ __global__ void __launch_bounds__(64 * SW, 1) rollout_split_kernel(const Rollout
     S.finish();
 }
 
-template <int T, int R, int K0S, int NOS>
+// ring-slot width: 2 tiles, or 1 tile where 2 would not fit the registers without spilling
+// (P = 3 at R = 2, or with three layer-0 / output chunks)
+template <int R, int P, int K0S, int NOS>
+constexpr int split_ts() { return (P == 2 || (R == 1 && K0S <= 2 && NOS <= 2)) ? 2 : 1; }
+
+template <int T, int R, int P, int K0S, int NOS>
 hipError_t launch_split_t(const RolloutArgs& A, hipStream_t stream) {
-    const auto fn = &rollout_split_kernel<T, R, K0S, NOS>;
+    const auto fn = &rollout_split_kernel<T, R, P, split_ts<R, P, K0S, NOS>(), K0S, NOS>;
     hipError_t err = ensure_dynamic_lds(reinterpret_cast<const void*>(fn), 160 * 1024);
     if (err != hipSuccess) return err;
     dim3 grid((A.N + 16 * R - 1) / (16 * R), A.E);
@@ -520,8 +543,9 @@ size_t rollout_split_lds_bytes(const RolloutArgs& A, int R) {
 
 #define MBRL_SPLIT_SHAPES(X) X(1, 1) X(2, 2) X(3, 1) X(1, 3) X(3, 3)
 
-bool rollout_split_supported(const RolloutArgs& A, int T, int R) {
+bool rollout_split_supported(const RolloutArgs& A, int T, int R, int P) {
     if (R != 1 && !(R == 2 && A.NOT == 2)) return false;
+    if (P != 2 && P != 3) return false;
     if (A.reward || (T != 4 && T != 8) || A.a > 16 * SMAXA) return false;
     if (A.s > 16 * (A.NOT) || A.NOT != 2 * (A.CS - A.K0S - (A.L - 1) * 2 * T)) return false;
     if (rollout_split_lds_bytes(A, R) > 160 * 1024) return false;
@@ -532,17 +556,21 @@ bool rollout_split_supported(const RolloutArgs& A, int T, int R) {
     return false;
 }
 
-hipError_t launch_rollout_split(const RolloutArgs& A, int T, int R, hipStream_t stream) {
+hipError_t launch_rollout_split(const RolloutArgs& A, int T, int R, int P, hipStream_t stream) {
     const int nos = A.NOT / 2;
     // R = 2 only where its registers fit without spilling (one output chunk: NOS == 1)
-#define MBRL_SPLIT_CASE(K, N)                                                                  \
-    if (A.K0S == K && nos == N) {                                                              \
-        if (T == 4 && R == 1) return launch_split_t<4, 1, K, N>(A, stream);                    \
-        if (T == 8 && R == 1) return launch_split_t<8, 1, K, N>(A, stream);                    \
-        if constexpr (N == 1) {                                                                \
-            if (T == 4 && R == 2) return launch_split_t<4, 2, K, N>(A, stream);                \
-            if (T == 8 && R == 2) return launch_split_t<8, 2, K, N>(A, stream);                \
-        }                                                                                      \
+#define MBRL_SPLIT_CASE(K, N)                                                                          \
+    if (A.K0S == K && nos == N) {                                                                      \
+        if (T == 4 && R == 1 && P == 2) return launch_split_t<4, 1, 2, K, N>(A, stream);               \
+        if (T == 8 && R == 1 && P == 2) return launch_split_t<8, 1, 2, K, N>(A, stream);               \
+        if (T == 4 && R == 1 && P == 3) return launch_split_t<4, 1, 3, K, N>(A, stream);               \
+        if (T == 8 && R == 1 && P == 3) return launch_split_t<8, 1, 3, K, N>(A, stream);               \
+        if constexpr (N == 1) {                                                                        \
+            if (T == 4 && R == 2 && P == 2) return launch_split_t<4, 2, 2, K, N>(A, stream);           \
+            if (T == 8 && R == 2 && P == 2) return launch_split_t<8, 2, 2, K, N>(A, stream);           \
+            if (T == 4 && R == 2 && P == 3) return launch_split_t<4, 2, 3, K, N>(A, stream);           \
+            if (T == 8 && R == 2 && P == 3) return launch_split_t<8, 2, 3, K, N>(A, stream);           \
+        }                                                                                              \
     }
     MBRL_SPLIT_SHAPES(MBRL_SPLIT_CASE)
 #undef MBRL_SPLIT_CASE

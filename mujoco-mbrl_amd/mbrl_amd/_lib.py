@@ -25,11 +25,13 @@ MBRL_NAN_LAST = 0
 MBRL_NAN_FIRST = 1
 MBRL_PRECISION_F32 = 0
 MBRL_PRECISION_F16X3 = 1
-PRECISIONS = {"f32": MBRL_PRECISION_F32, "f16x3": MBRL_PRECISION_F16X3}
+MBRL_PRECISION_F16X6 = 2
+PRECISIONS = {"f32": MBRL_PRECISION_F32, "f16x3": MBRL_PRECISION_F16X3, "f16x6": MBRL_PRECISION_F16X6}
 
 
 def precision_code(name):
-    """'f32' (exact fp32 MFMA) or 'f16x3' (fp32 emulated on the f16 matrix cores; mbrl_cem.h)."""
+    """'f32' (exact fp32 MFMA), 'f16x3' or 'f16x6' (fp32 emulated on the f16 matrix cores with 2 or 3
+    operand pieces; include/mbrl_cem.h)."""
     try:
         return PRECISIONS[str(name).lower()]
     except KeyError:
@@ -142,4 +144,5 @@ def require_gpu(t):
 
 __all__ = ["load", "check", "ptr", "stream_handle", "MlpShape", "Norm", "Cost", "Sampler", "CemParams",
            "EXPORTED", "MBRL_NAN_LAST", "MBRL_NAN_FIRST", "MBRL_COST_GOAL_STATE", "MBRL_COST_MODEL_REWARD",
-           "ABI_VERSION", "c_int64", "MBRL_PRECISION_F32", "MBRL_PRECISION_F16X3", "precision_code"]
+           "ABI_VERSION", "c_int64", "MBRL_PRECISION_F32", "MBRL_PRECISION_F16X3", "MBRL_PRECISION_F16X6",
+           "precision_code"]

@@ -36,12 +36,15 @@ def test_no_gpu_needed_for_sizing_calls():
     # 68 chunks x 8 KiB per wave x 4 waves + biases (3*512 + 32) + plain copies for the trajectory
     # kernel (W^T of layer 0 and the two hidden layers, row-major output layer), 64-float aligned
     plain = 23 * 512 + 2 * 512 * 512 + 17 * 512
-    # then the F16X3 split stream: 34 chunks of 32 K rows (1 + 2 x 16 + 1) x 8 waves x 8 KiB, one flag word
+    # then the split streams: 34 chunks of 32 K rows (1 + 2 x 16 + 1) x 8 waves x 8 KiB (F16X3: two
+    # pieces) or x 12 KiB (F16X6: three pieces), each followed by a flag word
     a64 = lambda x: (x + 63) // 64 * 64   # noqa: E731
-    split = 34 * 2048 * 8 + 64
+    split = 34 * 2048 * 8 + 64 + 34 * 3072 * 8 + 64
     assert lib.mbrl_mlp_packed_bytes(ctypes.byref(sh)) == a64(a64(68 * 8192 + 3 * 512 + 32 + plain) + split) * 4
     # precision does not change the packed layout; an unknown precision is rejected
     assert lib.mbrl_mlp_packed_bytes(ctypes.byref(_lib.MlpShape(17, 6, 512, 3, 1, 0, 1))) == \
+        lib.mbrl_mlp_packed_bytes(ctypes.byref(sh))
+    assert lib.mbrl_mlp_packed_bytes(ctypes.byref(_lib.MlpShape(17, 6, 512, 3, 1, 0, 2))) == \
         lib.mbrl_mlp_packed_bytes(ctypes.byref(sh))
     assert lib.mbrl_mlp_packed_bytes(ctypes.byref(_lib.MlpShape(17, 6, 512, 3, 1, 0, 7))) == 0
     bad = _lib.MlpShape(17, 6, 4096, 3, 1)
@@ -53,7 +56,7 @@ def test_no_gpu_needed_for_sizing_calls():
     # reward head: one more output row (17 + 1 still fits two 16-row tiles) and its plain copy
     shr = _lib.MlpShape(17, 6, 512, 2, 1, 1)
     plain_r = 23 * 512 + 512 * 512 + 18 * 512
-    split_r = 18 * 2048 * 8 + 64
+    split_r = 18 * 2048 * 8 + 64 + 18 * 3072 * 8 + 64
     assert lib.mbrl_mlp_packed_bytes(ctypes.byref(shr)) == a64(a64(36 * 8192 + 2 * 512 + 32 + plain_r) + split_r) * 4
     assert lib.mbrl_mlp_packed_bytes(ctypes.byref(_lib.MlpShape(17, 6, 512, 2, 1, 2))) == 0
 

@@ -1,5 +1,5 @@
-"""GPU parity of the F16X3 rollout (fp32 emulated on the f16 matrix cores; include/mbrl_cem.h,
-MBRL_PRECISION_F16X3) against the CPU oracle and the reference's golden vectors, with the same
+"""GPU parity of the split-operand rollouts F16X3 and F16X6 (fp32 emulated on the f16 matrix cores;
+include/mbrl_cem.h, MBRL_PRECISION_F16X3 / _F16X6) against the CPU oracle and the reference's golden vectors, with the same
 bars as the exact-fp32 path: elite index sets, mu and sigma bit-exact; returns within 1e-5
 relative (BASELINE.json north_star) to max(|ref|, 1). Also the fp32 redo of operands outside the
 split range, which must reproduce the F32 kernel bit for bit."""
@@ -15,38 +15,43 @@ from test_gpu_parity import CEM_CASES, DEV, RTOL, build, rel_err
 pytestmark = pytest.mark.gpu
 
 
-def problems(p):
+SPLITS = ["f16x3", "f16x6"]
+
+
+def problems(p, precision="f16x3"):
     from mbrl_amd import _lib, fused
     _, model_fn, cost_fn, _ = build(p)
     md = fused.describe_model(model_fn)
     cd = fused.describe_cost(cost_fn, md["s"], md)
     dev = torch.device(DEV)
     return (fused.device_problem(md, cd, dev, _lib.MBRL_PRECISION_F32),
-            fused.device_problem(md, cd, dev, _lib.MBRL_PRECISION_F16X3))
+            fused.device_problem(md, cd, dev, _lib.precision_code(precision)))
 
 
 @pytest.mark.parametrize("cid,over", [(2, dict(N=1000, H=20)), (3, dict(N=300, H=30)), (4, dict(N=200, H=7)),
                                       (5, dict(N=40, H=6)), (3, dict(N=17, H=2)), (3, dict(N=4096, H=30)),
                                       (4, dict(N=8200, H=5))])
-def test_f16x3_rollout_costs_and_states(cid, over):
+@pytest.mark.parametrize("precision", SPLITS)
+def test_f16x3_rollout_costs_and_states(cid, over, precision):
     from mbrl_amd import fused
     p = ocem.synth_problem(cid, **over)
     N, H, a, s, E = over["N"], over["H"], p["cfg"]["a"], p["cfg"]["s"], p["cfg"]["E"]
     A = cem_actions(np.zeros((H, a), np.float32), np.full((H, a), 0.5, np.float32), -1, 1, 11, 0, np.arange(N))
     ref_costs, ref_states = ocem.rollout(p["model"], p["norm"], p["cost"], p["s0"], A, store_states=True)
-    _, prob = problems(p)
+    _, prob = problems(p, precision)
     states = torch.empty((E, H, N, s), dtype=torch.float32, device=DEV)
     costs = fused.rollout(prob, torch.from_numpy(p["s0"]).to(DEV), N, H, actions=torch.from_numpy(A).to(DEV),
                           states_out=states)
     torch.cuda.synchronize()
     err = rel_err(costs, ref_costs)
-    print(f"config {cid} N={N} H={H}: F16X3 return max rel err {err:.3e}")
+    print(f"config {cid} N={N} H={H}: {precision} return max rel err {err:.3e}")
     assert err < RTOL
     assert np.allclose(states.cpu().numpy(), ref_states, rtol=1e-4, atol=1e-4)
 
 
 @pytest.mark.parametrize("name,cid,over", CEM_CASES, ids=[c[0] for c in CEM_CASES])
-def test_f16x3_cem_plan_against_reference_golden(golden, name, cid, over):
+@pytest.mark.parametrize("precision", SPLITS)
+def test_f16x3_cem_plan_against_reference_golden(golden, name, cid, over, precision):
     """The fixtures of test_cem_plan_against_reference_golden through precision='f16x3' (config 6,
     the reward-head model, runs the F32 kernel and must match as well)."""
     from mbrl_amd import CEMPlanner
@@ -56,7 +61,7 @@ def test_f16x3_cem_plan_against_reference_golden(golden, name, cid, over):
     res = CEMPlanner.plan_detailed(torch.from_numpy(p["s0"]), model_fn, cost_fn, sample_action, int(g["H"]),
                                    num_candidates=int(g["N"]), num_elites=int(g["K"]),
                                    num_iterations=int(g["I"]), alpha=float(g["alpha"]), seed=p["rng_seed"],
-                                   record=True, precision="f16x3")
+                                   record=True, precision=precision)
     for it in range(int(g["I"])):
         assert rel_err(res["returns"][it], g["returns"][it]) < RTOL, f"iteration {it}"
         assert np.array_equal(res["elites"][it].cpu().numpy(), g["elites"][it]), f"iteration {it}"
@@ -67,7 +72,8 @@ def test_f16x3_cem_plan_against_reference_golden(golden, name, cid, over):
 
 
 @pytest.mark.parametrize("cid", [3, 4])
-def test_f16x3_full_size_plan_sampled_candidates(cid):
+@pytest.mark.parametrize("precision", SPLITS)
+def test_f16x3_full_size_plan_sampled_candidates(cid, precision):
     """Full BASELINE sizes: sampled candidates' returns against the oracle, exact stable top-K of the
     device returns, exact refit, determinism."""
     from mbrl_amd import CEMPlanner
@@ -75,7 +81,7 @@ def test_f16x3_full_size_plan_sampled_candidates(cid):
     cfg = p["cfg"]
     N, H, a = cfg["N"], cfg["H"], cfg["a"]
     _, model_fn, cost_fn, sample_action = build(p)
-    kw = dict(num_candidates=N, num_iterations=3, seed=p["rng_seed"], record=True, precision="f16x3")
+    kw = dict(num_candidates=N, num_iterations=3, seed=p["rng_seed"], record=True, precision=precision)
     res = CEMPlanner.plan_detailed(torch.from_numpy(p["s0"]), model_fn, cost_fn, sample_action, H, **kw)
     res2 = CEMPlanner.plan_detailed(torch.from_numpy(p["s0"]), model_fn, cost_fn, sample_action, H, **kw)
     assert torch.equal(res["returns"], res2["returns"]) and torch.equal(res["mu"], res2["mu"])
@@ -98,7 +104,8 @@ def test_f16x3_full_size_plan_sampled_candidates(cid):
 
 
 @pytest.mark.parametrize("N,tile", [(256, 16), (8192, 32)])
-def test_f16x3_activation_overflow_redone_in_f32(N, tile):
+@pytest.mark.parametrize("precision", SPLITS)
+def test_f16x3_activation_overflow_redone_in_f32(N, tile, precision):
     """Candidates whose start state normalises past the split range (|x| >= 2048) are redone by the
     F32 kernel: their workgroups (16 candidates, or 32 once N >= 8192) carry fp32 results (equal to
     the F32 path's up to its summation order: the redo runs at the split kernel's tile height), the
@@ -106,7 +113,7 @@ def test_f16x3_activation_overflow_redone_in_f32(N, tile):
     from mbrl_amd import fused
     p = ocem.synth_problem(3, N=N, H=6)
     H, a, s = 6, p["cfg"]["a"], p["cfg"]["s"]
-    f32, f16 = problems(p)
+    f32, f16 = problems(p, precision)
     s0 = np.tile(p["s0"], (N, 1)).astype(np.float32)
     hot = [5, 40, 41, 200]
     s0[hot, 3] = 1.0e6
@@ -132,14 +139,15 @@ def test_f16x3_activation_overflow_redone_in_f32(N, tile):
     assert rel_err(c16n[~redone], c32n[~redone].astype(np.float64)) < RTOL
 
 
-def test_f16x3_weight_out_of_range_falls_back_to_f32():
+@pytest.mark.parametrize("precision", SPLITS)
+def test_f16x3_weight_out_of_range_falls_back_to_f32(precision):
     """A weight with |w| >= 128 cannot be split: the pack flags it and every workgroup is redone in
     F32, so the F16X3 call returns the F32 costs exactly."""
     from mbrl_amd import fused
     p = ocem.synth_problem(2, N=300, H=5)
     p["model"][0][1][0][7, 11] = 40000.0            # hidden layer weight
     N, H, a = 300, 5, p["cfg"]["a"]
-    f32, f16 = problems(p)
+    f32, f16 = problems(p, precision)
     A = torch.from_numpy(cem_actions(np.zeros((H, a), np.float32), np.full((H, a), 0.5, np.float32), -1, 1, 9, 0,
                                      np.arange(N))).to(DEV)
     s0 = torch.from_numpy(p["s0"]).to(DEV)
@@ -149,13 +157,14 @@ def test_f16x3_weight_out_of_range_falls_back_to_f32():
     assert torch.equal(c16.view(torch.int32), c32.view(torch.int32))
 
 
-def test_f16x3_batched_and_sharded_paths_accept_precision():
+@pytest.mark.parametrize("precision", SPLITS)
+def test_f16x3_batched_and_sharded_paths_accept_precision(precision):
     """plan_batch with precision='f16x3' equals B single plans of the same precision."""
     from mbrl_amd import CEMPlanner
     p = ocem.synth_problem(3, N=512, H=8)
     _, model_fn, cost_fn, sample_action = build(p)
     B = 3
     s0 = torch.from_numpy(np.stack([p["s0"] + 0.1 * b for b in range(B)]).astype(np.float32))
-    kw = dict(num_candidates=512, num_iterations=2, seed=21, precision="f16x3")
+    kw = dict(num_candidates=512, num_iterations=2, seed=21, precision=precision)
     states, actions = CEMPlanner.plan_batch(s0, model_fn, cost_fn, sample_action, 8, **kw)
     assert actions.shape == (B, 8, p["cfg"]["a"]) and torch.isfinite(states).all()
