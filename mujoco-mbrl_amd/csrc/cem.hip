@@ -799,8 +799,17 @@ static int traj_impl(const Geometry& g, const void* packed, const mbrl_norm* nor
         T.norm_s = norm->normalize_state; T.unnorm_s = norm->unnormalize_state; T.norm_a = norm->normalize_action;
     }
     T.s0 = s0; T.actions = actions; T.states_out = states_out;
-    if (xchg && status && traj_coop_supported(T, g.E) && xchg_bytes >= traj_coop_xchg_bytes(T, g.E))
-        return hip_check(launch_traj_coop(T, g.E, xchg, status, stream), "trajectory launch");
+    if (xchg && status && traj_coop_supported(T, g.E) && xchg_bytes >= traj_coop_xchg_bytes(T, g.E)) {
+        const char* dbg = getenv("MBRL_DEBUG_TRAJ_ABORT");
+        T.debug_abort = dbg != nullptr && atoi(dbg) != 0;
+        int rc = hip_check(launch_traj_coop(T, g.E, xchg, status, stream), "trajectory launch");
+        if (rc) return rc;
+        // The cooperative kernel needs its P*E workgroups co-resident; if a hand-off ever timed out
+        // (another process holding CUs, say) it set `status` and gave up. The single-workgroup kernel
+        // then recomputes the states; otherwise its E workgroups read the status word and exit.
+        T.gate = status;
+        T.debug_abort = 0;
+    }
     return hip_check(launch_traj(T, g.E, stream), "trajectory launch");
 }
 

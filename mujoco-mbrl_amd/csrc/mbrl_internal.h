@@ -184,6 +184,8 @@ struct TrajArgs {
     const float* s0;
     const float* actions;  // [H][a]
     float* states_out;     // [E][H][s]
+    const unsigned* gate;  // traj_kernel: when non-NULL, run only if *gate != 0 (the coop kernel gave up)
+    int debug_abort;       // traj_coop_kernel: give up at once (tests of the fallback; MBRL_DEBUG_TRAJ_ABORT)
 };
 hipError_t launch_traj(const TrajArgs& A, int E, hipStream_t stream);
 

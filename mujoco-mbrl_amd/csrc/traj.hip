@@ -57,6 +57,8 @@ __device__ __forceinline__ void traj_dense_relu(const float* __restrict__ wt, co
 
 __global__ void __launch_bounds__(TRAJ_THREADS) traj_kernel(const TrajArgs A) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
+    // fallback behind the cooperative kernel: only when that one gave up (status word set)
+    if (A.gate != nullptr && *A.gate == 0u) return;
     const int e = blockIdx.x;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int K0 = A.s + A.a;
@@ -219,6 +221,10 @@ __global__ void __launch_bounds__(COOP_THREADS) traj_coop_kernel(const TrajArgs 
     const float* tw = member + A.tw_base;
     gu64* xchg = (gu64*)(xchg_all + (size_t)e * 2 * Wp);
 
+    if (A.debug_abort) {                       // test hook: behave as a timed-out hand-off
+        if (tid == 0) atomicOr(status, 1u);
+        return;
+    }
     // ---- one-time staging ----------------------------------------------------------------------
     if (tid == 0) abort_flag = 0;
     for (int k = tid; k < K0R; k += COOP_THREADS) x0[k] = 0.0f;

@@ -313,6 +313,24 @@ def test_trajectory_states_match_oracle(cid, H):
     assert np.allclose(st.cpu().numpy(), np.mean(ref[:, :, 0, :], axis=0, dtype=np.float32), rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("cid,H", [(3, 12), (5, 7)])
+def test_trajectory_fallback_when_the_cooperative_kernel_gives_up(cid, H, monkeypatch):
+    """MBRL_DEBUG_TRAJ_ABORT makes the cooperative kernel behave as a timed-out hand-off (it sets the
+    status word and exits); the gated single-workgroup kernel behind it must then produce the states."""
+    from mbrl_amd import fused
+    monkeypatch.setenv("MBRL_DEBUG_TRAJ_ABORT", "1")
+    p = ocem.synth_problem(cid, N=1, H=H)
+    a, s, E = p["cfg"]["a"], p["cfg"]["s"], p["cfg"]["E"]
+    acts = np.random.default_rng(7 + cid).uniform(-1, 1, size=(H, a)).astype(np.float32)
+    prob = device_problem(p)
+    members = torch.full((E, H, s), float("nan"), dtype=torch.float32, device=DEV)
+    fused.trajectory(prob, torch.from_numpy(p["s0"]).to(DEV), torch.from_numpy(acts).to(DEV), H,
+                     member_states=members)
+    torch.cuda.synchronize()
+    _, ref = ocem.rollout(p["model"], p["norm"], p["cost"], p["s0"], acts[:, None, :], store_states=True)
+    assert np.allclose(members.cpu().numpy(), ref[:, :, 0, :], rtol=1e-4, atol=1e-4)
+
+
 @pytest.mark.parametrize("cid,N,H,world", [(3, 2048, 10, 2), (5, 512, 6, 4)])
 def test_sharded_protocol_with_fused_ops_matches_single_gpu_plan(cid, N, H, world):
     """The multi-GPU protocol with its math on the HIP extension: every rank's shard computed here on
