@@ -219,6 +219,20 @@ int mbrl_cem_plan_batch(const mbrl_mlp_shape* shape, const void* packed, const m
                         float* mu, float* sigma, float* actions_out, float* states_out, void* workspace,
                         size_t ws_bytes, mbrl_stream_t stream);
 
+/* ---- gradient-descent planner: replaces GradientDescentPlanner's
+ * _optimize_trajectory (planners.py:103-137) -- Adam(lr) on the action sequence through the dynamics
+ * with the goal-state cost, stopping once mean |delta a| < stop_condition -- as one persistent
+ * workgroup (forward, backward and the Adam step on the device; no host round trip per iteration).
+ * actions: [H][a] device, in: the initial sequence, out: the optimised one. states_out: [H+1][s]
+ * = the last iteration's rollout (computed before its update, as the reference returns it).
+ * iterations_out: device int32 (iterations run) or NULL. Needs ensemble == 1, reward_head == 0 and a
+ * GOAL_STATE cost (else MBRL_EUNSUPPORTED). workspace >= mbrl_gd_workspace_bytes(shape, H). */
+size_t mbrl_gd_workspace_bytes(const mbrl_mlp_shape* shape, int32_t H);
+int mbrl_gd_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_norm* norm, const mbrl_cost* cost,
+                 const float* s0, float* actions, int32_t H, int32_t num_iterations, float stop_condition,
+                 float lr, float* states_out, int32_t* iterations_out, void* workspace, size_t ws_bytes,
+                 mbrl_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1234,4 +1234,66 @@ int mbrl_cem_plan_batch(const mbrl_mlp_shape* shape, const void* packed, const m
     return hip_check(hipGetLastError(), "batched plan launch");
 }
 
+
+// ---- fused gradient-descent planner (gd.hip)
+static size_t gd_ws(const Geometry& g, int H, float** m, float** v, float** hist, void* base) {
+    char* b = static_cast<char*>(base);
+    size_t o = 0;
+    auto take = [&](size_t n) { void* r = b ? b + o : nullptr; o += align256(n); return r; };
+    const size_t ha = (size_t)H * g.a;
+    const int row = ((g.s + g.a + 3) & ~3) + g.L * g.Wpad;
+    float* pm = (float*)take(ha * 4);
+    float* pv = (float*)take(ha * 4);
+    float* ph = (float*)take((size_t)H * row * 4);
+    if (m) { *m = pm; *v = pv; *hist = ph; }
+    return o;
+}
+
+size_t mbrl_gd_workspace_bytes(const mbrl_mlp_shape* shape, int32_t H) {
+    Geometry g;
+    if (shape_geometry(shape, &g) != MBRL_OK || H < 1) return 0;
+    return gd_ws(g, H, nullptr, nullptr, nullptr, nullptr);
+}
+
+int mbrl_gd_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_norm* norm, const mbrl_cost* cost,
+                 const float* s0, float* actions, int32_t H, int32_t num_iterations, float stop_condition, float lr,
+                 float* states_out, int32_t* iterations_out, void* workspace, size_t ws_bytes, mbrl_stream_t stream) {
+    Geometry g;
+    int rc = shape_geometry(shape, &g);
+    if (rc) return rc;
+    if (g.E != 1 || g.reward) return fail(MBRL_EUNSUPPORTED, "gd_plan: needs ensemble == 1 and no reward head");
+    if (!cost || cost->kind != MBRL_COST_GOAL_STATE) return fail(MBRL_EUNSUPPORTED, "gd_plan: needs a GOAL_STATE cost");
+    if (!packed || !s0 || !actions || !states_out || !workspace) return fail(MBRL_EINVAL, "gd_plan: NULL argument");
+    if (H < 1 || num_iterations < 0) return fail(MBRL_EINVAL, "gd_plan: H=%d iterations=%d", H, num_iterations);
+    if (gd_lds_bytes(g.s, g.a, g.Wpad, H) > 160 * 1024) return fail(MBRL_EUNSUPPORTED, "gd_plan: H * a too large");
+    if (cost->has_state_cost && (!cost->weights || !cost->goal))
+        return fail(MBRL_EINVAL, "gd_plan: state cost without weights/goal");
+    GdArgs A{};
+    const size_t need = gd_ws(g, H, nullptr, nullptr, nullptr, nullptr);
+    if (ws_bytes < need) return fail(MBRL_EWORKSPACE, "gd workspace %zu < %zu", ws_bytes, need);
+    gd_ws(g, H, &A.m, &A.v, &A.hist, workspace);
+    A.packed = static_cast<const float*>(packed);
+    A.bias_off = g.stream_floats;
+    A.tw_base = g.stream_floats + g.bias_floats;
+    for (int l = 0; l <= g.L; ++l) A.tw_off[l] = g.tw_off[l];
+    A.s = g.s; A.a = g.a; A.W = g.W; A.Wpad = g.Wpad; A.L = g.L; A.H = H;
+    if (norm) {
+        A.obs_mean = norm->obs_mean; A.obs_std = norm->obs_std;
+        A.act_mean = norm->act_mean; A.act_std = norm->act_std;
+        A.norm_s = norm->normalize_state; A.unnorm_s = norm->unnormalize_state; A.norm_a = norm->normalize_action;
+        if ((A.norm_s || A.unnorm_s) && (!A.obs_mean || !A.obs_std))
+            return fail(MBRL_EINVAL, "state normalisation requested without obs_mean/obs_std");
+        if (A.norm_a && (!A.act_mean || !A.act_std))
+            return fail(MBRL_EINVAL, "action normalisation requested without act_mean/act_std");
+    }
+    A.cw = cost->weights; A.goal = cost->goal;
+    A.alpha_s = cost->alpha_state; A.alpha_a = cost->alpha_action;
+    A.has_sc = cost->has_state_cost; A.has_ac = cost->has_action_cost;
+    A.s0 = s0; A.actions = actions; A.states_out = states_out;
+    A.hist_row = ((g.s + g.a + 3) & ~3) + g.L * g.Wpad;
+    A.iterations = num_iterations; A.stop = stop_condition; A.lr = lr;
+    A.iterations_out = iterations_out;
+    return hip_check(launch_gd_plan(A, reinterpret_cast<hipStream_t>(stream)), "gd_plan launch");
+}
+
 }  // extern "C"

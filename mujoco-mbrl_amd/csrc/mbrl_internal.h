@@ -189,6 +189,31 @@ struct TrajArgs {
 };
 hipError_t launch_traj(const TrajArgs& A, int E, hipStream_t stream);
 
+// Fused gradient-descent planner (gd.hip): one persistent workgroup runs every Adam iteration of
+// planners.py:103-137 (goal-state cost, one ensemble member).
+struct GdArgs {
+    const float* packed;                   // member 0
+    size_t bias_off, tw_base;
+    size_t tw_off[MAX_LAYERS + 1];
+    int s, a, W, Wpad, L, H;
+    const float *obs_mean, *obs_std, *act_mean, *act_std;
+    int norm_s, unnorm_s, norm_a;
+    const float *cw, *goal;
+    float alpha_s, alpha_a;
+    int has_sc, has_ac;
+    const float* s0;                       // [s]
+    float* actions;                        // [H][a], in: initial sequence, out: optimised
+    float* states_out;                     // [H+1][s]: the last iteration's rollout
+    float *m, *v;                          // Adam moments [H][a] (workspace)
+    float* hist;                           // [H][hist_row] saved layer inputs (workspace)
+    int hist_row;                          // round4(s + a) + L * Wpad
+    int iterations;
+    float stop, lr;
+    int* iterations_out;                   // device int or NULL
+};
+size_t gd_lds_bytes(int s, int a, int Wpad, int H);
+hipError_t launch_gd_plan(const GdArgs& A, hipStream_t stream);
+
 // Cooperative variant: P = Wpad/16 workgroups per member each own 16 hidden units of every W -> W
 // layer (slices LDS-resident); layer 0 and the output layer are computed redundantly by every
 // workgroup; hidden activations are all-gathered through tagged 8-byte granules in `xchg`

@@ -43,7 +43,7 @@ EXPORTED = (
     "mbrl_rollout_cost", "mbrl_select_workspace_bytes", "mbrl_select_elites",
     "mbrl_refit_workspace_bytes", "mbrl_cem_refit", "mbrl_sample_actions",
     "mbrl_trajectory_workspace_bytes", "mbrl_trajectory", "mbrl_cem_workspace_bytes", "mbrl_cem_plan",
-    "mbrl_cem_plan_batch_workspace_bytes", "mbrl_cem_plan_batch",
+    "mbrl_cem_plan_batch_workspace_bytes", "mbrl_cem_plan_batch", "mbrl_gd_workspace_bytes", "mbrl_gd_plan",
 )
 
 
@@ -109,6 +109,9 @@ def load():
         "mbrl_cem_plan_batch": (c_int32, [POINTER(MlpShape), P, POINTER(Norm), POINTER(Cost), P, c_int32,
                                           POINTER(CemParams), P, P, P, P, P, c_size_t, P]),
         "mbrl_cem_workspace_bytes": (c_size_t, [POINTER(MlpShape), POINTER(CemParams)]),
+        "mbrl_gd_workspace_bytes": (c_size_t, [POINTER(MlpShape), c_int32]),
+        "mbrl_gd_plan": (c_int32, [POINTER(MlpShape), P, POINTER(Norm), POINTER(Cost), P, P, c_int32, c_int32,
+                                   c_float, c_float, P, P, P, c_size_t, P]),
         "mbrl_cem_plan": (c_int32, [POINTER(MlpShape), P, POINTER(Norm), POINTER(Cost), P, POINTER(CemParams),
                                     P, P, P, P, P, P, P, P, P, c_size_t, P]),
     }

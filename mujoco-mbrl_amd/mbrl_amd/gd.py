@@ -7,16 +7,20 @@ H+1 states of the LAST rollout (computed before the last update) and the updated
 lists of [1, s] / [1, a] tensors.
 
 Recognised closures (the same introspection as the CEM path: GoalStateAgent's and RewardAgent's
-wiring) run a device restatement of that loop. The MLP, normalisers and cost are rebuilt from the
-described nn.Linear weights and statistics as differentiable torch ops on the GPU. The whole
-forward + loss + backward of one iteration, a chain of H x (L + 1) batch-1 layers, is captured
-once in a HIP graph and replayed each iteration. The Adam step and the stop test stay eager, with
-one host read per iteration, like the reference's .numpy(). Unrecognised closures run the
-reference's loop on the callables as given.
+wiring) run on the device:
+  * a single model with the goal-state cost -> mbrl_gd_plan (csrc/gd.hip): one persistent
+    workgroup runs every iteration's rollout, backward pass, Adam step and stop test; the host
+    waits once per plan;
+  * ensembles and reward-head models -> a device restatement as differentiable torch ops: the MLP,
+    normalisers and cost rebuilt from the described nn.Linear weights and statistics; the
+    forward + loss + backward of one iteration (a chain of H x (L + 1) batch-1 layers) is captured
+    once in a HIP graph and replayed each iteration; the Adam step and the stop test stay eager,
+    with one host read per iteration, like the reference's .numpy().
+Unrecognised closures run the reference's loop on the callables as given.
 """
 import torch
 
-from . import fused
+from . import _lib, fused
 
 
 def _stats(norm, key, dev):
@@ -129,12 +133,47 @@ class _Iteration:
         self.graph.replay()
 
 
+def fused_supported(mdesc, cdesc, dev):
+    return (dev.type == "cuda" and mdesc["E"] == 1 and not mdesc.get("reward")
+            and cdesc is not None and cdesc["kind"] == _lib.MBRL_COST_GOAL_STATE)
+
+
+def plan_fused(initial_state, mdesc, cdesc, action_list, horizon, num_iterations, stop_condition, dev, lr=0.01):
+    """mbrl_gd_plan: the whole optimisation in one launch (csrc/gd.hip). Returns (states [H+1, s],
+    actions [H, a], iterations run) on `dev`."""
+    lib = _lib.load()
+    prob = fused.device_problem(mdesc, cdesc, dev)
+    H = int(horizon)
+    s0 = initial_state.to(device=dev, dtype=torch.float32).reshape(-1).contiguous()
+    actions = torch.cat([a.reshape(1, -1) for a in action_list], 0).to(device=dev, dtype=torch.float32).contiguous()
+    states = torch.empty((H + 1, mdesc["s"]), dtype=torch.float32, device=dev)
+    iters = torch.zeros(1, dtype=torch.int32, device=dev)
+    need = lib.mbrl_gd_workspace_bytes(fused.ctypes_ref(prob.shape), H)
+    ws = torch.empty(need, dtype=torch.uint8, device=dev)
+    _lib.check(lib.mbrl_gd_plan(fused.ctypes_ref(prob.shape), _lib.ptr(prob.packed), fused.ctypes_ref(prob.norm),
+                                fused.ctypes_ref(prob.cost), _lib.ptr(s0), _lib.ptr(actions), H, int(num_iterations),
+                                float(stop_condition), float(lr), _lib.ptr(states), _lib.ptr(iters), _lib.ptr(ws),
+                                need, _lib.stream_handle(dev)), "mbrl_gd_plan")
+    return states, actions, iters
+
+
 def plan_device(initial_state, mdesc, cdesc, action_list, horizon, num_iterations, stop_condition, dev,
-                use_graph=True):
+                use_graph=True, use_fused=True):
     """The reference's _optimize_trajectory (planners.py:103-137) on `dev` for described closures."""
+    if use_fused and fused_supported(mdesc, cdesc, dev):
+        states, actions, _ = plan_fused(initial_state, mdesc, cdesc, action_list, horizon, num_iterations,
+                                        stop_condition, dev)
+        return states, actions
     dm = _DeviceModel(mdesc, cdesc, dev)
     H = int(horizon)
     s0 = initial_state.to(device=dev, dtype=torch.float32).reshape(-1)
+    if int(num_iterations) <= 0:
+        # planners.py:115-135 with no iteration: the zero states tensor with s0 in row 0, and the
+        # initial actions
+        states = torch.zeros((H + 1, s0.shape[-1]), dtype=torch.float32, device=dev)
+        states[0] = s0
+        actions = torch.cat([a.reshape(1, -1) for a in action_list], 0).to(device=dev, dtype=torch.float32)
+        return states, actions
     actions = torch.cat([a.reshape(1, -1) for a in action_list], 0).to(device=dev, dtype=torch.float32)
     actions = actions.detach().clone().requires_grad_(True)
     opt = torch.optim.Adam([actions], lr=0.01)

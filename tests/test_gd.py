@@ -67,3 +67,27 @@ def test_gd_graph_replay_equals_eager():
     s1, a1 = gd.plan_device(torch.from_numpy(p["s0"]), mdesc, cdesc, acts, 10, 20, 0.0, dev, use_graph=True)
     s2, a2 = gd.plan_device(torch.from_numpy(p["s0"]), mdesc, cdesc, acts, 10, 20, 0.0, dev, use_graph=False)
     assert torch.equal(a1, a2) and torch.equal(s1, s2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cid,over,H,iters,stop", [(3, dict(W=50, L=2), 10, 25, 0.0), (2, {}, 12, 40, 0.002),
+                                                  (3, {}, 30, 15, 0.0), (3, dict(W=200, L=3), 8, 40, 0.01),
+                                                  (2, {}, 5, 0, 0.0)])
+def test_gd_fused_kernel_matches_graph_path(cid, over, H, iters, stop):
+    """mbrl_gd_plan (one persistent workgroup: forward, backward, Adam, stop test on the device) against
+    the graph-replayed torch restatement of the same loop, including early stops and zero iterations."""
+    from mbrl_amd import gd
+    p, model_fn, cost_fn = closures(cid, over)
+    mdesc, cdesc = gd.describe(model_fn, cost_fn)
+    dev = torch.device("cuda:0")
+    assert gd.fused_supported(mdesc, cdesc, dev)
+    a = p["cfg"]["a"]
+    A0 = mgd.initial_actions(H, a)
+    acts = [torch.from_numpy(A0[i:i + 1].copy()) for i in range(H)]
+    s0 = torch.from_numpy(p["s0"])
+    s1, a1, n = gd.plan_fused(s0, mdesc, cdesc, acts, H, iters, stop, dev)
+    s2, a2 = gd.plan_device(s0, mdesc, cdesc, acts, H, iters, stop, dev, use_fused=False)
+    torch.cuda.synchronize()
+    assert int(n.item()) <= iters
+    assert torch.allclose(a1, a2, rtol=1e-4, atol=1e-5), float((a1 - a2).abs().max())
+    assert torch.allclose(s1, s2, rtol=1e-4, atol=1e-4), float((s1 - s2).abs().max())

@@ -1,6 +1,7 @@
 """GradientDescentPlanner timing: one plan (40 Adam iterations, no early
-stop) on the cheetah model (3x512, H=30) -- GPU (graph-replayed iteration) vs the reference's loop on
-CPU (torch threads = this process's share). One JSON line."""
+stop) on the cheetah model (3x512, H=30) -- GPU (the fused mbrl_gd_plan kernel, and the
+graph-replayed torch iteration) vs the reference's loop on CPU (torch threads = this process's
+share). One JSON line."""
 import json
 import os
 import sys
@@ -30,14 +31,16 @@ def main():
     if torch.cuda.is_available():
         md, cd = gd.describe(prob["model"], prob["cost"])
         dev = torch.device("cuda:0")
-        gd.plan_device(prob["s0"], md, cd, acts, H, iters, 0.0, dev)          # warm-up
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        reps = 5
-        for _ in range(reps):
-            gd.plan_device(prob["s0"], md, cd, acts, H, iters, 0.0, dev)
-        torch.cuda.synchronize()
-        out["gpu_ms_per_plan"] = (time.perf_counter() - t0) * 1e3 / reps
+        for key, fused_on in (("gpu_fused_ms_per_plan", True), ("gpu_graph_ms_per_plan", False)):
+            gd.plan_device(prob["s0"], md, cd, acts, H, iters, 0.0, dev, use_fused=fused_on)   # warm-up
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            reps = 5
+            for _ in range(reps):
+                gd.plan_device(prob["s0"], md, cd, acts, H, iters, 0.0, dev, use_fused=fused_on)
+            torch.cuda.synchronize()
+            out[key] = (time.perf_counter() - t0) * 1e3 / reps
+        out["gpu_ms_per_plan"] = out["gpu_fused_ms_per_plan"]
         out["speedup"] = out["cpu_ms_per_plan"] / out["gpu_ms_per_plan"]
     print(json.dumps(out))
 
