@@ -1236,23 +1236,34 @@ int mbrl_cem_plan_batch(const mbrl_mlp_shape* shape, const void* packed, const m
 
 
 // ---- fused gradient-descent planner (gd.hip)
-static size_t gd_ws(const Geometry& g, int H, float** m, float** v, float** hist, void* base) {
+struct GdWs {
+    float *m, *v, *hist;
+    unsigned long long* xchg;
+    unsigned* status;
+    size_t bytes;
+};
+
+static GdWs gd_ws(const Geometry& g, int H, void* base) {
+    GdWs w{};
     char* b = static_cast<char*>(base);
     size_t o = 0;
     auto take = [&](size_t n) { void* r = b ? b + o : nullptr; o += align256(n); return r; };
     const size_t ha = (size_t)H * g.a;
-    const int row = ((g.s + g.a + 3) & ~3) + g.L * g.Wpad;
-    float* pm = (float*)take(ha * 4);
-    float* pv = (float*)take(ha * 4);
-    float* ph = (float*)take((size_t)H * row * 4);
-    if (m) { *m = pm; *v = pv; *hist = ph; }
-    return o;
+    const size_t row = (size_t)((g.s + g.a + 3) & ~3) + (size_t)g.L * g.Wpad;
+    const size_t coop = (size_t)(g.Wpad / 16) * H * g.L * g.Wpad;   // per-workgroup hidden-vector copies
+    w.xchg = (unsigned long long*)take((size_t)2 * g.Wpad * 8 + 16);   // granules, then the status word
+    w.status = w.xchg ? reinterpret_cast<unsigned*>(w.xchg + 2 * g.Wpad) : nullptr;
+    w.m = (float*)take(ha * 4);
+    w.v = (float*)take(ha * 4);
+    w.hist = (float*)take((H * row > coop ? H * row : coop) * 4);
+    w.bytes = o;
+    return w;
 }
 
 size_t mbrl_gd_workspace_bytes(const mbrl_mlp_shape* shape, int32_t H) {
     Geometry g;
     if (shape_geometry(shape, &g) != MBRL_OK || H < 1) return 0;
-    return gd_ws(g, H, nullptr, nullptr, nullptr, nullptr);
+    return gd_ws(g, H, nullptr).bytes;
 }
 
 int mbrl_gd_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_norm* norm, const mbrl_cost* cost,
@@ -1269,9 +1280,9 @@ int mbrl_gd_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_nor
     if (cost->has_state_cost && (!cost->weights || !cost->goal))
         return fail(MBRL_EINVAL, "gd_plan: state cost without weights/goal");
     GdArgs A{};
-    const size_t need = gd_ws(g, H, nullptr, nullptr, nullptr, nullptr);
-    if (ws_bytes < need) return fail(MBRL_EWORKSPACE, "gd workspace %zu < %zu", ws_bytes, need);
-    gd_ws(g, H, &A.m, &A.v, &A.hist, workspace);
+    const GdWs w = gd_ws(g, H, workspace);
+    if (ws_bytes < w.bytes) return fail(MBRL_EWORKSPACE, "gd workspace %zu < %zu", ws_bytes, w.bytes);
+    A.m = w.m; A.v = w.v; A.hist = w.hist;
     A.packed = static_cast<const float*>(packed);
     A.bias_off = g.stream_floats;
     A.tw_base = g.stream_floats + g.bias_floats;
@@ -1293,7 +1304,18 @@ int mbrl_gd_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_nor
     A.hist_row = ((g.s + g.a + 3) & ~3) + g.L * g.Wpad;
     A.iterations = num_iterations; A.stop = stop_condition; A.lr = lr;
     A.iterations_out = iterations_out;
-    return hip_check(launch_gd_plan(A, reinterpret_cast<hipStream_t>(stream)), "gd_plan launch");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const char* force_single = getenv("MBRL_GD_SINGLE");          // A/B and tests: the one-workgroup kernel
+    if (gd_coop_supported(A) && !(force_single && atoi(force_single) != 0)) {
+        const char* dbg = getenv("MBRL_DEBUG_GD_ABORT");
+        A.debug_abort = dbg != nullptr && atoi(dbg) != 0;
+        rc = hip_check(launch_gd_coop(A, w.xchg, w.status, st), "gd_plan coop launch");
+        if (rc) return rc;
+        // the one-workgroup kernel redoes the plan only if a cooperative hand-off timed out
+        A.gate = w.status;
+        A.debug_abort = 0;
+    }
+    return hip_check(launch_gd_plan(A, st), "gd_plan launch");
 }
 
 }  // extern "C"

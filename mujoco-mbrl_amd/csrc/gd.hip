@@ -125,6 +125,8 @@ __device__ float gd_block_sum(float v, float* red) {
 
 __global__ void __launch_bounds__(GD_THREADS) gd_plan_kernel(const GdArgs A) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
+    // behind the cooperative kernel: only when that one gave up (its status word set)
+    if (A.gate != nullptr && *A.gate == 0u) return;
     const GdLds m = gd_lds(A.s, A.a, A.Wpad, A.H, smem);
     const int tid = threadIdx.x;
     const int s = A.s, a = A.a, Wp = A.Wpad, K0 = s + a, L = A.L, H = A.H;
@@ -132,7 +134,15 @@ __global__ void __launch_bounds__(GD_THREADS) gd_plan_kernel(const GdArgs A) {
     const int K0p = (K0 + 3) & ~3;
     const float* bias = A.packed + A.bias_off;
     const float* tw = A.packed + A.tw_base;
-    const float* wout = tw + A.tw_off[L];              // [s][W] row-major
+    // per-layer W^T bases (constant-index copy: a runtime index into the kernel argument would
+    // move the whole argument block to scratch)
+    __shared__ const float* lw[MAX_LAYERS + 1];
+    if (tid == 0) {
+#pragma unroll
+        for (int l = 0; l <= MAX_LAYERS; ++l) lw[l] = tw + A.tw_off[l];
+    }
+    __syncthreads();
+    const float* wout = lw[L];                         // [s][W] row-major
     const float* bout = bias + (size_t)L * Wp;
     const float b1 = 0.9f, b2 = 0.999f, eps = 1e-8f;
 
@@ -161,10 +171,10 @@ __global__ void __launch_bounds__(GD_THREADS) gd_plan_kernel(const GdArgs A) {
                 hist[d] = v;
             }
             __syncthreads();
-            gd_dense_relu(tw + A.tw_off[0], bias, K0, Wp, m.x, m.part, m.h);
+            gd_dense_relu(lw[0], bias, K0, Wp, m.x, m.part, m.h);
             for (int n = tid; n < Wp; n += GD_THREADS) hist[K0p + n] = m.h[n];
             for (int l = 1; l < L; ++l) {
-                gd_dense_relu(tw + A.tw_off[l], bias + (size_t)l * Wp, A.W, Wp, m.h, m.part, m.x);
+                gd_dense_relu(lw[l], bias + (size_t)l * Wp, A.W, Wp, m.h, m.part, m.x);
                 for (int n = tid; n < Wp; n += GD_THREADS) { m.h[n] = m.x[n]; hist[K0p + l * Wp + n] = m.x[n]; }
                 __syncthreads();
             }
@@ -207,12 +217,12 @@ __global__ void __launch_bounds__(GD_THREADS) gd_plan_kernel(const GdArgs A) {
             }
             __syncthreads();
             for (int l = L - 1; l >= 1; --l) {
-                gd_dense_back(tw + A.tw_off[l], A.W, Wp, m.gz, m.gx);
+                gd_dense_back(lw[l], A.W, Wp, m.gz, m.gx);
                 const float* hp = hist + K0p + (size_t)(l - 1) * Wp;
                 for (int k = tid; k < Wp; k += GD_THREADS) m.gz[k] = (k < A.W && hp[k] > 0.f) ? m.gx[k] : 0.f;
                 __syncthreads();
             }
-            gd_dense_back(tw + A.tw_off[0], K0, Wp, m.gz, m.gx);
+            gd_dense_back(lw[0], K0, Wp, m.gz, m.gx);
             // split the input gradient: state part -> step t-1, action part -> grad of a_t
             for (int d = tid; d < K0; d += GD_THREADS) {
                 const float g = m.gx[d];
@@ -253,13 +263,354 @@ __global__ void __launch_bounds__(GD_THREADS) gd_plan_kernel(const GdArgs A) {
     if (tid == 0 && A.iterations_out != nullptr) *A.iterations_out = done;
 }
 
+// ------------------------------------------------------------------------------------------------
+// Cooperative variant (the traj_coop_kernel scheme of traj.hip, with a backward pass): P = Wpad/16
+// workgroups of 512 threads. Workgroup p keeps, LDS-resident for the whole plan, rows
+// [16p, 16p + 16) of every W -> W layer (forward: its 16 units) and the same rows of each layer's
+// W^T (backward: its 16 input gradients). Layer 0 and the output layer, forward and backward, are
+// computed redundantly by every workgroup from register-resident weights. The only cross-workgroup
+// traffic is one all-gather of a hidden vector per W -> W layer and direction: 2 (L - 1) hand-offs
+// per step, as R2 granules (cdna_hip_programming.md §6 G16: aligned 8-byte {epoch, value} agent-
+// scope stores, gathered by one wave until every tag matches). Adam and the stop test run
+// redundantly (bit-identical) in every workgroup, so no other exchange is needed. Every spin is
+// bounded; on a timeout `status` is set and the single-workgroup kernel (gated on it) redoes the plan.
+// ------------------------------------------------------------------------------------------------
+constexpr int GC_THREADS = 512;
+constexpr int GC_ROWS = 16;
+typedef unsigned long long gc_u64;
+typedef __attribute__((address_space(1))) gc_u64 gc_gu64;
+
+struct GcLds {
+    int rs;
+    size_t fw, bw, x0, hA, hB, gA, gB, out, gs, red, acts, m1, m2, grad, st, flag, total;
+};
+
+__host__ __device__ inline GcLds gc_lds(int s, int a, int W, int Wp, int L, int H, int K0R) {
+    GcLds m;
+    auto al4 = [](size_t n) { return (n + 3) & ~(size_t)3; };
+    m.rs = W + 32;
+    size_t o = 0;
+    m.fw = o;   o += (size_t)(L - 1) * GC_ROWS * m.rs;
+    m.bw = o;   o += (size_t)(L - 1) * GC_ROWS * m.rs;
+    m.x0 = o;   o += al4(K0R);
+    m.hA = o;   o += Wp;
+    m.hB = o;   o += Wp;
+    m.gA = o;   o += Wp;
+    m.gB = o;   o += Wp;
+    m.out = o;  o += 32;
+    m.gs = o;   o += 32;
+    m.red = o;  o += (size_t)(GC_THREADS / 64) * K0R;
+    m.acts = o; o += al4((size_t)H * a);
+    m.m1 = o;   o += al4((size_t)H * a);
+    m.m2 = o;   o += al4((size_t)H * a);
+    m.grad = o; o += al4((size_t)H * a);
+    m.st = o;   o += al4((size_t)(H + 1) * s);
+    m.flag = o; o += 4;
+    m.total = o * sizeof(float);
+    return m;
+}
+
+__device__ __forceinline__ float gc_half_sum(float v) {
+#pragma unroll
+    for (int o = 16; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Publish this workgroup's 16 values (lane c == 0 of half-wave g holds value g) and gather all P
+// slices into `dst`; returns false on a timeout (status set).
+__device__ __forceinline__ bool gc_exchange(gc_gu64* xchg, int Wp, int p, unsigned& phase, float val, float* dst,
+                                            int& abort_flag, unsigned* status) {
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = tid >> 5, c = tid & 31;
+    const unsigned epoch = phase + 1u;
+    gc_gu64* buf = xchg + (size_t)(phase & 1u) * Wp;
+    if (c == 0)
+        __hip_atomic_store(&buf[p * GC_ROWS + g], ((gc_u64)epoch << 32) | __float_as_uint(val), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    if (wave == 0) {
+        const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+        for (;;) {
+            bool ok = true;
+            for (int q = lane; q < Wp; q += 64) {
+                const gc_u64 v = __hip_atomic_load(&buf[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok &= (unsigned)(v >> 32) == epoch;
+                dst[q] = __uint_as_float((unsigned)v);
+            }
+            if (__all(ok)) break;
+            if (__builtin_amdgcn_s_memrealtime() - t_start > 20000000ull) {   // 200 ms
+                if (lane == 0) {
+                    abort_flag = 1;
+                    atomicOr(status, 1u);
+                }
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    __syncthreads();
+    ++phase;
+    return abort_flag == 0;
+}
+
+// K0R >= s + a: layer-0 inputs per thread; SM: output rows per half-wave (16 SM >= s); WI = W / 32.
+template <int K0R, int SM, int WI>
+__global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_u64* __restrict__ xchg_all,
+                                                             unsigned* __restrict__ status) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int p = blockIdx.x;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = tid >> 5, c = tid & 31;
+    const int s = A.s, a = A.a, W = A.W, Wp = A.Wpad, K0 = s + a, L = A.L, H = A.H;
+    const GcLds m = gc_lds(s, a, W, Wp, L, H, K0R);
+    float* fw = smem + m.fw;
+    float* bw = smem + m.bw;
+    float* x0 = smem + m.x0;
+    float* gout = smem + m.out;
+    float* gs = smem + m.gs;
+    float* red = smem + m.red;
+    float* acts = smem + m.acts;
+    float* m1 = smem + m.m1;
+    float* m2 = smem + m.m2;
+    float* grad = smem + m.grad;
+    float* st = smem + m.st;
+    int& abort_flag = *reinterpret_cast<int*>(smem + m.flag);
+    const float* bias = A.packed + A.bias_off;
+    const float* tw = A.packed + A.tw_base;
+    gc_gu64* xchg = (gc_gu64*)xchg_all;
+    float* hist = A.hist + (size_t)p * H * L * Wp;     // this workgroup's copy of the hidden vectors
+
+    if (A.debug_abort) {                       // test hook: behave as a timed-out hand-off
+        if (tid == 0) atomicOr(status, 1u);
+        return;
+    }
+    // ---- one-time staging: weight slices, register-resident layer 0 / output weights, actions
+    if (tid == 0) abort_flag = 0;
+    for (int k = tid; k < K0R; k += GC_THREADS) x0[k] = 0.0f;
+    for (int l = 1; l < L; ++l) {
+        const float* wt = tw + A.tw_off[l];                    // W^T_l [W][Wpad]
+        float* f = fw + (size_t)(l - 1) * GC_ROWS * m.rs;
+        float* b = bw + (size_t)(l - 1) * GC_ROWS * m.rs;
+        for (int i = tid; i < GC_ROWS * W; i += GC_THREADS) {
+            const int k = i >> 4, o = i & 15;
+            f[o * m.rs + k] = wt[(size_t)k * Wp + p * GC_ROWS + o];   // W_l[16p + o][k]
+        }
+        for (int i = tid; i < GC_ROWS * W; i += GC_THREADS) {
+            const int o = i / W, n = i - (i / W) * W;
+            b[o * m.rs + n] = wt[(size_t)(p * GC_ROWS + o) * Wp + n];  // W_l[n][16p + o]
+        }
+    }
+    for (int i = tid; i < H * a; i += GC_THREADS) { acts[i] = A.actions[i]; m1[i] = 0.f; m2[i] = 0.f; }
+    for (int i = tid; i < (H + 1) * s; i += GC_THREADS) st[i] = i < s ? A.s0[i] : 0.f;
+    for (int d = tid; d < 32; d += GC_THREADS) gout[d] = 0.f;   // entries >= s stay zero
+    const bool has_unit = tid < Wp;
+    const float b0 = has_unit ? bias[tid] : 0.0f;
+    float w0r[K0R];                                           // W0[tid][k]
+#pragma unroll
+    for (int k = 0; k < K0R; ++k) w0r[k] = (has_unit && k < K0) ? tw[A.tw_off[0] + (size_t)k * Wp + tid] : 0.0f;
+    const float* wo = tw + A.tw_off[L];                       // Wout [s][W]
+    float wor[SM][WI];                                        // forward: Wout[g + 16 mm][c + 32 i]
+#pragma unroll
+    for (int mm = 0; mm < SM; ++mm)
+#pragma unroll
+        for (int i = 0; i < WI; ++i) {
+            const int d = g + 16 * mm, k = c + 32 * i;
+            wor[mm][i] = (d < s && k < W) ? wo[(size_t)d * W + k] : 0.0f;
+        }
+    float wob[16 * SM];                                       // backward: Wout[n][tid]
+#pragma unroll
+    for (int n = 0; n < 16 * SM; ++n) wob[n] = (n < s && tid < W) ? wo[(size_t)n * W + tid] : 0.0f;
+    const float* hbias = bias;                                // [L][Wpad]
+    const float* obias = bias + (size_t)L * Wp;
+    __syncthreads();
+
+    const float b1 = 0.9f, b2 = 0.999f, eps = 1e-8f;
+    unsigned phase = 0;
+    int done = 0;
+    float* cur = smem + m.hA;
+    float* nxt = smem + m.hB;
+    for (int it = 0; it < A.iterations; ++it) {
+        // ================= forward
+        for (int t = 0; t < H; ++t) {
+            for (int d = tid; d < K0; d += GC_THREADS) {
+                if (d < s) {
+                    const float sv = st[t * s + d];
+                    x0[d] = A.norm_s ? (sv - A.obs_mean[d]) / A.obs_std[d] : sv;
+                } else {
+                    const float av = acts[t * a + d - s];
+                    x0[d] = A.norm_a ? (av - A.act_mean[d - s]) / A.act_std[d - s] : av;
+                }
+            }
+            __syncthreads();
+            float* ht = hist + (size_t)t * L * Wp;
+            if (has_unit) {
+                float v = b0;
+#pragma unroll
+                for (int k = 0; k < K0R; ++k) v += w0r[k] * x0[k];
+                v = fmaxf(v, 0.0f);
+                cur[tid] = v;
+                ht[tid] = v;
+            }
+            __syncthreads();
+            for (int l = 1; l < L; ++l) {
+                const float* f = fw + (size_t)(l - 1) * GC_ROWS * m.rs + (size_t)g * m.rs;
+                float v = 0.f;
+#pragma unroll
+                for (int i = 0; i < WI; ++i) v += f[c + 32 * i] * cur[c + 32 * i];
+                v = gc_half_sum(v);
+                v = fmaxf(v + hbias[(size_t)l * Wp + p * GC_ROWS + g], 0.0f);
+                if (!gc_exchange(xchg, Wp, p, phase, v, nxt, abort_flag, status)) return;
+                float* tmp = cur; cur = nxt; nxt = tmp;
+                if (has_unit) ht[(size_t)l * Wp + tid] = cur[tid];
+            }
+            // output layer (redundant): half-wave g owns rows g + 16 mm
+#pragma unroll
+            for (int mm = 0; mm < SM; ++mm) {
+                float v = 0.f;
+#pragma unroll
+                for (int i = 0; i < WI; ++i) v += wor[mm][i] * cur[c + 32 * i];
+                v = gc_half_sum(v);
+                const int d = g + 16 * mm;
+                if (c == 0 && d < s) {
+                    const float o = v + obias[d];
+                    st[(t + 1) * s + d] = A.unnorm_s ? o * A.obs_std[d] + A.obs_mean[d] : o;
+                }
+            }
+            __syncthreads();
+        }
+        // ================= backward, t = H-1 .. 0
+        for (int d = tid; d < 32; d += GC_THREADS) gs[d] = 0.f;
+        __syncthreads();
+        for (int t = H - 1; t >= 0; --t) {
+            const float* ht = hist + (size_t)t * L * Wp;
+            for (int d = tid; d < s; d += GC_THREADS) {
+                float gg = gs[d];
+                if (A.has_sc) {
+                    const float x = st[(t + 1) * s + d] - A.goal[d];
+                    const float wx = x * A.cw[d];
+                    gg += wx * A.cw[d] / sqrtf(wx * wx + A.alpha_s * A.alpha_s);
+                }
+                gout[d] = A.unnorm_s ? gg * A.obs_std[d] : gg;
+            }
+            __syncthreads();
+            // output layer backward (redundant): thread k = tid; ReLU mask of the last hidden layer
+            float* gcur = smem + m.gA;
+            float* gnxt = smem + m.gB;
+            if (has_unit) {
+                float v = 0.f;
+#pragma unroll
+                for (int n = 0; n < 16 * SM; ++n) v += wob[n] * gout[n];
+                gcur[tid] = ht[(size_t)(L - 1) * Wp + tid] > 0.f ? v : 0.f;
+            }
+            __syncthreads();
+            for (int l = L - 1; l >= 1; --l) {
+                // my 16 input gradients of layer l: k = 16p + g, lanes over n
+                const float* b = bw + (size_t)(l - 1) * GC_ROWS * m.rs + (size_t)g * m.rs;
+                float v = 0.f;
+#pragma unroll
+                for (int i = 0; i < WI; ++i) v += b[c + 32 * i] * gcur[c + 32 * i];
+                v = gc_half_sum(v);
+                const int k = p * GC_ROWS + g;
+                v = ht[(size_t)(l - 1) * Wp + k] > 0.f ? v : 0.f;     // ReLU' of layer l - 1's output
+                if (!gc_exchange(xchg, Wp, p, phase, v, gnxt, abort_flag, status)) return;
+                float* tmp = gcur; gcur = gnxt; gnxt = tmp;
+            }
+            // layer 0 backward (redundant): g_x0[k] = sum_u W0[u][k] g_z0[u], a block reduction per k
+            {
+                const float gu = has_unit ? gcur[tid] : 0.f;
+#pragma unroll
+                for (int k = 0; k < K0R; ++k) {
+                    float v = w0r[k] * gu;
+#pragma unroll
+                    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+                    if (lane == 0) red[wave * K0R + k] = v;
+                }
+                __syncthreads();
+                for (int k = tid; k < K0; k += GC_THREADS) {
+                    float v = 0.f;
+                    for (int w = 0; w < GC_THREADS / 64; ++w) v += red[w * K0R + k];
+                    if (k < s) {
+                        gs[k] = A.norm_s ? v / A.obs_std[k] : v;
+                    } else {
+                        const int j = k - s;
+                        float ga = A.norm_a ? v / A.act_std[j] : v;
+                        if (A.has_ac) ga += A.alpha_a * sinhf(acts[t * a + j] / A.alpha_a) / (float)a;
+                        grad[t * a + j] = ga;
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        // ================= Adam and the stop test (redundant, bit-identical in every workgroup)
+        const float kk = (float)(it + 1);
+        const float bc1 = 1.0f - powf(b1, kk), bc2 = 1.0f - powf(b2, kk);
+        const float stepsz = A.lr / bc1, bc2s = sqrtf(bc2);
+        float change = 0.f;
+        for (int i = tid; i < H * a; i += GC_THREADS) {
+            const float gg = grad[i];
+            float mm = m1[i];
+            mm = mm + (1.0f - b1) * (gg - mm);
+            const float vv = b2 * m2[i] + (1.0f - b2) * gg * gg;
+            m1[i] = mm;
+            m2[i] = vv;
+            const float old = acts[i];
+            const float nw = old - stepsz * (mm / (sqrtf(vv) / bc2s + eps));
+            acts[i] = nw;
+            change += fabsf(old - nw);
+        }
+        {
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) change += __shfl_xor(change, o, 64);
+            if (lane == 0) red[wave] = change;
+            __syncthreads();
+            change = 0.f;
+            for (int w = 0; w < GC_THREADS / 64; ++w) change += red[w];
+            __syncthreads();
+        }
+        done = it + 1;
+        if (change / (float)(H * a) < A.stop) break;
+    }
+    if (p == 0) {
+        for (int i = tid; i < H * a; i += GC_THREADS) A.actions[i] = acts[i];
+        for (int i = tid; i < (H + 1) * s; i += GC_THREADS) A.states_out[i] = st[i];
+        if (tid == 0 && A.iterations_out != nullptr) *A.iterations_out = done;
+    }
+}
+
 }  // namespace
+
+bool gd_coop_supported(const GdArgs& A) {
+    const int K0 = A.s + A.a;
+    if (A.L < 2 || A.W != A.Wpad || A.Wpad > GC_THREADS || A.Wpad < 64 || K0 > 32 || A.s > 32) return false;
+    return gc_lds(A.s, A.a, A.W, A.Wpad, A.L, A.H, 32).total <= 160 * 1024;
+}
+
+template <int WI>
+static hipError_t launch_gd_coop_w(const GdArgs& A, gc_u64* xchg, unsigned* status, hipStream_t stream) {
+    const auto fn = &gd_coop_kernel<32, 2, WI>;
+    hipError_t err = ensure_dynamic_lds(reinterpret_cast<const void*>(fn), 160 * 1024);
+    if (err != hipSuccess) return err;
+    hipLaunchKernelGGL(fn, dim3(A.Wpad / GC_ROWS), dim3(GC_THREADS), gc_lds(A.s, A.a, A.W, A.Wpad, A.L, A.H, 32).total,
+                       stream, A, xchg, status);
+    return hipGetLastError();
+}
+
+hipError_t launch_gd_coop(const GdArgs& A, unsigned long long* xchg, unsigned* status, hipStream_t stream) {
+    // zero the granules and the status word (adjacent: one memset)
+    hipError_t err = hipMemsetAsync(xchg, 0, (size_t)2 * A.Wpad * 8 + 16, stream);
+    if (err != hipSuccess) return err;
+    switch (A.Wpad) {
+        case 64: return launch_gd_coop_w<2>(A, xchg, status, stream);
+        case 128: return launch_gd_coop_w<4>(A, xchg, status, stream);
+        case 256: return launch_gd_coop_w<8>(A, xchg, status, stream);
+        case 512: return launch_gd_coop_w<16>(A, xchg, status, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
 
 size_t gd_lds_bytes(int s, int a, int Wpad, int H) { return gd_lds(s, a, Wpad, H, nullptr).floats * sizeof(float); }
 
 hipError_t launch_gd_plan(const GdArgs& A, hipStream_t stream) {
     const size_t lds = gd_lds_bytes(A.s, A.a, A.Wpad, A.H);
-    hipError_t err = ensure_dynamic_lds(reinterpret_cast<const void*>(&gd_plan_kernel), 160 * 1024);
+    // the kernel also has a few bytes of static LDS: raise the dynamic limit to what it needs, not 160 KiB
+    hipError_t err = ensure_dynamic_lds(reinterpret_cast<const void*>(&gd_plan_kernel), (int)lds);
     if (err != hipSuccess) return err;
     hipLaunchKernelGGL(gd_plan_kernel, dim3(1), dim3(GD_THREADS), lds, stream, A);
     return hipGetLastError();

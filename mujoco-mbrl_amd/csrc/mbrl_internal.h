@@ -210,9 +210,15 @@ struct GdArgs {
     int iterations;
     float stop, lr;
     int* iterations_out;                   // device int or NULL
+    const unsigned* gate;                  // gd_plan_kernel: when non-NULL, run only if *gate != 0
+    int debug_abort;                       // gd_coop_kernel: give up at once (MBRL_DEBUG_GD_ABORT)
 };
 size_t gd_lds_bytes(int s, int a, int Wpad, int H);
 hipError_t launch_gd_plan(const GdArgs& A, hipStream_t stream);
+// Cooperative variant (Wpad / 16 workgroups; hist = Wpad/16 copies of [H][L][Wpad]); `xchg` holds
+// 2 Wpad 8-byte granules immediately followed by the status word (zeroed by the launcher).
+bool gd_coop_supported(const GdArgs& A);
+hipError_t launch_gd_coop(const GdArgs& A, unsigned long long* xchg, unsigned* status, hipStream_t stream);
 
 // Cooperative variant: P = Wpad/16 workgroups per member each own 16 hidden units of every W -> W
 // layer (slices LDS-resident); layer 0 and the output layer are computed redundantly by every

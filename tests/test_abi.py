@@ -108,3 +108,11 @@ def test_ctypes_layout_matches_c_header():
             assert ctypes.sizeof(cls) == int(val), py
         else:
             assert getattr(cls, field).offset == int(val), (py, field)
+
+
+def test_library_resolves_every_symbol_at_load():
+    """RTLD_NOW: an internal symbol left undefined (a definition in the wrong namespace, say) fails
+    here instead of at the first call on a GPU box."""
+    import os
+    from mbrl_amd import _lib
+    ctypes.CDLL(_lib.LIB_PATH, mode=os.RTLD_NOW)
