@@ -112,7 +112,8 @@ class EnvWrapper:
         return self._parse_timestep(self._env.reset())
 
     def step(self, action):
-        return self._parse_timestep(self._env.step(np.array(action)))
+        a = action.detach().cpu().numpy() if torch.is_tensor(action) else np.array(action)
+        return self._parse_timestep(self._env.step(a))
 
     def _parse_timestep(self, t):
         if self._flat_obs:
