@@ -35,6 +35,7 @@ sys.path.insert(0, os.path.join(REPO, "mujoco-mbrl_amd"))
 sys.path.insert(0, REPO)
 
 PEAK_FP32_MFMA_TFLOPS = 157.3
+L2_STREAM_TBPS = 32.4   # tools/ubench/l2stream.hip: every CU streaming one L2-resident weight set
 ITERATIONS = 5
 
 
@@ -213,6 +214,17 @@ def main():
             var = dict(precision=other, value=cand_steps / v_elapsed, ms_per_step=v_elapsed / args.steps * 1e3,
                        rollout_avg_launch_ms=v_rollout_s * 1e3,
                        rollout_tflops_fp32_equivalent=flop_launch / v_rollout_s / 1e12, note=notes[other])
+            if other != "f32":
+                # the split kernels are bound by the per-CU L2 weight stream: algorithmic bytes = every
+                # workgroup's weight stream for H steps; peak = tools/ubench/l2stream.hip's
+                # measured 32.4 TB/s for this access pattern (MI355X_MICROARCH.md: 34.5 nominal)
+                R = 2 if n_local >= 256 * 32 else 1
+                wgs = -(-n_local // (16 * R)) * E
+                l2 = wgs * H * synthetic.split_stream_bytes_per_step(cfg, 3 if other == "f16x6" else 2)
+                var["roofline"] = {"bound": "l2", "achieved": l2 / v_rollout_s / 1e12, "peak": L2_STREAM_TBPS,
+                                   "unit": "TB/s", "frac": l2 / v_rollout_s / 1e12 / L2_STREAM_TBPS,
+                                   "kernel": "rollout_split_kernel", "algorithmic_bytes_per_launch": l2,
+                                   "pmc": "profiles/r01_split_rollout_pmc.json"}
             if rank == 0 and world == 1 and not args.no_cpu_baseline:
                 var["parity"] = parity_sample(prob, v_first)
             out["variants"].append(var)

@@ -37,6 +37,23 @@ def flop_per_candidate_step(cfg):
     return 2 * (trunk + W * s) * E
 
 
+def split_stream_bytes_per_step(cfg, pieces):
+    """Weight bytes one split-rollout workgroup streams from L2 per step (csrc/mbrl_internal.h
+    make_geometry): CS chunks of 32 K rows, 8 waves x T/2 tiles x `pieces` fragments of 1 KiB."""
+    s, a, W, L = cfg["s"], cfg["a"], cfg["W"], cfg["L"]
+    T = 1
+    while 64 * T < W:
+        T *= 2
+    k0s = (s + a + 31) // 32
+    nout = -(-(s + int(bool(cfg.get("reward")))) // 16)
+    nout += nout & 1
+    nos = nout // 2
+    if (k0s + nos) & 1:
+        k0s += 1
+    cs = k0s + (L - 1) * 2 * T + nos
+    return cs * 8 * (T // 2) * pieces * 1024
+
+
 def make_problem(config_id, **overrides):
     cfg = dict(CONFIGS[config_id])
     cfg.update(overrides)

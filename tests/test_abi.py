@@ -116,3 +116,14 @@ def test_library_resolves_every_symbol_at_load():
     import os
     from mbrl_amd import _lib
     ctypes.CDLL(_lib.LIB_PATH, mode=os.RTLD_NOW)
+
+
+def test_split_stream_bytes_match_the_packed_geometry():
+    """bench.py's L2 roofline for the split kernels uses synthetic.split_stream_bytes_per_step; it must
+    equal the stream the pack writes (the packed-size test above: 34 chunks for cheetah)."""
+    from mbrl_amd import synthetic
+    ch = synthetic.CONFIGS[3]
+    assert synthetic.split_stream_bytes_per_step(ch, 2) == 34 * 2048 * 8 * 4
+    assert synthetic.split_stream_bytes_per_step(ch, 3) == 34 * 3072 * 8 * 4
+    rw = dict(ch, L=2, reward=True)
+    assert synthetic.split_stream_bytes_per_step(rw, 2) == 18 * 2048 * 8 * 4
