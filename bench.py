@@ -78,7 +78,15 @@ def cpu_baseline(cfg_id, budget_s=20.0):
         elapsed += time.perf_counter() - t0
         plans += 1
     value = ITERATIONS * n_sample * H * plans / elapsed
-    return dict(value=value, unit="candidate-timesteps/s", cores=int(cores), kind="port",
+    cpu = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:  # pragma: no cover
+        pass
+    return dict(value=value, unit="candidate-timesteps/s", cores=int(cores), kind="port", cpu=cpu,
                 sample=f"{plans} full CEM plan(s) (I={ITERATIONS}, N={n_sample}, H={H}) of the NumPy oracle "
                        f"(oracle/cem.py), fp32, {elapsed:.1f} s")
 
