@@ -72,7 +72,7 @@ def cpu_baseline(cfg_id, budget_s=20.0):
     one_iter = time.perf_counter() - t0
     n_sample = N if one_iter * ITERATIONS <= budget_s else max(64, int(N * budget_s / (one_iter * ITERATIONS)))
     plans, elapsed = 0, 0.0
-    while elapsed < budget_s / 2 and plans < 3:
+    while elapsed < budget_s / 2 and plans < 10:
         t0 = time.perf_counter()
         ocem.cem_plan(p, N=n_sample, num_iterations=ITERATIONS, record=False)
         elapsed += time.perf_counter() - t0
