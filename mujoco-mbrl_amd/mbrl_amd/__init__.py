@@ -4,7 +4,7 @@ Drop-in for the reference's planner API (src/mbrl/planners.py) and DynamicsModel
 (src/mbrl/models.py); the compute runs in the in-tree HIP extension libmbrl_cem.so (C ABI:
 include/mbrl_cem.h). See DESIGN.md and INTEGRATION.md at the repository root.
 """
-from . import agents, data, env, env_wrappers, gd, models, planners  # noqa: F401
+from . import agents, data, env, env_wrappers, gd, models, parallel, planners  # noqa: F401
 from .agents import MPCPolicy  # noqa: F401
 from .env_wrappers import EnvWrapper  # noqa: F401
 from .models import (CoshLoss, DynamicsModel, EnsembleModel, Model, ModelWithReward, SmoothAbsLoss,  # noqa: F401
