@@ -6,22 +6,25 @@
 // CoshLoss(a_t) (agents.py:182-183) summed over t.
 //
 // Mapping:
-//   * one workgroup = 4 waves = M = 16*R candidates of one ensemble member, for all H steps; the
-//     candidates' activations live in LDS for the whole horizon (ping-pong buffers, never HBM).
-//   * every Linear is a chain of v_mfma_f32_16x16x4_f32 (exact fp32): wave w owns output columns
-//     [w*W/4, (w+1)*W/4) of each hidden layer (T = W/64 16-column tiles); the output layer splits
-//     K over the 4 waves and reduces through LDS.
+//   * one workgroup = M = 16*R candidates of one ensemble member, for all H steps; 8 waves (two per
+//     SIMD) for R = 1, 4 for R = 2. The candidates' activations live in LDS for the whole horizon
+//     (ping-pong buffers, never HBM).
+//   * every Linear is a chain of v_mfma_f32_16x16x4_f32 (exact fp32) with the weights as the A
+//     operand: wave w owns output columns [w*W/NW, (w+1)*W/NW) of each hidden layer; the output
+//     layer splits K over the waves (each wave's own columns, straight from its accumulators) and
+//     reduces through LDS.
 //   * weights are pre-packed (pack kernels in cem.hip) into the exact fragment order each wave
-//     consumes: one global_load_dwordx4 per lane = one 1 KiB coalesced B fragment. The per-step
+//     consumes: one buffer_load_dwordx4 per lane = one 1 KiB coalesced fragment. The per-step
 //     stream (~2.2 MB for 3x512) stays resident in every XCD's 4 MB L2; each wave streams its
-//     slice through a register double buffer that runs one chunk (32 MFMAs) ahead across layer and
-//     step boundaries. sched_barrier pins the issue order so hipcc cannot sink the prefetch next to
-//     its use (it did: the unpinned build drained vmcnt(0) every chunk).
-//   * the A operand (activations) is read from LDS one chunk ahead as well.
+//     slice through a 4-deep register ring that runs 3 chunks ahead across layer and step
+//     boundaries. sched_barrier pins the issue order so hipcc cannot sink the prefetch next to its
+//     use (it did: the unpinned build drained vmcnt(0) every chunk).
+//   * the activation fragments are read from LDS one chunk ahead as well.
 //   * candidate actions come from HBM ([H][N][a], written by the proposal kernel or given by the
 //     caller); a_{t+1} is loaded at the start of step t so its latency hides under the MFMAs.
-//   * the step epilogue (unnormalise, goal cost, renormalise) runs on the VALU out of LDS; per-row
-//     cost sums are wave shuffle reductions; the return is a register of the reducing lane.
+//   * the step epilogue (unnormalise, goal cost, renormalise) runs on the VALU out of LDS, waves 0-3
+//     for the state and waves 4-7 for the actions; per-row sums are DPP row reductions; the return
+//     is a register of the reducing lane.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
