@@ -9,7 +9,9 @@ elite top-K -> refit, plus the final mean's rollout) on the cheetah-run config (
 configs[2]: N=4096, H=30, 17/6, 3x512 MLP, I=5, K=N/10) with synthetic random weights.
 value = I * N_total * H * K_steps / (max over ranks of the timed wall clock).
 With N GPUs each rank owns 4096 candidates (weak scaling: N_total = 4096 * N); one RCCL
-all-gather of returns per CEM iteration.
+all-gather of returns per CEM iteration. `--strong` splits the config's N over the GPUs instead
+(e.g. `--config 4 --strong`: walker N=16384 over 8 GPUs, BASELINE.json configs[3]);
+`--candidates` overrides N (per GPU, or in total with --strong).
 
 Extra objects on the JSON line:
   roofline     -- the rollout kernel (dominant): algorithmic MLP FLOP per launch / average launch
@@ -18,8 +20,8 @@ Extra objects on the JSON line:
   cpu_baseline -- the CPU oracle (NumPy restatement of the reference rollout + CEM refit), rank 0,
                   N=1 only, on a bounded sample; a reported baseline, not the target.
   parity       -- iteration-0 returns of 256 sampled candidates re-computed by the CPU oracle.
-  variants     -- the same workload timed with the other rollout precision (default headline: exact
-                  fp32; variant: f16x3, fp32 emulated on the f16 matrix cores).
+  variants     -- the same workload timed with the other rollout precisions (default headline: exact
+                  fp32; variants: f16x6 and f16x3, fp32 emulated on the f16 matrix cores).
 """
 import argparse
 import json
@@ -50,6 +52,10 @@ def parse():
                     help="rollout matmul precision (include/mbrl_cem.h MBRL_PRECISION_*)")
     ap.add_argument("--no-variants", action="store_true",
                     help="skip the second-precision measurement (rocprof runs: only the headline launches)")
+    ap.add_argument("--candidates", type=int, default=None,
+                    help="candidates per GPU (weak) or in total (--strong); default: the config's N")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: the config's N split over the GPUs (default weak: N per GPU)")
     ap.add_argument("--traffic-bytes", type=float, default=None,
                     help="HBM bytes per rollout launch from a rocprofv3 PMC pass (profiles/)")
     return ap.parse_args()
@@ -129,8 +135,15 @@ def main():
     prob = synthetic.make_problem(args.config)
     prob["cfg_id"] = args.config
     cfg = prob["cfg"]
-    n_local, H, E = cfg["N"], cfg["H"], cfg["E"]
-    N = n_local * world
+    H, E = cfg["H"], cfg["E"]
+    n_cfg = args.candidates if args.candidates is not None else cfg["N"]
+    if args.strong:
+        if n_cfg % world:
+            raise SystemExit(f"--strong: {n_cfg} candidates do not split over {world} GPUs")
+        N, n_local = n_cfg, n_cfg // world
+    else:
+        n_local = n_cfg
+        N = n_local * world
     K = N // 10
     kw = dict(num_candidates=N, num_elites=K, num_iterations=ITERATIONS, alpha=0.1, seed=prob["rng_seed"],
               distributed=world > 1, device=dev, precision=args.precision)
@@ -190,7 +203,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.strong else "weak",
         "vs_baseline": None,
         "dtype": {"f32": "f32", "f16x3": "f32 (f16x3 split MFMA: fp32 emulated, 22-bit operands)",
                   "f16x6": "f32 (f16x6 split MFMA: fp32 emulated, 33-bit operands, fp32 accumulation)"}[args.precision],
