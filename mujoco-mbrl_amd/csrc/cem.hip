@@ -6,6 +6,7 @@
 #include <stdarg.h>
 #include <stdio.h>
 
+#include <map>
 #include <mutex>
 #include <set>
 #include <string>
@@ -33,6 +34,21 @@ static int fail(int code, const char* fmt, ...) {
 static int hip_check(hipError_t e, const char* what) {
     if (e == hipSuccess) return MBRL_OK;
     return fail(MBRL_EHIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+// Compute units of the current device (cached per device; 256 on MI355X).
+static int device_cus() {
+    static std::mutex mu;
+    static std::map<int, int> cache;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = cache.find(dev);
+    if (it != cache.end()) return it->second;
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cache[dev] = n;
+    return n;
 }
 
 hipError_t ensure_dynamic_lds(const void* fn, int bytes) {
@@ -88,6 +104,45 @@ __global__ void pack_out_kernel(const float* __restrict__ w, const float* __rest
             else if (w_r && n == out_real) v = w_r[k];
         }
         dst[i] = v;
+    }
+}
+
+// 8-candidate stream (rollout.hip rollout_m8_kernel): per 16-deep chunk, per wave (T of them), per
+// step s (4), lane l, element q: row 32 (2 pair + ((l >> 2) & 1)) + 4 (l >> 3) + (l & 3) -- the odd
+// 4-lane blocks carry the pair's second 32-row tile (ABID 1) -- and k = 16 kc + 4 q + s.
+// Hidden-type layers: chunk kc, pair = the wave's own tiles (rows 64 wave + ...).
+__global__ void pack_m8_hidden_kernel(const float* __restrict__ w, int in_real, int out_real, int nkc, int T,
+                                      float* __restrict__ dst) {
+    const size_t total = (size_t)nkc * T * 1024;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const int q = (int)(i & 3);
+        const int lane = (int)((i >> 2) & 63);
+        const int s = (int)((i >> 8) & 3);
+        const size_t cw = i >> 10;            // kc * T + wave
+        const int wave = (int)(cw % T);
+        const int kc = (int)(cw / T);
+        const int n = 64 * wave + 32 * ((lane >> 2) & 1) + 4 * (lane >> 3) + (lane & 3);
+        const int k = 16 * kc + 4 * q + s;
+        dst[i] = (n < out_real && k < in_real) ? w[(size_t)n * in_real + k] : 0.0f;
+    }
+}
+
+// Output layer: chunk o = kc * NOP + pair over the wave's own K rows 64 wave + 16 kc + ...; the pair
+// holds output tiles 2 pair (even blocks) and 2 pair + 1 (odd blocks) of 32 rows.
+__global__ void pack_m8_out_kernel(const float* __restrict__ w, int in_real, int out_real, int NOP, int T,
+                                   float* __restrict__ dst) {
+    const size_t total = (size_t)4 * NOP * T * 1024;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const int q = (int)(i & 3);
+        const int lane = (int)((i >> 2) & 63);
+        const int s = (int)((i >> 8) & 3);
+        const size_t cw = i >> 10;            // o * T + wave
+        const int wave = (int)(cw % T);
+        const int o = (int)(cw / T);
+        const int kc = o / NOP, pair = o % NOP;
+        const int n = 32 * (2 * pair + ((lane >> 2) & 1)) + 4 * (lane >> 3) + (lane & 3);
+        const int k = 64 * wave + 16 * kc + 4 * q + s;
+        dst[i] = (n < out_real && k < in_real) ? w[(size_t)n * in_real + k] : 0.0f;
     }
 }
 
@@ -774,6 +829,16 @@ static int rollout_impl(const Geometry& g, const void* packed, const mbrl_norm* 
             return hip_check(launch_rollout(X, g.T, RS, stream), "split redo launch");
         }
     }
+    // 8-candidate tiles (rollout_m8_kernel, bit-identical sums) when 16-candidate tiles would leave
+    // at least half the CUs idle: the shard of a strong-scaled plan, small plans. MBRL_ROLLOUT_M=8 /
+    // 16 forces a choice (tests, A/B).
+    if (g.m8_ok) {
+        A.m8_off = g.m8_off;
+        A.C8 = g.C8;
+        bool use8 = (size_t)((N + 15) / 16) * g.E * 2 <= (size_t)device_cus();
+        if (const char* env = getenv("MBRL_ROLLOUT_M")) use8 = atoi(env) == 8;
+        if (use8 && rollout_m8_supported(A, g.T)) return hip_check(launch_rollout_m8(A, g.T, stream), "rollout m8 launch");
+    }
     if (rollout_lds_bytes(A, 16 * R) > 160 * 1024) {
         R = 1;
         A.nw = g.T >= 2 ? 8 : 4;
@@ -907,6 +972,8 @@ int mbrl_mlp_pack(const mbrl_mlp_shape* shape, const float* const* weights, cons
         unsigned* split_bad[2] = {reinterpret_cast<unsigned*>(base + g.split_off + (size_t)g.CS * 2048 * g.T),
                                   reinterpret_cast<unsigned*>(base + g.split3_off + (size_t)g.CS * 3072 * g.T)};
         size_t split_chunk = 0;
+        float* m8_base = base + g.m8_off;
+        size_t m8_chunk = 0;
         if (g.split_ok)
             for (int q = 0; q < 2; ++q) {
                 hipError_t err = hipMemsetAsync(split_bad[q], 0, 4, stream);
@@ -932,6 +999,11 @@ int mbrl_mlp_pack(const mbrl_mlp_shape* shape, const float* const* weights, cons
                                            split_bad[P - 2]);
                     split_chunk += nks;
                 }
+                if (g.m8_ok) {
+                    hipLaunchKernelGGL(pack_m8_hidden_kernel, dim3(256), dim3(256), 0, stream, w, in_real, g.W, nkc,
+                                       g.T, m8_base + m8_chunk * 1024 * (size_t)g.T);
+                    m8_chunk += nkc;
+                }
                 chunk += nkc;
             } else {
                 const float* wr = g.reward ? weights[e * nl + g.L + 1] : nullptr;
@@ -943,6 +1015,9 @@ int mbrl_mlp_pack(const mbrl_mlp_shape* shape, const float* const* weights, cons
                         hipLaunchKernelGGL(pack_split_out_kernel, dim3(256), dim3(256), 0, stream, w, wr, g.W, g.s,
                                            g.NOS, g.T, P, split_base[P - 2] + split_chunk * 2048 * (size_t)g.T * P,
                                            split_bad[P - 2]);
+                if (g.m8_ok)
+                    hipLaunchKernelGGL(pack_m8_out_kernel, dim3(256), dim3(256), 0, stream, w, g.W, g.s, g.NOP8, g.T,
+                                       m8_base + m8_chunk * 1024 * (size_t)g.T);
                 float* ob = bias_base + (size_t)g.L * g.Wpad;
                 hipLaunchKernelGGL(pack_bias_kernel, dim3(1), dim3(256), 0, stream, b, g.s, 16 * g.NOT, ob);
                 hipLaunchKernelGGL(copy_kernel, dim3(64), dim3(256), 0, stream, w, (size_t)g.s * g.W, plain);

@@ -39,6 +39,14 @@ struct Geometry {
     size_t split_floats;   // CS * 2048 * T, then one flag word (nonzero: a weight is out of split range)
     size_t split3_off;     // the 3-piece stream (F16X6): CS * 3072 * T floats, then its flag word
     size_t split3_floats;
+    // 8-candidate fp32 stream (rollout.hip rollout_m8_kernel): 16-deep chunks, T waves x 4 KiB each;
+    // K0C + (L-1)*4T + 4*NOP8 chunks per step. Present when m8_ok (Wpad 256 or 512, no reward head,
+    // the ring shapes K0C, NOT in {2, 6}).
+    int m8_ok;
+    int NOP8;              // pairs of 32-row output tiles
+    int C8;                // chunks per step
+    size_t m8_off;         // floats from the member base (0: absent)
+    size_t m8_floats;      // C8 * 1024 * T
     size_t member_stride;  // floats per ensemble member (64-float aligned)
 };
 
@@ -83,6 +91,12 @@ inline bool make_geometry(int s, int a, int W, int L, int E, int reward, Geometr
     g->split3_off = g->split_off + g->split_floats;
     g->split3_floats = g->split_ok ? (size_t)g->CS * 3072 * T + 64 : 0;
     if (g->split_ok) end = g->split3_off + g->split3_floats;
+    g->m8_ok = ((T == 4 || T == 8) && !reward && (g->K0C == 2 || g->K0C == 6) && (g->NOT == 2 || g->NOT == 6)) ? 1 : 0;
+    g->NOP8 = (g->NOT / 2 + 1) / 2;
+    g->C8 = g->K0C + (L - 1) * 4 * T + 4 * g->NOP8;
+    g->m8_off = g->m8_ok ? (end + 63) / 64 * 64 : 0;
+    g->m8_floats = g->m8_ok ? (size_t)g->C8 * 1024 * T : 0;
+    if (g->m8_ok) end = g->m8_off + g->m8_floats;
     g->member_stride = (end + 63) / 64 * 64;
     return true;
 }
@@ -112,6 +126,9 @@ struct RolloutArgs {
     size_t split_off;
     int K0S, CS, sr;       // sr: LDS activation row stride in halves
     int redo;              // F32 kernel: only workgroups whose candidates carry MBRL_REDO_MARK run
+    // 8-candidate kernel (rollout_m8_kernel)
+    size_t m8_off;         // 0: no 8-candidate stream in the pack
+    int C8;
 };
 
 // F16X3 operand scales (exact powers of two): activations and weights are scaled before the f16
@@ -163,6 +180,8 @@ inline size_t rollout_lds_bytes(const RolloutArgs& A, int M) {
 hipError_t ensure_dynamic_lds(const void* fn, int bytes);
 
 hipError_t launch_rollout(const RolloutArgs& A, int T, int R, hipStream_t stream);
+bool rollout_m8_supported(const RolloutArgs& A, int T);
+hipError_t launch_rollout_m8(const RolloutArgs& A, int T, hipStream_t stream);
 
 // F16X3 rollout (8 waves, 16 R candidates per workgroup, goal-state cost). Supported for
 // geometry.split_ok; the caller follows it with launch_rollout(redo = 1) at the same R.

@@ -6,7 +6,8 @@
 // CoshLoss(a_t) (agents.py:182-183) summed over t.
 //
 // Mapping:
-//   * one workgroup = M = 16*R candidates of one ensemble member, for all H steps; 8 waves (two per
+//   * one workgroup = M = 16*R candidates of one ensemble member, for all H steps (8 candidates in
+//     rollout_m8_kernel at the end of this file); 8 waves (two per
 //     SIMD) for R = 1, 4 for R = 2. The candidates' activations live in LDS for the whole horizon
 //     (ping-pong buffers, never HBM).
 //   * every Linear is a chain of v_mfma_f32_16x16x4_f32 (exact fp32) with the weights as the A
@@ -611,6 +612,304 @@ hipError_t launch_rollout(const RolloutArgs& A, int T, int R, hipStream_t stream
     MBRL_CASE(1, 1) MBRL_CASE(2, 1) MBRL_CASE(4, 1) MBRL_CASE(8, 1) MBRL_CASE(16, 1)
     MBRL_CASE(1, 2) MBRL_CASE(2, 2) MBRL_CASE(4, 2) MBRL_CASE(8, 2)
 #undef MBRL_CASE
+    return hipErrorInvalidValue;
+}
+
+// ------------------------------------------------------------------------------------------------
+// 8-candidate tiles (DESIGN.md §3 "rollout_m8_kernel"): v_mfma_f32_4x4x1_16b_f32.
+//
+// A shard of N <= 2048 candidates fills at most 128 workgroups of 16, half the chip. The 4x4x1
+// MFMA runs at the same f32 rate as 16x16x4 but needs only 4 columns per block, so a workgroup can
+// own 8 candidates with no idle MFMA lanes, and twice as many CUs work. Its 16 blocks (b = l >> 2)
+// are 8 row groups x 2 candidate groups: A broadcast within block pairs (CBSZ = 1) lets ONE weight
+// register carry two 32-row tiles, even blocks tile 0 (ABID 0), odd blocks tile 1 (ABID 1):
+//   A (lane l): W[32 tile + 4 (l >> 3) + (l & 3)][k]     B (lane l): X[k][cand l & 7]
+//   D (lane l, v): row 32 tile + 4 (l >> 3) + v of cand l & 7 -> one float4 row store
+// (tools/ubench/mfma4x4.hip checks the layout on the GPU). Every accumulator consumes its k in the
+// 16-candidate kernel's order (16-deep chunk kc, step s, then q: k = 16 kc + 4 q + s): 16x16x4 is
+// an fmaf chain over its 4 k (same microtest), so both kernels give bit-identical sums, and a plan
+// does not depend on which tile height its shard size picked. The output layer mirrors the 8-wave
+// kernel's K split (one partial per 16 T/2 features, four chains (c0 + c1) + (c2 + c3)) and its
+// epilogue, operation for operation.
+// Wave w owns hidden features [64 w, 64 w + 64) (two 32-row tiles); T = Wpad / 64 waves.
+// Weight stream (packed by pack_m8_*_kernel in cem.hip): per 16-deep chunk, per wave, 4 x 64 lanes
+// x float4 (load s holds q = 0..3); chunks per step = K0C + (L-1) 4T + 4 NOP (output: own 4 K chunks
+// x 2-tile pairs), plus DUM ring-alignment slots that reload the last chunk (L2 hits).
+template <int T, int K0C_T, int NOT_T>
+__global__ void __launch_bounds__(64 * T, 1) rollout_m8_kernel(const RolloutArgs A) {
+    constexpr int M = 8;
+    constexpr int NW = T;
+    constexpr int NT = 64 * NW;
+    constexpr int KH = 4 * T;
+    constexpr int NOT8 = NOT_T / 2;          // 32-row output tiles
+    constexpr int NOP = (NOT8 + 1) / 2;      // pairs of them (one weight register each)
+    constexpr int NOC = 4 * NOP;
+#ifdef MBRL_M8_NB
+    constexpr int NB = MBRL_M8_NB;           // A/B override
+#else
+    constexpr int NB = 4;                    // ring slots (16 VGPRs each), 3 chunks ahead: 1 % faster than 8
+#endif                                       // (walker 2048-candidate shard, tools/ab.sh, r01)
+    constexpr int DUM = (NB - (K0C_T + NOC) % NB) % NB;
+    constexpr int TW16 = T / 2;              // the 16-candidate kernel's K chunks per output partial
+    constexpr int NPW = 4 / TW16;            // its partials inside this wave's 4 own chunks
+    constexpr int SS = NOT_T;
+    static_assert(KH % NB == 0 && (T == 4 || T == 8), "m8 geometry");
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const LdsMap L = lds_map(A, smem, M);
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int tile = blockIdx.x, e = blockIdx.y;
+    const float* member = A.packed + (size_t)e * A.member_stride;
+    float* const actX = L.act;
+    float* const actY = L.act2;
+    // epilogue roles as the 8-wave kernel's split mode: waves 0-1 the state rows (4 each), waves 2-3
+    // the actions of the same rows
+    const bool epi = wave < 2;
+    const bool actw = wave >= 2 && wave < 4;
+    const int awave = wave - 2;
+    float* acs = L.aterm;
+    const int cand = lane & 7;
+    float av[1][MAX_A_PER_LANE];
+    float acp[1];
+    auto fetch_a = [&](int t) {
+        const int n = min(tile * M + epi_row(0, awave, lane), A.N - 1);
+        const float* src = A.actions + ((size_t)t * A.N + n) * A.a;
+#pragma unroll
+        for (int k = 0; k < MAX_A_PER_LANE; ++k) av[0][k] = src[min((lane & 15) + 16 * k, A.a - 1)];
+    };
+    if (actw) fetch_a(0);
+    for (int i = tid; i < A.s; i += NT) {
+        L.obs_mean[i] = A.obs_mean ? A.obs_mean[i] : 0.f;
+        L.obs_std[i] = A.obs_std ? A.obs_std[i] : 1.f;
+        L.goal[i] = A.goal ? A.goal[i] : 0.f;
+        L.cw[i] = A.cw ? A.cw[i] : 0.f;
+    }
+    for (int i = tid; i < A.a; i += NT) {
+        L.act_mean[i] = A.act_mean ? A.act_mean[i] : 0.f;
+        L.act_std[i] = A.act_std ? A.act_std[i] : 1.f;
+    }
+    const float* bias_src = member + A.stream_floats;
+    for (int i = tid; i < A.L * A.Wpad + 16 * A.NOT; i += NT) L.hbias[i] = bias_src[i];
+    __syncthreads();
+    for (int i = tid; i < M * A.s; i += NT) {
+        const int m = i / A.s, d = i - (i / A.s) * A.s;
+        const int n = min(tile * M + m, A.N - 1);
+        const float sv = A.s0_per_cand ? A.s0[(size_t)n * A.s + d] : A.s0[d];
+        actX[m * A.lda + d] = A.norm_s ? (sv - L.obs_mean[d]) / L.obs_std[d] : sv;
+    }
+    for (int i = tid; i < M * A.k0pad_extra; i += NT) {
+        const int m = i / A.k0pad_extra, j = i - (i / A.k0pad_extra) * A.k0pad_extra;
+        actX[m * A.lda + A.s + A.a + j] = 0.f;
+    }
+    EpiParams<SS> P;
+    load_epi_params<SS>(A, L, lane, P);
+    if (actw) {
+        stage_actions<1, SS>(A, P, actX, L.aterm, awave, lane, av, acp);
+        const float v = rowsum16(acp[0]);
+        if ((lane & 15) == 0) acs[epi_row(0, awave, lane)] = v;
+    }
+    __syncthreads();
+
+    // ---- weight stream: chunk g of this wave at byte (g T + wave) 4096 + s 1024 + lane 16
+    const int C8 = A.C8;
+    const int CSQ = C8 + DUM;
+    const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(member + A.m8_off), 0, (int)((size_t)C8 * 4096 * T), 0x00020000);
+    const unsigned lane_off = (unsigned)(wave * 4096 + lane * 16);
+    f32x4 ring[NB][4];
+#define M8_LOAD(SLOT, G)                                                                          \
+    do {                                                                                          \
+        int gg_ = (G);                                                                            \
+        if (gg_ >= CSQ) gg_ -= CSQ;                                                               \
+        gg_ = gg_ < C8 ? gg_ : C8 - 1;                                                            \
+        const int so_ = gg_ * (4096 * T);                                                         \
+        _Pragma("unroll") for (int s_ = 0; s_ < 4; ++s_) ring[SLOT][s_] = __builtin_bit_cast(     \
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, lane_off + s_ * 1024, so_, 0));   \
+    } while (0)
+#pragma unroll
+    for (int q = 0; q < NB - 1; ++q) M8_LOAD(q, q);
+    f32x4 bb[2][4];     // B: X[cand][16 kc + 4 q' .. +3], double-buffered over chunks
+    f32x4 acc[2];
+    f32x4 bias[2];
+    float total = 0.f;
+    auto read_b = [&](f32x4 (&b)[4], const float* in, int col) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) b[q] = *reinterpret_cast<const f32x4*>(in + cand * A.lda + col + 4 * q);
+    };
+    auto mma_pair = [&](const f32x4 (&w)[4], const f32x4 (&b)[4]) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                acc[0] = __builtin_amdgcn_mfma_f32_4x4x1f32(w[s][q], b[q][s], acc[0], 1, 0, 0);
+                acc[1] = __builtin_amdgcn_mfma_f32_4x4x1f32(w[s][q], b[q][s], acc[1], 1, 1, 0);
+            }
+    };
+    auto store_layer = [&](float* out) {
+        const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            f32x4 v = acc[u] + bias[u];
+            v = __builtin_elementwise_max(v, zero);
+            *reinterpret_cast<f32x4*>(out + cand * A.lda + 64 * wave + 32 * u + 4 * (lane >> 3)) = v;
+        }
+    };
+    auto load_bias8 = [&](const float* hb) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) bias[u] = *reinterpret_cast<const f32x4*>(hb + 64 * wave + 32 * u + 4 * (lane >> 3));
+    };
+// one hidden-type chunk: refill the slot chunk c-1 vacated, read the next chunk's B, MFMAs of chunk c
+#define M8_CHUNK(SLOT, KC, NK, IN)                                          \
+    do {                                                                    \
+        M8_LOAD(((SLOT) + NB - 1) % NB, g + NB - 1);                         \
+        if ((KC) + 1 < (NK)) read_b(bb[((KC) + 1) & 1], IN, 16 * ((KC) + 1)); \
+        mma_pair(ring[SLOT], bb[(KC) & 1]);                                 \
+        MBRL_PIN();                                                         \
+        ++g;                                                                \
+    } while (0)
+
+    for (int t = 0; t < A.H; ++t) {
+        int g = 0;
+        if (actw && t + 1 < A.H) fetch_a(t + 1);
+        // ---- layer 0: actX [s | a | 0-pad] -> actY
+        acc[0] = acc[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+        load_bias8(L.hbias);
+        read_b(bb[0], actX, 0);
+#pragma unroll
+        for (int kc = 0; kc < K0C_T; ++kc) M8_CHUNK(kc % NB, kc, K0C_T, actX);
+        store_layer(actY);
+        if (A.L > 1) __syncthreads();
+        float* in = actY;
+        float* out = actX;
+        for (int l = 1; l < A.L; ++l) {
+            acc[0] = acc[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+            load_bias8(L.hbias + l * A.Wpad);
+            read_b(bb[0], in, 0);
+#pragma unroll
+            for (int kc = 0; kc < KH; ++kc) M8_CHUNK((K0C_T + kc) % NB, kc, KH, in);
+            store_layer(out);
+            if (l + 1 < A.L) __syncthreads();   // the last hidden layer is read back by its own wave only
+            float* tmp = in; in = out; out = tmp;
+        }
+        // ---- output layer over this wave's own 64 features (from LDS: its own stores, in order)
+        {
+            f32x4 ch[NPW][NOT8][4];
+#pragma unroll
+            for (int j = 0; j < NPW; ++j)
+#pragma unroll
+                for (int u = 0; u < NOT8; ++u)
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) ch[j][u][s] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kc = 0; kc < 4; ++kc) {
+                f32x4 b[4];
+                read_b(b, in, 64 * wave + 16 * kc);
+#pragma unroll
+                for (int p = 0; p < NOP; ++p) {
+                    constexpr int base = K0C_T;   // slots fold: kc, p are unrolled
+                    M8_LOAD(((base + kc * NOP + p) + NB - 1) % NB, g + NB - 1);
+                    const int j = kc / TW16;
+#pragma unroll
+                    for (int s = 0; s < 4; ++s)
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const float w = ring[(base + kc * NOP + p) % NB][s][q];
+                            ch[j][2 * p][s] = __builtin_amdgcn_mfma_f32_4x4x1f32(w, b[q][s], ch[j][2 * p][s], 1, 0, 0);
+                            if (2 * p + 1 < NOT8)
+                                ch[j][2 * p + 1][s] =
+                                    __builtin_amdgcn_mfma_f32_4x4x1f32(w, b[q][s], ch[j][2 * p + 1][s], 1, 1, 0);
+                        }
+                    MBRL_PIN();
+                    ++g;
+                }
+            }
+#pragma unroll
+            for (int d = 0; d < DUM; ++d) {
+                M8_LOAD((K0C_T + NOC + d + NB - 1) % NB, g + NB - 1);
+                ++g;
+            }
+#pragma unroll
+            for (int j = 0; j < NPW; ++j)
+#pragma unroll
+                for (int u = 0; u < NOT8; ++u) {
+                    const f32x4 v = (ch[j][u][0] + ch[j][u][1]) + (ch[j][u][2] + ch[j][u][3]);
+                    *reinterpret_cast<f32x4*>(L.part + (wave * NPW + j) * (M * A.pw) + cand * A.pw + 32 * u +
+                                              4 * (lane >> 3)) = v;
+                }
+        }
+        __syncthreads();
+        // ---- epilogue: the 8-wave kernel's split-mode goal-state epilogue for rows 0..7
+        if (epi) {
+            const int ws = M * A.pw;
+            const int j = lane & 15;
+            const int m = epi_row(0, wave, lane);
+            const int n = tile * M + m;
+            float sc = 0.f;
+            auto slot = [&](int d, float om, float os, float goal, float cw, float bo) {
+                const int ro = m * A.pw + d;
+                float o = L.part[ro] + L.part[ws + ro] + L.part[2 * ws + ro] + L.part[3 * ws + ro];
+                o = o + ((L.part[4 * ws + ro] + L.part[5 * ws + ro]) + (L.part[6 * ws + ro] + L.part[7 * ws + ro]));
+                o = o + bo;
+                const float sn = A.unnorm_s ? o * os + om : o;
+                if (A.has_sc) {
+                    const float x = (sn - goal) * cw;
+                    sc += sqrtf(x * x + A.alpha_s2) - A.alpha_s;
+                }
+                actX[m * A.lda + d] = A.norm_s ? (sn - om) / os : sn;
+                if (A.states_out != nullptr && n < A.N)
+                    A.states_out[(((size_t)e * A.H + t) * A.N + n) * A.s + d] = sn;
+            };
+#pragma unroll
+            for (int k = 0; k < SS; ++k)
+                if (j + 16 * k < A.s) slot(j + 16 * k, P.om[k], P.os[k], P.goal[k], P.cw[k], P.bo[k]);
+            for (int d = A.s + A.a + j; d < A.s + A.a + A.k0pad_extra; d += 16) actX[m * A.lda + d] = 0.f;
+            sc = rowsum16(sc);
+            const float ac = acs[(t & 1) * M + m];
+            total += sc + A.alpha_a2 * (ac / (float)A.a);
+        } else if (actw && t + 1 < A.H) {
+            stage_actions<1, SS>(A, P, actX, L.aterm, awave, lane, av, acp);
+            const float v = rowsum16(acp[0]);
+            if ((lane & 15) == 0) acs[((t + 1) & 1) * M + epi_row(0, awave, lane)] = v;
+        }
+        __syncthreads();
+    }
+#undef M8_CHUNK
+#undef M8_LOAD
+    if (epi && (lane & 15) == 0) {
+        const int n = tile * M + epi_row(0, wave, lane);
+        if (n < A.N) A.costs[(size_t)e * A.N + n] = total;
+    }
+}
+
+bool rollout_m8_supported(const RolloutArgs& A, int T) {
+    if (A.reward || A.redo || A.m8_off == 0) return false;
+    if (T != 4 && T != 8) return false;
+    return (A.K0C == 2 || A.K0C == 6) && (A.NOT == 2 || A.NOT == 6) && rollout_lds_bytes(A, 8) <= 160 * 1024;
+}
+
+template <int T, int K0C_T, int NOT_T>
+static hipError_t launch_m8_tr(const RolloutArgs& A_in, hipStream_t stream) {
+    RolloutArgs A = A_in;
+    A.nw = 8;   // output partials: the 8-wave kernel's count
+    dim3 grid((A.N + 7) / 8, A.E);
+    const size_t lds = rollout_lds_bytes(A, 8);
+    hipError_t e = ensure_dynamic_lds(reinterpret_cast<const void*>(&rollout_m8_kernel<T, K0C_T, NOT_T>), 160 * 1024);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((rollout_m8_kernel<T, K0C_T, NOT_T>), grid, dim3(64 * T), lds, stream, A);
+    return hipGetLastError();
+}
+
+template <int T>
+static hipError_t launch_m8_t(const RolloutArgs& A, hipStream_t stream) {
+    if (A.K0C == 2 && A.NOT == 2) return launch_m8_tr<T, 2, 2>(A, stream);
+    if (A.K0C == 6 && A.NOT == 6) return launch_m8_tr<T, 6, 6>(A, stream);
+    if (A.K0C == 2 && A.NOT == 6) return launch_m8_tr<T, 2, 6>(A, stream);
+    if (A.K0C == 6 && A.NOT == 2) return launch_m8_tr<T, 6, 2>(A, stream);
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_rollout_m8(const RolloutArgs& A, int T, hipStream_t stream) {
+    if (T == 4) return launch_m8_t<4>(A, stream);
+    if (T == 8) return launch_m8_t<8>(A, stream);
     return hipErrorInvalidValue;
 }
 

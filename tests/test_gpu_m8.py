@@ -1,0 +1,57 @@
+"""The 8-candidate rollout tile (rollout_m8_kernel, v_mfma_f32_4x4x1_16b_f32) against
+the 16-candidate kernel and the CPU oracle. The two kernels consume every accumulator's k in the
+same order, so their costs and states must agree BIT FOR BIT (that keeps a sharded plan independent
+of the tile height its shard size picks); both stay within the oracle bars of test_gpu_parity.py.
+MBRL_ROLLOUT_M=8 / 16 forces the tile height (cem.hip rollout_impl)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import cem as ocem
+from oracle.philox import cem_actions
+
+from test_gpu_parity import DEV, RTOL, build, device_problem, rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+def _rollout(monkeypatch, prob, p, N, H, m, A):
+    from mbrl_amd import fused
+    E, s = p["cfg"]["E"], p["cfg"]["s"]
+    monkeypatch.setenv("MBRL_ROLLOUT_M", str(m))
+    states = torch.empty((E, H, N, s), dtype=torch.float32, device=DEV)
+    costs = fused.rollout(prob, torch.from_numpy(p["s0"]).to(DEV), N, H, actions=torch.from_numpy(A).to(DEV),
+                          states_out=states)
+    torch.cuda.synchronize()
+    return costs, states
+
+
+@pytest.mark.parametrize("cid,N,H", [(2, 1000, 20), (2, 9, 5), (3, 2048, 6), (3, 300, 30), (3, 1, 3),
+                                     (4, 517, 7), (5, 40, 6), (5, 250, 3)])
+def test_m8_matches_m16_bitwise_and_the_oracle(monkeypatch, cid, N, H):
+    p = ocem.synth_problem(cid, N=N, H=H)
+    a = p["cfg"]["a"]
+    A = cem_actions(np.zeros((H, a), np.float32), np.full((H, a), 0.5, np.float32), -1, 1, 5, 0, np.arange(N))
+    prob = device_problem(p)
+    c8, s8 = _rollout(monkeypatch, prob, p, N, H, 8, A)
+    c16, s16 = _rollout(monkeypatch, prob, p, N, H, 16, A)
+    assert torch.equal(c8, c16), float((c8 - c16).abs().max())
+    assert torch.equal(s8, s16)
+    ref_costs, ref_states = ocem.rollout(p["model"], p["norm"], p["cost"], p["s0"], A, store_states=True)
+    assert rel_err(c8, ref_costs) < RTOL
+    assert np.allclose(s8.cpu().numpy(), ref_states, rtol=1e-4, atol=1e-4)
+
+
+def test_m8_plan_equals_m16_plan(monkeypatch):
+    """A whole CEM plan at a strong-scaling shard size (walker, 2048 candidates): identical
+    returns, elites, mu and sigma with either tile height."""
+    from mbrl_amd import CEMPlanner
+    p = ocem.synth_problem(4, N=2048, H=10)
+    _, model_fn, cost_fn, sample_action = build(p)
+    out = {}
+    for m in (8, 16):
+        monkeypatch.setenv("MBRL_ROLLOUT_M", str(m))
+        out[m] = CEMPlanner.plan_detailed(torch.from_numpy(p["s0"]), model_fn, cost_fn, sample_action, 10,
+                                          num_candidates=2048, num_iterations=3, seed=p["rng_seed"], record=True)
+    for k in ("returns", "elites", "mu", "sigma", "actions", "states"):
+        assert torch.equal(out[8][k], out[16][k]), k
