@@ -127,11 +127,12 @@ __global__ void pack_m8_hidden_kernel(const float* __restrict__ w, int in_real, 
     }
 }
 
-// Output layer: chunk o = kc * NOP + pair over the wave's own K rows 64 wave + 16 kc + ...; the pair
-// holds output tiles 2 pair (even blocks) and 2 pair + 1 (odd blocks) of 32 rows.
-__global__ void pack_m8_out_kernel(const float* __restrict__ w, int in_real, int out_real, int NOP, int T,
-                                   float* __restrict__ dst) {
-    const size_t total = (size_t)4 * NOP * T * 1024;
+// Output layer over the wave's own K rows 64 wave + 16 kc + ...: with one 32-row tile (kpair) chunk o
+// holds own K chunks 2o (even blocks) and 2o + 1 (odd blocks); else chunk o = kc * NOP + pair holds
+// output tiles 2 pair (even blocks) and 2 pair + 1 (odd blocks).
+__global__ void pack_m8_out_kernel(const float* __restrict__ w, int in_real, int out_real, int NOP, int kpair,
+                                   int T, float* __restrict__ dst) {
+    const size_t total = (size_t)(kpair ? 2 : 4 * NOP) * T * 1024;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
         const int q = (int)(i & 3);
         const int lane = (int)((i >> 2) & 63);
@@ -139,8 +140,10 @@ __global__ void pack_m8_out_kernel(const float* __restrict__ w, int in_real, int
         const size_t cw = i >> 10;            // o * T + wave
         const int wave = (int)(cw % T);
         const int o = (int)(cw / T);
-        const int kc = o / NOP, pair = o % NOP;
-        const int n = 32 * (2 * pair + ((lane >> 2) & 1)) + 4 * (lane >> 3) + (lane & 3);
+        const int odd = (lane >> 2) & 1;
+        const int kc = kpair ? 2 * o + odd : o / NOP;
+        const int tile = kpair ? 0 : 2 * (o % NOP) + odd;
+        const int n = 32 * tile + 4 * (lane >> 3) + (lane & 3);
         const int k = 64 * wave + 16 * kc + 4 * q + s;
         dst[i] = (n < out_real && k < in_real) ? w[(size_t)n * in_real + k] : 0.0f;
     }
@@ -1016,7 +1019,7 @@ int mbrl_mlp_pack(const mbrl_mlp_shape* shape, const float* const* weights, cons
                                            g.NOS, g.T, P, split_base[P - 2] + split_chunk * 2048 * (size_t)g.T * P,
                                            split_bad[P - 2]);
                 if (g.m8_ok)
-                    hipLaunchKernelGGL(pack_m8_out_kernel, dim3(256), dim3(256), 0, stream, w, g.W, g.s, g.NOP8, g.T,
+                    hipLaunchKernelGGL(pack_m8_out_kernel, dim3(256), dim3(256), 0, stream, w, g.W, g.s, g.NOP8, g.NOC8 == 2, g.T,
                                        m8_base + m8_chunk * 1024 * (size_t)g.T);
                 float* ob = bias_base + (size_t)g.L * g.Wpad;
                 hipLaunchKernelGGL(pack_bias_kernel, dim3(1), dim3(256), 0, stream, b, g.s, 16 * g.NOT, ob);

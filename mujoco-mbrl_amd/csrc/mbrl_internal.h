@@ -40,10 +40,11 @@ struct Geometry {
     size_t split3_off;     // the 3-piece stream (F16X6): CS * 3072 * T floats, then its flag word
     size_t split3_floats;
     // 8-candidate fp32 stream (rollout.hip rollout_m8_kernel): 16-deep chunks, T waves x 4 KiB each;
-    // K0C + (L-1)*4T + 4*NOP8 chunks per step. Present when m8_ok (Wpad 256 or 512, no reward head,
+    // K0C + (L-1)*4T + NOC8 chunks per step. Present when m8_ok (Wpad 256 or 512, no reward head,
     // the ring shapes K0C, NOT in {2, 6}).
     int m8_ok;
     int NOP8;              // pairs of 32-row output tiles
+    int NOC8;              // output chunks per step
     int C8;                // chunks per step
     size_t m8_off;         // floats from the member base (0: absent)
     size_t m8_floats;      // C8 * 1024 * T
@@ -93,7 +94,8 @@ inline bool make_geometry(int s, int a, int W, int L, int E, int reward, Geometr
     if (g->split_ok) end = g->split3_off + g->split3_floats;
     g->m8_ok = ((T == 4 || T == 8) && !reward && (g->K0C == 2 || g->K0C == 6) && (g->NOT == 2 || g->NOT == 6)) ? 1 : 0;
     g->NOP8 = (g->NOT / 2 + 1) / 2;
-    g->C8 = g->K0C + (L - 1) * 4 * T + 4 * g->NOP8;
+    g->NOC8 = g->NOT == 2 ? 2 : 4 * g->NOP8;   // one 32-row output tile: K-chunk pairs (rollout_m8_kernel)
+    g->C8 = g->K0C + (L - 1) * 4 * T + g->NOC8;
     g->m8_off = g->m8_ok ? (end + 63) / 64 * 64 : 0;
     g->m8_floats = g->m8_ok ? (size_t)g->C8 * 1024 * T : 0;
     if (g->m8_ok) end = g->m8_off + g->m8_floats;

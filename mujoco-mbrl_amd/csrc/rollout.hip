@@ -633,8 +633,9 @@ hipError_t launch_rollout(const RolloutArgs& A, int T, int R, hipStream_t stream
 // epilogue, operation for operation.
 // Wave w owns hidden features [64 w, 64 w + 64) (two 32-row tiles); T = Wpad / 64 waves.
 // Weight stream (packed by pack_m8_*_kernel in cem.hip): per 16-deep chunk, per wave, 4 x 64 lanes
-// x float4 (load s holds q = 0..3); chunks per step = K0C + (L-1) 4T + 4 NOP (output: own 4 K chunks
-// x 2-tile pairs), plus DUM ring-alignment slots that reload the last chunk (L2 hits).
+// x float4 (load s holds q = 0..3); chunks per step = K0C + (L-1) 4T + NOC (output: 2 K-chunk pairs
+// of the one 32-row tile, or own 4 K chunks x 2-tile pairs), plus DUM ring-alignment slots that
+// reload the last chunk (L2 hits; none for the BASELINE shapes).
 template <int T, int K0C_T, int NOT_T>
 __global__ void __launch_bounds__(64 * T, 1) rollout_m8_kernel(const RolloutArgs A) {
     constexpr int M = 8;
@@ -643,7 +644,10 @@ __global__ void __launch_bounds__(64 * T, 1) rollout_m8_kernel(const RolloutArgs
     constexpr int KH = 4 * T;
     constexpr int NOT8 = NOT_T / 2;          // 32-row output tiles
     constexpr int NOP = (NOT8 + 1) / 2;      // pairs of them (one weight register each)
-    constexpr int NOC = 4 * NOP;
+    // output chunks: one 32-row tile (s <= 32) pairs two own K chunks in one register (even blocks
+    // chunk 2o, odd blocks 2o + 1: no idle half); wider outputs pair two tiles per K chunk
+    constexpr bool KPAIR = NOT8 == 1;
+    constexpr int NOC = KPAIR ? 2 : 4 * NOP;
 #ifdef MBRL_M8_NB
     constexpr int NB = MBRL_M8_NB;           // A/B override
 #else
@@ -799,6 +803,32 @@ __global__ void __launch_bounds__(64 * T, 1) rollout_m8_kernel(const RolloutArgs
                 for (int u = 0; u < NOT8; ++u)
 #pragma unroll
                     for (int s = 0; s < 4; ++s) ch[j][u][s] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if constexpr (KPAIR) {
+#pragma unroll
+                for (int o = 0; o < 2; ++o) {
+                    f32x4 b0[4], b1[4];
+                    read_b(b0, in, 64 * wave + 32 * o);
+                    read_b(b1, in, 64 * wave + 32 * o + 16);
+                    constexpr int base = K0C_T;
+                    M8_LOAD((base + o + NB - 1) % NB, g + NB - 1);
+                    const int j0 = (2 * o) / TW16, j1 = (2 * o + 1) / TW16;
+                    // chain s: chunk 2o (q = 0..3, ABID 0), then chunk 2o + 1 (ABID 1) -- the
+                    // 16-candidate kernel's kc-then-q order
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) {
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            ch[j0][0][s] = __builtin_amdgcn_mfma_f32_4x4x1f32(ring[(base + o) % NB][s][q], b0[q][s],
+                                                                              ch[j0][0][s], 1, 0, 0);
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            ch[j1][0][s] = __builtin_amdgcn_mfma_f32_4x4x1f32(ring[(base + o) % NB][s][q], b1[q][s],
+                                                                              ch[j1][0][s], 1, 1, 0);
+                    }
+                    MBRL_PIN();
+                    ++g;
+                }
+            } else {
 #pragma unroll
             for (int kc = 0; kc < 4; ++kc) {
                 f32x4 b[4];
@@ -821,6 +851,7 @@ __global__ void __launch_bounds__(64 * T, 1) rollout_m8_kernel(const RolloutArgs
                     MBRL_PIN();
                     ++g;
                 }
+            }
             }
 #pragma unroll
             for (int d = 0; d < DUM; ++d) {

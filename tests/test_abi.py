@@ -40,8 +40,8 @@ def test_no_gpu_needed_for_sizing_calls():
     # pieces) or x 12 KiB (F16X6: three pieces), each followed by a flag word
     a64 = lambda x: (x + 63) // 64 * 64   # noqa: E731
     split = 34 * 2048 * 8 + 64 + 34 * 3072 * 8 + 64
-    # then the 8-candidate stream: 2 + 2 x 32 + 4 chunks of 16 K rows x 8 waves x 4 KiB
-    m8 = 70 * 8192
+    # then the 8-candidate stream: 2 + 2 x 32 + 2 chunks of 16 K rows x 8 waves x 4 KiB
+    m8 = 68 * 8192
     assert lib.mbrl_mlp_packed_bytes(ctypes.byref(sh)) == a64(a64(68 * 8192 + 3 * 512 + 32 + plain) + split + m8) * 4
     # precision does not change the packed layout; an unknown precision is rejected
     assert lib.mbrl_mlp_packed_bytes(ctypes.byref(_lib.MlpShape(17, 6, 512, 3, 1, 0, 1))) == \
