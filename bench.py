@@ -230,7 +230,10 @@ def main():
                           "significant bits), the 6 partial products x_i w_j with i + j < 3 (exact), fp32 "
                           "accumulation; same parity bars (tests/test_gpu_f16x3.py)"}
         out["variants"] = []
-        for other in [p for p in ("f32", "f16x6", "f16x3") if p != args.precision]:
+        # the split kernels serve goal-state costs only (include/mbrl_cem.h); a reward-head model
+        # would run fp32 under every precision, so it has no variants
+        others = [] if cfg.get("reward") else [p for p in ("f32", "f16x6", "f16x3") if p != args.precision]
+        for other in others:
             v_elapsed, v_rollout_s, v_first = timed(other)
             var = dict(precision=other, value=cand_steps / v_elapsed, ms_per_step=v_elapsed / args.steps * 1e3,
                        rollout_avg_launch_ms=v_rollout_s * 1e3,
