@@ -108,3 +108,8 @@ def sample_action_1d(batch_size=None):
 
 def zero_action(state_and_obs):
     return torch.zeros(1)
+
+
+def dying_env(env_name, task_name, flat_obs=True, index=0):
+    import os
+    os._exit(3)

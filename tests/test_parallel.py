@@ -121,3 +121,9 @@ def test_gpu_planner_service_serves_cem_batches():
     for i, r in enumerate(rs):
         assert len(r) == 4
         assert all(torch.equal(torch.as_tensor(x).reshape(-1), y) for x, y in zip(r.actions[:-1], answers[i]))
+
+
+def test_a_dead_worker_is_reported():
+    with pytest.raises(RuntimeError, match="died"):
+        parallel.get_rollouts_parallel("linear", "run", True, 2, dict(num_steps=3), num_workers=2,
+                                       env_factory=se.dying_env)
