@@ -26,10 +26,12 @@ def _rollout(monkeypatch, prob, p, N, H, m, A):
     return costs, states
 
 
-@pytest.mark.parametrize("cid,N,H", [(2, 1000, 20), (2, 9, 5), (3, 2048, 6), (3, 300, 30), (3, 1, 3),
-                                     (4, 517, 7), (5, 40, 6), (5, 250, 3)])
-def test_m8_matches_m16_bitwise_and_the_oracle(monkeypatch, cid, N, H):
-    p = ocem.synth_problem(cid, N=N, H=H)
+@pytest.mark.parametrize("cid,N,H,over", [(2, 1000, 20, {}), (2, 9, 5, {}), (3, 2048, 6, {}), (3, 300, 30, {}),
+                                          (3, 1, 3, {}), (4, 517, 7, {}), (5, 40, 6, {}), (5, 250, 3, {}),
+                                          (3, 33, 1, {}), (2, 300, 5, dict(L=1)), (3, 100, 4, dict(W=200)),
+                                          (4, 64, 3, dict(W=256, L=4))])
+def test_m8_matches_m16_bitwise_and_the_oracle(monkeypatch, cid, N, H, over):
+    p = ocem.synth_problem(cid, N=N, H=H, **over)
     a = p["cfg"]["a"]
     A = cem_actions(np.zeros((H, a), np.float32), np.full((H, a), 0.5, np.float32), -1, 1, 5, 0, np.arange(N))
     prob = device_problem(p)
