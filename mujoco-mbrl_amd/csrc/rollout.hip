@@ -376,6 +376,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
 #ifdef MBRL_STAMPS
     unsigned long long seg[NSEG] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long tprev = __builtin_amdgcn_s_memtime();
+    const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz: seg[7] -> clock
 #endif
 
 // One chunk of a hidden-type layer: refill the slot chunk (c-1) vacated with chunk c+NB-1, read the
@@ -563,6 +564,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
 #undef MBRL_HIDDEN_CHUNK
 #undef MBRL_LOAD_CHUNK
 #ifdef MBRL_STAMPS
+    seg[NSEG - 1] = __builtin_amdgcn_s_memrealtime() - rt0;
     if (lane == 0 && g_mbrl_stamps != nullptr) {
         unsigned long long* dst = g_mbrl_stamps + (((size_t)e * gridDim.x + tile) * NW + wave) * NSEG;
 #pragma unroll
@@ -735,6 +737,11 @@ __global__ void __launch_bounds__(64 * T, 1) rollout_m8_kernel(const RolloutArgs
     f32x4 acc[2];
     f32x4 bias[2];
     float total = 0.f;
+#ifdef MBRL_STAMPS
+    unsigned long long seg[NSEG] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long tprev = __builtin_amdgcn_s_memtime();
+    const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz: seg[7] -> clock
+#endif
     auto read_b = [&](f32x4 (&b)[4], const float* in, int col) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) b[q] = *reinterpret_cast<const f32x4*>(in + cand * A.lda + col + 4 * q);
@@ -780,8 +787,10 @@ __global__ void __launch_bounds__(64 * T, 1) rollout_m8_kernel(const RolloutArgs
         read_b(bb[0], actX, 0);
 #pragma unroll
         for (int kc = 0; kc < K0C_T; ++kc) M8_CHUNK(kc % NB, kc, K0C_T, actX);
+        STAMP(0);
         store_layer(actY);
         if (A.L > 1) __syncthreads();
+        STAMP(1);
         float* in = actY;
         float* out = actX;
         for (int l = 1; l < A.L; ++l) {
@@ -790,8 +799,10 @@ __global__ void __launch_bounds__(64 * T, 1) rollout_m8_kernel(const RolloutArgs
             read_b(bb[0], in, 0);
 #pragma unroll
             for (int kc = 0; kc < KH; ++kc) M8_CHUNK((K0C_T + kc) % NB, kc, KH, in);
+            STAMP(2);
             store_layer(out);
             if (l + 1 < A.L) __syncthreads();   // the last hidden layer is read back by its own wave only
+            STAMP(3);
             float* tmp = in; in = out; out = tmp;
         }
         // ---- output layer over this wave's own 64 features (from LDS: its own stores, in order)
@@ -867,7 +878,9 @@ __global__ void __launch_bounds__(64 * T, 1) rollout_m8_kernel(const RolloutArgs
                                               4 * (lane >> 3)) = v;
                 }
         }
+        STAMP(4);
         __syncthreads();
+        STAMP(5);
         // ---- epilogue: the 8-wave kernel's split-mode goal-state epilogue for rows 0..7
         if (epi) {
             const int ws = M * A.pw;
@@ -902,7 +915,16 @@ __global__ void __launch_bounds__(64 * T, 1) rollout_m8_kernel(const RolloutArgs
             if ((lane & 15) == 0) acs[((t + 1) & 1) * M + epi_row(0, awave, lane)] = v;
         }
         __syncthreads();
+        STAMP(6);
     }
+#ifdef MBRL_STAMPS
+    seg[NSEG - 1] = __builtin_amdgcn_s_memrealtime() - rt0;
+    if (lane == 0 && g_mbrl_stamps != nullptr) {
+        unsigned long long* dst = g_mbrl_stamps + (((size_t)e * gridDim.x + tile) * 8 + wave) * NSEG;
+#pragma unroll
+        for (int k = 0; k < NSEG; ++k) dst[k] = seg[k];
+    }
+#endif
 #undef M8_CHUNK
 #undef M8_LOAD
     if (epi && (lane & 15) == 0) {

@@ -18,7 +18,8 @@ import torch  # noqa: E402
 from mbrl_amd import _lib, fused, synthetic  # noqa: E402
 
 SEGS = ["layer0 mma", "layer0 store+bar", "hidden mma", "hidden store+bar", "output mma", "output bar",
-        "epilogue+bar", "(unused)"]
+        "epilogue+bar"]
+NSEG = 8   # slot 7: s_memrealtime ticks (100 MHz) over the same loop -> the shader clock
 
 
 def main():
@@ -35,8 +36,10 @@ def main():
     p = fused.device_problem(md, cd, dev)
     R = 2 if (N >= 2 * 16 * 256 and md["W"] <= 512) else 1
     tiles = (N + 16 * R - 1) // (16 * R)
+    if os.environ.get("MBRL_ROLLOUT_M") == "8":     # rollout_m8_kernel: 8 candidates per workgroup
+        R, tiles = 0.5, (N + 7) // 8
     NWMAX = 8   # waves per workgroup (4 or 8); unused slots stay zero and are dropped below
-    buf = torch.zeros(E * tiles * NWMAX * len(SEGS), dtype=torch.int64, device=dev)
+    buf = torch.zeros(E * tiles * NWMAX * NSEG, dtype=torch.int64, device=dev)
     assert lib.mbrl_diag_set_stamps(buf.data_ptr()) == 0
     mu = torch.zeros((H, a), device=dev)
     sg = torch.full((H, a), 0.5, device=dev)
@@ -45,14 +48,16 @@ def main():
     for _ in range(3):
         fused.rollout(p, s0, N, H, sampler=fused.make_sampler(1, 0, mu, sg, -1, 1), actions_out=acts)
     torch.cuda.synchronize()
-    st = buf.view(E * tiles * NWMAX, len(SEGS)).cpu().numpy().astype(np.float64)
+    st = buf.view(E * tiles * NWMAX, NSEG).cpu().numpy().astype(np.float64)
     st = st[st.sum(1) > 0]
-    per_step = st.mean(0) / H
+    ghz = st[:, :7].sum(1).mean() / (st[:, 7].mean() * 10.0)
+    per_step = st[:, :7].mean(0) / H
     tot = per_step.sum()
+    print(f"  shader clock over the step loop: {ghz:.2f} GHz (s_memtime / s_memrealtime)")
     print(f"config {cid} N={N} R={R} tiles={tiles}: mean cycles per step per wave {tot:.0f} (diag build; shares only)")
     for name, v in zip(SEGS, per_step):
         print(f"  {name:18s} {v:9.0f}  {100 * v / tot:5.1f}%")
-    mfma = 2176 * R if cid in (3, 4) else None
+    mfma = int(2176 * R) if cid in (3, 4) and R >= 1 else None
     if mfma:
         print(f"  ideal MFMA issue per step per wave: {mfma * 32} cycles; hidden-loop efficiency "
               f"{2048 * R * 32 / per_step[2]:.3f}")
