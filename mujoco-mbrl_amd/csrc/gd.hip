@@ -317,7 +317,10 @@ __device__ __forceinline__ float gc_half_sum(float v) {
 }
 
 // Publish this workgroup's 16 values (lane c == 0 of half-wave g holds value g) and gather all P
-// slices into `dst`; returns false on a timeout (status set).
+// slices into `dst`; returns false on a timeout (status set). GR = Wp / 64 granules per lane: every
+// load of a sweep pass is in flight before the first compare (a runtime-bounded loop waited for
+// each load in turn: GR dependent fabric round trips per pass).
+template <int GR>
 __device__ __forceinline__ bool gc_exchange(gc_gu64* xchg, int Wp, int p, unsigned& phase, float val, float* dst,
                                             int& abort_flag, unsigned* status) {
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = tid >> 5, c = tid & 31;
@@ -329,11 +332,15 @@ __device__ __forceinline__ bool gc_exchange(gc_gu64* xchg, int Wp, int p, unsign
     if (wave == 0) {
         const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
         for (;;) {
+            gc_u64 gv[GR];
+#pragma unroll
+            for (int q = 0; q < GR; ++q)
+                gv[q] = __hip_atomic_load(&buf[lane + 64 * q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             bool ok = true;
-            for (int q = lane; q < Wp; q += 64) {
-                const gc_u64 v = __hip_atomic_load(&buf[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ok &= (unsigned)(v >> 32) == epoch;
-                dst[q] = __uint_as_float((unsigned)v);
+#pragma unroll
+            for (int q = 0; q < GR; ++q) {
+                ok &= (unsigned)(gv[q] >> 32) == epoch;
+                dst[lane + 64 * q] = __uint_as_float((unsigned)gv[q]);
             }
             if (__all(ok)) break;
             if (__builtin_amdgcn_s_memrealtime() - t_start > 20000000ull) {   // 200 ms
@@ -349,6 +356,41 @@ __device__ __forceinline__ bool gc_exchange(gc_gu64* xchg, int Wp, int p, unsign
     __syncthreads();
     ++phase;
     return abort_flag == 0;
+}
+
+// Wave-wide reduce-scatter of 32 values per lane by recursive halving: returns the sum over the
+// 64 lanes of v[lane >> 1] (both lanes of a pair hold it). 32 shuffles where a butterfly per value
+// takes 192.
+__device__ __forceinline__ float wave_reduce_scatter32(const float (&v)[32], int lane) {
+    float a16[16], a8[8], a4[4], a2[2];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const bool hi = lane & 32;
+        const float keep = hi ? v[j + 16] : v[j], send = hi ? v[j] : v[j + 16];
+        a16[j] = keep + __shfl_xor(send, 32, 64);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const bool hi = lane & 16;
+        const float keep = hi ? a16[j + 8] : a16[j], send = hi ? a16[j] : a16[j + 8];
+        a8[j] = keep + __shfl_xor(send, 16, 64);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const bool hi = lane & 8;
+        const float keep = hi ? a8[j + 4] : a8[j], send = hi ? a8[j] : a8[j + 4];
+        a4[j] = keep + __shfl_xor(send, 8, 64);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const bool hi = lane & 4;
+        const float keep = hi ? a4[j + 2] : a4[j], send = hi ? a4[j] : a4[j + 2];
+        a2[j] = keep + __shfl_xor(send, 4, 64);
+    }
+    const bool hi = lane & 2;
+    const float keep = hi ? a2[1] : a2[0], send = hi ? a2[0] : a2[1];
+    const float a1 = keep + __shfl_xor(send, 2, 64);
+    return a1 + __shfl_xor(a1, 1, 64);
 }
 
 // K0R >= s + a: layer-0 inputs per thread; SM: output rows per half-wave (16 SM >= s); WI = W / 32.
@@ -456,7 +498,7 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
                 for (int i = 0; i < WI; ++i) v += f[c + 32 * i] * cur[c + 32 * i];
                 v = gc_half_sum(v);
                 v = fmaxf(v + hbias[(size_t)l * Wp + p * GC_ROWS + g], 0.0f);
-                if (!gc_exchange(xchg, Wp, p, phase, v, nxt, abort_flag, status)) return;
+                if (!gc_exchange<WI / 2>(xchg, Wp, p, phase, v, nxt, abort_flag, status)) return;
                 float* tmp = cur; cur = nxt; nxt = tmp;
                 if (has_unit) ht[(size_t)l * Wp + tid] = cur[tid];
             }
@@ -509,19 +551,18 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
                 v = gc_half_sum(v);
                 const int k = p * GC_ROWS + g;
                 v = ht[(size_t)(l - 1) * Wp + k] > 0.f ? v : 0.f;     // ReLU' of layer l - 1's output
-                if (!gc_exchange(xchg, Wp, p, phase, v, gnxt, abort_flag, status)) return;
+                if (!gc_exchange<WI / 2>(xchg, Wp, p, phase, v, gnxt, abort_flag, status)) return;
                 float* tmp = gcur; gcur = gnxt; gnxt = tmp;
             }
             // layer 0 backward (redundant): g_x0[k] = sum_u W0[u][k] g_z0[u], a block reduction per k
             {
+                static_assert(K0R == 32, "wave_reduce_scatter32");
                 const float gu = has_unit ? gcur[tid] : 0.f;
+                float vk[K0R];
 #pragma unroll
-                for (int k = 0; k < K0R; ++k) {
-                    float v = w0r[k] * gu;
-#pragma unroll
-                    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-                    if (lane == 0) red[wave * K0R + k] = v;
-                }
+                for (int k = 0; k < K0R; ++k) vk[k] = w0r[k] * gu;
+                const float r = wave_reduce_scatter32(vk, lane);
+                if ((lane & 1) == 0) red[wave * K0R + (lane >> 1)] = r;
                 __syncthreads();
                 for (int k = tid; k < K0; k += GC_THREADS) {
                     float v = 0.f;
