@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=3, help="SURVEY.md §8d config id (default: cheetah-run CEM)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=20.0,
+                    help="seconds of CPU oracle work the cpu_baseline sample may take (about half is used)")
     ap.add_argument("--precision", default="f32", choices=["f32", "f16x3", "f16x6"],
                     help="rollout matmul precision (include/mbrl_cem.h MBRL_PRECISION_*)")
     ap.add_argument("--no-variants", action="store_true",
@@ -253,7 +255,7 @@ def main():
                 var["parity"] = parity_sample(prob, v_first)
             out["variants"].append(var)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.config)
+        out["cpu_baseline"] = cpu_baseline(args.config, budget_s=args.cpu_budget)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
