@@ -19,6 +19,8 @@ Extra objects on the JSON line:
                   the timed region; peak = fp32 MFMA dense 157.3 TFLOP/s (MI355X_MICROARCH.md).
   cpu_baseline -- the CPU oracle (NumPy restatement of the reference rollout + CEM refit), rank 0,
                   N=1 only, on a bounded sample; a reported baseline, not the target.
+  cpu_baseline_torch -- the reference's own CPU arrangement beside it: torch on the host with
+                  autograd on (planners.py:199-210), NumPy refit; same conditions.
   parity       -- iteration-0 returns of 256 sampled candidates re-computed by the CPU oracle.
   variants     -- the same workload timed with the other rollout precisions (default headline: exact
                   fp32; variants: f16x6 and f16x3, fp32 emulated on the f16 matrix cores).
@@ -97,6 +99,53 @@ def cpu_baseline(cfg_id, budget_s=20.0):
     return dict(value=value, unit="candidate-timesteps/s", cores=int(cores), kind="port", cpu=cpu,
                 sample=f"{plans} full CEM plan(s) (I={ITERATIONS}, N={n_sample}, H={H}) of the NumPy oracle "
                        f"(oracle/cem.py), fp32, {elapsed:.1f} s")
+
+
+def cpu_torch_baseline(prob, budget_s=20.0):
+    """The reference's own CPU arrangement, timed beside the NumPy oracle: torch on the host with
+    autograd ON, as RandomShootingPlanner._generate_trajectories runs it (planners.py:199-210: H
+    model calls writing state_list slices, then one cost call, view(H, N).sum(0)); the model is
+    mbrl_amd.models on CPU (the reference's DynamicsModel math). CEM proposal / select / refit in
+    NumPy (stable argsort, population variance). A bounded sample of the same workload."""
+    cfg = prob["cfg"]
+    N, H, a, s = cfg["N"], cfg["H"], cfg["a"], cfg["s"]
+    threads = min(16, len(os.sched_getaffinity(0)))
+    torch.set_num_threads(threads)
+    rng = np.random.default_rng(0)
+    model, cost = prob["model"], prob["cost"]
+    s0 = prob["s0"].reshape(1, s).float()
+
+    def plan(n):
+        mu = np.zeros((H, a), np.float32)
+        sg = np.full((H, a), 0.5, np.float32)
+        for _ in range(ITERATIONS):
+            A = np.clip(mu[:, None, :] + sg[:, None, :] * rng.standard_normal((H, n, a), dtype=np.float32), -1.0, 1.0)
+            action_list = torch.from_numpy(A.reshape(H * n, a))
+            state_list = torch.zeros((H * n, s))
+            states = s0.expand(n, s)
+            for t in range(H):
+                states = model(states, action_list[t * n:(t + 1) * n])
+                state_list[t * n:(t + 1) * n] = states
+            costs = cost(state_list, action_list).view(H, n).sum(0).detach().numpy()
+            el = A[:, np.argsort(costs, kind="stable")[:max(1, n // 10)], :]
+            mu = 0.1 * mu + 0.9 * el.mean(axis=1)
+            sg = np.sqrt(0.1 * sg * sg + 0.9 * el.var(axis=1)).astype(np.float32)
+        return mu
+
+    t0 = time.perf_counter()
+    plan(max(64, N // 16))
+    probe = (time.perf_counter() - t0) * 16
+    n_sample = N if probe <= budget_s / 2 else max(64, int(N * budget_s / 2 / probe))
+    plans, elapsed = 0, 0.0
+    while elapsed < budget_s / 2 and plans < 10:
+        t0 = time.perf_counter()
+        plan(n_sample)
+        elapsed += time.perf_counter() - t0
+        plans += 1
+    return dict(value=ITERATIONS * n_sample * H * plans / elapsed, unit="candidate-timesteps/s", cores=threads,
+                kind="port", autograd=True,
+                sample=f"{plans} CEM plan(s) (I={ITERATIONS}, N={n_sample}, H={H}): torch on the host, autograd on, "
+                       f"the reference's _generate_trajectories loop + NumPy refit, {elapsed:.1f} s")
 
 
 def parity_sample(prob, res, n=256):
@@ -256,6 +305,7 @@ def main():
             out["variants"].append(var)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.config, budget_s=args.cpu_budget)
+        out["cpu_baseline_torch"] = cpu_torch_baseline(prob, budget_s=args.cpu_budget)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -30,5 +30,7 @@ def test_bench_json_line_contract():
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-9
     c = d["cpu_baseline"]
     assert c["kind"] == "port" and c["cores"] >= 1 and c["value"] > 0 and c["sample"]
+    ct = d["cpu_baseline_torch"]
+    assert ct["autograd"] is True and ct["value"] > 0 and ct["cores"] >= 1
     assert d["parity"]["return_max_rel_err"] < 1e-5
     assert [v["precision"] for v in d["variants"]] == ["f16x6", "f16x3"]
