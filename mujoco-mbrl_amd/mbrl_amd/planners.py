@@ -155,8 +155,8 @@ class CEMPlanner(ModelPlanner):
     num_iterations (5), alpha (0.1), seed (None -> drawn from the global NumPy RNG, like the
     reference's sampler), init_std (None -> (hi - lo) / 4), action_bounds (None -> from
     sample_action's action_spec, else (-1, 1)), distributed (False), return_device (False),
-    precision ("f32": exact fp32 MFMA; "f16x3": fp32 emulated on the f16 matrix cores, see
-    include/mbrl_cem.h).
+    precision ("f32": exact fp32 MFMA; "f16x6" / "f16x3": fp32 emulated on the f16 matrix cores
+    with 33 / 22 significant operand bits, see include/mbrl_cem.h).
     Returns the final Gaussian mean (clipped) and its predicted states (ensemble mean)."""
     defaults = dict(num_candidates=1000, num_elites=None, num_iterations=5, alpha=0.1, seed=None, init_std=None,
                     action_bounds=None, distributed=False, return_device=False, precision="f32")
