@@ -175,7 +175,11 @@ int mbrl_select_elites(const float* costs, int32_t E, int32_t N, int32_t K, int3
 
 /* ---- CEM refit (not in the reference). Regenerates each elite's actions from
  * the counter RNG (so every rank can refit from the global elite list with no moment collective),
- * sums them in the canonical chunked order, writes mu' / sigma' ([H][a]). */
+ * sums them in the canonical chunked order, writes mu' / sigma' ([H][a]).
+ * Multi-GPU split step: SURVEY.md §8b proposed an mbrl_topk_moments (local elite moments, then an
+ * all-gather of [G][2][H][a]). Here every rank runs mbrl_select_elites on the all-gathered
+ * returns and mbrl_cem_refit on the global elite list: one collective per iteration instead of
+ * two, and the result does not depend on the GPU count. */
 size_t mbrl_refit_workspace_bytes(int32_t H, int32_t a, int32_t K);
 int mbrl_cem_refit(const mbrl_sampler* sampler, int32_t H, int32_t a, const int64_t* elite_idx,
                    int32_t K, float alpha, float* mu_out, float* sigma_out, void* workspace,
