@@ -225,8 +225,9 @@ int mbrl_cem_plan_batch(const mbrl_mlp_shape* shape, const void* packed, const m
 
 /* ---- gradient-descent planner: replaces GradientDescentPlanner's
  * _optimize_trajectory (planners.py:103-137) -- Adam(lr) on the action sequence through the dynamics
- * with the goal-state cost, stopping once mean |delta a| < stop_condition -- as one persistent
- * workgroup (forward, backward and the Adam step on the device; no host round trip per iteration).
+ * with the goal-state cost, stopping once mean |delta a| < stop_condition -- as one launch (forward,
+ * backward and the Adam step on the device; no host round trip per iteration): Wpad/16 cooperating
+ * workgroups that hand hidden vectors to each other, or one workgroup where those do not apply.
  * actions: [H][a] device, in: the initial sequence, out: the optimised one. states_out: [H+1][s]
  * = the last iteration's rollout (computed before its update, as the reference returns it).
  * iterations_out: device int32 (iterations run) or NULL. Needs ensemble == 1, reward_head == 0 and a
