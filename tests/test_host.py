@@ -185,3 +185,24 @@ def test_mpc_policy_host_logic():
     assert it[0].shape == (3, 2) and it[1].shape == (4, 1) and float(it[1][0, 0]) == 10.0
     pol.get_action({"timestep": 0, "observation": torch.zeros(2)})
     assert calls[2][0] is None
+
+
+def test_policy_and_closures_pickle_like_the_reference_agent():
+    """agents.save pickles the whole agent, planner and model included (agents.py:22-27), and
+    parallel.py pickles policies into workers: the planner class, the model closures (partials
+    over normalize_field) and the cost closure must round-trip, with no device handles in them."""
+    import pickle
+
+    from mbrl_amd import CEMPlanner, MPCPolicy, fused, synthetic
+    prob = synthetic.make_problem(3, N=64, H=4)
+    pol = MPCPolicy(prob["model"], prob["cost"], CEMPlanner, prob["sample_action"], 4, num_candidates=64, seed=3)
+    back = pickle.loads(pickle.dumps(pol))
+    assert back.planner is CEMPlanner and back.plan_kwargs == pol.plan_kwargs
+    md0, md1 = fused.describe_model(pol.model), fused.describe_model(back.model)
+    assert md1 is not None and (md0["s"], md0["a"], md0["W"], md0["L"]) == (md1["s"], md1["a"], md1["W"], md1["L"])
+    for l0, l1 in zip(md0["members"][0], md1["members"][0]):
+        assert torch.equal(l0.weight, l1.weight) and torch.equal(l0.bias, l1.bias)
+    assert fused.describe_cost(back.cost, md1["s"], md1) is not None
+    s = torch.randn(5, 17)
+    a = torch.rand(5, 6) * 2 - 1
+    assert torch.equal(pol.model(s, a), back.model(s, a))

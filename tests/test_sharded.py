@@ -1,4 +1,4 @@
-"""CPU, world_size 2 (gloo): the sharded CEM protocol (planners.cem_sharded_protocol).
+"""CPU, world_size 2, 4 and 8 (gloo): the sharded CEM protocol (planners.cem_sharded_protocol).
 
 The protocol -- candidate ranges per rank, proposals keyed by the global index, the all-gather
 layout, replicated select + refit -- runs here with its math bound to the CPU oracle (the checker)
@@ -81,11 +81,12 @@ def _worker(rank, world, init_file, case, out_dir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("case", [(3, 64, 4, 6, 3), (5, 32, 3, 4, 2)])   # (config, N, H, K, I); config 5: E=5
-def test_sharded_protocol_bit_identical_to_single_process(case):
+# (config, N, H, K, I) x ranks; config 5: E=5. SURVEY.md §4 asks for 1/2/4/8 ranks on one node.
+@pytest.mark.parametrize("case,world", [((3, 64, 4, 6, 3), 2), ((5, 32, 3, 4, 2), 2), ((3, 64, 4, 6, 3), 4),
+                                        ((3, 64, 3, 6, 2), 8)])
+def test_sharded_protocol_bit_identical_to_single_process(case, world):
     from oracle import cem as ocem
     cid, N, H, K, I = case
-    world = 2
     with tempfile.TemporaryDirectory() as d:
         mp.start_processes(_worker, args=(world, os.path.join(d, "pg"), case, d), nprocs=world, join=True,
                            start_method="spawn")
