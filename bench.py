@@ -65,6 +65,55 @@ def parse():
     return ap.parse_args()
 
 
+class TimingEvent:
+    """A HIP event for timing only: hipEventCreateWithFlags(hipEventDisableSystemFence). A
+    torch.cuda.Event record ends in a system-scope fence (cache writeback and invalidate) that left
+    the GPU idle ~5.5 us at every record, ~55 us of a cheetah plan with two records per rollout
+    (hip_runtime_api.h documents the flag for exactly this use). Same interface as torch's event
+    where bench.py and the planners use it: .cuda_event, .record(), .elapsed_time(end)."""
+    _hip = None
+
+    @classmethod
+    def _lib(cls):
+        if cls._hip is None:
+            import ctypes
+            # torch's own HIP runtime (the one its streams and our extension live in), by path
+            path = next(ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64.so" in ln)
+            lib = ctypes.CDLL(path)
+            lib.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+            lib.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+            lib.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p]
+            lib.hipEventDestroy.argtypes = [ctypes.c_void_p]
+            cls._hip = lib
+        return cls._hip
+
+    def __init__(self):
+        import ctypes
+        h = ctypes.c_void_p()
+        if self._lib().hipEventCreateWithFlags(ctypes.byref(h), 0x20000000) != 0:   # hipEventDisableSystemFence
+            raise RuntimeError("hipEventCreateWithFlags failed")
+        self.cuda_event = h.value
+
+    def record(self):
+        import ctypes
+        if self._lib().hipEventRecord(ctypes.c_void_p(self.cuda_event),
+                                      ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)) != 0:
+            raise RuntimeError("hipEventRecord failed")
+
+    def elapsed_time(self, end):
+        import ctypes
+        ms = ctypes.c_float()
+        if self._lib().hipEventElapsedTime(ctypes.byref(ms), ctypes.c_void_p(self.cuda_event),
+                                           ctypes.c_void_p(end.cuda_event)) != 0:
+            raise RuntimeError("hipEventElapsedTime failed")
+        return ms.value
+
+    def __del__(self):
+        import ctypes
+        if self._hip is not None and getattr(self, "cuda_event", None):
+            self._hip.hipEventDestroy(ctypes.c_void_p(self.cuda_event))
+
+
 def cpu_baseline(cfg_id, budget_s=20.0):
     """Time the CPU oracle (rank 0, N=1 only) on a bounded sample of the same workload."""
     from oracle import cem as ocem
@@ -213,12 +262,7 @@ def main():
         first = plan(record=True)           # also warms the weight pack / workspaces
         for _ in range(max(0, args.warmup - 1)):
             plan()
-        events = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                   for _ in range(ITERATIONS)] for _ in range(args.steps)]
-        for ev in events:          # torch creates events lazily: record once so the C ABI gets live handles
-            for s_, e_ in ev:
-                s_.record()
-                e_.record()
+        events = [[(TimingEvent(), TimingEvent()) for _ in range(ITERATIONS)] for _ in range(args.steps)]
         barrier()
         t0 = time.perf_counter()
         for k in range(args.steps):
