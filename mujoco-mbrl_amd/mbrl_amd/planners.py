@@ -221,8 +221,15 @@ class CEMPlanner(ModelPlanner):
                 if a is None:
                     a = sample_action(batch_size=1).shape[1]
                 res = _cem_generic(model, cost, s0, st, a, dev)
-            res["states"] = _to_host(res["states"], st["keep"])
-            res["actions"] = _to_host(res["actions"], st["keep"])
+            both = res.pop("_both", None)
+            if both is not None and not st["keep"]:
+                host = both.cpu()              # one device-to-host copy for states and actions
+                H, s = res["states"].shape
+                res["states"] = host[:H * s].view(H, s)
+                res["actions"] = host[H * s:].view(H, -1)
+            else:
+                res["states"] = _to_host(res["states"], st["keep"])
+                res["actions"] = _to_host(res["actions"], st["keep"])
             return res
 
 
@@ -289,8 +296,10 @@ def _cem_fused_single(prob, s0, st):
     ws = _workspace(("cem", str(dev)), need, dev)
     mu = torch.empty((H, a), dtype=torch.float32, device=dev)
     sigma = torch.empty((H, a), dtype=torch.float32, device=dev)
-    actions = torch.empty((H, a), dtype=torch.float32, device=dev)
-    states = torch.empty((H, s), dtype=torch.float32, device=dev)
+    # states and actions side by side: plan() hands both back to the host in ONE copy
+    both = torch.empty(H * (s + a), dtype=torch.float32, device=dev)
+    states = both[:H * s].view(H, s)
+    actions = both[H * s:].view(H, a)
     rec = st["record"]
     cost_hist = torch.empty((I, E, N), dtype=torch.float32, device=dev) if rec else None
     ret_hist = torch.empty((I, N), dtype=torch.float32, device=dev) if rec else None
@@ -304,7 +313,7 @@ def _cem_fused_single(prob, s0, st):
                                  _lib.ptr(sigma), _lib.ptr(actions), _lib.ptr(states), _lib.ptr(cost_hist),
                                  _lib.ptr(ret_hist), _lib.ptr(elite_hist), ev_arr, _lib.ptr(ws), ws.numel(),
                                  _lib.stream_handle(dev)), "mbrl_cem_plan")
-    out = dict(states=states, actions=actions, mu=mu, sigma=sigma)
+    out = dict(states=states, actions=actions, mu=mu, sigma=sigma, _both=both)
     if rec:
         out.update(costs=cost_hist, returns=ret_hist, elites=elite_hist)
     return out
