@@ -262,7 +262,17 @@ def main():
         first = plan(record=True)           # also warms the weight pack / workspaces
         for _ in range(max(0, args.warmup - 1)):
             plan()
-        events = [[(TimingEvent(), TimingEvent()) for _ in range(ITERATIONS)] for _ in range(args.steps)]
+        try:
+            make_event = TimingEvent
+            make_event()
+        except (StopIteration, OSError, AttributeError, RuntimeError):   # no libamdhip64 mapping found
+            def make_event():
+                return torch.cuda.Event(enable_timing=True)
+        events = [[(make_event(), make_event()) for _ in range(ITERATIONS)] for _ in range(args.steps)]
+        for ev in events:          # torch creates its events lazily: record once so the C ABI gets live handles
+            for s_, e_ in ev:
+                s_.record()
+                e_.record()
         barrier()
         t0 = time.perf_counter()
         for k in range(args.steps):
