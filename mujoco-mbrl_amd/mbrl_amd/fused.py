@@ -118,7 +118,8 @@ def describe_norm(normalize_state, normalize_action, unnormalize_state, s, a):
     if ns is False or us is False or na is False:
         return None
     obs = ns or us
-    if ns and us and not (torch.equal(ns[1].float(), us[1].float()) and torch.equal(ns[2].float(), us[2].float())):
+    if ns and us and not ((ns[1] is us[1] or torch.equal(ns[1].float(), us[1].float()))
+                          and (ns[2] is us[2] or torch.equal(ns[2].float(), us[2].float()))):
         return None  # one obs-stat pair serves both directions in the kernel
     if obs and (obs[1].numel() != s or obs[2].numel() != s):
         return None

@@ -188,7 +188,8 @@ class Model(DynamicsModel):
         self.noise = noise
 
     def linears(self):
-        return [getattr(self, f"linear{i + 1}") for i in range(self.n_hidden + 1)]
+        m = self._modules   # the registered submodules (what getattr resolves to), without its overhead
+        return [m[f"linear{i + 1}"] for i in range(self.n_hidden + 1)]
 
     def _forward(self, x):
         lins = self.linears()
@@ -244,7 +245,8 @@ class ModelWithReward(nn.Module):
 
     def linears(self):
         """Trunk layers, state head, reward head (the packing order of mbrl_mlp_pack)."""
-        return [getattr(self, f"linear{i + 1}") for i in range(self.n_hidden + 2)]
+        m = self._modules
+        return [m[f"linear{i + 1}"] for i in range(self.n_hidden + 2)]
 
     def _forward(self, x):
         lins = self.linears()
