@@ -15,8 +15,9 @@ all-gather of returns per CEM iteration. `--strong` splits the config's N over t
 
 Extra objects on the JSON line:
   roofline     -- the rollout kernel (dominant): algorithmic MLP FLOP per launch / average launch
-                  time from HIP events recorded on the launch stream around every rollout launch of
-                  the timed region; peak = fp32 MFMA dense 157.3 TFLOP/s (MI355X_MICROARCH.md).
+                  time from fence-free HIP events recorded on the launch stream around the rollout
+                  launch of CEM iteration MEASURED_IT in every timed plan (each record idles the GPU
+                  ~4 us, so not all five); peak = fp32 MFMA dense 157.3 TFLOP/s (MI355X_MICROARCH.md).
   cpu_baseline -- the CPU oracle (NumPy restatement of the reference rollout + CEM refit), rank 0,
                   N=1 only, on a bounded sample; a reported baseline, not the target.
   cpu_baseline_torch -- the reference's own CPU arrangement beside it: torch on the host with
@@ -41,6 +42,7 @@ sys.path.insert(0, REPO)
 PEAK_FP32_MFMA_TFLOPS = 157.3
 L2_STREAM_TBPS = 32.4   # tools/ubench/l2stream.hip: every CU streaming one L2-resident weight set
 ITERATIONS = 5
+MEASURED_IT = 2     # the CEM iteration whose rollout launch bench.py brackets with events
 
 
 def parse():
@@ -268,11 +270,15 @@ def main():
         except (StopIteration, OSError, AttributeError, RuntimeError):   # no libamdhip64 mapping found
             def make_event():
                 return torch.cuda.Event(enable_timing=True)
-        events = [[(make_event(), make_event()) for _ in range(ITERATIONS)] for _ in range(args.steps)]
+        # one bracketed rollout per plan (iteration MEASURED_IT of every timed plan): an event record
+        # leaves the GPU idle ~4 us, so bracketing all five would cost the plan ~40 us
+        events = [[(make_event(), make_event()) if it == MEASURED_IT else None for it in range(ITERATIONS)]
+                  for _ in range(args.steps)]
         for ev in events:          # torch creates its events lazily: record once so the C ABI gets live handles
-            for s_, e_ in ev:
-                s_.record()
-                e_.record()
+            for pair in ev:
+                if pair is not None:
+                    pair[0].record()
+                    pair[1].record()
         barrier()
         t0 = time.perf_counter()
         for k in range(args.steps):
@@ -283,7 +289,7 @@ def main():
             t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
-        rollout_ms = [s_.elapsed_time(e_) for ev in events for (s_, e_) in ev]
+        rollout_ms = [pair[0].elapsed_time(pair[1]) for ev in events for pair in ev if pair is not None]
         return elapsed, float(np.mean(rollout_ms)) / 1e3, first
 
     elapsed, avg_rollout_s, first = timed(args.precision)

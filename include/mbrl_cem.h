@@ -201,7 +201,8 @@ int mbrl_trajectory(const mbrl_mlp_shape* shape, const void* packed, const mbrl_
  * mu / sigma: [H][a] final distribution. actions_out: [H][a] = clip(mu, lo, hi);
  * states_out: [H][s] rollout of actions_out (ensemble mean over members).
  * cost_hist [I][E][N], returns_hist [I][N], elite_hist [I][K]: optional per-iteration records (NULL = off).
- * rollout_events: NULL or 2*I events; pair i brackets iteration i's rollout launch on `stream`. */
+ * rollout_events: NULL or 2*I events; pair i brackets iteration i's rollout launch on `stream`
+ * (a NULL pair skips iteration i: each record leaves the GPU idle a few microseconds). */
 size_t mbrl_cem_workspace_bytes(const mbrl_mlp_shape* shape, const mbrl_cem_params* params);
 int mbrl_cem_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_norm* norm,
                   const mbrl_cost* cost, const float* s0, const mbrl_cem_params* params,

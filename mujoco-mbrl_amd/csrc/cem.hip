@@ -1187,13 +1187,13 @@ int mbrl_cem_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_no
         float* costs = cost_hist ? cost_hist + (size_t)it * g.E * p->N : w.costs;
         int64_t* elites = elite_hist ? elite_hist + (size_t)it * p->K : w.elites;
         float* rets = returns_hist ? returns_hist + (size_t)it * p->N : nullptr;
-        if (rollout_events) {
+        if (rollout_events && rollout_events[2 * it]) {
             rc = hip_check(hipEventRecord(reinterpret_cast<hipEvent_t>(rollout_events[2 * it]), stream), "event");
             if (rc) return rc;
         }
         rc = rollout_impl(g, packed, norm, cost, s0, 0, nullptr, &sp, p->N, p->H, 0, costs, w.actions, nullptr, stream);
         if (rc) return rc;
-        if (rollout_events) {
+        if (rollout_events && rollout_events[2 * it + 1]) {
             rc = hip_check(hipEventRecord(reinterpret_cast<hipEvent_t>(rollout_events[2 * it + 1]), stream), "event");
             if (rc) return rc;
         }

@@ -307,7 +307,8 @@ def _cem_fused_single(prob, s0, st):
     events = st["events"]
     ev_arr = None
     if events is not None:
-        ev_arr = (_lib.c_void_p * (2 * I))(*[e.cuda_event for pair in events for e in pair])
+        ev_arr = (_lib.c_void_p * (2 * I))(*[(e.cuda_event if pair is not None else None)
+                                             for pair in events for e in (pair or (None, None))])
     _lib.check(lib.mbrl_cem_plan(fused.ctypes_ref(prob.shape), _lib.ptr(prob.packed), fused.ctypes_ref(prob.norm),
                                  fused.ctypes_ref(prob.cost), _lib.ptr(s0), fused.ctypes_ref(params), _lib.ptr(mu),
                                  _lib.ptr(sigma), _lib.ptr(actions), _lib.ptr(states), _lib.ptr(cost_hist),
