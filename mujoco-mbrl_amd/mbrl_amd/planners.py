@@ -294,12 +294,14 @@ def _cem_fused_single(prob, s0, st):
                             int(st["seed"]) & 0xFFFFFFFFFFFFFFFF)
     need = lib.mbrl_cem_workspace_bytes(fused.ctypes_ref(prob.shape), fused.ctypes_ref(params))
     ws = _workspace(("cem", str(dev)), need, dev)
-    mu = torch.empty((H, a), dtype=torch.float32, device=dev)
-    sigma = torch.empty((H, a), dtype=torch.float32, device=dev)
-    # states and actions side by side: plan() hands both back to the host in ONE copy
-    both = torch.empty(H * (s + a), dtype=torch.float32, device=dev)
+    # one allocation for the outputs; states and actions side by side, so that plan() hands both
+    # back to the host in ONE copy
+    buf = torch.empty(H * (s + 3 * a), dtype=torch.float32, device=dev)
+    both = buf[:H * (s + a)]
     states = both[:H * s].view(H, s)
     actions = both[H * s:].view(H, a)
+    mu = buf[H * (s + a):H * (s + 2 * a)].view(H, a)
+    sigma = buf[H * (s + 2 * a):].view(H, a)
     rec = st["record"]
     cost_hist = torch.empty((I, E, N), dtype=torch.float32, device=dev) if rec else None
     ret_hist = torch.empty((I, N), dtype=torch.float32, device=dev) if rec else None
