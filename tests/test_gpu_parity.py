@@ -488,3 +488,22 @@ def test_batched_plans_match_per_problem_oracle(cid, N, H, B):
         assert np.array_equal(actions[b].numpy(), fa), b
         _, st = ocem.rollout(p["model"], p["norm"], p["cost"], S0[b], fa[:, None, :], store_states=True)
         assert np.allclose(states[b].numpy(), np.mean(st[:, :, 0, :], axis=0), rtol=1e-4, atol=1e-4), b
+
+
+@pytest.mark.parametrize("cid,N,H,K,I", [(3, 1, 1, 1, 1), (3, 17, 3, 17, 2), (2, 33, 4, 5, 3), (5, 9, 2, 2, 2)])
+def test_cem_plan_edge_sizes_against_oracle(cid, N, H, K, I):
+    """Degenerate plans: one candidate, every candidate an elite, sizes off the 8/16 tile grid,
+    ensembles with a handful of candidates -- elites, mu, sigma and the final actions exactly as
+    the oracle's, returns within 1e-5."""
+    from mbrl_amd import CEMPlanner
+    p = ocem.synth_problem(cid, N=N, H=H)
+    _, model_fn, cost_fn, sample_action = build(p)
+    res = CEMPlanner.plan_detailed(torch.from_numpy(p["s0"]), model_fn, cost_fn, sample_action, H, num_candidates=N,
+                                   num_elites=K, num_iterations=I, seed=p["rng_seed"], record=True)
+    ref = ocem.cem_plan(p, N=N, H=H, K=K, num_iterations=I)
+    for it in range(I):
+        assert rel_err(res["returns"][it], ref["returns"][it]) < RTOL
+        assert np.array_equal(res["elites"][it].cpu().numpy(), ref["elites"][it])
+    assert np.array_equal(res["mu"].cpu().numpy(), ref["mu"][-1])
+    assert np.array_equal(res["sigma"].cpu().numpy(), ref["sigma"][-1])
+    assert np.array_equal(res["actions"].numpy(), ref["final_actions"])
