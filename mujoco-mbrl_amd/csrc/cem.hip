@@ -111,18 +111,42 @@ __global__ void pack_out_kernel(const float* __restrict__ w, const float* __rest
 // step s (4), lane l, element q: row 32 (2 pair + ((l >> 2) & 1)) + 4 (l >> 3) + (l & 3) -- the odd
 // 4-lane blocks carry the pair's second 32-row tile (ABID 1) -- and k = 16 kc + 4 q + s.
 // Hidden-type layers: chunk kc, pair = the wave's own tiles (rows 64 wave + ...).
+// KP mode (Wpad 256, one 32-row output tile; rollout.hip m8_kp): 8 waves of one tile, per chunk
+// per wave 2 loads x 64 lanes x float4; pair pi = 4 j + e, position p = 2 pi + ((l >> 2) & 1) of
+// the chunk order p = 4 s + q, row 32 wave + 4 (l >> 3) + (l & 3).
+__device__ __forceinline__ void m8kp_index(size_t i, int& lane, int& wave, size_t& chunk, int& s, int& q) {
+    const int e = (int)(i & 3);
+    lane = (int)((i >> 2) & 63);
+    const int j = (int)((i >> 8) & 1);
+    const size_t cw = i >> 9;                 // chunk * 8 + wave
+    wave = (int)(cw & 7);
+    chunk = cw >> 3;
+    const int p = 2 * (4 * j + e) + ((lane >> 2) & 1);
+    s = p >> 2;
+    q = p & 3;
+}
+
 __global__ void pack_m8_hidden_kernel(const float* __restrict__ w, int in_real, int out_real, int nkc, int T,
-                                      float* __restrict__ dst) {
+                                      int kp, float* __restrict__ dst) {
     const size_t total = (size_t)nkc * T * 1024;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-        const int q = (int)(i & 3);
-        const int lane = (int)((i >> 2) & 63);
-        const int s = (int)((i >> 8) & 3);
-        const size_t cw = i >> 10;            // kc * T + wave
-        const int wave = (int)(cw % T);
-        const int kc = (int)(cw / T);
-        const int n = 64 * wave + 32 * ((lane >> 2) & 1) + 4 * (lane >> 3) + (lane & 3);
-        const int k = 16 * kc + 4 * q + s;
+        int n, k;
+        if (kp) {
+            int lane, wave, s, q;
+            size_t kc;
+            m8kp_index(i, lane, wave, kc, s, q);
+            n = 32 * wave + 4 * (lane >> 3) + (lane & 3);
+            k = 16 * (int)kc + 4 * q + s;
+        } else {
+            const int q = (int)(i & 3);
+            const int lane = (int)((i >> 2) & 63);
+            const int s = (int)((i >> 8) & 3);
+            const size_t cw = i >> 10;            // kc * T + wave
+            const int wave = (int)(cw % T);
+            const int kc = (int)(cw / T);
+            n = 64 * wave + 32 * ((lane >> 2) & 1) + 4 * (lane >> 3) + (lane & 3);
+            k = 16 * kc + 4 * q + s;
+        }
         dst[i] = (n < out_real && k < in_real) ? w[(size_t)n * in_real + k] : 0.0f;
     }
 }
@@ -131,9 +155,18 @@ __global__ void pack_m8_hidden_kernel(const float* __restrict__ w, int in_real, 
 // holds own K chunks 2o (even blocks) and 2o + 1 (odd blocks); else chunk o = kc * NOP + pair holds
 // output tiles 2 pair (even blocks) and 2 pair + 1 (odd blocks).
 __global__ void pack_m8_out_kernel(const float* __restrict__ w, int in_real, int out_real, int NOP, int kpair,
-                                   int T, float* __restrict__ dst) {
+                                   int T, int kp, float* __restrict__ dst) {
     const size_t total = (size_t)(kpair ? 2 : 4 * NOP) * T * 1024;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        if (kp) {   // own K chunk o of the wave's 32 features, one 32-row output tile
+            int lane, wave, s, q;
+            size_t o;
+            m8kp_index(i, lane, wave, o, s, q);
+            const int n = 4 * (lane >> 3) + (lane & 3);
+            const int k = 32 * wave + 16 * (int)o + 4 * q + s;
+            dst[i] = (n < out_real && k < in_real) ? w[(size_t)n * in_real + k] : 0.0f;
+            continue;
+        }
         const int q = (int)(i & 3);
         const int lane = (int)((i >> 2) & 63);
         const int s = (int)((i >> 8) & 3);
@@ -1004,7 +1037,7 @@ int mbrl_mlp_pack(const mbrl_mlp_shape* shape, const float* const* weights, cons
                 }
                 if (g.m8_ok) {
                     hipLaunchKernelGGL(pack_m8_hidden_kernel, dim3(256), dim3(256), 0, stream, w, in_real, g.W, nkc,
-                                       g.T, m8_base + m8_chunk * 1024 * (size_t)g.T);
+                                       g.T, (int)(g.T == 4 && g.NOT == 2), m8_base + m8_chunk * 1024 * (size_t)g.T);
                     m8_chunk += nkc;
                 }
                 chunk += nkc;
@@ -1020,6 +1053,7 @@ int mbrl_mlp_pack(const mbrl_mlp_shape* shape, const float* const* weights, cons
                                            split_bad[P - 2]);
                 if (g.m8_ok)
                     hipLaunchKernelGGL(pack_m8_out_kernel, dim3(256), dim3(256), 0, stream, w, g.W, g.s, g.NOP8, g.NOC8 == 2, g.T,
+                                       (int)(g.T == 4 && g.NOT == 2),
                                        m8_base + m8_chunk * 1024 * (size_t)g.T);
                 float* ob = bias_base + (size_t)g.L * g.Wpad;
                 hipLaunchKernelGGL(pack_bias_kernel, dim3(1), dim3(256), 0, stream, b, g.s, 16 * g.NOT, ob);

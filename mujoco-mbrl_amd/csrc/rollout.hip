@@ -633,15 +633,27 @@ hipError_t launch_rollout(const RolloutArgs& A, int T, int R, hipStream_t stream
 // does not depend on which tile height its shard size picked. The output layer mirrors the 8-wave
 // kernel's K split (one partial per 16 T/2 features, four chains (c0 + c1) + (c2 + c3)) and its
 // epilogue, operation for operation.
-// Wave w owns hidden features [64 w, 64 w + 64) (two 32-row tiles); T = Wpad / 64 waves.
+// Wave w owns hidden features [64 w, 64 w + 64) (two 32-row tiles); T = Wpad / 64 waves. In KP mode
+// (below) wave w owns [32 w, 32 w + 32) of 8 waves.
 // Weight stream (packed by pack_m8_*_kernel in cem.hip): per 16-deep chunk, per wave, 4 x 64 lanes
 // x float4 (load s holds q = 0..3); chunks per step = K0C + (L-1) 4T + NOC (output: 2 K-chunk pairs
 // of the one 32-row tile, or own 4 K chunks x 2-tile pairs), plus DUM ring-alignment slots that
 // reload the last chunk (L2 hits; none for the BASELINE shapes).
+// KP mode (Wpad 256 with one 32-row output tile, e.g. cartpole): 8 waves of ONE 32-row tile each,
+// so two waves share every SIMD, and a weight register carries two consecutive k of that tile
+// (even blocks position 2i, odd blocks 2i + 1 of the chunk's order; ABID 0 / 1). Otherwise wave w
+// owns two tiles (ABID 0 / 1) and T = Wpad / 64 waves run (one per SIMD at Wpad 256).
+constexpr bool m8_kp(int T, int NOT) { return T == 4 && NOT == 2; }
+constexpr int m8_waves(int T, int NOT) { return m8_kp(T, NOT) ? 8 : T; }
+
 template <int T, int K0C_T, int NOT_T>
-__global__ void __launch_bounds__(64 * T, 1) rollout_m8_kernel(const RolloutArgs A) {
+__global__ void __launch_bounds__(64 * m8_waves(T, NOT_T), 1) rollout_m8_kernel(const RolloutArgs A) {
     constexpr int M = 8;
-    constexpr int NW = T;
+    constexpr bool KP = m8_kp(T, NOT_T);
+    constexpr int NW = m8_waves(T, NOT_T);
+    constexpr int TPW = KP ? 1 : 2;          // 32-row tiles per wave
+    constexpr int FPW = 32 * TPW;            // hidden features per wave
+    constexpr int RSL = KP ? 2 : 4;          // float4 loads per lane per ring slot
     constexpr int NT = 64 * NW;
     constexpr int KH = 4 * T;
     constexpr int NOT8 = NOT_T / 2;          // 32-row output tiles
@@ -657,7 +669,7 @@ __global__ void __launch_bounds__(64 * T, 1) rollout_m8_kernel(const RolloutArgs
 #endif                                       // (walker 2048-candidate shard, tools/ab.sh, r01)
     constexpr int DUM = (NB - (K0C_T + NOC) % NB) % NB;
     constexpr int TW16 = T / 2;              // the 16-candidate kernel's K chunks per output partial
-    constexpr int NPW = 4 / TW16;            // its partials inside this wave's 4 own chunks
+    constexpr int NPW = (FPW / 16) / TW16;   // its partials inside this wave's own chunks
     constexpr int SS = NOT_T;
     static_assert(KH % NB == 0 && (T == 4 || T == 8), "m8 geometry");
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -720,22 +732,22 @@ __global__ void __launch_bounds__(64 * T, 1) rollout_m8_kernel(const RolloutArgs
     const int CSQ = C8 + DUM;
     const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(member + A.m8_off), 0, (int)((size_t)C8 * 4096 * T), 0x00020000);
-    const unsigned lane_off = (unsigned)(wave * 4096 + lane * 16);
-    f32x4 ring[NB][4];
+    const unsigned lane_off = (unsigned)(wave * RSL * 1024 + lane * 16);
+    f32x4 ring[NB][RSL];
 #define M8_LOAD(SLOT, G)                                                                          \
     do {                                                                                          \
         int gg_ = (G);                                                                            \
         if (gg_ >= CSQ) gg_ -= CSQ;                                                               \
         gg_ = gg_ < C8 ? gg_ : C8 - 1;                                                            \
         const int so_ = gg_ * (4096 * T);                                                         \
-        _Pragma("unroll") for (int s_ = 0; s_ < 4; ++s_) ring[SLOT][s_] = __builtin_bit_cast(     \
+        _Pragma("unroll") for (int s_ = 0; s_ < RSL; ++s_) ring[SLOT][s_] = __builtin_bit_cast(   \
             f32x4, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, lane_off + s_ * 1024, so_, 0));   \
     } while (0)
 #pragma unroll
     for (int q = 0; q < NB - 1; ++q) M8_LOAD(q, q);
     f32x4 bb[2][4];     // B: X[cand][16 kc + 4 q' .. +3], double-buffered over chunks
-    f32x4 acc[2];
-    f32x4 bias[2];
+    f32x4 acc[TPW];
+    f32x4 bias[TPW];
     float total = 0.f;
 #ifdef MBRL_STAMPS
     unsigned long long seg[NSEG] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -746,27 +758,42 @@ __global__ void __launch_bounds__(64 * T, 1) rollout_m8_kernel(const RolloutArgs
 #pragma unroll
         for (int q = 0; q < 4; ++q) b[q] = *reinterpret_cast<const f32x4*>(in + cand * A.lda + col + 4 * q);
     };
-    auto mma_pair = [&](const f32x4 (&w)[4], const f32x4 (&b)[4]) {
+    auto mma_pair = [&](const f32x4 (&w)[RSL], const f32x4 (&b)[4]) {
+        if constexpr (KP) {
+            // pair i: chunk positions 2i (ABID 0) and 2i + 1 (ABID 1), position p = 4 s + q
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                acc[0] = __builtin_amdgcn_mfma_f32_4x4x1f32(w[s][q], b[q][s], acc[0], 1, 0, 0);
-                acc[1] = __builtin_amdgcn_mfma_f32_4x4x1f32(w[s][q], b[q][s], acc[1], 1, 1, 0);
+            for (int i = 0; i < 8; ++i) {
+                const float a = w[i >> 2][i & 3];
+                acc[0] = __builtin_amdgcn_mfma_f32_4x4x1f32(a, b[(2 * i) & 3][(2 * i) >> 2], acc[0], 1, 0, 0);
+                acc[0] = __builtin_amdgcn_mfma_f32_4x4x1f32(a, b[(2 * i + 1) & 3][(2 * i + 1) >> 2], acc[0], 1, 1, 0);
             }
+        } else {
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    acc[0] = __builtin_amdgcn_mfma_f32_4x4x1f32(w[s][q], b[q][s], acc[0], 1, 0, 0);
+                    acc[TPW - 1] = __builtin_amdgcn_mfma_f32_4x4x1f32(w[s][q], b[q][s], acc[TPW - 1], 1, 1, 0);
+                }
+        }
     };
     auto store_layer = [&](float* out) {
         const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < TPW; ++u) {
             f32x4 v = acc[u] + bias[u];
             v = __builtin_elementwise_max(v, zero);
-            *reinterpret_cast<f32x4*>(out + cand * A.lda + 64 * wave + 32 * u + 4 * (lane >> 3)) = v;
+            *reinterpret_cast<f32x4*>(out + cand * A.lda + FPW * wave + 32 * u + 4 * (lane >> 3)) = v;
         }
     };
     auto load_bias8 = [&](const float* hb) {
 #pragma unroll
-        for (int u = 0; u < 2; ++u) bias[u] = *reinterpret_cast<const f32x4*>(hb + 64 * wave + 32 * u + 4 * (lane >> 3));
+        for (int u = 0; u < TPW; ++u)
+            bias[u] = *reinterpret_cast<const f32x4*>(hb + FPW * wave + 32 * u + 4 * (lane >> 3));
+    };
+    auto zero_acc8 = [&]() {
+#pragma unroll
+        for (int u = 0; u < TPW; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
     };
 // one hidden-type chunk: refill the slot chunk c-1 vacated, read the next chunk's B, MFMAs of chunk c
 #define M8_CHUNK(SLOT, KC, NK, IN)                                          \
@@ -782,7 +809,7 @@ __global__ void __launch_bounds__(64 * T, 1) rollout_m8_kernel(const RolloutArgs
         int g = 0;
         if (actw && t + 1 < A.H) fetch_a(t + 1);
         // ---- layer 0: actX [s | a | 0-pad] -> actY
-        acc[0] = acc[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+        zero_acc8();
         load_bias8(L.hbias);
         read_b(bb[0], actX, 0);
 #pragma unroll
@@ -794,7 +821,7 @@ __global__ void __launch_bounds__(64 * T, 1) rollout_m8_kernel(const RolloutArgs
         float* in = actY;
         float* out = actX;
         for (int l = 1; l < A.L; ++l) {
-            acc[0] = acc[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+            zero_acc8();
             load_bias8(L.hbias + l * A.Wpad);
             read_b(bb[0], in, 0);
 #pragma unroll
@@ -814,12 +841,33 @@ __global__ void __launch_bounds__(64 * T, 1) rollout_m8_kernel(const RolloutArgs
                 for (int u = 0; u < NOT8; ++u)
 #pragma unroll
                     for (int s = 0; s < 4; ++s) ch[j][u][s] = f32x4{0.f, 0.f, 0.f, 0.f};
-            if constexpr (KPAIR) {
+            if constexpr (KP) {
+                // own 32 features = two K chunks, each a chunk of k pairs; chain s takes the pairs
+                // whose positions carry step s (both positions of pair i do: s = i >> 1)
+#pragma unroll
+                for (int o = 0; o < 2; ++o) {
+                    f32x4 b[4];
+                    read_b(b, in, 32 * wave + 16 * o);
+                    constexpr int base = K0C_T;
+                    M8_LOAD((base + o + NB - 1) % NB, g + NB - 1);
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        const float a = ring[(base + o) % NB][i >> 2][i & 3];
+                        const int sc = i >> 1;
+                        ch[0][0][sc] = __builtin_amdgcn_mfma_f32_4x4x1f32(a, b[(2 * i) & 3][(2 * i) >> 2], ch[0][0][sc],
+                                                                          1, 0, 0);
+                        ch[0][0][sc] = __builtin_amdgcn_mfma_f32_4x4x1f32(a, b[(2 * i + 1) & 3][(2 * i + 1) >> 2],
+                                                                          ch[0][0][sc], 1, 1, 0);
+                    }
+                    MBRL_PIN();
+                    ++g;
+                }
+            } else if constexpr (KPAIR) {
 #pragma unroll
                 for (int o = 0; o < 2; ++o) {
                     f32x4 b0[4], b1[4];
-                    read_b(b0, in, 64 * wave + 32 * o);
-                    read_b(b1, in, 64 * wave + 32 * o + 16);
+                    read_b(b0, in, FPW * wave + 32 * o);
+                    read_b(b1, in, FPW * wave + 32 * o + 16);
                     constexpr int base = K0C_T;
                     M8_LOAD((base + o + NB - 1) % NB, g + NB - 1);
                     const int j0 = (2 * o) / TW16, j1 = (2 * o + 1) / TW16;
@@ -843,7 +891,7 @@ __global__ void __launch_bounds__(64 * T, 1) rollout_m8_kernel(const RolloutArgs
 #pragma unroll
             for (int kc = 0; kc < 4; ++kc) {
                 f32x4 b[4];
-                read_b(b, in, 64 * wave + 16 * kc);
+                read_b(b, in, FPW * wave + 16 * kc);
 #pragma unroll
                 for (int p = 0; p < NOP; ++p) {
                     constexpr int base = K0C_T;   // slots fold: kc, p are unrolled
@@ -947,7 +995,7 @@ static hipError_t launch_m8_tr(const RolloutArgs& A_in, hipStream_t stream) {
     const size_t lds = rollout_lds_bytes(A, 8);
     hipError_t e = ensure_dynamic_lds(reinterpret_cast<const void*>(&rollout_m8_kernel<T, K0C_T, NOT_T>), 160 * 1024);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((rollout_m8_kernel<T, K0C_T, NOT_T>), grid, dim3(64 * T), lds, stream, A);
+    hipLaunchKernelGGL((rollout_m8_kernel<T, K0C_T, NOT_T>), grid, dim3(64 * m8_waves(T, NOT_T)), lds, stream, A);
     return hipGetLastError();
 }
 
