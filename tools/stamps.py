@@ -49,6 +49,13 @@ def main():
         fused.rollout(p, s0, N, H, sampler=fused.make_sampler(1, 0, mu, sg, -1, 1), actions_out=acts)
     torch.cuda.synchronize()
     st = buf.view(E * tiles * NWMAX, NSEG).cpu().numpy().astype(np.float64)
+    if os.environ.get("MBRL_STAMPS_BY_WAVE"):      # per wave slot: waves 0-3 state epilogue, 4-7 actions
+        byw = st.reshape(-1, NWMAX, NSEG)
+        for w in range(NWMAX):
+            sw = byw[:, w, :]
+            sw = sw[sw.sum(1) > 0]
+            if len(sw):
+                print(f"  wave {w}: " + " ".join(f"{v / H:8.0f}" for v in sw[:, :7].mean(0)))
     st = st[st.sum(1) > 0]
     ghz = st[:, :7].sum(1).mean() / (st[:, 7].mean() * 10.0)
     per_step = st[:, :7].mean(0) / H
