@@ -42,6 +42,11 @@
 #ifndef MBRL_GLOBAL_LOAD
 #define MBRL_BUFFER_LOAD 1
 #endif
+// State slots per lane (ceil(s / 16)) up to which the 8/16-candidate epilogues keep their per-lane
+// parameter copies in registers; wider states read them from LDS (the copies spilled on humanoid).
+#ifndef MBRL_EPI_REG_SLOTS
+#define MBRL_EPI_REG_SLOTS 2
+#endif
 
 namespace mbrl {
 
@@ -535,10 +540,17 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
                     if (A.states_out != nullptr && n < A.N)
                         A.states_out[(((size_t)e * A.H + t) * A.N + n) * A.s + d] = sn;
                 };
-                if constexpr (RING) {
+                if constexpr (RING && SS <= MBRL_EPI_REG_SLOTS) {
 #pragma unroll
                     for (int k = 0; k < SS; ++k)
                         if (j + 16 * k < A.s) slot(j + 16 * k, P.om[k], P.os[k], P.goal[k], P.cw[k], P.bo[k]);
+                } else if constexpr (RING) {
+                    // wide states: the 5 SS per-lane copies would spill; same values from LDS, same order
+#pragma unroll
+                    for (int k = 0; k < SS; ++k) {
+                        const int d = j + 16 * k;
+                        if (d < A.s) slot(d, L.obs_mean[d], L.obs_std[d], L.goal[d], L.cw[d], bout[d]);
+                    }
                 } else {
                     for (int d = j; d < A.s; d += 16)
                         slot(d, L.obs_mean[d], L.obs_std[d], L.goal[d], L.cw[d], bout[d]);
