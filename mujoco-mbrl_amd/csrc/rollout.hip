@@ -244,7 +244,7 @@ __device__ __forceinline__ void load_epi_params(const RolloutArgs& A, const LdsM
 
 // a_t -> normalised MLP input columns [s, s+a); returns this lane's share of sum_d (cosh(a_d/alpha)-1).
 template <int R, int SS>
-__device__ __forceinline__ void stage_actions(const RolloutArgs& A, const EpiParams<SS>& P, float* act, float* asave,
+__device__ __forceinline__ void stage_actions(const RolloutArgs& A, const EpiParams<SS>& P, const LdsMap& L, float* act,
                                               int wave, int lane, const float (&av)[R][MAX_A_PER_LANE],
                                               float (&acp)[R]) {
 #pragma unroll
@@ -256,9 +256,12 @@ __device__ __forceinline__ void stage_actions(const RolloutArgs& A, const EpiPar
             const int d = (lane & 15) + 16 * k;
             if (d < A.a) {
                 const float x = av[r][k];
-                const float xn = A.norm_a ? (x - P.am[k]) / P.as[k] : x;
+                // wide states keep no per-lane copies (see MBRL_EPI_REG_SLOTS): same values from LDS
+                const float am = SS <= MBRL_EPI_REG_SLOTS ? P.am[k] : L.act_mean[d];
+                const float as = SS <= MBRL_EPI_REG_SLOTS ? P.as[k] : L.act_std[d];
+                const float xn = A.norm_a ? (x - am) / as : x;
                 act[m * A.lda + A.s + d] = xn;
-                if (A.reward) asave[m * A.a + d] = xn;   // the state pass re-reads a_t
+                if (A.reward) L.aterm[m * A.a + d] = xn;   // the state pass re-reads a_t
                 if (A.has_ac) c += coshf(x / A.alpha_a) - 1.0f;
             }
         }
@@ -338,7 +341,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
     EpiParams<SS> P;
     load_epi_params<SS>(A, L, lane, P);
     if (actw) {
-        stage_actions<R, SS>(A, P, actX, L.aterm, awave, lane, av, acp);
+        stage_actions<R, SS>(A, P, L, actX, awave, lane, av, acp);
         if (split)
 #pragma unroll
             for (int r = 0; r < R; ++r) {
@@ -514,7 +517,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
                     total[r] += rowsum16(rc);
                 }
             }
-            if (pass == 1 && t + 1 < A.H) stage_actions<R, SS>(A, P, actX, L.aterm, wave, lane, av, acp);
+            if (pass == 1 && t + 1 < A.H) stage_actions<R, SS>(A, P, L, actX, wave, lane, av, acp);
         } else if (epi) {
             const float* bout = L.hbias + A.L * A.Wpad;
             const int ws = M * A.pw;
@@ -560,10 +563,10 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
                 const float ac = split ? acs[(t & 1) * M + m] : rowsum16(acp[r]);
                 total[r] += sc + A.alpha_a2 * (ac / (float)A.a);
             }
-            if (!split && t + 1 < A.H) stage_actions<R, SS>(A, P, actX, L.aterm, wave, lane, av, acp);
+            if (!split && t + 1 < A.H) stage_actions<R, SS>(A, P, L, actX, wave, lane, av, acp);
         } else if (split && actw && t + 1 < A.H) {
             // waves 4-7, concurrently: a_{t+1} into the next MLP input, its CoshLoss row sum into LDS
-            stage_actions<R, SS>(A, P, actX, L.aterm, awave, lane, av, acp);
+            stage_actions<R, SS>(A, P, L, actX, awave, lane, av, acp);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const float v = rowsum16(acp[r]);
@@ -733,7 +736,7 @@ __global__ void __launch_bounds__(64 * m8_waves(T, NOT_T), 1) rollout_m8_kernel(
     EpiParams<SS> P;
     load_epi_params<SS>(A, L, lane, P);
     if (actw) {
-        stage_actions<1, SS>(A, P, actX, L.aterm, awave, lane, av, acp);
+        stage_actions<1, SS>(A, P, L, actX, awave, lane, av, acp);
         const float v = rowsum16(acp[0]);
         if ((lane & 15) == 0) acs[epi_row(0, awave, lane)] = v;
     }
@@ -970,7 +973,7 @@ __global__ void __launch_bounds__(64 * m8_waves(T, NOT_T), 1) rollout_m8_kernel(
             const float ac = acs[(t & 1) * M + m];
             total += sc + A.alpha_a2 * (ac / (float)A.a);
         } else if (actw && t + 1 < A.H) {
-            stage_actions<1, SS>(A, P, actX, L.aterm, awave, lane, av, acp);
+            stage_actions<1, SS>(A, P, L, actX, awave, lane, av, acp);
             const float v = rowsum16(acp[0]);
             if ((lane & 15) == 0) acs[((t + 1) & 1) * M + epi_row(0, awave, lane)] = v;
         }
