@@ -4,6 +4,10 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
+`--gpus N` without a launcher (no WORLD_SIZE in the environment) starts the N rank processes itself
+(one per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, 127.0.0.1) before this process touches
+the GPU, waits for them and exits with their status; rank 0 prints the line.
+
 A "step" is one CEMPlanner.plan() call (I iterations of proposal draw -> rollout ->
 elite top-K -> refit, plus the final mean's rollout) on the cheetah-run config (BASELINE.json
 configs[2]: N=4096, H=30, 17/6, 3x512 MLP, I=5, K=N/10) with synthetic random weights.
@@ -23,6 +27,9 @@ Extra objects on the JSON line:
   cpu_baseline_torch -- the reference's own CPU arrangement beside it: torch on the host with
                   autograd on (planners.py:199-210), NumPy refit; same conditions.
   parity       -- iteration-0 returns of 256 sampled candidates re-computed by the CPU oracle.
+  strong       -- BASELINE.json configs[3]: walker-walk N=16384 H=30 split over the ranks (strong
+                  scaling, N/G candidates per GPU), same timing rules; at N=1 the single-GPU plan the
+                  split is measured against.
   variants     -- the same workload timed with the other rollout precisions (default headline: exact
                   fp32; variants: f16x6 and f16x3, fp32 emulated on the f16 matrix cores).
 """
@@ -64,7 +71,45 @@ def parse():
                     help="strong scaling: the config's N split over the GPUs (default weak: N per GPU)")
     ap.add_argument("--traffic-bytes", type=float, default=None,
                     help="HBM bytes per rollout launch from a rocprofv3 PMC pass (profiles/)")
+    ap.add_argument("--no-strong", action="store_true",
+                    help="skip the strong-scaling walker object (BASELINE.json configs[3])")
     return ap.parse_args()
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n, script=None, argv=None):
+    """`bench.py --gpus N` run directly: start N rank processes (this same script, its argv) and wait.
+    Nothing here touches the GPU (no torch.cuda call at all), so the children are plain fresh
+    processes; if one fails the others are stopped and its exit status is returned."""
+    import subprocess
+    port = str(_free_port())
+    script = os.path.abspath(__file__) if script is None else script
+    argv = sys.argv[1:] if argv is None else argv
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, script] + list(argv), env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for pr in list(live):
+            code = pr.poll()
+            if code is None:
+                continue
+            live.remove(pr)
+            if code != 0 and rc == 0:
+                rc = code
+                for other in live:
+                    other.terminate()
+        time.sleep(0.05)
+    return rc
 
 
 class TimingEvent:
@@ -116,38 +161,70 @@ class TimingEvent:
             self._hip.hipEventDestroy(ctypes.c_void_p(self.cuda_event))
 
 
-def cpu_baseline(cfg_id, budget_s=20.0):
-    """Time the CPU oracle (rank 0, N=1 only) on a bounded sample of the same workload."""
-    from oracle import cem as ocem
+def host_cores():
+    """(cores used, how they were counted): the CPUs this process may run on
+    (len(os.sched_getaffinity(0))), capped by the cgroup CPU quota when one is set
+    (cpu.max / cfs_quota_us) -- threads beyond the quota only get throttled."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
     try:
-        from threadpoolctl import threadpool_info
-        cores = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
-    except Exception:  # pragma: no cover
-        cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    p = ocem.synth_problem(cfg_id)
-    cfg = p["cfg"]
-    N, H = cfg["N"], cfg["H"]
-    # sample: whole CEM plans at the full N and H while they fit the budget, else fewer candidates
-    t0 = time.perf_counter()
-    ocem.cem_plan(p, num_iterations=1, record=False)
-    one_iter = time.perf_counter() - t0
-    n_sample = N if one_iter * ITERATIONS <= budget_s else max(64, int(N * budget_s / (one_iter * ITERATIONS)))
-    plans, elapsed = 0, 0.0
-    while elapsed < budget_s / 2 and plans < 10:
-        t0 = time.perf_counter()
-        ocem.cem_plan(p, N=n_sample, num_iterations=ITERATIONS, record=False)
-        elapsed += time.perf_counter() - t0
-        plans += 1
-    value = ITERATIONS * n_sample * H * plans / elapsed
-    cpu = "unknown"
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(period)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            period = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / period
+        except (OSError, ValueError):
+            pass
+    cores = aff if quota is None else max(1, min(aff, int(quota + 0.5)))
+    how = f"sched_getaffinity {aff}" + ("" if quota is None else f", cgroup quota {quota:g} CPUs")
+    return cores, how
+
+
+def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
             if line.startswith("model name"):
-                cpu = line.split(":", 1)[1].strip()
-                break
+                return line.split(":", 1)[1].strip()
     except OSError:  # pragma: no cover
         pass
-    return dict(value=value, unit="candidate-timesteps/s", cores=int(cores), kind="port", cpu=cpu,
+    return "unknown"
+
+
+def cpu_baseline(cfg_id, budget_s=20.0):
+    """Time the CPU oracle (rank 0, N=1 only) on a bounded sample of the same workload, with its BLAS
+    on every core this process may use (host_cores)."""
+    from oracle import cem as ocem
+    cores, how = host_cores()
+    try:
+        from threadpoolctl import threadpool_limits
+        limiter = threadpool_limits(limits=cores)
+    except Exception:  # pragma: no cover
+        limiter = None
+    try:
+        p = ocem.synth_problem(cfg_id)
+        cfg = p["cfg"]
+        N, H = cfg["N"], cfg["H"]
+        # sample: whole CEM plans at the full N and H while they fit the budget, else fewer candidates
+        t0 = time.perf_counter()
+        ocem.cem_plan(p, num_iterations=1, record=False)
+        one_iter = time.perf_counter() - t0
+        n_sample = N if one_iter * ITERATIONS <= budget_s else max(64, int(N * budget_s / (one_iter * ITERATIONS)))
+        plans, elapsed = 0, 0.0
+        while elapsed < budget_s / 2 and plans < 10:
+            t0 = time.perf_counter()
+            ocem.cem_plan(p, N=n_sample, num_iterations=ITERATIONS, record=False)
+            elapsed += time.perf_counter() - t0
+            plans += 1
+    finally:
+        if limiter is not None:
+            limiter.unregister()
+    value = ITERATIONS * n_sample * H * plans / elapsed
+    return dict(value=value, unit="candidate-timesteps/s", cores=int(cores), cores_counted=how, kind="port",
+                cpu=_cpu_model(),
                 sample=f"{plans} full CEM plan(s) (I={ITERATIONS}, N={n_sample}, H={H}) of the NumPy oracle "
                        f"(oracle/cem.py), fp32, {elapsed:.1f} s")
 
@@ -157,10 +234,13 @@ def cpu_torch_baseline(prob, budget_s=20.0):
     autograd ON, as RandomShootingPlanner._generate_trajectories runs it (planners.py:199-210: H
     model calls writing state_list slices, then one cost call, view(H, N).sum(0)); the model is
     mbrl_amd.models on CPU (the reference's DynamicsModel math). CEM proposal / select / refit in
-    NumPy (stable argsort, population variance). A bounded sample of the same workload."""
+    NumPy (stable argsort, population variance). A bounded sample of the same workload, on every core
+    this process may use (host_cores), and the same again under torch.no_grad() (labelled
+    value_no_grad; the reference never disables autograd)."""
     cfg = prob["cfg"]
     N, H, a, s = cfg["N"], cfg["H"], cfg["a"], cfg["s"]
-    threads = min(16, len(os.sched_getaffinity(0)))
+    threads, how = host_cores()
+    prev_threads = torch.get_num_threads()
     torch.set_num_threads(threads)
     rng = np.random.default_rng(0)
     model, cost = prob["model"], prob["cost"]
@@ -183,20 +263,30 @@ def cpu_torch_baseline(prob, budget_s=20.0):
             sg = np.sqrt(0.1 * sg * sg + 0.9 * el.var(axis=1)).astype(np.float32)
         return mu
 
-    t0 = time.perf_counter()
-    plan(max(64, N // 16))
-    probe = (time.perf_counter() - t0) * 16
-    n_sample = N if probe <= budget_s / 2 else max(64, int(N * budget_s / 2 / probe))
-    plans, elapsed = 0, 0.0
-    while elapsed < budget_s / 2 and plans < 10:
+    def measure(budget):
         t0 = time.perf_counter()
-        plan(n_sample)
-        elapsed += time.perf_counter() - t0
-        plans += 1
-    return dict(value=ITERATIONS * n_sample * H * plans / elapsed, unit="candidate-timesteps/s", cores=threads,
-                kind="port", autograd=True,
+        plan(max(64, N // 16))
+        probe = (time.perf_counter() - t0) * 16
+        n_sample = N if probe <= budget else max(64, int(N * budget / probe))
+        plans, elapsed = 0, 0.0
+        while elapsed < budget and plans < 10:
+            t0 = time.perf_counter()
+            plan(n_sample)
+            elapsed += time.perf_counter() - t0
+            plans += 1
+        return ITERATIONS * n_sample * H * plans / elapsed, n_sample, plans, elapsed
+
+    try:
+        v, n_sample, plans, elapsed = measure(budget_s / 2)
+        with torch.no_grad():
+            v_ng, n_ng, plans_ng, el_ng = measure(budget_s / 4)
+    finally:
+        torch.set_num_threads(prev_threads)
+    return dict(value=v, unit="candidate-timesteps/s", cores=threads, cores_counted=how, kind="port",
+                autograd=True, value_no_grad=v_ng, cpu=_cpu_model(),
                 sample=f"{plans} CEM plan(s) (I={ITERATIONS}, N={n_sample}, H={H}): torch on the host, autograd on, "
-                       f"the reference's _generate_trajectories loop + NumPy refit, {elapsed:.1f} s")
+                       f"the reference's _generate_trajectories loop + NumPy refit, {elapsed:.1f} s; "
+                       f"value_no_grad: {plans_ng} plan(s) at N={n_ng} under torch.no_grad(), {el_ng:.1f} s")
 
 
 def parity_sample(prob, res, n=256):
@@ -216,7 +306,11 @@ def parity_sample(prob, res, n=256):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     # one GPU per rank; on a box with fewer GPUs than ranks (a gloo rehearsal, MBRL_DIST_BACKEND=gloo)
@@ -232,6 +326,7 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
 
     from mbrl_amd import CEMPlanner, synthetic
     prob = synthetic.make_problem(args.config)
@@ -255,12 +350,15 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(dev)
 
-    def timed(precision):
+    def timed(precision, problem=None, plan_kw=None):
         """W warm-up plans, then K timed plans between barriers; (max-over-ranks seconds, mean rollout
         launch seconds from HIP events on the launch stream, the first plan's record)."""
+        pr = prob if problem is None else problem
+        pkw = kw if plan_kw is None else plan_kw
+
         def plan(**extra):
-            return CEMPlanner.plan_detailed(prob["s0"], prob["model"], prob["cost"], prob["sample_action"], H,
-                                            **dict(kw, precision=precision), **extra)
+            return CEMPlanner.plan_detailed(pr["s0"], pr["model"], pr["cost"], pr["sample_action"], pr["cfg"]["H"],
+                                            **dict(pkw, precision=precision), **extra)
         first = plan(record=True)           # also warms the weight pack / workspaces
         for _ in range(max(0, args.warmup - 1)):
             plan()
@@ -286,7 +384,8 @@ def main():
         barrier()
         elapsed = time.perf_counter() - t0
         if dist is not None:
-            t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+            t = torch.tensor([elapsed], dtype=torch.float64,
+                             device="cpu" if dist.get_backend() == "gloo" else dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
         rollout_ms = [pair[0].elapsed_time(pair[1]) for ev in events for pair in ev if pair is not None]
@@ -323,6 +422,8 @@ def main():
                                f"{cfg['L']}x{cfg['W']} MLP E={E} I={ITERATIONS} K={K}",
                    "candidates_per_gpu": n_local, "horizon": H, "iterations": ITERATIONS, "elites": K,
                    "parallelism": f"candidates sharded x{world}" if world > 1 else "single GPU",
+                   "world_size": world,
+                   "backend": (dist.get_backend() if dist is not None else None),
                    "precision": args.precision},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / PEAK_FP32_MFMA_TFLOPS, "traffic": traffic,
@@ -363,6 +464,23 @@ def main():
             if rank == 0 and world == 1 and not args.no_cpu_baseline:
                 var["parity"] = parity_sample(prob, v_first)
             out["variants"].append(var)
+    if not args.no_strong and not args.strong:
+        # BASELINE.json configs[3]: walker-walk N=16384 H=30 split over the ranks (strong scaling)
+        wprob = synthetic.make_problem(4)
+        wcfg = wprob["cfg"]
+        Nw = wcfg["N"]
+        if Nw % world == 0:
+            wkw = dict(num_candidates=Nw, num_elites=Nw // 10, num_iterations=ITERATIONS, alpha=0.1,
+                       seed=wprob["rng_seed"], distributed=world > 1, device=dev)
+            w_elapsed, w_rollout_s, _ = timed("f32", wprob, wkw)
+            w_flop = Nw // world * wcfg["H"] * synthetic.flop_per_candidate_step(wcfg)
+            out["strong"] = dict(
+                workload=f"{wcfg['name']} CEM N={Nw} H={wcfg['H']} s={wcfg['s']} a={wcfg['a']} "
+                         f"{wcfg['L']}x{wcfg['W']} MLP I={ITERATIONS} K={Nw // 10} (BASELINE.json configs[3])",
+                scaling="strong", candidates_per_gpu=Nw // world, n_gpus=world,
+                value=ITERATIONS * Nw * wcfg["H"] * args.steps / w_elapsed, unit="candidate-timesteps/s",
+                ms_per_step=w_elapsed / args.steps * 1e3, rollout_avg_launch_ms=w_rollout_s * 1e3,
+                rollout_frac=w_flop / w_rollout_s / 1e12 / PEAK_FP32_MFMA_TFLOPS)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.config, budget_s=args.cpu_budget)
         out["cpu_baseline_torch"] = cpu_torch_baseline(prob, budget_s=args.cpu_budget)

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MBRL_ABI_VERSION 3
+#define MBRL_ABI_VERSION 4
 
 typedef struct ihipStream_t* mbrl_stream_t; /* == hipStream_t */
 typedef struct ihipEvent_t* mbrl_event_t;   /* == hipEvent_t  */
@@ -141,6 +141,21 @@ typedef struct {
 
 int mbrl_abi_version(void);
 const char* mbrl_last_error(void);
+
+/* ---- process-wide switches for A/B runs and for tests that force a fallback. Every option starts
+ * at 0 (automatic choice); the library never reads them from the environment, so a production launch
+ * cannot be redirected by a stray variable. mbrl_set_option returns the previous value, or
+ * MBRL_EINVAL for an unknown option or value. Not part of any reference interface. */
+enum {
+    MBRL_OPT_ROLLOUT_TILE = 0,      /* fp32 rollout candidates per workgroup: 0 auto, 8, 16 (16 R)   */
+    MBRL_OPT_SPLIT_TILE = 1,        /* F16X3 / F16X6 rollout candidates per workgroup: 0 auto, 16, 32 */
+    MBRL_OPT_DEBUG_TRAJ_ABORT = 2,  /* 1: the cooperative trajectory kernel gives up at once          */
+    MBRL_OPT_GD_SINGLE = 3,         /* 1: mbrl_gd_plan runs its one-workgroup kernel                  */
+    MBRL_OPT_DEBUG_GD_ABORT = 4,    /* 1: the cooperative gd kernel gives up at once                  */
+    MBRL_OPT_COUNT = 5
+};
+int mbrl_set_option(int32_t option, int32_t value);
+int mbrl_get_option(int32_t option);
 
 /* ---- model upload: replaces the per-call nn.Linear weight reads of Model._forward (models.py:106-110) */
 size_t mbrl_mlp_packed_bytes(const mbrl_mlp_shape* shape);

@@ -6,6 +6,7 @@
 #include <stdarg.h>
 #include <stdio.h>
 
+#include <atomic>
 #include <map>
 #include <mutex>
 #include <set>
@@ -19,6 +20,9 @@
 namespace mbrl {
 
 static thread_local std::string g_err;
+
+// mbrl_set_option switches (include/mbrl_cem.h MBRL_OPT_*); 0 = automatic.
+static std::atomic<int> g_opt[MBRL_OPT_COUNT];
 
 static int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 static int fail(int code, const char* fmt, ...) {
@@ -62,6 +66,25 @@ hipError_t ensure_dynamic_lds(const void* fn, int bytes) {
     err = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
     if (err == hipSuccess) done.insert({fn, dev, bytes});
     return err;
+}
+
+bool grid_fits(const void* fn, int threads, size_t lds, int blocks) {
+    static std::mutex mu;
+    static std::map<std::tuple<const void*, int, size_t, int>, int> cache;   // -> resident workgroups
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return false;
+    const auto key = std::make_tuple(fn, threads, lds, dev);
+    {
+        std::lock_guard<std::mutex> lock(mu);
+        auto it = cache.find(key);
+        if (it != cache.end()) return blocks <= it->second;
+    }
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, lds) != hipSuccess) per_cu = 0;
+    const int capacity = per_cu * device_cus();
+    std::lock_guard<std::mutex> lock(mu);
+    cache[key] = capacity;
+    return blocks <= capacity;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -849,7 +872,7 @@ static int rollout_impl(const Geometry& g, const void* packed, const mbrl_norm* 
         // split kernel is bound by the L2 weight stream, which R = 2 halves per candidate. At
         // N = 4096 R = 2 would idle half the CUs: 0.607 vs 0.571 ms per F16X3 rollout (cheetah, r01).
         int RS = N >= 256 * 32 ? 2 : 1;
-        if (const char* env = getenv("MBRL_SPLIT_R")) RS = atoi(env) == 2 ? 2 : 1;   // tuning override
+        if (const int o = g_opt[MBRL_OPT_SPLIT_TILE].load(std::memory_order_relaxed)) RS = o == 32 ? 2 : 1;
         RolloutArgs X = A;                 // the fp32 redo pass at the same tile height
         X.redo = 1;
         X.nw = RS == 1 && g.T >= 2 ? 8 : 4;
@@ -866,13 +889,13 @@ static int rollout_impl(const Geometry& g, const void* packed, const mbrl_norm* 
         }
     }
     // 8-candidate tiles (rollout_m8_kernel, bit-identical sums) when 16-candidate tiles would leave
-    // at least half the CUs idle: the shard of a strong-scaled plan, small plans. MBRL_ROLLOUT_M=8 /
-    // 16 forces a choice (tests, A/B).
+    // at least half the CUs idle: the shard of a strong-scaled plan, small plans.
+    // MBRL_OPT_ROLLOUT_TILE = 8 / 16 forces a choice (tests, A/B).
     if (g.m8_ok) {
         A.m8_off = g.m8_off;
         A.C8 = g.C8;
         bool use8 = (size_t)((N + 15) / 16) * g.E * 2 <= (size_t)device_cus();
-        if (const char* env = getenv("MBRL_ROLLOUT_M")) use8 = atoi(env) == 8;
+        if (const int o = g_opt[MBRL_OPT_ROLLOUT_TILE].load(std::memory_order_relaxed)) use8 = o == 8;
         if (use8 && rollout_m8_supported(A, g.T)) return hip_check(launch_rollout_m8(A, g.T, stream), "rollout m8 launch");
     }
     if (rollout_lds_bytes(A, 16 * R) > 160 * 1024) {
@@ -901,14 +924,16 @@ static int traj_impl(const Geometry& g, const void* packed, const mbrl_norm* nor
     }
     T.s0 = s0; T.actions = actions; T.states_out = states_out;
     if (xchg && status && traj_coop_supported(T, g.E) && xchg_bytes >= traj_coop_xchg_bytes(T, g.E)) {
-        const char* dbg = getenv("MBRL_DEBUG_TRAJ_ABORT");
-        T.debug_abort = dbg != nullptr && atoi(dbg) != 0;
-        int rc = hip_check(launch_traj_coop(T, g.E, xchg, status, stream), "trajectory launch");
-        if (rc) return rc;
-        // The cooperative kernel needs its P*E workgroups co-resident; if a hand-off ever timed out
-        // (another process holding CUs, say) it set `status` and gave up. The single-workgroup kernel
-        // then recomputes the states; otherwise its E workgroups read the status word and exit.
-        T.gate = status;
+        T.debug_abort = g_opt[MBRL_OPT_DEBUG_TRAJ_ABORT].load(std::memory_order_relaxed) != 0;
+        const hipError_t err = launch_traj_coop(T, g.E, xchg, status, stream);
+        if (err != hipErrorCooperativeLaunchTooLarge) {   // too large: the grid cannot be co-resident
+            int rc = hip_check(err, "trajectory launch");
+            if (rc) return rc;
+            // The cooperative kernel needs its P*E workgroups co-resident; if a hand-off ever timed
+            // out (another process holding CUs, say) it set `status` and gave up. The single-workgroup
+            // kernel then recomputes the states; otherwise its E workgroups read the status word and exit.
+            T.gate = status;
+        }
         T.debug_abort = 0;
     }
     return hip_check(launch_traj(T, g.E, stream), "trajectory launch");
@@ -983,6 +1008,23 @@ extern "C" {
 int mbrl_abi_version(void) { return MBRL_ABI_VERSION; }
 
 const char* mbrl_last_error(void) { return g_err.c_str(); }
+
+int mbrl_set_option(int32_t option, int32_t value) {
+    if (option < 0 || option >= MBRL_OPT_COUNT) return fail(MBRL_EINVAL, "unknown option %d", option);
+    bool ok = false;
+    switch (option) {
+        case MBRL_OPT_ROLLOUT_TILE: ok = value == 0 || value == 8 || value == 16; break;
+        case MBRL_OPT_SPLIT_TILE: ok = value == 0 || value == 16 || value == 32; break;
+        default: ok = value == 0 || value == 1; break;
+    }
+    if (!ok) return fail(MBRL_EINVAL, "option %d: value %d not allowed", option, value);
+    return g_opt[option].exchange(value);
+}
+
+int mbrl_get_option(int32_t option) {
+    if (option < 0 || option >= MBRL_OPT_COUNT) return fail(MBRL_EINVAL, "unknown option %d", option);
+    return g_opt[option].load();
+}
 
 size_t mbrl_mlp_packed_bytes(const mbrl_mlp_shape* shape) {
     Geometry g;
@@ -1417,14 +1459,16 @@ int mbrl_gd_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_nor
     A.iterations = num_iterations; A.stop = stop_condition; A.lr = lr;
     A.iterations_out = iterations_out;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    const char* force_single = getenv("MBRL_GD_SINGLE");          // A/B and tests: the one-workgroup kernel
-    if (gd_coop_supported(A) && !(force_single && atoi(force_single) != 0)) {
-        const char* dbg = getenv("MBRL_DEBUG_GD_ABORT");
-        A.debug_abort = dbg != nullptr && atoi(dbg) != 0;
-        rc = hip_check(launch_gd_coop(A, w.xchg, w.status, st), "gd_plan coop launch");
-        if (rc) return rc;
-        // the one-workgroup kernel redoes the plan only if a cooperative hand-off timed out
-        A.gate = w.status;
+    // MBRL_OPT_GD_SINGLE (A/B and tests): the one-workgroup kernel
+    if (gd_coop_supported(A) && g_opt[MBRL_OPT_GD_SINGLE].load(std::memory_order_relaxed) == 0) {
+        A.debug_abort = g_opt[MBRL_OPT_DEBUG_GD_ABORT].load(std::memory_order_relaxed) != 0;
+        const hipError_t err = launch_gd_coop(A, w.xchg, w.status, st);
+        if (err != hipErrorCooperativeLaunchTooLarge) {   // too large: the grid cannot be co-resident
+            rc = hip_check(err, "gd_plan coop launch");
+            if (rc) return rc;
+            // the one-workgroup kernel redoes the plan only if a cooperative hand-off timed out
+            A.gate = w.status;
+        }
         A.debug_abort = 0;
     }
     return hip_check(launch_gd_plan(A, st), "gd_plan launch");

@@ -628,8 +628,10 @@ static hipError_t launch_gd_coop_w(const GdArgs& A, gc_u64* xchg, unsigned* stat
     const auto fn = &gd_coop_kernel<32, 2, WI>;
     hipError_t err = ensure_dynamic_lds(reinterpret_cast<const void*>(fn), 160 * 1024);
     if (err != hipSuccess) return err;
-    hipLaunchKernelGGL(fn, dim3(A.Wpad / GC_ROWS), dim3(GC_THREADS), gc_lds(A.s, A.a, A.W, A.Wpad, A.L, A.H, 32).total,
-                       stream, A, xchg, status);
+    const size_t lds = gc_lds(A.s, A.a, A.W, A.Wpad, A.L, A.H, 32).total;
+    if (!grid_fits(reinterpret_cast<const void*>(fn), GC_THREADS, lds, A.Wpad / GC_ROWS))
+        return hipErrorCooperativeLaunchTooLarge;
+    hipLaunchKernelGGL(fn, dim3(A.Wpad / GC_ROWS), dim3(GC_THREADS), lds, stream, A, xchg, status);
     return hipGetLastError();
 }
 

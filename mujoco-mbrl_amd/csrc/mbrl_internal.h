@@ -169,6 +169,19 @@ __host__ __device__ inline LdsMap lds_map(const RolloutArgs& A, float* base, int
     return L;
 }
 
+// The output row value at LDS offset ro from the NP stored partials (stride ws): the canonical tree
+// of rollout.hip mma_out's comment (every fp32 rollout kernel and the split kernels use it).
+// NP = 8 (8-wave and 8-candidate kernels) or 4 (4-wave kernels).
+template <int NP>
+__device__ __forceinline__ float sum_partials(const float* part, int ws, int ro) {
+    static_assert(NP == 4 || NP == 8, "partials");
+    if constexpr (NP == 8)
+        return ((part[ro] + part[ws + ro]) + (part[2 * ws + ro] + part[3 * ws + ro])) +
+               ((part[4 * ws + ro] + part[5 * ws + ro]) + (part[6 * ws + ro] + part[7 * ws + ro]));
+    else
+        return (part[ro] + part[ws + ro]) + (part[2 * ws + ro] + part[3 * ws + ro]);
+}
+
 // At least 82 KiB so that one workgroup owns a CU: 256 workgroups of N = 4096 then land one per CU
 // instead of doubling up on some CUs (the kernel is sized for one wave per SIMD).
 inline size_t rollout_lds_bytes(const RolloutArgs& A, int M) {
@@ -180,6 +193,11 @@ inline size_t rollout_lds_bytes(const RolloutArgs& A, int M) {
 // Raise `fn`'s dynamic-LDS limit to `bytes` on the current device, once per (kernel, device,
 // bytes); thread-safe (cem.hip).
 hipError_t ensure_dynamic_lds(const void* fn, int bytes);
+
+// Whether `blocks` workgroups of kernel `fn` (threads each, `lds` bytes of dynamic LDS) can all be
+// resident on the current device at once (occupancy query x CU count, cached; cem.hip). Kernels with
+// grid-wide hand-offs check it and return hipErrorCooperativeLaunchTooLarge instead of launching.
+bool grid_fits(const void* fn, int threads, size_t lds, int blocks);
 
 hipError_t launch_rollout(const RolloutArgs& A, int T, int R, hipStream_t stream);
 bool rollout_m8_supported(const RolloutArgs& A, int T);
@@ -244,7 +262,7 @@ hipError_t launch_gd_coop(const GdArgs& A, unsigned long long* xchg, unsigned* s
 // Cooperative variant: P = Wpad/16 workgroups per member each own 16 hidden units of every W -> W
 // layer (slices LDS-resident); layer 0 and the output layer are computed redundantly by every
 // workgroup; hidden activations are all-gathered through tagged 8-byte granules in `xchg`
-// (E * 2 * Wpad granules, zeroed by the launcher before every launch). Needs P*E <= 256 and
+// (E * 2 * Wpad granules, zeroed by the launcher before every launch). Needs the P*E workgroups co-resident (grid_fits) and
 // s <= 64. `status` (one uint32, zeroed by the launcher) becomes nonzero if a bounded spin gave up.
 bool traj_coop_supported(const TrajArgs& A, int E);
 size_t traj_coop_xchg_bytes(const TrajArgs& A, int E);

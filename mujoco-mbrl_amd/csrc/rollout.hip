@@ -134,27 +134,38 @@ __device__ __forceinline__ void mma_hidden(f32x4 (&acc)[R][T], const f32x4 (&a)[
                 acc[r][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[j][s], a[r][s], acc[r][j], 0, 0, 0);
 }
 
-// Output-type chunk: one 16-column output tile over this wave's W/4-deep K range; four accumulator
+// Output-type chunk: one 16-column output tile over this wave's own K range; four accumulator
 // chains so consecutive MFMAs never wait on each other.
-template <int T, int R>
+// Canonical output sum (the same bits for every tile height, wave count and shard size): the hidden
+// features split into 8 "halves" of T/2 tiles each (NW = 8: one per wave; NW = 4, T >= 2: two per
+// wave, NH = 2); a half is four chains (k = 16 kc + 4 s + i, chain s) closed as (c0 + c1) + (c2 + c3);
+// the output is ((h0 + h1) + (h2 + h3)) + ((h4 + h5) + (h6 + h7)) -- sum_partials below. A 4-wave
+// workgroup stores (h_2w + h_2w+1) per wave, which is exactly the inner pair of that tree.
+template <int T, int R, int NH>
 __device__ __forceinline__ void mma_out(const f32x4 (&aout)[R][T], const f32x4 (&b)[T], float* part, int pw,
                                         int tile, int lane) {
-    f32x4 o[R][4];
+    static_assert(NH == 1 || (NH == 2 && T % 2 == 0), "halves");
+    constexpr int TH = T / NH;
+    f32x4 o[NH][R][4];
 #pragma unroll
-    for (int r = 0; r < R; ++r)
+    for (int h = 0; h < NH; ++h)
 #pragma unroll
-        for (int s = 0; s < 4; ++s) o[r][s] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) o[h][r][s] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kc = 0; kc < T; ++kc)
 #pragma unroll
         for (int s = 0; s < 4; ++s)
 #pragma unroll
             for (int r = 0; r < R; ++r)
-                o[r][s] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[kc][s], aout[r][kc][s], o[r][s], 0, 0, 0);
+                o[kc / TH][r][s] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[kc][s], aout[r][kc][s], o[kc / TH][r][s], 0, 0, 0);
 #pragma unroll
-    for (int r = 0; r < R; ++r)
-        *reinterpret_cast<f32x4*>(part + (16 * r + (lane & 15)) * pw + 16 * tile + 4 * (lane >> 4)) =
-            (o[r][0] + o[r][1]) + (o[r][2] + o[r][3]);
+    for (int r = 0; r < R; ++r) {
+        f32x4 v = (o[0][r][0] + o[0][r][1]) + (o[0][r][2] + o[0][r][3]);
+        if constexpr (NH == 2) v = v + ((o[1][r][0] + o[1][r][1]) + (o[1][r][2] + o[1][r][3]));
+        *reinterpret_cast<f32x4*>(part + (16 * r + (lane & 15)) * pw + 16 * tile + 4 * (lane >> 4)) = v;
+    }
 }
 
 // acc + bias -> ReLU -> next activation buffer (float4 row stores); one barrier (ping-pong buffers).
@@ -280,6 +291,7 @@ template <int T, int R, int K0C_T, int NOT_T, int NW>
 __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A) {
     constexpr int M = 16 * R;
     constexpr int TW = 4 * T / NW;
+    constexpr int NHO = (NW == 4 && TW >= 2) ? 2 : 1;   // output halves per wave (mma_out)
     constexpr int NT = 64 * NW;
     static_assert(TW >= 1 && TW * NW == 4 * T, "tiles per wave");
     constexpr bool RING = K0C_T > 0;
@@ -454,7 +466,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
     do {                                                                          \
         MBRL_LOAD_CHUNK(ring[((SLOT) + NB - 1) % NB], g + NB - 1);                \
         MBRL_PIN();                                                               \
-        mma_out<TW, R>(aout, ring[SLOT], part, A.pw, J, lane);                    \
+        mma_out<TW, R, NHO>(aout, ring[SLOT], part, A.pw, J, lane);               \
         MBRL_PIN();                                                               \
         ++g;                                                                      \
     } while (0)
@@ -491,8 +503,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
                     const int ro = m * A.pw + d;
                     float o = 0.f;
                     if (pass == 0 || d == A.s) {
-                        for (int q = 0; q < NW; ++q) o = q == 0 ? L.part[ro] : o + L.part[q * ws + ro];
-                        o = o + bout[d];
+                        o = sum_partials<NW>(L.part, ws, ro) + bout[d];
                     }
                     if (d < A.s) {
                         float xn;
@@ -529,10 +540,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
                 float sc = 0.f;
                 auto slot = [&](int d, float om, float os, float goal, float cw, float bo) {
                     const int ro = m * A.pw + d;
-                    float o = L.part[ro] + L.part[ws + ro] + L.part[2 * ws + ro] + L.part[3 * ws + ro];
-                    if constexpr (NW == 8)
-                        o = o + ((L.part[4 * ws + ro] + L.part[5 * ws + ro]) + (L.part[6 * ws + ro] + L.part[7 * ws + ro]));
-
+                    float o = sum_partials<NW>(L.part, ws, ro);
                     o = o + bo;
                     const float sn = A.unnorm_s ? o * os + om : o;
                     if (A.has_sc) {
@@ -953,8 +961,7 @@ __global__ void __launch_bounds__(64 * m8_waves(T, NOT_T), 1) rollout_m8_kernel(
             float sc = 0.f;
             auto slot = [&](int d, float om, float os, float goal, float cw, float bo) {
                 const int ro = m * A.pw + d;
-                float o = L.part[ro] + L.part[ws + ro] + L.part[2 * ws + ro] + L.part[3 * ws + ro];
-                o = o + ((L.part[4 * ws + ro] + L.part[5 * ws + ro]) + (L.part[6 * ws + ro] + L.part[7 * ws + ro]));
+                float o = sum_partials<8>(L.part, ws, ro);
                 o = o + bo;
                 const float sn = A.unnorm_s ? o * os + om : o;
                 if (A.has_sc) {

@@ -430,8 +430,7 @@ struct SplitRollout {
                     const int d = j + 16 * k;
                     if (d < A.s) {
                         const int ro = m * A.pw + d;
-                        float o = L.part[ro] + L.part[ws + ro] + L.part[2 * ws + ro] + L.part[3 * ws + ro];
-                        o = o + ((L.part[4 * ws + ro] + L.part[5 * ws + ro]) + (L.part[6 * ws + ro] + L.part[7 * ws + ro]));
+                        float o = sum_partials<8>(L.part, ws, ro);
                         const float om = L.obs_mean[d], os = L.obs_std[d];
                         o = o + L.hbias[A.L * A.Wpad + d];
                         const float sn = A.unnorm_s ? o * os + om : o;

@@ -371,7 +371,8 @@ static int coop_k0r(const TrajArgs& A) {
 bool traj_coop_supported(const TrajArgs& A, int E) {
     const int P = A.Wpad / COOP_ROWS;
     const int k0r = coop_k0r(A);
-    if (k0r == 0 || A.L < 2 || A.W != A.Wpad || A.Wpad > COOP_MAX_W || P * E > 256) return false;
+    // P * E workgroups must be co-resident: launch_coop_variant checks the device's occupancy
+    if (k0r == 0 || A.L < 2 || A.W != A.Wpad || A.Wpad > COOP_MAX_W || P * E > 1024) return false;
     return coop_lds(A.s, A.a, A.W, A.Wpad, A.L, A.H, k0r).total <= 150 * 1024;
 }
 
@@ -382,6 +383,9 @@ static hipError_t launch_coop_variant(const TrajArgs& A, int E, u64* xchg, unsig
     hipError_t err = ensure_dynamic_lds(reinterpret_cast<const void*>(&traj_coop_kernel<K0R, SM, WI>), 160 * 1024);
     if (err != hipSuccess) return err;
     const size_t lds = coop_lds(A.s, A.a, A.W, A.Wpad, A.L, A.H, K0R).total;
+    if (!grid_fits(reinterpret_cast<const void*>(&traj_coop_kernel<K0R, SM, WI>), COOP_THREADS, lds,
+                   A.Wpad / COOP_ROWS * E))
+        return hipErrorCooperativeLaunchTooLarge;
     hipLaunchKernelGGL((traj_coop_kernel<K0R, SM, WI>), dim3(A.Wpad / COOP_ROWS, E), dim3(COOP_THREADS), lds,
                        stream, A, xchg, status);
     return hipGetLastError();

@@ -20,13 +20,15 @@ LIB_PATH = os.environ.get("MBRL_AMD_LIB") or os.path.join(os.path.dirname(os.pat
 MBRL_OK = 0
 MBRL_COST_GOAL_STATE = 0
 MBRL_COST_MODEL_REWARD = 1
-ABI_VERSION = 3
+ABI_VERSION = 4
 MBRL_NAN_LAST = 0
 MBRL_NAN_FIRST = 1
 MBRL_PRECISION_F32 = 0
 MBRL_PRECISION_F16X3 = 1
 MBRL_PRECISION_F16X6 = 2
 PRECISIONS = {"f32": MBRL_PRECISION_F32, "f16x3": MBRL_PRECISION_F16X3, "f16x6": MBRL_PRECISION_F16X6}
+# mbrl_set_option switches (include/mbrl_cem.h MBRL_OPT_*): A/B runs and forced fallbacks in tests
+OPTIONS = {"rollout_tile": 0, "split_tile": 1, "debug_traj_abort": 2, "gd_single": 3, "debug_gd_abort": 4}
 
 
 def precision_code(name):
@@ -39,7 +41,8 @@ def precision_code(name):
 
 # Every symbol include/mbrl_cem.h declares (tests/test_abi.py checks the two lists agree).
 EXPORTED = (
-    "mbrl_abi_version", "mbrl_last_error", "mbrl_mlp_packed_bytes", "mbrl_mlp_pack",
+    "mbrl_abi_version", "mbrl_last_error", "mbrl_set_option", "mbrl_get_option", "mbrl_mlp_packed_bytes",
+    "mbrl_mlp_pack",
     "mbrl_rollout_cost", "mbrl_select_workspace_bytes", "mbrl_select_elites",
     "mbrl_refit_workspace_bytes", "mbrl_cem_refit", "mbrl_sample_actions",
     "mbrl_trajectory_workspace_bytes", "mbrl_trajectory", "mbrl_cem_workspace_bytes", "mbrl_cem_plan",
@@ -93,6 +96,8 @@ def load():
     sig = {
         "mbrl_abi_version": (c_int32, []),
         "mbrl_last_error": (ctypes.c_char_p, []),
+        "mbrl_set_option": (c_int32, [c_int32, c_int32]),
+        "mbrl_get_option": (c_int32, [c_int32]),
         "mbrl_mlp_packed_bytes": (c_size_t, [POINTER(MlpShape)]),
         "mbrl_mlp_pack": (c_int32, [POINTER(MlpShape), POINTER(c_void_p), POINTER(c_void_p), P, P]),
         "mbrl_rollout_cost": (c_int32, [POINTER(MlpShape), P, POINTER(Norm), POINTER(Cost), P, c_int32, P,
@@ -131,6 +136,26 @@ def check(rc, what):
         raise RuntimeError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
 
 
+class option:
+    """Context manager around mbrl_set_option: `with option("rollout_tile", 8): ...` sets a
+    process-wide switch and restores its previous value on exit (include/mbrl_cem.h MBRL_OPT_*)."""
+
+    def __init__(self, name, value):
+        self.code, self.value = OPTIONS[name], int(value)
+
+    def __enter__(self):
+        lib = load()
+        prev = lib.mbrl_set_option(self.code, self.value)
+        if prev < 0:
+            check(prev, "mbrl_set_option")
+        self.prev = prev
+        return self
+
+    def __exit__(self, *exc):
+        load().mbrl_set_option(self.code, self.prev)
+        return False
+
+
 def ptr(t):
     """Device pointer of a tensor (None -> NULL)."""
     return None if t is None else c_void_p(t.data_ptr())
@@ -148,4 +173,4 @@ def require_gpu(t):
 __all__ = ["load", "check", "ptr", "stream_handle", "MlpShape", "Norm", "Cost", "Sampler", "CemParams",
            "EXPORTED", "MBRL_NAN_LAST", "MBRL_NAN_FIRST", "MBRL_COST_GOAL_STATE", "MBRL_COST_MODEL_REWARD",
            "ABI_VERSION", "c_int64", "MBRL_PRECISION_F32", "MBRL_PRECISION_F16X3", "MBRL_PRECISION_F16X6",
-           "precision_code"]
+           "precision_code", "option", "OPTIONS"]

@@ -202,7 +202,14 @@ def make_rs(data, models, planners, out_dir):
     print("config1: idx", int(np.argmin(costs[0])), "cost", float(costs[0].min()))
 
 
-def make_cem(data, models, planners, out_dir, config_id, **over):
+def make_cem(data, models, planners, out_dir, config_id, full=False, **over):
+    """One CEM plan (I iterations) with the reference's _generate_trajectories as rollout + cost.
+
+    full=True is the BASELINE full-size mode (walker N=16384 H=30; humanoid N=32768 H=50 E=5). It
+    runs the reference rollout under torch.no_grad(): the reference builds an autograd graph it never
+    uses (planners.py:199-210 without no_grad), which at humanoid size would hold ~10 GB of saved
+    activations per member; the forward arithmetic is the same with or without the graph. The
+    fixture then keeps the member-mean returns (not the per-member costs) to stay small."""
     p = ocem.synth_problem(config_id, **over)
     cfg = p["cfg"]
     N, H, a = cfg["N"], cfg["H"], cfg["a"]
@@ -215,9 +222,11 @@ def make_cem(data, models, planners, out_dir, config_id, **over):
     mu = np.zeros((H, a), np.float32)
     sigma = np.full((H, a), np.float32((hi - lo) / 4.0), np.float32)
     rec = dict(costs=[], returns=[], elites=[], mu=[], sigma=[], gap=[])
+    grad_ctx = torch.no_grad if full else torch.enable_grad
     for it in range(I):
         A = cem_actions(mu, sigma, lo, hi, p["rng_seed"], it, np.arange(N))
-        costs, _ = ref_rollout_costs(planners, model_fns, cost_fns, p["s0"], A)
+        with grad_ctx():
+            costs, _ = ref_rollout_costs(planners, model_fns, cost_fns, p["s0"], A)
         ret = ocem.ensemble_returns(costs)
         order = np.argsort(ret, kind="stable")
         elites = np.sort(order[:K])
@@ -229,14 +238,18 @@ def make_cem(data, models, planners, out_dir, config_id, **over):
     final_actions = np.clip(mu, np.float32(lo), np.float32(hi)).astype(np.float32)
     st = []
     for mf, cf in zip(model_fns, cost_fns):
-        _, tr = ref_rollout_costs(planners, [mf], [cf], p["s0"], final_actions[:, None, :])
+        with grad_ctx():
+            _, tr = ref_rollout_costs(planners, [mf], [cf], p["s0"], final_actions[:, None, :])
         st.append(tr[0][0][0].detach().numpy())
     final_states = np.mean(np.stack(st), axis=0, dtype=np.float32) if len(st) > 1 else st[0]
     name = f"config{config_id}_cem" + ("" if not over else "_" + "_".join(f"{k}{v}" for k, v in over.items()))
+    if full:
+        name += "_full"
+    extra = {} if full else dict(costs=np.stack(rec["costs"]))
     np.savez_compressed(
         os.path.join(out_dir, name + ".npz"), weights_sha256=ocem.weights_sha256(p["model"]),
-        N=N, H=H, K=K, I=I, alpha=alpha, lo=lo, hi=hi,
-        costs=np.stack(rec["costs"]), returns=np.stack(rec["returns"]),
+        N=N, H=H, K=K, I=I, alpha=alpha, lo=lo, hi=hi, gap=np.array(rec["gap"], np.float64), **extra,
+        returns=np.stack(rec["returns"]),
         elites=np.stack(rec["elites"]).astype(np.int32), mu=np.stack(rec["mu"]),
         sigma=np.stack(rec["sigma"]), final_actions=final_actions, final_states=final_states)
     print(name, "min K-boundary gap (rel)", float(np.min(rec["gap"])),
@@ -276,6 +289,10 @@ def main():
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     if len(sys.argv) > 1 and sys.argv[1] == "6":           # regenerate only the reward-head fixture
         make_cem(data, models, planners, out_dir, 6, N=512, H=10)
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "full":        # BASELINE configs 4 and 5 at full size
+        for cid in sys.argv[2:] or ("4", "5"):
+            make_cem(data, models, planners, out_dir, int(cid), full=True)
         return
     make_toy(planners, out_dir)
     make_rs(data, models, planners, out_dir)

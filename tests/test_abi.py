@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     assert decl == sorted(_lib.EXPORTED)
     for name in decl:
         assert hasattr(lib, name), name
-    assert lib.mbrl_abi_version() == _lib.ABI_VERSION == 3
+    assert lib.mbrl_abi_version() == _lib.ABI_VERSION == 4
 
 
 def test_no_gpu_needed_for_sizing_calls():
@@ -129,3 +129,28 @@ def test_split_stream_bytes_match_the_packed_geometry():
     assert synthetic.split_stream_bytes_per_step(ch, 3) == 34 * 3072 * 8 * 4
     rw = dict(ch, L=2, reward=True)
     assert synthetic.split_stream_bytes_per_step(rw, 2) == 18 * 2048 * 8 * 4
+
+
+def test_options_are_set_through_the_abi_not_the_environment():
+    """mbrl_set_option / mbrl_get_option (MBRL_OPT_*): set, restore, reject unknown options and
+    values; no source of the library reads the environment (a stray variable cannot redirect a
+    production launch)."""
+    from mbrl_amd import _lib
+    lib = _lib.load()
+    for name, code in _lib.OPTIONS.items():
+        assert lib.mbrl_get_option(code) == 0, name
+    with _lib.option("rollout_tile", 8):
+        assert lib.mbrl_get_option(_lib.OPTIONS["rollout_tile"]) == 8
+        with _lib.option("rollout_tile", 16):
+            assert lib.mbrl_get_option(_lib.OPTIONS["rollout_tile"]) == 16
+        assert lib.mbrl_get_option(_lib.OPTIONS["rollout_tile"]) == 8
+    assert lib.mbrl_get_option(_lib.OPTIONS["rollout_tile"]) == 0
+    assert lib.mbrl_set_option(_lib.OPTIONS["rollout_tile"], 12) < 0
+    assert lib.mbrl_get_option(_lib.OPTIONS["rollout_tile"]) == 0
+    assert lib.mbrl_set_option(99, 1) < 0 and lib.mbrl_get_option(99) < 0
+    with pytest.raises(RuntimeError):
+        with _lib.option("gd_single", 5):
+            pass
+    csrc = os.path.join(REPO, "mujoco-mbrl_amd", "csrc")
+    for f in os.listdir(csrc):
+        assert "getenv" not in open(os.path.join(csrc, f)).read(), f

@@ -95,11 +95,11 @@ def test_gd_fused_kernel_matches_graph_path(cid, over, H, iters, stop):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", ["single", "abort"])
-def test_gd_cooperative_kernel_and_its_fallback(mode, monkeypatch):
+def test_gd_cooperative_kernel_and_its_fallback(mode):
     """mbrl_gd_plan runs the cooperative kernel for W in {64..512}: it must agree with the
-    one-workgroup kernel (MBRL_GD_SINGLE=1), and when a hand-off gives up (MBRL_DEBUG_GD_ABORT=1)
+    one-workgroup kernel (MBRL_OPT_GD_SINGLE), and when a hand-off gives up (MBRL_OPT_DEBUG_GD_ABORT)
     the gated one-workgroup kernel must produce the plan instead."""
-    from mbrl_amd import gd
+    from mbrl_amd import _lib, gd
     p, model_fn, cost_fn = closures(3, dict(W=256, L=3))
     mdesc, cdesc = gd.describe(model_fn, cost_fn)
     dev = torch.device("cuda:0")
@@ -108,8 +108,8 @@ def test_gd_cooperative_kernel_and_its_fallback(mode, monkeypatch):
     acts = [torch.from_numpy(A0[i:i + 1].copy()) for i in range(H)]
     s0 = torch.from_numpy(p["s0"])
     s1, a1, n1 = gd.plan_fused(s0, mdesc, cdesc, acts, H, 30, 0.001, dev)
-    monkeypatch.setenv("MBRL_GD_SINGLE" if mode == "single" else "MBRL_DEBUG_GD_ABORT", "1")
-    s2, a2, n2 = gd.plan_fused(s0, mdesc, cdesc, acts, H, 30, 0.001, dev)
+    with _lib.option("gd_single" if mode == "single" else "debug_gd_abort", 1):
+        s2, a2, n2 = gd.plan_fused(s0, mdesc, cdesc, acts, H, 30, 0.001, dev)
     torch.cuda.synchronize()
     assert int(n1.item()) == int(n2.item())
     assert torch.allclose(a1, a2, rtol=1e-4, atol=1e-5), float((a1 - a2).abs().max())

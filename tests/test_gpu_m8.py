@@ -2,7 +2,7 @@
 the 16-candidate kernel and the CPU oracle. The two kernels consume every accumulator's k in the
 same order, so their costs and states must agree BIT FOR BIT (that keeps a sharded plan independent
 of the tile height its shard size picks); both stay within the oracle bars of test_gpu_parity.py.
-MBRL_ROLLOUT_M=8 / 16 forces the tile height (cem.hip rollout_impl)."""
+mbrl_set_option(MBRL_OPT_ROLLOUT_TILE, 8 / 16) forces the tile height (cem.hip rollout_impl)."""
 import numpy as np
 import pytest
 import torch
@@ -15,13 +15,13 @@ from test_gpu_parity import DEV, RTOL, build, device_problem, rel_err
 pytestmark = pytest.mark.gpu
 
 
-def _rollout(monkeypatch, prob, p, N, H, m, A):
-    from mbrl_amd import fused
+def _rollout(prob, p, N, H, m, A):
+    from mbrl_amd import _lib, fused
     E, s = p["cfg"]["E"], p["cfg"]["s"]
-    monkeypatch.setenv("MBRL_ROLLOUT_M", str(m))
     states = torch.empty((E, H, N, s), dtype=torch.float32, device=DEV)
-    costs = fused.rollout(prob, torch.from_numpy(p["s0"]).to(DEV), N, H, actions=torch.from_numpy(A).to(DEV),
-                          states_out=states)
+    with _lib.option("rollout_tile", m):
+        costs = fused.rollout(prob, torch.from_numpy(p["s0"]).to(DEV), N, H, actions=torch.from_numpy(A).to(DEV),
+                              states_out=states)
     torch.cuda.synchronize()
     return costs, states
 
@@ -30,13 +30,13 @@ def _rollout(monkeypatch, prob, p, N, H, m, A):
                                           (3, 1, 3, {}), (4, 517, 7, {}), (5, 40, 6, {}), (5, 250, 3, {}),
                                           (3, 33, 1, {}), (2, 300, 5, dict(L=1)), (3, 100, 4, dict(W=200)),
                                           (4, 64, 3, dict(W=256, L=4))])
-def test_m8_matches_m16_bitwise_and_the_oracle(monkeypatch, cid, N, H, over):
+def test_m8_matches_m16_bitwise_and_the_oracle(cid, N, H, over):
     p = ocem.synth_problem(cid, N=N, H=H, **over)
     a = p["cfg"]["a"]
     A = cem_actions(np.zeros((H, a), np.float32), np.full((H, a), 0.5, np.float32), -1, 1, 5, 0, np.arange(N))
     prob = device_problem(p)
-    c8, s8 = _rollout(monkeypatch, prob, p, N, H, 8, A)
-    c16, s16 = _rollout(monkeypatch, prob, p, N, H, 16, A)
+    c8, s8 = _rollout(prob, p, N, H, 8, A)
+    c16, s16 = _rollout(prob, p, N, H, 16, A)
     assert torch.equal(c8, c16), float((c8 - c16).abs().max())
     assert torch.equal(s8, s16)
     ref_costs, ref_states = ocem.rollout(p["model"], p["norm"], p["cost"], p["s0"], A, store_states=True)
@@ -44,16 +44,17 @@ def test_m8_matches_m16_bitwise_and_the_oracle(monkeypatch, cid, N, H, over):
     assert np.allclose(s8.cpu().numpy(), ref_states, rtol=1e-4, atol=1e-4)
 
 
-def test_m8_plan_equals_m16_plan(monkeypatch):
+def test_m8_plan_equals_m16_plan():
     """A whole CEM plan at a strong-scaling shard size (walker, 2048 candidates): identical
     returns, elites, mu and sigma with either tile height."""
-    from mbrl_amd import CEMPlanner
+    from mbrl_amd import CEMPlanner, _lib
     p = ocem.synth_problem(4, N=2048, H=10)
     _, model_fn, cost_fn, sample_action = build(p)
     out = {}
     for m in (8, 16):
-        monkeypatch.setenv("MBRL_ROLLOUT_M", str(m))
-        out[m] = CEMPlanner.plan_detailed(torch.from_numpy(p["s0"]), model_fn, cost_fn, sample_action, 10,
-                                          num_candidates=2048, num_iterations=3, seed=p["rng_seed"], record=True)
+        with _lib.option("rollout_tile", m):
+            out[m] = CEMPlanner.plan_detailed(torch.from_numpy(p["s0"]), model_fn, cost_fn, sample_action, 10,
+                                              num_candidates=2048, num_iterations=3, seed=p["rng_seed"],
+                                              record=True)
     for k in ("returns", "elites", "mu", "sigma", "actions", "states"):
         assert torch.equal(out[8][k], out[16][k]), k

@@ -94,3 +94,32 @@ def test_cem_actions_are_the_ones_rolled_out():
     c1 = ocem.rollout(p["model"], p["norm"], p["cost"], p["s0"], A)
     c2 = ocem.rollout(p["model"], p["norm"], p["cost"], p["s0"], A[:, ::-1].copy())
     assert np.allclose(c1[0], c2[0][::-1], rtol=1e-6)
+
+
+FULL_CASES = [("config4_cem_full", 4), ("config5_cem_full", 5)]
+
+
+@pytest.mark.parametrize("name,cid", FULL_CASES, ids=[c[0] for c in FULL_CASES])
+def test_full_size_fixture_sampled(golden, name, cid):
+    """The full-size reference fixtures (walker N=16384; humanoid N=32768 H=50 E=5): for 24 sampled
+    candidates per iteration the oracle, teacher-forced on the fixture's mu / sigma, reproduces the
+    reference returns within 1e-5; the oracle refit of the fixture's elite set reproduces its mu /
+    sigma bit for bit; the fixture's elites are the stable top-K of its returns."""
+    g = golden(name)
+    p = ocem.synth_problem(cid)
+    assert ocem.weights_sha256(p["model"]) == str(g["weights_sha256"])
+    N, H, K = int(g["N"]), int(g["H"]), int(g["K"])
+    a = p["cfg"]["a"]
+    mu = np.zeros((H, a), np.float32)
+    sg = np.full((H, a), 0.5, np.float32)
+    rng = np.random.default_rng(cid)
+    for it in range(int(g["I"])):
+        assert np.array_equal(g["elites"][it], ocem.select_elites(g["returns"][it], K))
+        idx = np.sort(rng.choice(N, size=24, replace=False))
+        A = cem_actions(mu, sg, -1.0, 1.0, p["rng_seed"], it, idx)
+        ref = ocem.ensemble_returns(ocem.rollout(p["model"], p["norm"], p["cost"], p["s0"], A))
+        assert rel_err(ref, g["returns"][it][idx]) < RTOL, f"iteration {it}"
+        Ael = cem_actions(mu, sg, -1.0, 1.0, p["rng_seed"], it, g["elites"][it])
+        mu, sg = ocem.refit(mu, sg, np.ascontiguousarray(Ael.transpose(1, 0, 2)), 0.1)
+        assert np.array_equal(mu, g["mu"][it]) and np.array_equal(sg, g["sigma"][it]), f"iteration {it}"
+    assert np.array_equal(np.clip(mu, -1.0, 1.0), g["final_actions"])

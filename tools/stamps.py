@@ -38,6 +38,7 @@ def main():
     tiles = (N + 16 * R - 1) // (16 * R)
     if os.environ.get("MBRL_ROLLOUT_M") == "8":     # rollout_m8_kernel: 8 candidates per workgroup
         R, tiles = 0.5, (N + 7) // 8
+        lib.mbrl_set_option(_lib.OPTIONS["rollout_tile"], 8)   # the library reads no environment
     NWMAX = 8   # waves per workgroup (4 or 8); unused slots stay zero and are dropped below
     buf = torch.zeros(E * tiles * NWMAX * NSEG, dtype=torch.int64, device=dev)
     assert lib.mbrl_diag_set_stamps(buf.data_ptr()) == 0
