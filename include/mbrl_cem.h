@@ -152,7 +152,8 @@ enum {
     MBRL_OPT_DEBUG_TRAJ_ABORT = 2,  /* 1: the cooperative trajectory kernel gives up at once          */
     MBRL_OPT_GD_SINGLE = 3,         /* 1: mbrl_gd_plan runs its one-workgroup kernel                  */
     MBRL_OPT_DEBUG_GD_ABORT = 4,    /* 1: the cooperative gd kernel gives up at once                  */
-    MBRL_OPT_COUNT = 5
+    MBRL_OPT_UNFUSED_UPDATE = 5,    /* 1: plans run select / refit / proposal draw as separate launches */
+    MBRL_OPT_COUNT = 6
 };
 int mbrl_set_option(int32_t option, int32_t value);
 int mbrl_get_option(int32_t option);

@@ -432,14 +432,11 @@ constexpr int SEL_HIST_WORDS = 2 * 16 * 257;
 // Segmented over blockIdx.x (independent problems of N candidates each, batched planning): segment
 // b reads costs[e * member_stride + b * N + n] and writes elite_idx[b * K ..] (local indices) and
 // returns_out[b * N ..].
-template <int KPT>
-__global__ void __launch_bounds__(1024) select_reg_kernel(const float* __restrict__ costs, int E, int N, int K,
-                                                          int nan_policy, int64_t* __restrict__ elite_idx,
-                                                          float* __restrict__ returns_out, int member_stride) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t sel_smem[];
-    costs += (size_t)blockIdx.x * N;
-    elite_idx += (size_t)blockIdx.x * K;
-    if (returns_out) returns_out += (size_t)blockIdx.x * N;
+// The body is shared with cem_update_kernel; emit(pos, n) receives the elites in ascending index.
+template <int KPT, typename Emit>
+__device__ __forceinline__ void select_reg_body(const float* __restrict__ costs, int E, int N, int K, int nan_policy,
+                                                float* __restrict__ returns_out, int member_stride,
+                                                uint32_t* sel_smem, Emit emit) {
     uint32_t(*hist)[16][257] = reinterpret_cast<uint32_t(*)[16][257]>(sel_smem);  // [2][16][257], aliases keys
     __shared__ uint32_t scan_ws[16];
     __shared__ uint32_t sel[2];
@@ -549,9 +546,23 @@ __global__ void __launch_bounds__(1024) select_reg_kernel(const float* __restric
     uint32_t pos = block_exclusive_scan(cnt, scan_ws, &tot);
 #pragma unroll
     for (int k = 0; k < KPT; ++k)
-        if (take[k] && pos < (uint32_t)K) elite_idx[pos++] = n0 + k;
+        if (take[k] && pos < (uint32_t)K) emit(pos++, n0 + k);
     CSTAMP(6);
 }
+
+template <int KPT>
+__global__ void __launch_bounds__(1024) select_reg_kernel(const float* __restrict__ costs, int E, int N, int K,
+                                                          int nan_policy, int64_t* __restrict__ elite_idx,
+                                                          float* __restrict__ returns_out, int member_stride) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t sel_smem[];
+    costs += (size_t)blockIdx.x * N;
+    elite_idx += (size_t)blockIdx.x * K;
+    if (returns_out) returns_out += (size_t)blockIdx.x * N;
+    select_reg_body<KPT>(costs, E, N, K, nan_policy, returns_out, member_stride, sel_smem,
+                         [&](uint32_t pos, int n) { elite_idx[pos] = n; });
+}
+
+static size_t select_reg_lds(int KPT) { return 4 * (size_t)max(33 * 32 * KPT, SEL_HIST_WORDS); }
 
 // ------------------------------------------------------------------------------------------------
 // CEM refit. gather: regenerate every elite's a_t from the counter RNG into aelite[t][e][a].
@@ -624,42 +635,39 @@ __global__ void refit_kernel(const float* __restrict__ aelite, int a, int K, flo
 constexpr int REFIT_THREADS = 1024;
 constexpr size_t REFIT_LDS_MAX = 96 * 1024;
 
-__global__ void __launch_bounds__(REFIT_THREADS) refit_fused_kernel(
-    uint64_t seed, int iteration, const float* __restrict__ mu, const float* __restrict__ sigma, float lo, float hi,
-    int a, const int64_t* __restrict__ elite_idx, int K, float alpha, float oma, float* __restrict__ mu_out,
-    float* __restrict__ sigma_out, float* __restrict__ fin_mu, float* __restrict__ fin_sigma,
-    float* __restrict__ fin_actions, int n_env) {
+// LDS floats refit_rows works in: [K][a] elite actions, [nch][a] chunk partials, mean, this row's mu, sigma.
+__host__ __device__ inline size_t refit_rows_floats(int a, int K) {
+    const size_t nch = (size_t)(K + ELITE_CHUNK - 1) / ELITE_CHUNK;
+    const size_t a4 = ((size_t)a + 3) & ~(size_t)3;
+    return (((size_t)K * a + 3) & ~(size_t)3) + ((nch * a + 3) & ~(size_t)3) + 3 * a4;
+}
+
+// Row t of the refit (mu, sigma, outputs already offset to the problem; NULL outputs are skipped): eidx
+// = the K elites' global candidate indices in LDS (visible after refit_rows' first barrier). With
+// `next` (LDS [2][a4]) the new mu_t, sigma_t are also left there for the next proposal draw.
+__device__ __forceinline__ void refit_rows(int t, const uint32_t* eidx, float* smem, uint64_t seed, int iteration,
+                                           const float* __restrict__ mu, const float* __restrict__ sigma, float lo,
+                                           float hi, int a, int K, float alpha, float oma, float* __restrict__ mu_out,
+                                           float* __restrict__ sigma_out, float* __restrict__ fin_mu,
+                                           float* __restrict__ fin_sigma, float* __restrict__ fin_actions,
+                                           float* next) {
 #pragma clang fp contract(off)
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    // batched planning: blockIdx.y = problem b, whose [H][a] distribution rows sit at b*H*a, whose
-    // K elites (local indices) at b*K, and whose candidates are global n = b*n_env + local
-    const int t = blockIdx.x, H = gridDim.x;
-    {
-        const size_t eo = (size_t)blockIdx.y * H * a;
-        mu += eo; sigma += eo; mu_out += eo; sigma_out += eo;
-        if (fin_mu) fin_mu += eo;
-        if (fin_sigma) fin_sigma += eo;
-        if (fin_actions) fin_actions += eo;
-        elite_idx += (size_t)blockIdx.y * K;
-    }
-    const uint32_t nbase = (uint32_t)blockIdx.y * (uint32_t)n_env;
     const int G = (a + 3) >> 2;
     const int nch = (K + ELITE_CHUNK - 1) / ELITE_CHUNK;
+    const int a4 = (a + 3) & ~3;
     float* ael = smem;                                   // [K][a]
     float* part = smem + (((size_t)K * a + 3) & ~(size_t)3);   // [nch][a]
     float* mean = part + (((size_t)nch * a + 3) & ~(size_t)3);  // [a]
-    float* musg = mean + ((a + 3) & ~3);                         // [2][a]: this step's mu, sigma
-    uint32_t* eidx = reinterpret_cast<uint32_t*>(musg + 2 * ((a + 3) & ~3));  // [K]
+    float* musg = mean + a4;                                     // [2][a]: this step's mu, sigma
     // stage every global operand first (all loads in flight together), then compute from LDS
-    for (int e = threadIdx.x; e < K; e += REFIT_THREADS) eidx[e] = nbase + (uint32_t)elite_idx[e];
-    for (int d = threadIdx.x; d < a; d += REFIT_THREADS) {
+    for (int d = threadIdx.x; d < a; d += blockDim.x) {
         musg[d] = mu[t * a + d];
-        musg[((a + 3) & ~3) + d] = sigma[t * a + d];
+        musg[a4 + d] = sigma[t * a + d];
     }
     __syncthreads();
     const float* smu = musg;
-    const float* ssg = musg + ((a + 3) & ~3);
-    for (int idx = threadIdx.x; idx < K * G; idx += REFIT_THREADS) {
+    const float* ssg = musg + a4;
+    for (int idx = threadIdx.x; idx < K * G; idx += blockDim.x) {
         const int e = idx / G, g = idx - (idx / G) * G;
         float z[4];
         cem_normal4(seed, eidx[e], (uint32_t)t, (uint32_t)iteration, (uint32_t)g, z);
@@ -671,7 +679,7 @@ __global__ void __launch_bounds__(REFIT_THREADS) refit_fused_kernel(
     }
     __syncthreads();
     for (int pass = 0; pass < 2; ++pass) {
-        for (int idx = threadIdx.x; idx < nch * a; idx += REFIT_THREADS) {
+        for (int idx = threadIdx.x; idx < nch * a; idx += blockDim.x) {
             const int c = idx / a, d = idx - (idx / a) * a;
             const int e0 = c * ELITE_CHUNK, n = min(K - e0, ELITE_CHUNK);
             const float md = pass == 1 ? mean[d] : 0.f;
@@ -700,8 +708,9 @@ __global__ void __launch_bounds__(REFIT_THREADS) refit_fused_kernel(
                 const float mn = __fadd_rn(__fmul_rn(alpha, mu0), __fmul_rn(oma, mean[d]));
                 const float v = __fadd_rn(__fmul_rn(alpha, __fmul_rn(s0, s0)), __fmul_rn(oma, m));
                 const float sn = exact_sqrt(v);
-                mu_out[t * a + d] = mn;
-                sigma_out[t * a + d] = sn;
+                if (mu_out) mu_out[t * a + d] = mn;
+                if (sigma_out) sigma_out[t * a + d] = sn;
+                if (next) { next[d] = mn; next[a4 + d] = sn; }
                 if (fin_actions) {
                     if (fin_mu) fin_mu[t * a + d] = mn;
                     if (fin_sigma) fin_sigma[t * a + d] = sn;
@@ -713,10 +722,125 @@ __global__ void __launch_bounds__(REFIT_THREADS) refit_fused_kernel(
     }
 }
 
-static size_t refit_fused_lds(int a, int K) {
-    const size_t nch = (size_t)(K + ELITE_CHUNK - 1) / ELITE_CHUNK;
-    const size_t a4 = ((size_t)a + 3) & ~(size_t)3;
-    return ((((size_t)K * a + 3) & ~(size_t)3) + ((nch * a + 3) & ~(size_t)3) + 3 * a4 + (size_t)K) * sizeof(float);
+__global__ void __launch_bounds__(REFIT_THREADS) refit_fused_kernel(
+    uint64_t seed, int iteration, const float* __restrict__ mu, const float* __restrict__ sigma, float lo, float hi,
+    int a, const int64_t* __restrict__ elite_idx, int K, float alpha, float oma, float* __restrict__ mu_out,
+    float* __restrict__ sigma_out, float* __restrict__ fin_mu, float* __restrict__ fin_sigma,
+    float* __restrict__ fin_actions, int n_env) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    // batched planning: blockIdx.y = problem b, whose [H][a] distribution rows sit at b*H*a, whose
+    // K elites (local indices) at b*K, and whose candidates are global n = b*n_env + local
+    const int t = blockIdx.x, H = gridDim.x;
+    const size_t eo = (size_t)blockIdx.y * H * a;
+    const uint32_t nbase = (uint32_t)blockIdx.y * (uint32_t)n_env;
+    uint32_t* eidx = reinterpret_cast<uint32_t*>(smem + refit_rows_floats(a, K));   // [K]
+    elite_idx += (size_t)blockIdx.y * K;
+    for (int e = threadIdx.x; e < K; e += REFIT_THREADS) eidx[e] = nbase + (uint32_t)elite_idx[e];
+    refit_rows(t, eidx, smem, seed, iteration, mu + eo, sigma + eo, lo, hi, a, K, alpha, oma, mu_out + eo,
+               sigma_out + eo, fin_mu ? fin_mu + eo : nullptr, fin_sigma ? fin_sigma + eo : nullptr,
+               fin_actions ? fin_actions + eo : nullptr, nullptr);
+}
+
+static size_t refit_fused_lds(int a, int K) { return (refit_rows_floats(a, K) + (size_t)K) * sizeof(float); }
+
+// ------------------------------------------------------------------------------------------------
+// One launch per CEM iteration after the rollout (DESIGN.md §3 "update"): workgroup (t * S + j, b)
+// selects the elites of problem b (every workgroup of the problem the same, deterministic), refits
+// row t, and draws row t of the next iteration's proposals for candidate slice j of S from the new
+// mu_t, sigma_t. Bit-identical to select_reg_kernel + refit_fused_kernel + sample_kernel: the same
+// bodies in the same order. Three launches and their gaps become one; the selection and the row's
+// refit are repeated by the workgroups side by side instead of run once (no longer critical path),
+// and the draw -- ~400 VALU ops per Philox block -- is spread over S x H workgroups (~256 CUs).
+// ------------------------------------------------------------------------------------------------
+struct UpdateArgs {
+    const float* costs;
+    int E, N, K, member_stride, H, a;
+    int64_t* elite_out;          // [B][K] local indices (block t = 0 of each problem writes them), or NULL
+    float* returns_out;          // [B][N] member-mean returns (block t = 0), or NULL
+    uint64_t seed;
+    int iteration;
+    const float *mu, *sigma;     // [B][H][a] this iteration's distribution
+    float lo, hi, alpha, oma;
+    float *mu_out, *sigma_out;   // [B][H][a] the refit
+    float *fin_mu, *fin_sigma, *fin_actions;   // last iteration: plan outputs (or NULL)
+    float* next_actions;         // [H][B*N][a] proposals of iteration + 1, or NULL
+};
+
+__host__ __device__ inline size_t update_lds_words(int KPT, int a, int K) {
+    const size_t sel = (size_t)(33 * 32 * KPT > SEL_HIST_WORDS ? 33 * 32 * KPT : SEL_HIST_WORDS);
+    const size_t ref = refit_rows_floats(a, K);
+    return (((size_t)K + 3) & ~(size_t)3) + 2 * (((size_t)a + 3) & ~(size_t)3) + (sel > ref ? sel : ref);
+}
+
+template <int KPT>
+__global__ void __launch_bounds__(1024) cem_update_kernel(const UpdateArgs U) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t usmem[];
+    const int S = gridDim.x / U.H;                      // draw slices per row
+    const int t = blockIdx.x / S, j = blockIdx.x - (blockIdx.x / S) * S, b = blockIdx.y;
+    const bool lead = t == 0 && j == 0;                 // writes the elites and returns
+    const int K = U.K, N = U.N, a = U.a, a4 = (a + 3) & ~3;
+    uint32_t* eidx = usmem;                                                  // [K] global candidate index
+    float* next = reinterpret_cast<float*>(usmem + ((K + 3) & ~3));          // [2][a4] mu', sigma' of row t
+    uint32_t* work = usmem + ((K + 3) & ~3) + 2 * a4;                        // select, then refit
+    const uint32_t nbase = (uint32_t)b * (uint32_t)N;
+    int64_t* eo = (U.elite_out && lead) ? U.elite_out + (size_t)b * K : nullptr;
+    float* ro = (U.returns_out && lead) ? U.returns_out + (size_t)b * N : nullptr;
+    select_reg_body<KPT>(U.costs + (size_t)b * N, U.E, N, K, MBRL_NAN_LAST, ro, U.member_stride, work,
+                         [&](uint32_t pos, int n) {
+                             eidx[pos] = nbase + (uint32_t)n;
+                             if (eo) eo[pos] = n;
+                         });
+    __syncthreads();   // eidx complete; the selection's LDS becomes the refit's
+    const size_t rb = (size_t)b * U.H * a;
+    const bool w = j == 0;   // slice 0 of the row writes its refit
+    refit_rows(t, eidx, reinterpret_cast<float*>(work), U.seed, U.iteration, U.mu + rb, U.sigma + rb, U.lo, U.hi, a,
+               K, U.alpha, U.oma, w ? U.mu_out + rb : nullptr, w ? U.sigma_out + rb : nullptr,
+               (w && U.fin_mu) ? U.fin_mu + rb : nullptr, (w && U.fin_sigma) ? U.fin_sigma + rb : nullptr,
+               (w && U.fin_actions) ? U.fin_actions + rb : nullptr, U.next_actions ? next : nullptr);
+    if (U.next_actions) {   // refit_rows ended on a barrier: next[] is visible
+        const int G = (a + 3) >> 2;
+        const size_t BN = (size_t)gridDim.y * N;
+        const int NS = (N + S - 1) / S, n0 = j * NS, n1 = min(N, n0 + NS);
+        for (int idx = threadIdx.x; idx < (n1 - n0) * G; idx += 1024) {
+            const int n = n0 + idx / G, g = idx - (idx / G) * G;
+            float z[4];
+            cem_normal4(U.seed, nbase + (uint32_t)n, (uint32_t)t, (uint32_t)(U.iteration + 1), (uint32_t)g, z);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int d = 4 * g + j;
+                if (d < a)
+                    U.next_actions[((size_t)t * BN + nbase + n) * a + d] = cem_action(next[d], next[a4 + d], z[j], U.lo, U.hi);
+            }
+        }
+    }
+}
+
+// The plan's first launch: workgroup (t * S + j, b) sets row t of problem b's distribution to
+// (init_mu, init_sigma) and, with `actions`, draws row t of iteration 0's proposals for candidate
+// slice j (fill2_kernel + sample_kernel, bit-identical: the same floats go into cem_action).
+__global__ void __launch_bounds__(1024) cem_init_kernel(uint64_t seed, float init_mu, float init_sigma, float lo,
+                                                        float hi, int H, int a, int N, float* __restrict__ mu,
+                                                        float* __restrict__ sigma, float* __restrict__ actions) {
+    const int S = gridDim.x / H;
+    const int t = blockIdx.x / S, j = blockIdx.x - (blockIdx.x / S) * S, b = blockIdx.y;
+    const size_t ro = ((size_t)b * H + t) * a;
+    if (j == 0)
+        for (int d = threadIdx.x; d < a; d += blockDim.x) { mu[ro + d] = init_mu; sigma[ro + d] = init_sigma; }
+    if (!actions) return;
+    const int G = (a + 3) >> 2;
+    const size_t BN = (size_t)gridDim.y * N;
+    const uint32_t nbase = (uint32_t)b * (uint32_t)N;
+    const int NS = (N + S - 1) / S, n0 = j * NS, n1 = min(N, n0 + NS);
+    for (int idx = threadIdx.x; idx < (n1 - n0) * G; idx += blockDim.x) {
+        const int n = n0 + idx / G, g = idx - (idx / G) * G;
+        float z[4];
+        cem_normal4(seed, nbase + (uint32_t)n, (uint32_t)t, 0u, (uint32_t)g, z);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int d = 4 * g + j;
+            if (d < a) actions[((size_t)t * BN + nbase + n) * a + d] = cem_action(init_mu, init_sigma, z[j], lo, hi);
+        }
+    }
 }
 
 // Batched planning: local candidate n belongs to problem n / n_env, whose distribution rows sit at
@@ -949,7 +1073,7 @@ static int select_impl(const float* costs, int E, int N, int K, int nan_policy, 
     const int member_stride = N * segments;
 #define MBRL_SEL(KPT)                                                                                       \
     if (N <= 1024 * (KPT)) {                                                                                \
-        const size_t lds = 4 * (size_t)max(33 * 32 * (KPT), SEL_HIST_WORDS);                               \
+        const size_t lds = select_reg_lds(KPT);                                                             \
         hipError_t err = ensure_dynamic_lds(reinterpret_cast<const void*>(&select_reg_kernel<KPT>), (int)lds); \
         if (err != hipSuccess) return hip_check(err, "select attribute");                                   \
         hipLaunchKernelGGL(select_reg_kernel<KPT>, dim3(segments), dim3(1024), lds, stream, costs, E, N, K,  \
@@ -994,6 +1118,46 @@ static int refit_impl(const mbrl_sampler* sp, int H, int a, const int64_t* elite
         hipLaunchKernelGGL(finalize_kernel, dim3((H * a + 255) / 256), dim3(256), 0, stream, mu_out, sigma_out,
                            sp->lo, sp->hi, H * a, fin_mu, fin_sigma, fin_actions);
     return hip_check(hipGetLastError(), "refit launch");
+}
+
+// The fused per-iteration update (cem_update_kernel) when its selection fits in registers (N <= 32768)
+// and the selection or refit working set fits LDS; KPT of that selection, 0 if not fusable.
+static int update_kpt(int N, int K, int a) {
+    if (a > 64 || K < 1 || K > N) return 0;
+    for (int kpt = 1; kpt <= 32; kpt *= 2)
+        if (N <= 1024 * kpt) return update_lds_words(kpt, a, K) * 4 + 1024 <= 160 * 1024 ? kpt : 0;   // + static LDS
+    return 0;
+}
+
+// Whether the update also draws the next iteration's proposals: at most 64 Philox blocks per thread
+// (the H blocks of the launch draw N x H x a values between them).
+static bool update_samples(int N, int a) { return (size_t)N * ((a + 3) / 4) <= 64 * 1024; }
+
+// Candidate slices per row for the fused draw: about 256 workgroups in all (one per CU; each runs the
+// selection too), and no slice under 256 Philox blocks.
+static int draw_slices(int H, int B, int N, int a) {
+    const long hb = (long)H * B;
+    long s = 256 / hb;
+    const long cap = ((long)N * ((a + 3) / 4) + 255) / 256;
+    if (s > cap) s = cap;
+    return s < 1 ? 1 : (int)s;
+}
+
+static int update_impl(const UpdateArgs& U, int B, hipStream_t stream) {
+    const int kpt = update_kpt(U.N, U.K, U.a);
+    if (!kpt) return fail(MBRL_EUNSUPPORTED, "update: N=%d K=%d a=%d not fusable", U.N, U.K, U.a);
+    const size_t lds = update_lds_words(kpt, U.a, U.K) * 4;
+    const int S = U.next_actions ? draw_slices(U.H, B, U.N, U.a) : 1;
+#define MBRL_UPD(KPT)                                                                                            \
+    if (kpt == KPT) {                                                                                           \
+        hipError_t err = ensure_dynamic_lds(reinterpret_cast<const void*>(&cem_update_kernel<KPT>), (int)lds);   \
+        if (err != hipSuccess) return hip_check(err, "update attribute");                                       \
+        hipLaunchKernelGGL(cem_update_kernel<KPT>, dim3(U.H * S, B), dim3(1024), lds, stream, U);                \
+        return hip_check(hipGetLastError(), "update launch");                                                   \
+    }
+    MBRL_UPD(1) MBRL_UPD(2) MBRL_UPD(4) MBRL_UPD(8) MBRL_UPD(16) MBRL_UPD(32)
+#undef MBRL_UPD
+    return fail(MBRL_EUNSUPPORTED, "update: KPT %d", kpt);
 }
 
 }  // namespace mbrl
@@ -1254,8 +1418,17 @@ int mbrl_cem_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_no
     PlanWs w = plan_ws(g, p, workspace);
     if (ws_bytes < w.bytes) return fail(MBRL_EWORKSPACE, "workspace %zu < %zu", ws_bytes, w.bytes);
     const int Ha = p->H * g.a;
-    hipLaunchKernelGGL(fill2_kernel, dim3((Ha + 255) / 256), dim3(256), 0, stream, w.mu[0], p->init_mu, w.sigma[0],
-                       p->init_sigma, Ha);
+    // Launches per iteration: rollout + one fused update (select, refit, next proposals) where it fits;
+    // else the proposal draw, rollout, select and refit as separate launches.
+    const bool fuse = update_kpt(p->N, p->K, g.a) != 0 && g_opt[MBRL_OPT_UNFUSED_UPDATE].load(std::memory_order_relaxed) == 0;
+    const bool fuse_draw = fuse && update_samples(p->N, g.a);
+    if (fuse_draw)
+        hipLaunchKernelGGL(cem_init_kernel, dim3(p->H * draw_slices(p->H, 1, p->N, g.a), 1), dim3(1024), 0, stream,
+                           p->seed, p->init_mu, p->init_sigma, p->lo, p->hi, p->H, g.a, p->N, w.mu[0], w.sigma[0],
+                           w.actions);
+    else
+        hipLaunchKernelGGL(fill2_kernel, dim3((Ha + 255) / 256), dim3(256), 0, stream, w.mu[0], p->init_mu, w.sigma[0],
+                           p->init_sigma, Ha);
     int cur = 0;
     for (int it = 0; it < p->iterations; ++it) {
         mbrl_sampler sp{};
@@ -1267,17 +1440,30 @@ int mbrl_cem_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_no
             rc = hip_check(hipEventRecord(reinterpret_cast<hipEvent_t>(rollout_events[2 * it]), stream), "event");
             if (rc) return rc;
         }
-        rc = rollout_impl(g, packed, norm, cost, s0, 0, nullptr, &sp, p->N, p->H, 0, costs, w.actions, nullptr, stream);
+        rc = rollout_impl(g, packed, norm, cost, s0, 0, fuse_draw ? w.actions : nullptr, fuse_draw ? nullptr : &sp, p->N,
+                          p->H, 0, costs, w.actions, nullptr, stream);
         if (rc) return rc;
         if (rollout_events && rollout_events[2 * it + 1]) {
             rc = hip_check(hipEventRecord(reinterpret_cast<hipEvent_t>(rollout_events[2 * it + 1]), stream), "event");
             if (rc) return rc;
         }
-        rc = select_impl(costs, g.E, p->N, p->K, MBRL_NAN_LAST, elites, rets, w.keys, align256((size_t)p->N * 4), stream);
-        if (rc) return rc;
         const bool last = it + 1 == p->iterations;   // the last refit also writes mu / sigma / clip(mu)
-        rc = refit_impl(&sp, p->H, g.a, elites, p->K, p->alpha, w.aelite, w.mu[cur ^ 1], w.sigma[cur ^ 1], stream,
-                        last ? mu : nullptr, last ? sigma : nullptr, last ? actions_out : nullptr);
+        if (fuse) {
+            UpdateArgs U{};
+            U.costs = costs; U.E = g.E; U.N = p->N; U.K = p->K; U.member_stride = p->N; U.H = p->H; U.a = g.a;
+            U.elite_out = elites; U.returns_out = rets;
+            U.seed = p->seed; U.iteration = it; U.mu = w.mu[cur]; U.sigma = w.sigma[cur];
+            U.lo = p->lo; U.hi = p->hi; U.alpha = p->alpha; U.oma = 1.0f - p->alpha;
+            U.mu_out = w.mu[cur ^ 1]; U.sigma_out = w.sigma[cur ^ 1];
+            U.fin_mu = last ? mu : nullptr; U.fin_sigma = last ? sigma : nullptr; U.fin_actions = last ? actions_out : nullptr;
+            U.next_actions = (fuse_draw && !last) ? w.actions : nullptr;
+            rc = update_impl(U, 1, stream);
+        } else {
+            rc = select_impl(costs, g.E, p->N, p->K, MBRL_NAN_LAST, elites, rets, w.keys, align256((size_t)p->N * 4), stream);
+            if (rc) return rc;
+            rc = refit_impl(&sp, p->H, g.a, elites, p->K, p->alpha, w.aelite, w.mu[cur ^ 1], w.sigma[cur ^ 1], stream,
+                            last ? mu : nullptr, last ? sigma : nullptr, last ? actions_out : nullptr);
+        }
         if (rc) return rc;
         cur ^= 1;
     }
@@ -1353,25 +1539,46 @@ int mbrl_cem_plan_batch(const mbrl_mlp_shape* shape, const void* packed, const m
     BatchWs w = batch_ws(g, p, B, workspace);
     if (ws_bytes < w.bytes) return fail(MBRL_EWORKSPACE, "workspace %zu < %zu", ws_bytes, w.bytes);
     const int BN = B * p->N, BHa = B * p->H * g.a;
-    hipLaunchKernelGGL(fill2_kernel, dim3((BHa + 255) / 256), dim3(256), 0, stream, w.mu[0], p->init_mu, w.sigma[0],
-                       p->init_sigma, BHa);
+    // as mbrl_cem_plan: one fused update launch per iteration where it fits (grid (H, B))
+    const bool fuse = update_kpt(p->N, p->K, g.a) != 0 && g_opt[MBRL_OPT_UNFUSED_UPDATE].load(std::memory_order_relaxed) == 0;
+    const bool fuse_draw = fuse && update_samples(p->N, g.a);
+    if (fuse_draw)
+        hipLaunchKernelGGL(cem_init_kernel, dim3(p->H * draw_slices(p->H, B, p->N, g.a), B), dim3(1024), 0, stream,
+                           p->seed, p->init_mu, p->init_sigma, p->lo, p->hi, p->H, g.a, p->N, w.mu[0], w.sigma[0],
+                           w.actions);
+    else
+        hipLaunchKernelGGL(fill2_kernel, dim3((BHa + 255) / 256), dim3(256), 0, stream, w.mu[0], p->init_mu,
+                           w.sigma[0], p->init_sigma, BHa);
     hipLaunchKernelGGL(expand_rows_kernel, dim3(256), dim3(256), 0, stream, s0, B, p->N, g.s, w.s0x);
     int cur = 0;
     for (int it = 0; it < p->iterations; ++it) {
         mbrl_sampler sp{};
         sp.seed = p->seed; sp.iteration = it; sp.mu = w.mu[cur]; sp.sigma = w.sigma[cur]; sp.lo = p->lo; sp.hi = p->hi;
         // problem b's candidate n is global candidate b*N + n (its Philox counter)
-        rc = sample_impl(&sp, p->H, g.a, BN, 0, w.actions, stream, p->N);
-        if (rc) return rc;
+        if (!fuse_draw) {
+            rc = sample_impl(&sp, p->H, g.a, BN, 0, w.actions, stream, p->N);
+            if (rc) return rc;
+        }
         rc = rollout_impl(g, packed, norm, cost, w.s0x, 1, w.actions, nullptr, BN, p->H, 0, w.costs, nullptr, nullptr,
                           stream);
         if (rc) return rc;
-        rc = select_impl(w.costs, g.E, p->N, p->K, MBRL_NAN_LAST, w.elites, nullptr, w.keys, align256((size_t)BN * 4),
-                         stream, B);
-        if (rc) return rc;
         const bool last = it + 1 == p->iterations;
-        rc = refit_impl(&sp, p->H, g.a, w.elites, p->K, p->alpha, nullptr, w.mu[cur ^ 1], w.sigma[cur ^ 1], stream,
-                        last ? mu : nullptr, last ? sigma : nullptr, last ? actions_out : nullptr, B, p->N);
+        if (fuse) {
+            UpdateArgs U{};
+            U.costs = w.costs; U.E = g.E; U.N = p->N; U.K = p->K; U.member_stride = BN; U.H = p->H; U.a = g.a;
+            U.seed = p->seed; U.iteration = it; U.mu = w.mu[cur]; U.sigma = w.sigma[cur];
+            U.lo = p->lo; U.hi = p->hi; U.alpha = p->alpha; U.oma = 1.0f - p->alpha;
+            U.mu_out = w.mu[cur ^ 1]; U.sigma_out = w.sigma[cur ^ 1];
+            U.fin_mu = last ? mu : nullptr; U.fin_sigma = last ? sigma : nullptr; U.fin_actions = last ? actions_out : nullptr;
+            U.next_actions = (fuse_draw && !last) ? w.actions : nullptr;
+            rc = update_impl(U, B, stream);
+        } else {
+            rc = select_impl(w.costs, g.E, p->N, p->K, MBRL_NAN_LAST, w.elites, nullptr, w.keys,
+                             align256((size_t)BN * 4), stream, B);
+            if (rc) return rc;
+            rc = refit_impl(&sp, p->H, g.a, w.elites, p->K, p->alpha, nullptr, w.mu[cur ^ 1], w.sigma[cur ^ 1], stream,
+                            last ? mu : nullptr, last ? sigma : nullptr, last ? actions_out : nullptr, B, p->N);
+        }
         if (rc) return rc;
         cur ^= 1;
     }

@@ -2,7 +2,7 @@
 
     python tools/plan_timeline.py <prof dir> <bench json log> <steps> <out json>
 
-A plan starts at its fill2_kernel (mbrl_cem_plan's first launch). Over the last `steps` plans (the
+A plan starts at its fill2_kernel or cem_init_kernel (mbrl_cem_plan's first launch). Over the last `steps` plans (the
 timed ones) it reports: the rollout kernel's mean dispatch duration next to bench.py's HIP-event
 figure (they must agree: the roofline's `achieved` divides by the latter), GPU busy time per kernel
 family per plan, the idle gaps inside a plan (launch-to-launch), and the idle time between plans
@@ -14,9 +14,9 @@ import os
 import re
 import sys
 
-FAMILIES = [("rollout", r"rollout(_m8|_split)?_kernel<"), ("sample", r"sample_kernel"),
+FAMILIES = [("rollout", r"rollout(_m8|_split)?_kernel<"), ("update", r"cem_update_kernel"), ("sample", r"sample_kernel"),
             ("select", r"select(_reg)?_kernel"), ("refit", r"refit|gather_elites|finalize_kernel"),
-            ("trajectory", r"traj(_coop)?_kernel|member_mean"), ("fill", r"fill2_kernel"),
+            ("trajectory", r"traj(_coop)?_kernel|member_mean"), ("fill", r"fill2_kernel|cem_init_kernel"),
             ("memset", r"fillBuffer|[Mm]emset")]
 
 
@@ -32,7 +32,7 @@ def main():
     trace = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)[0]
     rows = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"])
                   for r in csv.DictReader(open(trace)))
-    starts = [i for i, r in enumerate(rows) if "fill2_kernel" in r[2]]
+    starts = [i for i, r in enumerate(rows) if "fill2_kernel" in r[2] or "cem_init_kernel" in r[2]]
     plans = [rows[a:b] for a, b in zip(starts, starts[1:] + [len(rows)])][-steps:]
     fams = sorted({family(r[2]) for p in plans for r in p})
     busy = {f: 0.0 for f in fams}
