@@ -242,13 +242,16 @@ int mbrl_cem_plan_batch(const mbrl_mlp_shape* shape, const void* packed, const m
 
 /* ---- gradient-descent planner: replaces GradientDescentPlanner's
  * _optimize_trajectory (planners.py:103-137) -- Adam(lr) on the action sequence through the dynamics
- * with the goal-state cost, stopping once mean |delta a| < stop_condition -- as one launch (forward,
+ * with the goal-state cost (or, for a reward_head model, the MODEL_REWARD cost of RewardAgent,
+ * agents.py:336-362), stopping once mean |delta a| < stop_condition -- as one launch (forward,
  * backward and the Adam step on the device; no host round trip per iteration): Wpad/16 cooperating
- * workgroups that hand hidden vectors to each other, or one workgroup where those do not apply.
+ * workgroups that hand hidden vectors to each other, or one workgroup where those do not apply
+ * (reward-head models, shapes outside the cooperative kernel's).
  * actions: [H][a] device, in: the initial sequence, out: the optimised one. states_out: [H+1][s]
  * = the last iteration's rollout (computed before its update, as the reference returns it).
- * iterations_out: device int32 (iterations run) or NULL. Needs ensemble == 1, reward_head == 0 and a
- * GOAL_STATE cost (else MBRL_EUNSUPPORTED). workspace >= mbrl_gd_workspace_bytes(shape, H). */
+ * iterations_out: device int32 (iterations run) or NULL. Needs ensemble == 1 and a GOAL_STATE cost
+ * (reward_head == 0) or a MODEL_REWARD cost (reward_head == 1), else MBRL_EUNSUPPORTED.
+ * workspace >= mbrl_gd_workspace_bytes(shape, H). */
 size_t mbrl_gd_workspace_bytes(const mbrl_mlp_shape* shape, int32_t H);
 int mbrl_gd_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_norm* norm, const mbrl_cost* cost,
                  const float* s0, float* actions, int32_t H, int32_t num_iterations, float stop_condition,

@@ -1610,7 +1610,7 @@ static GdWs gd_ws(const Geometry& g, int H, void* base) {
     size_t o = 0;
     auto take = [&](size_t n) { void* r = b ? b + o : nullptr; o += align256(n); return r; };
     const size_t ha = (size_t)H * g.a;
-    const size_t row = (size_t)((g.s + g.a + 3) & ~3) + (size_t)g.L * g.Wpad;
+    const size_t row = ((size_t)((g.s + g.a + 3) & ~3) + (size_t)g.L * g.Wpad) * (g.reward ? 2 : 1);
     const size_t coop = (size_t)(g.Wpad / 16) * H * g.L * g.Wpad;   // per-workgroup hidden-vector copies
     w.xchg = (unsigned long long*)take((size_t)2 * g.Wpad * 8 + 16);   // granules, then the status word
     w.status = w.xchg ? reinterpret_cast<unsigned*>(w.xchg + 2 * g.Wpad) : nullptr;
@@ -1633,12 +1633,13 @@ int mbrl_gd_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_nor
     Geometry g;
     int rc = shape_geometry(shape, &g);
     if (rc) return rc;
-    if (g.E != 1 || g.reward) return fail(MBRL_EUNSUPPORTED, "gd_plan: needs ensemble == 1 and no reward head");
-    if (!cost || cost->kind != MBRL_COST_GOAL_STATE) return fail(MBRL_EUNSUPPORTED, "gd_plan: needs a GOAL_STATE cost");
+    if (g.E != 1) return fail(MBRL_EUNSUPPORTED, "gd_plan: needs ensemble == 1");
+    if (!cost || cost->kind != (g.reward ? MBRL_COST_MODEL_REWARD : MBRL_COST_GOAL_STATE))
+        return fail(MBRL_EUNSUPPORTED, "gd_plan: needs a GOAL_STATE cost, or MODEL_REWARD with a reward-head model");
     if (!packed || !s0 || !actions || !states_out || !workspace) return fail(MBRL_EINVAL, "gd_plan: NULL argument");
     if (H < 1 || num_iterations < 0) return fail(MBRL_EINVAL, "gd_plan: H=%d iterations=%d", H, num_iterations);
     if (gd_lds_bytes(g.s, g.a, g.Wpad, H) > 160 * 1024) return fail(MBRL_EUNSUPPORTED, "gd_plan: H * a too large");
-    if (cost->has_state_cost && (!cost->weights || !cost->goal))
+    if (!g.reward && cost->has_state_cost && (!cost->weights || !cost->goal))
         return fail(MBRL_EINVAL, "gd_plan: state cost without weights/goal");
     GdArgs A{};
     const GdWs w = gd_ws(g, H, workspace);
@@ -1657,12 +1658,18 @@ int mbrl_gd_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_nor
             return fail(MBRL_EINVAL, "state normalisation requested without obs_mean/obs_std");
         if (A.norm_a && (!A.act_mean || !A.act_std))
             return fail(MBRL_EINVAL, "action normalisation requested without act_mean/act_std");
+        A.unnorm_r = g.reward ? norm->unnormalize_reward : 0;
+        A.rew_std = norm->rew_std;
+        if (A.unnorm_r && !A.rew_std) return fail(MBRL_EINVAL, "reward unnormalisation requested without rew_std");
     }
-    A.cw = cost->weights; A.goal = cost->goal;
-    A.alpha_s = cost->alpha_state; A.alpha_a = cost->alpha_action;
-    A.has_sc = cost->has_state_cost; A.has_ac = cost->has_action_cost;
+    A.reward = g.reward;
+    if (!g.reward) {
+        A.cw = cost->weights; A.goal = cost->goal;
+        A.alpha_s = cost->alpha_state; A.alpha_a = cost->alpha_action;
+        A.has_sc = cost->has_state_cost; A.has_ac = cost->has_action_cost;
+    }
     A.s0 = s0; A.actions = actions; A.states_out = states_out;
-    A.hist_row = ((g.s + g.a + 3) & ~3) + g.L * g.Wpad;
+    A.hist_row = (((g.s + g.a + 3) & ~3) + g.L * g.Wpad) * (g.reward ? 2 : 1);
     A.iterations = num_iterations; A.stop = stop_condition; A.lr = lr;
     A.iterations_out = iterations_out;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);

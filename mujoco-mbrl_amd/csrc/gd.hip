@@ -11,6 +11,9 @@
 // Semantics per iteration (planners.py:117-135 with the GoalStateAgent closures, agents.py:219-233):
 //   s_{t+1} = unnorm(MLP(norm(s_t), norm(a_t)))       for t < H      (states_out rows 1..H)
 //   loss    = sum_t SmoothAbs(s_{t+1}) + CoshLoss(a_t)                (models.py:244-272)
+// or, for a reward-head model behind RewardAgent's closures (agents.py:336-362; one-workgroup kernel):
+//   loss    = sum_t unnorm_r(reward head of the trunk at (norm(s_{t+1}), norm(a_t)))
+//   -- a second trunk pass per step, whose activations are saved and back-propagated as well.
 //   grad    = d loss / d a  (reverse mode through the chain; ReLU' = [output > 0] as torch)
 //   Adam(lr, betas = (0.9, 0.999), eps = 1e-8) as torch.optim.Adam: m.lerp_(g, 1 - b1),
 //   v = b2 v + (1 - b2) g^2, a -= (lr / (1 - b1^k)) m / (sqrt(v) / sqrt(1 - b2^k) + eps)
@@ -190,12 +193,64 @@ __global__ void __launch_bounds__(GD_THREADS) gd_plan_kernel(const GdArgs A) {
             }
             __threadfence_block();
             __syncthreads();
+            if (A.reward) {
+                // the cost call's trunk pass on (s_{t+1}, a_t): only its activations are needed (the
+                // reward's derivative w.r.t. its head is the constant rew_std)
+                float* hb = hist + rowf / 2;
+                for (int d = tid; d < K0; d += GD_THREADS) {
+                    float v;
+                    if (d < s) {
+                        const float sv = A.states_out[(size_t)(t + 1) * s + d];
+                        v = A.norm_s ? (sv - A.obs_mean[d]) / A.obs_std[d] : sv;
+                    } else {
+                        v = hist[d];   // norm(a_t), as the state pass
+                    }
+                    m.x[d] = v;
+                    hb[d] = v;
+                }
+                __syncthreads();
+                gd_dense_relu(lw[0], bias, K0, Wp, m.x, m.part, m.h);
+                for (int n = tid; n < Wp; n += GD_THREADS) hb[K0p + n] = m.h[n];
+                for (int l = 1; l < L; ++l) {
+                    gd_dense_relu(lw[l], bias + (size_t)l * Wp, A.W, Wp, m.h, m.part, m.x);
+                    for (int n = tid; n < Wp; n += GD_THREADS) { m.h[n] = m.x[n]; hb[K0p + l * Wp + n] = m.x[n]; }
+                    __syncthreads();
+                }
+            }
         }
         // ---------------- backward: d loss / d a, t = H-1 .. 0
         for (int d = tid; d < s; d += GD_THREADS) m.gs[d] = 0.f;
         __syncthreads();
         for (int t = H - 1; t >= 0; --t) {
             const float* hist = A.hist + (size_t)t * rowf;
+            if (A.reward) {
+                // reward pass backward: d r_t / d head = rew_std (unnormalise_reward), through the
+                // reward row of the output block and the pass's saved ReLU masks to its input
+                // (norm(s_{t+1}), norm(a_t)); the state part joins gs, the action part waits in m.ga
+                const float* hb = hist + rowf / 2;
+                const float gr = A.unnorm_r ? A.rew_std[0] : 1.0f;
+                const float* hl = hb + K0p + (size_t)(L - 1) * Wp;
+                for (int k = tid; k < Wp; k += GD_THREADS)
+                    m.gz[k] = (k < A.W && hl[k] > 0.f) ? wout[(size_t)s * A.W + k] * gr : 0.f;
+                __syncthreads();
+                for (int l = L - 1; l >= 1; --l) {
+                    gd_dense_back(lw[l], A.W, Wp, m.gz, m.gx);
+                    const float* hp = hb + K0p + (size_t)(l - 1) * Wp;
+                    for (int k = tid; k < Wp; k += GD_THREADS) m.gz[k] = (k < A.W && hp[k] > 0.f) ? m.gx[k] : 0.f;
+                    __syncthreads();
+                }
+                gd_dense_back(lw[0], K0, Wp, m.gz, m.gx);
+                for (int d = tid; d < K0; d += GD_THREADS) {
+                    const float g = m.gx[d];
+                    if (d < s) {
+                        m.gs[d] += A.norm_s ? g / A.obs_std[d] : g;
+                    } else {
+                        const int j = d - s;
+                        m.ga[t * a + j] = A.norm_a ? g / A.act_std[j] : g;
+                    }
+                }
+                __syncthreads();
+            }
             // gs += d SmoothAbs / d s_{t+1}; g_out = gs * obs_std (s_{t+1} = out * std + mean)
             for (int d = tid; d < s; d += GD_THREADS) {
                 float g = m.gs[d];
@@ -233,6 +288,7 @@ __global__ void __launch_bounds__(GD_THREADS) gd_plan_kernel(const GdArgs A) {
                     float ga = A.norm_a ? g / A.act_std[j] : g;
                     if (A.has_ac)
                         ga += A.alpha_a * sinhf(A.actions[t * a + j] / A.alpha_a) / (float)a;
+                    if (A.reward) ga += m.ga[t * a + j];   // the reward pass's share (above)
                     m.ga[t * a + j] = ga;
                 }
             }
@@ -619,7 +675,7 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
 
 bool gd_coop_supported(const GdArgs& A) {
     const int K0 = A.s + A.a;
-    if (A.L < 2 || A.W != A.Wpad || A.Wpad > GC_THREADS || A.Wpad < 64 || K0 > 32 || A.s > 32) return false;
+    if (A.reward || A.L < 2 || A.W != A.Wpad || A.Wpad > GC_THREADS || A.Wpad < 64 || K0 > 32 || A.s > 32) return false;
     return gc_lds(A.s, A.a, A.W, A.Wpad, A.L, A.H, 32).total <= 160 * 1024;
 }
 

@@ -240,12 +240,15 @@ struct GdArgs {
     const float *cw, *goal;
     float alpha_s, alpha_a;
     int has_sc, has_ac;
+    int reward;                            // cost = unnormalised reward head at (s_{t+1}, a_t): 2 passes / step
+    int unnorm_r;
+    const float* rew_std;                  // [1] (device) when unnorm_r
     const float* s0;                       // [s]
     float* actions;                        // [H][a], in: initial sequence, out: optimised
     float* states_out;                     // [H+1][s]: the last iteration's rollout
     float *m, *v;                          // Adam moments [H][a] (workspace)
     float* hist;                           // [H][hist_row] saved layer inputs (workspace)
-    int hist_row;                          // round4(s + a) + L * Wpad
+    int hist_row;                          // (round4(s + a) + L * Wpad), twice with a reward head
     int iterations;
     float stop, lr;
     int* iterations_out;                   // device int or NULL

@@ -8,10 +8,10 @@ lists of [1, s] / [1, a] tensors.
 
 Recognised closures (the same introspection as the CEM path: GoalStateAgent's and RewardAgent's
 wiring) run on the device:
-  * a single model with the goal-state cost -> mbrl_gd_plan (csrc/gd.hip): one persistent
-    workgroup runs every iteration's rollout, backward pass, Adam step and stop test; the host
-    waits once per plan;
-  * ensembles and reward-head models -> a device restatement as differentiable torch ops: the MLP,
+  * a single model with the goal-state cost, or a reward-head model with RewardAgent's reward cost
+    -> mbrl_gd_plan (csrc/gd.hip): one launch runs every iteration's rollout, backward pass, Adam
+    step and stop test; the host waits once per plan;
+  * ensembles -> a device restatement as differentiable torch ops: the MLP,
     normalisers and cost rebuilt from the described nn.Linear weights and statistics; the
     forward + loss + backward of one iteration (a chain of H x (L + 1) batch-1 layers) is captured
     once in a HIP graph and replayed each iteration; the Adam step and the stop test stay eager,
@@ -134,8 +134,8 @@ class _Iteration:
 
 
 def fused_supported(mdesc, cdesc, dev):
-    return (dev.type == "cuda" and mdesc["E"] == 1 and not mdesc.get("reward")
-            and cdesc is not None and cdesc["kind"] == _lib.MBRL_COST_GOAL_STATE)
+    want = _lib.MBRL_COST_MODEL_REWARD if mdesc.get("reward") else _lib.MBRL_COST_GOAL_STATE
+    return dev.type == "cuda" and mdesc["E"] == 1 and cdesc is not None and cdesc["kind"] == want
 
 
 def plan_fused(initial_state, mdesc, cdesc, action_list, horizon, num_iterations, stop_condition, dev, lr=0.01):

@@ -6,6 +6,10 @@ GoalStateAgent wires model and cost (agents.py:219-233).
 
 Problems come from oracle.cem.synth_problem (weights pinned by SHA-256). The initial action
 sequence is given explicitly (PCG64 seed 99), so no RNG is involved in the plan itself.
+
+gd_toy_abs_H5 is the reference's own known-answer script, src/mbrl/test_gradient_planner.py:5-27
+(s' = s + a, cost |s - 9|, s0 = [2], horizon 5, 40 Adam iterations, the initial sequence drawn by
+sample_action = torch.randn((batch, 1)) under torch.manual_seed(0)); the draw is stored with it.
 """
 import functools
 import os
@@ -57,5 +61,41 @@ def main():
         print(name, "states", st.shape, "actions[0]", ac[0])
 
 
+TOY = dict(s0=2.0, goal=9.0, H=5, iterations=40, seed=0)
+
+
+def toy_model(states, actions):
+    """test_gradient_planner.py:13-14"""
+    return states + actions
+
+
+def toy_cost(states, actions, goal=torch.tensor(TOY["goal"], dtype=torch.float)):
+    """test_gradient_planner.py:19-20"""
+    return torch.abs(states - goal)
+
+
+def main_toy():
+    sys.path.insert(0, REF)
+    from src.mbrl import planners
+    torch.manual_seed(TOY["seed"])
+    drawn = []
+
+    def sample_action(batch_size):   # test_gradient_planner.py:16-17, recording the draw
+        x = torch.randn((batch_size, 1))
+        drawn.append(x.clone())
+        return x
+
+    states, actions = planners.GradientDescentPlanner.plan(
+        torch.tensor([TOY["s0"]], dtype=torch.float), toy_model, toy_cost, sample_action, TOY["H"], None,
+        num_iterations=TOY["iterations"])
+    st = torch.cat(states).numpy()
+    ac = torch.cat(actions).numpy()
+    total = float(toy_cost(torch.stack(states), torch.cat(actions)).sum())
+    np.savez_compressed(os.path.join(HERE, "gd_toy_abs_H5.npz"), sampled=drawn[0].numpy(), states=st, actions=ac,
+                        total_cost=np.float32(total))
+    print("gd_toy_abs_H5 states", st.ravel(), "actions", ac.ravel(), "cost", total)
+
+
 if __name__ == "__main__":
     main()
+    main_toy()

@@ -72,10 +72,12 @@ def test_gd_graph_replay_equals_eager():
 @pytest.mark.gpu
 @pytest.mark.parametrize("cid,over,H,iters,stop", [(3, dict(W=50, L=2), 10, 25, 0.0), (2, {}, 12, 40, 0.002),
                                                   (3, {}, 30, 15, 0.0), (3, dict(W=200, L=3), 8, 40, 0.01),
-                                                  (2, {}, 5, 0, 0.0)])
+                                                  (2, {}, 5, 0, 0.0), (6, dict(W=64, L=2), 8, 30, 0.002),
+                                                  (6, {}, 10, 20, 0.0), (6, dict(W=100, L=3), 6, 25, 0.001)])
 def test_gd_fused_kernel_matches_graph_path(cid, over, H, iters, stop):
-    """mbrl_gd_plan (one persistent workgroup: forward, backward, Adam, stop test on the device) against
-    the graph-replayed torch restatement of the same loop, including early stops and zero iterations."""
+    """mbrl_gd_plan (forward, backward, Adam, stop test on the device in one launch) against the
+    graph-replayed torch restatement of the same loop, including early stops and zero iterations, and
+    reward-head models (config 6: RewardAgent's reward cost, two trunk passes per step)."""
     from mbrl_amd import gd
     p, model_fn, cost_fn = closures(cid, over)
     mdesc, cdesc = gd.describe(model_fn, cost_fn)
@@ -114,3 +116,26 @@ def test_gd_cooperative_kernel_and_its_fallback(mode):
     assert int(n1.item()) == int(n2.item())
     assert torch.allclose(a1, a2, rtol=1e-4, atol=1e-5), float((a1 - a2).abs().max())
     assert torch.allclose(s1, s2, rtol=1e-4, atol=1e-4), float((s1 - s2).abs().max())
+
+
+def test_gd_reference_toy_known_answer(golden):
+    """The reference's own gradient-planner script (src/mbrl/test_gradient_planner.py:5-27): s' = s + a,
+    cost |s - 9|, s0 = [2], horizon 5, 40 Adam steps from a torch.randn draw. Plain callables take the
+    generic path; states, actions and the printed total cost match the reference run
+    (tests/golden/make_golden_gd.py main_toy, which stores the draw)."""
+    from mbrl_amd import GradientDescentPlanner
+    g = golden("gd_toy_abs_H5")
+    drawn = torch.from_numpy(g["sampled"])
+
+    def sample_action(batch_size):
+        assert batch_size == 5
+        return drawn.clone()
+
+    states, actions = GradientDescentPlanner.plan(torch.tensor([2.0]), mgd.toy_model, mgd.toy_cost, sample_action, 5,
+                                                  None, num_iterations=40)
+    assert len(states) == 6 and len(actions) == 5
+    st, ac = torch.cat(states).numpy(), torch.cat(actions).numpy()
+    assert np.allclose(st, g["states"], rtol=1e-6, atol=1e-6), (st.ravel(), g["states"].ravel())
+    assert np.allclose(ac, g["actions"], rtol=1e-6, atol=1e-6)
+    total = float(mgd.toy_cost(torch.stack(states), torch.cat(actions)).sum())
+    assert abs(total - float(g["total_cost"])) < 1e-4
