@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MBRL_ABI_VERSION 4
+#define MBRL_ABI_VERSION 5
 
 typedef struct ihipStream_t* mbrl_stream_t; /* == hipStream_t */
 typedef struct ihipEvent_t* mbrl_event_t;   /* == hipEvent_t  */
@@ -239,6 +239,19 @@ int mbrl_cem_plan_batch(const mbrl_mlp_shape* shape, const void* packed, const m
                         const mbrl_cost* cost, const float* s0, int32_t B, const mbrl_cem_params* params,
                         float* mu, float* sigma, float* actions_out, float* states_out, void* workspace,
                         size_t ws_bytes, mbrl_stream_t stream);
+
+/* ---- one CEM iteration's update after the rollout, as ONE launch (cem_update_kernel): the stable
+ * top-K of the member-mean returns (as mbrl_select_elites, NAN_LAST), the refit of every row (as
+ * mbrl_cem_refit) and, with next_actions, iteration sampler->iteration + 1's proposals for global
+ * candidates [draw_offset, draw_offset + draw_count) drawn from the new mu / sigma (as
+ * mbrl_sample_actions with n_offset = draw_offset). Bit-identical to those three calls; used by the
+ * sharded (multi-GPU) plan, where every rank updates on the all-gathered costs and draws its shard.
+ * costs: [E][N]; elite_idx: [K] or NULL; returns_out: [N] or NULL; mu_out / sigma_out: [H][a];
+ * next_actions: [H][draw_count][a] or NULL. MBRL_EUNSUPPORTED when N > 32768 or the selection /
+ * refit working set exceeds LDS: use the three calls. Not part of any reference interface. */
+int mbrl_cem_update(const float* costs, int32_t E, int32_t N, int32_t K, const mbrl_sampler* sampler, int32_t H,
+                    int32_t a, float alpha, int64_t* elite_idx, float* returns_out, float* mu_out, float* sigma_out,
+                    float* next_actions, int32_t draw_offset, int32_t draw_count, mbrl_stream_t stream);
 
 /* ---- gradient-descent planner: replaces GradientDescentPlanner's
  * _optimize_trajectory (planners.py:103-137) -- Adam(lr) on the action sequence through the dynamics

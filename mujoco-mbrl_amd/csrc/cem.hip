@@ -763,7 +763,8 @@ struct UpdateArgs {
     float lo, hi, alpha, oma;
     float *mu_out, *sigma_out;   // [B][H][a] the refit
     float *fin_mu, *fin_sigma, *fin_actions;   // last iteration: plan outputs (or NULL)
-    float* next_actions;         // [H][B*N][a] proposals of iteration + 1, or NULL
+    float* next_actions;         // [H][B*draw_n][a] proposals of iteration + 1, or NULL
+    int draw_off, draw_n;        // problem b draws candidates b*N + draw_off + [0, draw_n) (a plan: 0, N)
 };
 
 __host__ __device__ inline size_t update_lds_words(int KPT, int a, int K) {
@@ -799,17 +800,20 @@ __global__ void __launch_bounds__(1024) cem_update_kernel(const UpdateArgs U) {
                (w && U.fin_actions) ? U.fin_actions + rb : nullptr, U.next_actions ? next : nullptr);
     if (U.next_actions) {   // refit_rows ended on a barrier: next[] is visible
         const int G = (a + 3) >> 2;
-        const size_t BN = (size_t)gridDim.y * N;
-        const int NS = (N + S - 1) / S, n0 = j * NS, n1 = min(N, n0 + NS);
+        const int Dn = U.draw_n;
+        const size_t row = (size_t)gridDim.y * Dn;
+        const uint32_t cbase = nbase + (uint32_t)U.draw_off;   // global candidate of local index 0
+        const int NS = (Dn + S - 1) / S, n0 = j * NS, n1 = min(Dn, n0 + NS);
         for (int idx = threadIdx.x; idx < (n1 - n0) * G; idx += 1024) {
             const int n = n0 + idx / G, g = idx - (idx / G) * G;
             float z[4];
-            cem_normal4(U.seed, nbase + (uint32_t)n, (uint32_t)t, (uint32_t)(U.iteration + 1), (uint32_t)g, z);
+            cem_normal4(U.seed, cbase + (uint32_t)n, (uint32_t)t, (uint32_t)(U.iteration + 1), (uint32_t)g, z);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int d = 4 * g + j;
+            for (int q = 0; q < 4; ++q) {
+                const int d = 4 * g + q;
                 if (d < a)
-                    U.next_actions[((size_t)t * BN + nbase + n) * a + d] = cem_action(next[d], next[a4 + d], z[j], U.lo, U.hi);
+                    U.next_actions[((size_t)t * row + (size_t)b * Dn + n) * a + d] =
+                        cem_action(next[d], next[a4 + d], z[q], U.lo, U.hi);
             }
         }
     }
@@ -1147,7 +1151,7 @@ static int update_impl(const UpdateArgs& U, int B, hipStream_t stream) {
     const int kpt = update_kpt(U.N, U.K, U.a);
     if (!kpt) return fail(MBRL_EUNSUPPORTED, "update: N=%d K=%d a=%d not fusable", U.N, U.K, U.a);
     const size_t lds = update_lds_words(kpt, U.a, U.K) * 4;
-    const int S = U.next_actions ? draw_slices(U.H, B, U.N, U.a) : 1;
+    const int S = U.next_actions ? draw_slices(U.H, B, U.draw_n, U.a) : 1;
 #define MBRL_UPD(KPT)                                                                                            \
     if (kpt == KPT) {                                                                                           \
         hipError_t err = ensure_dynamic_lds(reinterpret_cast<const void*>(&cem_update_kernel<KPT>), (int)lds);   \
@@ -1315,6 +1319,29 @@ int mbrl_sample_actions(const mbrl_sampler* sampler, int32_t H, int32_t a, int32
     return sample_impl(sampler, H, a, N, n_offset, actions_out, reinterpret_cast<hipStream_t>(stream));
 }
 
+int mbrl_cem_update(const float* costs, int32_t E, int32_t N, int32_t K, const mbrl_sampler* sampler, int32_t H,
+                    int32_t a, float alpha, int64_t* elite_idx, float* returns_out, float* mu_out, float* sigma_out,
+                    float* next_actions, int32_t draw_offset, int32_t draw_count, mbrl_stream_t stream) {
+    if (!costs || !sampler || !sampler->mu || !sampler->sigma || !mu_out || !sigma_out)
+        return fail(MBRL_EINVAL, "cem_update: NULL argument");
+    if (N < 1 || K < 1 || K > N || E < 1 || H < 1 || a < 1)
+        return fail(MBRL_EINVAL, "cem_update: need 1 <= K (%d) <= N (%d), E, H, a >= 1", K, N);
+    if (next_actions && (draw_count < 1 || draw_offset < 0 || (int64_t)draw_offset + draw_count > N))
+        return fail(MBRL_EINVAL, "cem_update: draw range [%d, %d + %d) outside [0, %d)", draw_offset, draw_offset,
+                    draw_count, N);
+    if (!update_kpt(N, K, a))
+        return fail(MBRL_EUNSUPPORTED, "cem_update: N=%d K=%d a=%d exceeds the fused kernel (select + refit + draw)",
+                    N, K, a);
+    UpdateArgs U{};
+    U.costs = costs; U.E = E; U.N = N; U.K = K; U.member_stride = N; U.H = H; U.a = a;
+    U.elite_out = elite_idx; U.returns_out = returns_out;
+    U.seed = sampler->seed; U.iteration = sampler->iteration; U.mu = sampler->mu; U.sigma = sampler->sigma;
+    U.lo = sampler->lo; U.hi = sampler->hi; U.alpha = alpha; U.oma = 1.0f - alpha;
+    U.mu_out = mu_out; U.sigma_out = sigma_out;
+    U.next_actions = next_actions; U.draw_off = next_actions ? draw_offset : 0; U.draw_n = next_actions ? draw_count : N;
+    return update_impl(U, 1, reinterpret_cast<hipStream_t>(stream));
+}
+
 // Workspace for mbrl_trajectory: per-member states, exchange granules, status word.
 struct TrajWs {
     float* states;
@@ -1457,6 +1484,7 @@ int mbrl_cem_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_no
             U.mu_out = w.mu[cur ^ 1]; U.sigma_out = w.sigma[cur ^ 1];
             U.fin_mu = last ? mu : nullptr; U.fin_sigma = last ? sigma : nullptr; U.fin_actions = last ? actions_out : nullptr;
             U.next_actions = (fuse_draw && !last) ? w.actions : nullptr;
+            U.draw_off = 0; U.draw_n = p->N;
             rc = update_impl(U, 1, stream);
         } else {
             rc = select_impl(costs, g.E, p->N, p->K, MBRL_NAN_LAST, elites, rets, w.keys, align256((size_t)p->N * 4), stream);
@@ -1571,6 +1599,7 @@ int mbrl_cem_plan_batch(const mbrl_mlp_shape* shape, const void* packed, const m
             U.mu_out = w.mu[cur ^ 1]; U.sigma_out = w.sigma[cur ^ 1];
             U.fin_mu = last ? mu : nullptr; U.fin_sigma = last ? sigma : nullptr; U.fin_actions = last ? actions_out : nullptr;
             U.next_actions = (fuse_draw && !last) ? w.actions : nullptr;
+            U.draw_off = 0; U.draw_n = p->N;
             rc = update_impl(U, B, stream);
         } else {
             rc = select_impl(w.costs, g.E, p->N, p->K, MBRL_NAN_LAST, w.elites, nullptr, w.keys,

@@ -18,9 +18,10 @@ LIB_PATH = os.environ.get("MBRL_AMD_LIB") or os.path.join(os.path.dirname(os.pat
                                                           "libmbrl_cem.so")
 
 MBRL_OK = 0
+MBRL_EUNSUPPORTED = -2
 MBRL_COST_GOAL_STATE = 0
 MBRL_COST_MODEL_REWARD = 1
-ABI_VERSION = 4
+ABI_VERSION = 5
 MBRL_NAN_LAST = 0
 MBRL_NAN_FIRST = 1
 MBRL_PRECISION_F32 = 0
@@ -48,6 +49,7 @@ EXPORTED = (
     "mbrl_refit_workspace_bytes", "mbrl_cem_refit", "mbrl_sample_actions",
     "mbrl_trajectory_workspace_bytes", "mbrl_trajectory", "mbrl_cem_workspace_bytes", "mbrl_cem_plan",
     "mbrl_cem_plan_batch_workspace_bytes", "mbrl_cem_plan_batch", "mbrl_gd_workspace_bytes", "mbrl_gd_plan",
+    "mbrl_cem_update",
 )
 
 
@@ -109,6 +111,8 @@ def load():
         "mbrl_cem_refit": (c_int32, [POINTER(Sampler), c_int32, c_int32, P, c_int32, c_float, P, P, P,
                                      c_size_t, P]),
         "mbrl_sample_actions": (c_int32, [POINTER(Sampler), c_int32, c_int32, c_int32, c_int32, P, P]),
+        "mbrl_cem_update": (c_int32, [P, c_int32, c_int32, c_int32, POINTER(Sampler), c_int32, c_int32, c_float, P, P,
+                                      P, P, P, c_int32, c_int32, P]),
         "mbrl_trajectory_workspace_bytes": (c_size_t, [POINTER(MlpShape), c_int32]),
         "mbrl_trajectory": (c_int32, [POINTER(MlpShape), P, POINTER(Norm), P, P, c_int32, P, P, P, c_size_t, P]),
         "mbrl_cem_plan_batch_workspace_bytes": (c_size_t, [POINTER(MlpShape), POINTER(CemParams), c_int32]),

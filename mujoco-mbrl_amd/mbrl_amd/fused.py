@@ -396,6 +396,27 @@ def sample_actions(sampler, H, a, N, n_offset, out):
     return out
 
 
+def cem_update(costs, K, sampler, H, a, alpha, mu_out, sigma_out, elites=None, returns_out=None, next_actions=None,
+               draw_offset=0):
+    """mbrl_cem_update: select + refit + (optionally) the next iteration's proposals for global
+    candidates [draw_offset, draw_offset + next_actions.shape[1]) in one launch. costs: [E, N].
+    Returns the elites [K] (int64), or None when the shape exceeds the fused kernel
+    (MBRL_EUNSUPPORTED: the caller runs select + refit + sample_actions instead)."""
+    lib = _lib.load()
+    E, N = costs.shape
+    dev = costs.device
+    if elites is None:
+        elites = torch.empty(K, dtype=torch.int64, device=dev)
+    dn = 0 if next_actions is None else int(next_actions.shape[1])
+    rc = lib.mbrl_cem_update(_lib.ptr(costs), E, N, K, ctypes_ref(sampler), H, a, float(alpha), _lib.ptr(elites),
+                             _lib.ptr(returns_out), _lib.ptr(mu_out), _lib.ptr(sigma_out), _lib.ptr(next_actions),
+                             int(draw_offset), dn, _lib.stream_handle(dev))
+    if rc == _lib.MBRL_EUNSUPPORTED:
+        return None
+    _lib.check(rc, "mbrl_cem_update")
+    return elites
+
+
 def make_sampler(seed, iteration, mu, sigma, lo, hi):
     return _lib.Sampler(int(seed) & 0xFFFFFFFFFFFFFFFF, int(iteration), 0, _lib.ptr(mu), _lib.ptr(sigma),
                         float(lo), float(hi))

@@ -334,7 +334,9 @@ def cem_sharded_protocol(ops, st, world, rank):
     ops: .device; .rollout(it, mu, sigma, n_offset, n_local, costs_out[E, n_local], events) (events: None
     or a (start, end) pair to record around the rollout kernel alone);
     .all_gather(out_flat[G*E*n_local], local[E, n_local]); .select(costs[E, N], K, returns_out) -> elites;
-    .refit(it, mu, sigma, elites, mu_out, sigma_out); .trajectory(actions[H, a]) -> states[H, s].
+    .refit(it, mu, sigma, elites, mu_out, sigma_out); .trajectory(actions[H, a]) -> states[H, s]; optionally
+    .update(it, mu, sigma, costs, K, returns_out, mu_out, sigma_out, draw_next, n_offset, n_local) -> elites
+    or None: select + refit (+ this rank's next proposals) at once, None when it does not apply.
     The fused path binds them to the HIP extension + RCCL; tests bind them to the CPU oracle + gloo."""
     N, K, H, I, E, a = st["N"], st["K"], st["H"], st["I"], st["E"], st["a"]
     if N % world:
@@ -355,8 +357,11 @@ def cem_sharded_protocol(ops, st, world, rank):
         # candidate r*Nl + j lives at gathered[r, :, j]
         costs = gathered.view(world, E, Nl).permute(1, 0, 2).reshape(E, N) if world > 1 else gathered.view(E, N)
         rets = torch.empty(N, dtype=torch.float32, device=dev) if rec else None
-        elites = ops.select(costs, K, rets)
-        ops.refit(it, mu, sigma, elites, mu_n, sigma_n)
+        upd = getattr(ops, "update", None)
+        elites = None if upd is None else upd(it, mu, sigma, costs, K, rets, mu_n, sigma_n, it + 1 < I, rank * Nl, Nl)
+        if elites is None:
+            elites = ops.select(costs, K, rets)
+            ops.refit(it, mu, sigma, elites, mu_n, sigma_n)
         mu, mu_n = mu_n, mu
         sigma, sigma_n = sigma_n, sigma
         if rec:
@@ -379,6 +384,8 @@ class _FusedShardOps:
         H, a, N, K = st["H"], prob.mdesc["a"], st["N"], st["K"]
         lib = _lib.load()
         self._acts = None
+        self._drawn = None      # (iteration, n_offset, n_local) whose proposals self._acts holds
+        self._fused_update = True
         self._sel_ws = _workspace(("sel", str(self.device)), lib.mbrl_select_workspace_bytes(N), self.device)
         self._refit_ws = _workspace(("refit", str(self.device)), lib.mbrl_refit_workspace_bytes(H, a, K), self.device)
         self._traj_ws = _workspace(("traj", str(self.device)),
@@ -391,8 +398,12 @@ class _FusedShardOps:
         H, a = self.st["H"], self.prob.mdesc["a"]
         if self._acts is None or self._acts.shape[1] != n_local:
             self._acts = torch.empty((H, n_local, a), dtype=torch.float32, device=self.device)
-        # proposal draw, then the rollout kernel alone between the events (bench.py's roofline)
-        fused.sample_actions(self._sampler(it, mu, sigma), H, a, n_local, n_offset, self._acts)
+            self._drawn = None
+        # proposal draw (unless the last update drew this shard already), then the rollout kernel
+        # alone between the events (bench.py's roofline)
+        if self._drawn != (it, n_offset, n_local):
+            fused.sample_actions(self._sampler(it, mu, sigma), H, a, n_local, n_offset, self._acts)
+        self._drawn = None
         if events is not None:
             events[0].record()
         fused.rollout(self.prob, self.s0, n_local, H, actions=self._acts, costs=costs_out)
@@ -409,6 +420,23 @@ class _FusedShardOps:
             out_flat.copy_(host)
         else:
             dist.all_gather_into_tensor(out_flat, local.reshape(-1))
+
+    def update(self, it, mu, sigma, costs, K, returns_out, mu_out, sigma_out, draw_next, n_offset, n_local):
+        """mbrl_cem_update: selection, refit and (draw_next) this rank's proposals of iteration it + 1 in
+        one launch, bit-identical to select + refit + sample_actions; None where it does not apply."""
+        if not self._fused_update:
+            return None
+        H, a = self.st["H"], self.prob.mdesc["a"]
+        nxt = self._acts if (draw_next and self._acts is not None and self._acts.shape[1] == n_local) else None
+        if costs.stride(-1) != 1 or not costs.is_contiguous():
+            costs = costs.contiguous()
+        el = fused.cem_update(costs, K, self._sampler(it, mu, sigma), H, a, self.st["alpha"], mu_out, sigma_out,
+                              returns_out=returns_out, next_actions=nxt, draw_offset=n_offset)
+        if el is None:
+            self._fused_update = False
+            return None
+        self._drawn = (it + 1, n_offset, n_local) if nxt is not None else None
+        return el
 
     def select(self, costs, K, returns_out):
         return fused.select(costs, K, returns_out=returns_out, workspace=self._sel_ws)
