@@ -1051,6 +1051,8 @@ static int traj_impl(const Geometry& g, const void* packed, const mbrl_norm* nor
         T.norm_s = norm->normalize_state; T.unnorm_s = norm->unnormalize_state; T.norm_a = norm->normalize_action;
     }
     T.s0 = s0; T.actions = actions; T.states_out = states_out;
+    if (traj_reg_supported(T) && g_opt[MBRL_OPT_DEBUG_TRAJ_ABORT].load(std::memory_order_relaxed) == 0)
+        return hip_check(launch_traj_reg(T, g.E, stream), "trajectory launch");
     if (xchg && status && traj_coop_supported(T, g.E) && xchg_bytes >= traj_coop_xchg_bytes(T, g.E)) {
         T.debug_abort = g_opt[MBRL_OPT_DEBUG_TRAJ_ABORT].load(std::memory_order_relaxed) != 0;
         const hipError_t err = launch_traj_coop(T, g.E, xchg, status, stream);

@@ -268,6 +268,10 @@ hipError_t launch_gd_coop(const GdArgs& A, unsigned long long* xchg, unsigned* s
 // (E * 2 * Wpad granules, zeroed by the launcher before every launch). Needs the P*E workgroups co-resident (grid_fits) and
 // s <= 64. `status` (one uint32, zeroed by the launcher) becomes nonzero if a bounded spin gave up.
 bool traj_coop_supported(const TrajArgs& A, int E);
+// Register-resident variant for narrow models (Wpad <= 256, few hidden layers): one 1024-thread
+// workgroup per member with every weight in registers; no hand-off, no workspace (traj.hip).
+bool traj_reg_supported(const TrajArgs& A);
+hipError_t launch_traj_reg(const TrajArgs& A, int E, hipStream_t stream);
 size_t traj_coop_xchg_bytes(const TrajArgs& A, int E);
 hipError_t launch_traj_coop(const TrajArgs& A, int E, unsigned long long* xchg, unsigned* status,
                             hipStream_t stream);

@@ -417,6 +417,177 @@ hipError_t launch_traj_coop(const TrajArgs& A, int E, unsigned long long* xchg, 
                              : launch_coop_width<96, 5>(A, E, xchg, status, stream);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Register-resident single-trajectory rollout for narrow models (Wpad <= 256: cartpole's 2x256, the
+// reference's default widths 50 / 200): one workgroup of 1024 threads per member holds EVERY weight
+// in registers for the whole horizon -- W0 and the hidden W_l rows split over TPR = 1024 / Wpad threads
+// (K0J / KPT columns each; hidden columns in float4 groups k = 4 (q + TPR j) + i, so that a wave's LDS
+// reads of the input vector are 16-byte broadcasts), Wout one row per wave. A step is four barriers and
+// no global load (no cross-workgroup hop, no hand-off memset, no fallback launch): ~1 us per step
+// where traj_coop_kernel pays a ~3.4 us hop per hidden layer.
+// ------------------------------------------------------------------------------------------------
+constexpr int REG_THREADS = 1024;
+
+__host__ __device__ inline int reg_max_hidden(int Wp) { return Wp <= 64 ? 3 : (Wp <= 128 ? 3 : (Wp <= 256 ? 1 : 0)); }
+
+template <int WP, int NHL, int K0R>
+__global__ void __launch_bounds__(REG_THREADS) traj_reg_kernel(const TrajArgs A) {
+    constexpr int TPR = REG_THREADS / WP;   // threads per hidden row
+    constexpr int KPT = WP / TPR;           // columns per thread (a multiple of 4)
+    static_assert(KPT % 4 == 0, "float4 column groups");
+    constexpr int OI = WP / 64;             // output-layer columns per lane
+    constexpr int SM = 2;                   // output rows per wave (s <= 32)
+    constexpr int K0J = (K0R + TPR - 1) / TPR;   // layer-0 columns per thread
+    static_assert(K0J * TPR <= 32, "x0 holds 32 inputs");
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int e = blockIdx.x;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int r = tid / TPR, q = tid - (tid / TPR) * TPR;
+    const int s = A.s, a = A.a, W = A.W, Wp = A.Wpad, K0 = s + a;
+    float* x0 = smem;                        // [32]
+    float* hA = x0 + 32;                     // [WP]
+    float* hB = hA + WP;                     // [WP]
+    float* out = hB + WP;                    // [32]
+    float* prm = out + 32;                   // [4][32]: output bias, obs mean, obs std, (pad)
+    float* acts = prm + 128;                 // [H][a] normalised actions
+    const float* member = A.packed + (size_t)e * A.member_stride;
+    const float* bias = member + A.bias_off;
+    const float* tw = member + A.tw_base;
+
+    for (int k = tid; k < 32; k += REG_THREADS) {
+        float v = 0.f;
+        if (k < s) {
+            const float sv = A.s0[k];
+            v = A.norm_s ? (sv - A.obs_mean[k]) / A.obs_std[k] : sv;
+        }
+        x0[k] = v;
+    }
+    for (int d = tid; d < s; d += REG_THREADS) {
+        prm[d] = bias[(size_t)A.L * Wp + d];
+        prm[32 + d] = A.obs_mean ? A.obs_mean[d] : 0.f;
+        prm[64 + d] = A.obs_std ? A.obs_std[d] : 1.f;
+    }
+    for (int i = tid; i < A.H * a; i += REG_THREADS) {
+        const int d = i % a;
+        const float av = A.actions[i];
+        acts[i] = A.norm_a ? (av - A.act_mean[d]) / A.act_std[d] : av;
+    }
+    // weights into registers (zero past the real sizes)
+    float w0r[K0J];                                      // W0[r][q + TPR j] (W^T_0 [K0][Wpad])
+    const float b0 = r < W ? bias[r] : 0.f;
+#pragma unroll
+    for (int j = 0; j < K0J; ++j) {
+        const int k = q + TPR * j;
+        w0r[j] = (r < W && k < K0) ? tw[A.tw_off[0] + (size_t)k * Wp + r] : 0.f;
+    }
+    float wh[NHL > 0 ? NHL : 1][KPT];
+    float bh[NHL > 0 ? NHL : 1];
+#pragma unroll
+    for (int l = 0; l < NHL; ++l) {
+        const float* wt = tw + A.tw_off[l + 1];          // W^T_l [W][Wpad]: W_l[r][k] = wt[k * Wpad + r]
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            const int k = 4 * (q + TPR * (j >> 2)) + (j & 3);
+            wh[l][j] = (r < W && k < W) ? wt[(size_t)k * Wp + r] : 0.f;
+        }
+        bh[l] = r < W ? bias[(size_t)(l + 1) * Wp + r] : 0.f;
+    }
+    float wor[SM][OI];
+    const float* wo = tw + A.tw_off[A.L];               // Wout row-major [so][W]
+#pragma unroll
+    for (int m = 0; m < SM; ++m)
+#pragma unroll
+        for (int i = 0; i < OI; ++i) {
+            const int d = wave + 16 * m, k = lane + 64 * i;
+            wor[m][i] = (d < s && k < W) ? wo[(size_t)d * W + k] : 0.f;
+        }
+    __syncthreads();
+
+    for (int t = 0; t < A.H; ++t) {
+        for (int d = tid; d < a; d += REG_THREADS) x0[s + d] = acts[t * a + d];
+        __syncthreads();
+        float* cur = hA;
+        float* nxt = hB;
+        {                                                // layer 0: row r over TPR lanes
+            float v = 0.f;
+#pragma unroll
+            for (int j = 0; j < K0J; ++j) v += w0r[j] * x0[q + TPR * j];
+#pragma unroll
+            for (int o = TPR / 2; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+            if (q == 0) cur[r] = fmaxf(v + b0, 0.f);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int l = 0; l < NHL; ++l) {                  // W -> W: row r over TPR lanes, fixed butterfly
+            float v = 0.f;
+#pragma unroll
+            for (int j4 = 0; j4 < KPT / 4; ++j4) {
+                const f32x4 x = *reinterpret_cast<const f32x4*>(cur + 4 * (q + TPR * j4));
+#pragma unroll
+                for (int i = 0; i < 4; ++i) v += wh[l][4 * j4 + i] * x[i];
+            }
+#pragma unroll
+            for (int o = TPR / 2; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+            if (q == 0) nxt[r] = fmaxf(v + bh[l], 0.f);
+            __syncthreads();
+            float* tmp = cur; cur = nxt; nxt = tmp;
+        }
+#pragma unroll
+        for (int m = 0; m < SM; ++m) {                   // output rows wave + 16 m
+            float v = 0.f;
+#pragma unroll
+            for (int i = 0; i < OI; ++i) v += wor[m][i] * cur[lane + 64 * i];
+            v = wave_sum64(v);
+            const int d = wave + 16 * m;
+            if (lane == 0 && d < s) out[d] = v + prm[d];
+        }
+        __syncthreads();
+        for (int d = tid; d < s; d += REG_THREADS) {
+            const float sn = A.unnorm_s ? out[d] * prm[64 + d] + prm[32 + d] : out[d];
+            A.states_out[((size_t)e * A.H + t) * s + d] = sn;
+            x0[d] = A.norm_s ? (sn - prm[32 + d]) / prm[64 + d] : sn;
+        }
+        // x0 and out are next touched after the barrier at the top of the next step
+    }
+}
+
+bool traj_reg_supported(const TrajArgs& A) {
+    const int K0 = A.s + A.a;
+    if (A.Wpad > 256 || A.L - 1 > reg_max_hidden(A.Wpad) || K0 > 32 || A.s > 32) return false;
+    return (size_t)(32 + 2 * A.Wpad + 32 + 128 + A.H * A.a) * sizeof(float) <= 64 * 1024;
+}
+
+template <int WP, int NHL>
+static hipError_t launch_reg_k0(const TrajArgs& A, int E, hipStream_t stream) {
+    const int K0 = A.s + A.a;
+    const size_t lds = (size_t)(32 + 2 * WP + 32 + 128 + A.H * A.a) * sizeof(float);
+    if (K0 <= 8)
+        hipLaunchKernelGGL((traj_reg_kernel<WP, NHL, 8>), dim3(E), dim3(REG_THREADS), lds, stream, A);
+    else
+        hipLaunchKernelGGL((traj_reg_kernel<WP, NHL, 32>), dim3(E), dim3(REG_THREADS), lds, stream, A);
+    return hipGetLastError();
+}
+
+template <int WP>
+static hipError_t launch_reg_w(const TrajArgs& A, int E, hipStream_t stream) {
+    switch (A.L - 1) {
+        case 0: return launch_reg_k0<WP, 0>(A, E, stream);
+        case 1: return launch_reg_k0<WP, 1>(A, E, stream);
+        case 2: if constexpr (WP <= 128) return launch_reg_k0<WP, 2>(A, E, stream); else return hipErrorInvalidValue;
+        case 3: if constexpr (WP <= 128) return launch_reg_k0<WP, 3>(A, E, stream); else return hipErrorInvalidValue;
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_traj_reg(const TrajArgs& A, int E, hipStream_t stream) {
+    switch (A.Wpad) {
+        case 64: return launch_reg_w<64>(A, E, stream);
+        case 128: return launch_reg_w<128>(A, E, stream);
+        case 256: return launch_reg_w<256>(A, E, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
 }  // namespace mbrl
 
 #ifdef MBRL_STAMPS

@@ -360,11 +360,15 @@ def test_full_size_iterations_against_reference_golden(golden, name, cid, capsys
 
 
 # ------------------------------------------------------------------------------------------------ trajectory / sharding
-@pytest.mark.parametrize("cid,H", [(2, 20), (3, 30), (4, 7), (5, 50)])
-def test_trajectory_states_match_oracle(cid, H):
-    """mbrl_trajectory (cooperative kernel) vs the oracle's N=1 rollout, per member and member mean."""
+@pytest.mark.parametrize("cid,H,over", [(2, 20, {}), (3, 30, {}), (4, 7, {}), (5, 50, {}), (3, 9, dict(W=50, L=2)),
+                                        (3, 6, dict(W=50, L=4)), (2, 11, dict(W=100, L=3)), (6, 8, dict(W=200, L=2)),
+                                        (5, 5, dict(W=128, L=4)), (2, 4, dict(W=64, L=1))])
+def test_trajectory_states_match_oracle(cid, H, over):
+    """mbrl_trajectory vs the oracle's N=1 rollout, per member and member mean: the register-resident
+    kernel (Wpad <= 256: cartpole, the reference's default widths 50 / 200, ensembles) and the
+    cooperative kernel (Wpad 512)."""
     from mbrl_amd import fused
-    p = ocem.synth_problem(cid, N=1, H=H)
+    p = ocem.synth_problem(cid, N=1, H=H, **over)
     a, s, E = p["cfg"]["a"], p["cfg"]["s"], p["cfg"]["E"]
     acts = np.random.default_rng(cid).uniform(-1, 1, size=(H, a)).astype(np.float32)
     prob = device_problem(p)
