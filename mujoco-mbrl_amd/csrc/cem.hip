@@ -1026,9 +1026,17 @@ static int rollout_impl(const Geometry& g, const void* packed, const mbrl_norm* 
         if (const int o = g_opt[MBRL_OPT_ROLLOUT_TILE].load(std::memory_order_relaxed)) use8 = o == 8;
         if (use8 && rollout_m8_supported(A, g.T)) return hip_check(launch_rollout_m8(A, g.T, stream), "rollout m8 launch");
     }
+    // partials in the activation buffer the last hidden layer does not read (rollout.hip): layer 0
+    // writes act2, hidden layer l reads act2 for odd l, so with L odd the last one reads act and act2
+    // is free from the barrier after layer L-2 until the next step's layer 0
+    auto alias_ok = [&]() {
+        return !A.reward && g.L >= 3 && (g.L & 1) && (size_t)(A.nw > 4 ? A.nw : 4) * g.pw <= (size_t)g.lda;
+    };
+    A.part_alias = alias_ok() ? 1 : 0;
     if (rollout_lds_bytes(A, 16 * R) > 160 * 1024) {
         R = 1;
         A.nw = g.T >= 2 ? 8 : 4;
+        A.part_alias = alias_ok() ? 1 : 0;
         if (rollout_lds_bytes(A, 16) > 160 * 1024)
             return fail(MBRL_EUNSUPPORTED, "LDS footprint %zu B exceeds 160 KiB", rollout_lds_bytes(A, 16));
     }

@@ -131,6 +131,9 @@ struct RolloutArgs {
     // 8-candidate kernel (rollout_m8_kernel)
     size_t m8_off;         // 0: no 8-candidate stream in the pack
     int C8;
+    // 16-candidate kernel, L odd >= 3, no reward head: the output partials live in the activation
+    // buffer the last hidden layer does not read (act2), so 32-candidate tiles of wide states fit LDS
+    int part_alias;
 };
 
 // F16X3 operand scales (exact powers of two): activations and weights are scaled before the f16
@@ -155,7 +158,7 @@ __host__ __device__ inline LdsMap lds_map(const RolloutArgs& A, float* base, int
     auto take = [&](size_t n) { float* p = base ? base + o : nullptr; o += lds_round4(n); return p; };
     L.act = take((size_t)M * A.lda);
     L.act2 = take((size_t)M * A.lda);
-    L.part = take((size_t)(A.nw > 4 ? A.nw : 4) * M * A.pw);
+    L.part = A.part_alias ? L.act2 : take((size_t)(A.nw > 4 ? A.nw : 4) * M * A.pw);
     L.sterm = take((size_t)M * A.s);
     L.aterm = take((size_t)2 * M * A.a);
     L.obs_mean = take(A.s);

@@ -58,3 +58,24 @@ def test_m8_plan_equals_m16_plan():
                                               record=True)
     for k in ("returns", "elites", "mu", "sigma", "actions", "states"):
         assert torch.equal(out[8][k], out[16][k]), k
+
+
+@pytest.mark.parametrize("cid,N,H", [(5, 8192, 4), (4, 8200, 3), (3, 8192, 5)])
+def test_32_candidate_tiles_match_smaller_shards_bitwise(cid, N, H):
+    """N >= 8192 runs 32-candidate tiles (R = 2, 4 waves); humanoid's wide state fits them only with the
+    output partials aliased onto the activation buffer the last hidden layer does not read
+    (RolloutArgs.part_alias). Costs must equal, bit for bit, the same candidates rolled out as shards
+    of <= 2048 (8- and 16-candidate tiles): the canonical output-layer sum of every tile height."""
+    p = ocem.synth_problem(cid, N=N, H=H)
+    a = p["cfg"]["a"]
+    A = cem_actions(np.zeros((H, a), np.float32), np.full((H, a), 0.5, np.float32), -1, 1, 5, 0, np.arange(N))
+    prob = device_problem(p)
+    full, _ = _rollout(prob, p, N, H, 16, A)
+    parts = []
+    for lo in range(0, N, 2048):
+        hi = min(N, lo + 2048)
+        c, _ = _rollout(prob, p, hi - lo, H, 8 if (hi - lo) % 2 == 0 else 16, np.ascontiguousarray(A[:, lo:hi]))
+        parts.append(c)
+    assert torch.equal(full, torch.cat(parts, dim=1))
+    ref = ocem.ensemble_returns(ocem.rollout(p["model"], p["norm"], p["cost"], p["s0"], A[:, :64]))
+    assert rel_err(full.mean(0)[:64] if p["cfg"]["E"] > 1 else full[0, :64], ref) < RTOL
