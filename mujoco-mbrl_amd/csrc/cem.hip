@@ -1029,6 +1029,9 @@ static int rollout_impl(const Geometry& g, const void* packed, const mbrl_norm* 
     // partials in the activation buffer the last hidden layer does not read (rollout.hip): layer 0
     // writes act2, hidden layer l reads act2 for odd l, so with L odd the last one reads act and act2
     // is free from the barrier after layer L-2 until the next step's layer 0
+    // 32-candidate tiles on 8 waves (two per SIMD) when the 8 partials fit the aliased activation
+    // buffer: walker rollout 3.91 -> 3.83 ms, frac 0.883 -> 0.901 (profiles/r02_ab_r2_8waves.txt)
+    if (R == 2 && g.T >= 2 && !A.reward && g.L >= 3 && (g.L & 1) && (size_t)8 * g.pw <= (size_t)g.lda) A.nw = 8;
     auto alias_ok = [&]() {
         return !A.reward && g.L >= 3 && (g.L & 1) && (size_t)(A.nw > 4 ? A.nw : 4) * g.pw <= (size_t)g.lda;
     };

@@ -254,7 +254,7 @@ __device__ __forceinline__ void load_epi_params(const RolloutArgs& A, const LdsM
 }
 
 // a_t -> normalised MLP input columns [s, s+a); returns this lane's share of sum_d (cosh(a_d/alpha)-1).
-template <int R, int SS>
+template <int R, int SS, bool REG = (SS <= MBRL_EPI_REG_SLOTS)>
 __device__ __forceinline__ void stage_actions(const RolloutArgs& A, const EpiParams<SS>& P, const LdsMap& L, float* act,
                                               int wave, int lane, const float (&av)[R][MAX_A_PER_LANE],
                                               float (&acp)[R]) {
@@ -268,8 +268,8 @@ __device__ __forceinline__ void stage_actions(const RolloutArgs& A, const EpiPar
             if (d < A.a) {
                 const float x = av[r][k];
                 // wide states keep no per-lane copies (see MBRL_EPI_REG_SLOTS): same values from LDS
-                const float am = SS <= MBRL_EPI_REG_SLOTS ? P.am[k] : L.act_mean[d];
-                const float as = SS <= MBRL_EPI_REG_SLOTS ? P.as[k] : L.act_std[d];
+                const float am = REG ? P.am[k] : L.act_mean[d];
+                const float as = REG ? P.as[k] : L.act_std[d];
                 const float xn = A.norm_a ? (x - am) / as : x;
                 act[m * A.lda + A.s + d] = xn;
                 if (A.reward) L.aterm[m * A.a + d] = xn;   // the state pass re-reads a_t
@@ -297,6 +297,9 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
     constexpr bool RING = K0C_T > 0;
     constexpr int NB = RING ? 4 : 2;
     constexpr int SS = RING ? NOT_T : 1;    // register state slots per lane (ceil(s / 16) <= NOT); generic: LDS
+    // per-lane epilogue parameter copies in registers (else the same values from LDS): not at 32
+    // candidates x 8 waves, whose MFMA loop already takes the whole 256-VGPR budget
+    constexpr bool EREG = SS <= MBRL_EPI_REG_SLOTS && !(R == 2 && NW == 8);
     static_assert(!RING || ((K0C_T + NOT_T) % NB == 0 && K0C_T % 2 == 0 && NOT_T % 2 == 0), "ring layout");
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const LdsMap L = lds_map(A, smem, M);
@@ -353,7 +356,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
     EpiParams<SS> P;
     load_epi_params<SS>(A, L, lane, P);
     if (actw) {
-        stage_actions<R, SS>(A, P, L, actX, awave, lane, av, acp);
+        stage_actions<R, SS, EREG>(A, P, L, actX, awave, lane, av, acp);
         if (split)
 #pragma unroll
             for (int r = 0; r < R; ++r) {
@@ -528,7 +531,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
                     total[r] += rowsum16(rc);
                 }
             }
-            if (pass == 1 && t + 1 < A.H) stage_actions<R, SS>(A, P, L, actX, wave, lane, av, acp);
+            if (pass == 1 && t + 1 < A.H) stage_actions<R, SS, EREG>(A, P, L, actX, wave, lane, av, acp);
         } else if (epi) {
             const float* bout = L.hbias + A.L * A.Wpad;
             const int ws = M * A.pw;
@@ -551,7 +554,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
                     if (A.states_out != nullptr && n < A.N)
                         A.states_out[(((size_t)e * A.H + t) * A.N + n) * A.s + d] = sn;
                 };
-                if constexpr (RING && SS <= MBRL_EPI_REG_SLOTS) {
+                if constexpr (RING && EREG) {
 #pragma unroll
                     for (int k = 0; k < SS; ++k)
                         if (j + 16 * k < A.s) slot(j + 16 * k, P.om[k], P.os[k], P.goal[k], P.cw[k], P.bo[k]);
@@ -571,10 +574,10 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
                 const float ac = split ? acs[(t & 1) * M + m] : rowsum16(acp[r]);
                 total[r] += sc + A.alpha_a2 * (ac / (float)A.a);
             }
-            if (!split && t + 1 < A.H) stage_actions<R, SS>(A, P, L, actX, wave, lane, av, acp);
+            if (!split && t + 1 < A.H) stage_actions<R, SS, EREG>(A, P, L, actX, wave, lane, av, acp);
         } else if (split && actw && t + 1 < A.H) {
             // waves 4-7, concurrently: a_{t+1} into the next MLP input, its CoshLoss row sum into LDS
-            stage_actions<R, SS>(A, P, L, actX, awave, lane, av, acp);
+            stage_actions<R, SS, EREG>(A, P, L, actX, awave, lane, av, acp);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const float v = rowsum16(acp[r]);
@@ -617,11 +620,8 @@ static hipError_t launch_rollout_tr(const RolloutArgs& A_in, hipStream_t stream)
     return hipGetLastError();
 }
 
-template <int T, int R>
-static hipError_t launch_rollout_t(const RolloutArgs& A, hipStream_t stream) {
-    // two waves per SIMD (8 waves, T/2 tiles each) where the tile count and LDS allow it
-    // (16 waves, T/4 tiles each, measured 8 % slower than 8: the 128-VGPR budget spills)
-    constexpr int NW = (T >= 2 && R == 1 && MBRL_ROLLOUT_NW >= 8) ? 8 : 4;
+template <int T, int R, int NW>
+static hipError_t launch_rollout_tn(const RolloutArgs& A, hipStream_t stream) {
     if constexpr (4 * T / NW <= 8) {  // the 4-deep ring needs 4*TW*4 VGPRs
         if (A.K0C == 2 && A.NOT == 2) return launch_rollout_tr<T, R, 2, 2, NW>(A, stream);
         if (A.K0C == 6 && A.NOT == 6) return launch_rollout_tr<T, R, 6, 6, NW>(A, stream);
@@ -629,6 +629,18 @@ static hipError_t launch_rollout_t(const RolloutArgs& A, hipStream_t stream) {
         if (A.K0C == 6 && A.NOT == 2) return launch_rollout_tr<T, R, 6, 2, NW>(A, stream);
     }
     return launch_rollout_tr<T, R, 0, 0, NW>(A, stream);
+}
+
+template <int T, int R>
+static hipError_t launch_rollout_t(const RolloutArgs& A, hipStream_t stream) {
+    // two waves per SIMD (8 waves, T/2 tiles each) where the tile count and LDS allow it: always for
+    // R = 1; for R = 2 when the launcher asks (A.nw == 8: the aliased partials fit LDS)
+    // (16 waves, T/4 tiles each, measured 8 % slower than 8: the 128-VGPR budget spills)
+    if constexpr (R == 2 && T >= 2 && MBRL_ROLLOUT_NW >= 8) {
+        if (A.nw == 8) return launch_rollout_tn<T, R, 8>(A, stream);
+    }
+    constexpr int NW = (T >= 2 && R == 1 && MBRL_ROLLOUT_NW >= 8) ? 8 : 4;
+    return launch_rollout_tn<T, R, NW>(A, stream);
 }
 
 hipError_t launch_rollout(const RolloutArgs& A, int T, int R, hipStream_t stream) {
