@@ -443,7 +443,40 @@ __device__ __forceinline__ void select_reg_body(const float* __restrict__ costs,
     CSTAMP(0);
     const int tid = threadIdx.x, wave = tid >> 6;
     const int n0 = tid * KPT;
-    {
+    uint32_t key[KPT];
+    // KPT >= 4 with 16-byte aligned rows: each thread loads its own contiguous KPT returns as float4
+    // (no LDS transpose); the member sum keeps the same per-candidate order, so the bits are the same
+    const bool vec = KPT >= 4 && (N & 3) == 0 && (member_stride & 3) == 0;
+    if (vec) {
+        typedef float f4 __attribute__((ext_vector_type(4)));
+        constexpr int G4 = KPT >= 4 ? KPT / 4 : 1;
+        f4 r4[G4];
+#pragma unroll
+        for (int j = 0; j < G4; ++j)
+            r4[j] = n0 + 4 * j < N ? *reinterpret_cast<const f4*>(costs + n0 + 4 * j) : f4{0.f, 0.f, 0.f, 0.f};
+        for (int e = 1; e < E; ++e)
+#pragma unroll
+            for (int j = 0; j < G4; ++j)
+                if (n0 + 4 * j < N) {
+                    const f4 c = *reinterpret_cast<const f4*>(costs + (size_t)e * member_stride + n0 + 4 * j);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) r4[j][i] = __fadd_rn(r4[j][i], c[i]);
+                }
+#pragma unroll
+        for (int j = 0; j < G4; ++j) {
+            if (n0 + 4 * j < N) {
+                f4 v;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) v[i] = E > 1 ? __fdiv_rn(r4[j][i], (float)E) : r4[j][i];
+                if (returns_out) *reinterpret_cast<f4*>(returns_out + n0 + 4 * j) = v;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) key[4 * j + i] = order_key(v[i], nan_policy);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) key[4 * j + i] = 0xFFFFFFFFu;
+            }
+        }
+    } else {
         float r[KPT];                                   // every load in flight before the first use
 #pragma unroll
         for (int k = 0; k < KPT; ++k) {
@@ -465,23 +498,40 @@ __device__ __forceinline__ void select_reg_body(const float* __restrict__ costs,
                 sel_smem[n + (n >> 5)] = order_key(v, nan_policy);  // one pad word per 32: conflict-free reads
             }
         }
-    }
-    __syncthreads();
-    uint32_t key[KPT];
+        __syncthreads();
 #pragma unroll
-    for (int k = 0; k < KPT; ++k) {
-        const int n = n0 + k;
-        key[k] = n < N ? sel_smem[n + (n >> 5)] : 0xFFFFFFFFu;
+        for (int k = 0; k < KPT; ++k) {
+            const int n = n0 + k;
+            key[k] = n < N ? sel_smem[n + (n >> 5)] : 0xFFFFFFFFu;
+        }
     }
-    __syncthreads();
-    // 4 radix passes over 8-bit digits; the histogram buffer of pass p+1 is cleared during pass p,
-    // and the bucket search is a 256-entry scan by waves 0-3 only: 3 barriers per pass
+    // leading bits every key shares (block min / max): their radix passes would select the one
+    // populated bucket, so the first pass starts at the first byte that differs (returns of one plan
+    // usually share sign and exponent: one pass of four saved)
+    uint32_t kmin = 0xFFFFFFFFu, kmax = 0u;
+#pragma unroll
+    for (int k = 0; k < KPT; ++k)
+        if (n0 + k < N) { kmin = min(kmin, key[k]); kmax = max(kmax, key[k]); }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, o, 64));
+        kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o, 64));
+    }
+    __shared__ uint32_t mm_ws[2][16];
+    if ((tid & 63) == 0) { mm_ws[0][wave] = kmin; mm_ws[1][wave] = kmax; }
+    __syncthreads();   // also: every thread has taken its keys out of sel_smem (non-vector path)
+#pragma unroll
+    for (int w = 0; w < 16; ++w) { kmin = min(kmin, mm_ws[0][w]); kmax = max(kmax, mm_ws[1][w]); }
+    const int skip = (kmin == kmax ? 32 : __clz(kmin ^ kmax)) >> 3;   // whole shared bytes (0..4)
+    // radix passes over the remaining 8-bit digits; the histogram buffer of pass p+1 is cleared
+    // during pass p, and the bucket search is a 256-entry scan by waves 0-3 only: 3 barriers per pass
     CSTAMP(1);
-    uint32_t prefix = 0, mask = 0, kk = (uint32_t)K;
+    const uint32_t hi = skip == 0 ? 0u : (skip >= 4 ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> (8 * skip)));
+    uint32_t prefix = kmin & hi, mask = hi, kk = (uint32_t)K;
     for (int i = tid; i < 16 * 257; i += 1024) (&hist[0][0][0])[i] = 0;
     __syncthreads();
     int buf = 0;
-    for (int shift = 24; shift >= 0; shift -= 8, buf ^= 1) {
+    for (int shift = 24 - 8 * skip; shift >= 0; shift -= 8, buf ^= 1) {
         // returns cluster (most candidates share the leading digits): when every pending lane of a
         // wave has the same digit, one lane adds the count; otherwise plain per-lane atomics (more
         // aggregation rounds cost more VALU issue than the contention they save). Rows padded to

@@ -403,14 +403,16 @@ def _trajectory_fallback(fused, cid, H):
     assert np.allclose(members.cpu().numpy(), ref[:, :, 0, :], rtol=1e-4, atol=1e-4)
 
 
-@pytest.mark.parametrize("cid,N,H,world", [(3, 2048, 10, 2), (5, 512, 6, 4), (4, 16384, 30, 4), (4, 16384, 30, 8)])
+@pytest.mark.parametrize("cid,N,H,world", [(3, 2048, 10, 2), (5, 512, 6, 4), (4, 16384, 30, 4), (4, 16384, 30, 8),
+                                           (2, 40000, 4, 2)])
 def test_sharded_protocol_with_fused_ops_matches_single_gpu_plan(cid, N, H, world):
     """The multi-GPU protocol with its math on the HIP extension: every rank's shard computed here on
     one GPU (the all-gather stitches the shards' rollouts), against the single-call mbrl_cem_plan.
     Elites, mu and sigma must be bit-identical (no floating-point reduction crosses ranks). Walker
     N=16384 (BASELINE configs[3]) is the case where the tile heights differ: one GPU runs 32-candidate
-    4-wave tiles, a 4-way shard 16-candidate 8-wave tiles, an 8-way shard 8-candidate tiles; all
-    three close the output layer in the same canonical order (rollout.hip mma_out)."""
+    tiles, a 4-way shard 16-candidate tiles, an 8-way shard 8-candidate tiles; all three close the
+    output layer in the same canonical order (rollout.hip mma_out). N=40000 is past the fused update
+    (mbrl_cem_update returns MBRL_EUNSUPPORTED): the ranks fall back to select + refit + draw."""
     from mbrl_amd import CEMPlanner, fused, planners
     p = ocem.synth_problem(cid, N=N, H=H)
     _, model_fn, cost_fn, sample_action = build(p)
