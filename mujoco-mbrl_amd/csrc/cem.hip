@@ -1703,7 +1703,7 @@ static GdWs gd_ws(const Geometry& g, int H, void* base) {
     auto take = [&](size_t n) { void* r = b ? b + o : nullptr; o += align256(n); return r; };
     const size_t ha = (size_t)H * g.a;
     const size_t row = ((size_t)((g.s + g.a + 3) & ~3) + (size_t)g.L * g.Wpad) * (g.reward ? 2 : 1);
-    const size_t coop = (size_t)(g.Wpad / 16) * H * g.L * g.Wpad;   // per-workgroup hidden-vector copies
+    const size_t coop = (size_t)(g.Wpad / 16) * H * g.L * g.Wpad * (g.reward ? 2 : 1);   // per-workgroup hidden-vector copies
     w.xchg = (unsigned long long*)take((size_t)2 * g.Wpad * 8 + 16);   // granules, then the status word
     w.status = w.xchg ? reinterpret_cast<unsigned*>(w.xchg + 2 * g.Wpad) : nullptr;
     w.m = (float*)take(ha * 4);

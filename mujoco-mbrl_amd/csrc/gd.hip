@@ -473,7 +473,9 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
     const float* bias = A.packed + A.bias_off;
     const float* tw = A.packed + A.tw_base;
     gc_gu64* xchg = (gc_gu64*)xchg_all;
-    float* hist = A.hist + (size_t)p * H * L * Wp;     // this workgroup's copy of the hidden vectors
+    // this workgroup's copy of the hidden vectors: [H][L][Wp] per pass (state pass, then the reward
+    // pass of a reward-head model at rows H..2H-1)
+    float* hist = A.hist + (size_t)p * (A.reward ? 2 : 1) * H * L * Wp;
 
     if (A.debug_abort) {                       // test hook: behave as a timed-out hand-off
         if (tid == 0) atomicOr(status, 1u);
@@ -515,6 +517,9 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
     float wob[16 * SM];                                       // backward: Wout[n][tid]
 #pragma unroll
     for (int n = 0; n < 16 * SM; ++n) wob[n] = (n < s && tid < W) ? wo[(size_t)n * W + tid] : 0.0f;
+    // reward head (row s of the output block) and d r / d head = rew_std (unnormalise_reward)
+    const float wrb = (A.reward && tid < W) ? wo[(size_t)s * W + tid] : 0.0f;
+    const float grw = (A.reward && A.unnorm_r) ? A.rew_std[0] : 1.0f;
     const float* hbias = bias;                                // [L][Wpad]
     const float* obias = bias + (size_t)L * Wp;
     __syncthreads();
@@ -524,6 +529,65 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
     int done = 0;
     float* cur = smem + m.hA;
     float* nxt = smem + m.hB;
+    float* gcur = smem + m.gA;
+    float* gnxt = smem + m.gB;
+    // the trunk on x0 (layer 0 redundant, hidden layers through the hand-offs), activations into ht;
+    // leaves the last hidden vector in cur. false: a hand-off gave up.
+    auto trunk = [&](float* ht) -> bool {
+        if (has_unit) {
+            float v = b0;
+#pragma unroll
+            for (int k = 0; k < K0R; ++k) v += w0r[k] * x0[k];
+            v = fmaxf(v, 0.0f);
+            cur[tid] = v;
+            ht[tid] = v;
+        }
+        __syncthreads();
+        for (int l = 1; l < L; ++l) {
+            const float* f = fw + (size_t)(l - 1) * GC_ROWS * m.rs + (size_t)g * m.rs;
+            float v = 0.f;
+#pragma unroll
+            for (int i = 0; i < WI; ++i) v += f[c + 32 * i] * cur[c + 32 * i];
+            v = gc_half_sum(v);
+            v = fmaxf(v + hbias[(size_t)l * Wp + p * GC_ROWS + g], 0.0f);
+            if (!gc_exchange<WI / 2>(xchg, Wp, p, phase, v, nxt, abort_flag, status)) return false;
+            float* tmp = cur; cur = nxt; nxt = tmp;
+            if (has_unit) ht[(size_t)l * Wp + tid] = cur[tid];
+        }
+        return true;
+    };
+    // reverse mode from gcur (d loss / d last hidden output, ReLU mask applied) through the hidden
+    // layers (hand-offs) and layer 0 (redundant block reduction): use(k, d loss / d x0[k]), k < K0
+    auto trunk_back = [&](const float* ht, auto&& use) -> bool {
+        for (int l = L - 1; l >= 1; --l) {
+            // my 16 input gradients of layer l: k = 16p + g, lanes over n
+            const float* b = bw + (size_t)(l - 1) * GC_ROWS * m.rs + (size_t)g * m.rs;
+            float v = 0.f;
+#pragma unroll
+            for (int i = 0; i < WI; ++i) v += b[c + 32 * i] * gcur[c + 32 * i];
+            v = gc_half_sum(v);
+            const int k = p * GC_ROWS + g;
+            v = ht[(size_t)(l - 1) * Wp + k] > 0.f ? v : 0.f;     // ReLU' of layer l - 1's output
+            if (!gc_exchange<WI / 2>(xchg, Wp, p, phase, v, gnxt, abort_flag, status)) return false;
+            float* tmp = gcur; gcur = gnxt; gnxt = tmp;
+        }
+        // layer 0 backward (redundant): g_x0[k] = sum_u W0[u][k] g_z0[u], a block reduction per k
+        static_assert(K0R == 32, "wave_reduce_scatter32");
+        const float gu = has_unit ? gcur[tid] : 0.f;
+        float vk[K0R];
+#pragma unroll
+        for (int k = 0; k < K0R; ++k) vk[k] = w0r[k] * gu;
+        const float r = wave_reduce_scatter32(vk, lane);
+        if ((lane & 1) == 0) red[wave * K0R + (lane >> 1)] = r;
+        __syncthreads();
+        for (int k = tid; k < K0; k += GC_THREADS) {
+            float v = 0.f;
+            for (int w = 0; w < GC_THREADS / 64; ++w) v += red[w * K0R + k];
+            use(k, v);
+        }
+        __syncthreads();
+        return true;
+    };
     for (int it = 0; it < A.iterations; ++it) {
         // ================= forward
         for (int t = 0; t < H; ++t) {
@@ -538,26 +602,7 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
             }
             __syncthreads();
             float* ht = hist + (size_t)t * L * Wp;
-            if (has_unit) {
-                float v = b0;
-#pragma unroll
-                for (int k = 0; k < K0R; ++k) v += w0r[k] * x0[k];
-                v = fmaxf(v, 0.0f);
-                cur[tid] = v;
-                ht[tid] = v;
-            }
-            __syncthreads();
-            for (int l = 1; l < L; ++l) {
-                const float* f = fw + (size_t)(l - 1) * GC_ROWS * m.rs + (size_t)g * m.rs;
-                float v = 0.f;
-#pragma unroll
-                for (int i = 0; i < WI; ++i) v += f[c + 32 * i] * cur[c + 32 * i];
-                v = gc_half_sum(v);
-                v = fmaxf(v + hbias[(size_t)l * Wp + p * GC_ROWS + g], 0.0f);
-                if (!gc_exchange<WI / 2>(xchg, Wp, p, phase, v, nxt, abort_flag, status)) return;
-                float* tmp = cur; cur = nxt; nxt = tmp;
-                if (has_unit) ht[(size_t)l * Wp + tid] = cur[tid];
-            }
+            if (!trunk(ht)) return;
             // output layer (redundant): half-wave g owns rows g + 16 mm
 #pragma unroll
             for (int mm = 0; mm < SM; ++mm) {
@@ -572,12 +617,35 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
                 }
             }
             __syncthreads();
+            if (A.reward) {
+                // the cost call's trunk pass on (norm(s_{t+1}), norm(a_t)): x0's action part still
+                // holds norm(a_t); only its activations are needed for the backward pass
+                for (int d = tid; d < s; d += GC_THREADS) {
+                    const float sv = st[(t + 1) * s + d];
+                    x0[d] = A.norm_s ? (sv - A.obs_mean[d]) / A.obs_std[d] : sv;
+                }
+                __syncthreads();
+                if (!trunk(hist + (size_t)(H + t) * L * Wp)) return;
+                __syncthreads();
+            }
         }
         // ================= backward, t = H-1 .. 0
         for (int d = tid; d < 32; d += GC_THREADS) gs[d] = 0.f;
         __syncthreads();
         for (int t = H - 1; t >= 0; --t) {
             const float* ht = hist + (size_t)t * L * Wp;
+            if (A.reward) {
+                // reward pass: d r_t / d head = grw through the reward row and the pass's ReLU masks;
+                // the state part joins d loss / d s_{t+1}, the action part waits in grad[t]
+                const float* hb = hist + (size_t)(H + t) * L * Wp;
+                if (has_unit) gcur[tid] = hb[(size_t)(L - 1) * Wp + tid] > 0.f ? wrb * grw : 0.f;
+                __syncthreads();
+                const bool ok = trunk_back(hb, [&](int k, float v) {
+                    if (k < s) gs[k] += A.norm_s ? v / A.obs_std[k] : v;
+                    else grad[t * a + k - s] = A.norm_a ? v / A.act_std[k - s] : v;
+                });
+                if (!ok) return;
+            }
             for (int d = tid; d < s; d += GC_THREADS) {
                 float gg = gs[d];
                 if (A.has_sc) {
@@ -589,8 +657,6 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
             }
             __syncthreads();
             // output layer backward (redundant): thread k = tid; ReLU mask of the last hidden layer
-            float* gcur = smem + m.gA;
-            float* gnxt = smem + m.gB;
             if (has_unit) {
                 float v = 0.f;
 #pragma unroll
@@ -598,42 +664,18 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
                 gcur[tid] = ht[(size_t)(L - 1) * Wp + tid] > 0.f ? v : 0.f;
             }
             __syncthreads();
-            for (int l = L - 1; l >= 1; --l) {
-                // my 16 input gradients of layer l: k = 16p + g, lanes over n
-                const float* b = bw + (size_t)(l - 1) * GC_ROWS * m.rs + (size_t)g * m.rs;
-                float v = 0.f;
-#pragma unroll
-                for (int i = 0; i < WI; ++i) v += b[c + 32 * i] * gcur[c + 32 * i];
-                v = gc_half_sum(v);
-                const int k = p * GC_ROWS + g;
-                v = ht[(size_t)(l - 1) * Wp + k] > 0.f ? v : 0.f;     // ReLU' of layer l - 1's output
-                if (!gc_exchange<WI / 2>(xchg, Wp, p, phase, v, gnxt, abort_flag, status)) return;
-                float* tmp = gcur; gcur = gnxt; gnxt = tmp;
-            }
-            // layer 0 backward (redundant): g_x0[k] = sum_u W0[u][k] g_z0[u], a block reduction per k
-            {
-                static_assert(K0R == 32, "wave_reduce_scatter32");
-                const float gu = has_unit ? gcur[tid] : 0.f;
-                float vk[K0R];
-#pragma unroll
-                for (int k = 0; k < K0R; ++k) vk[k] = w0r[k] * gu;
-                const float r = wave_reduce_scatter32(vk, lane);
-                if ((lane & 1) == 0) red[wave * K0R + (lane >> 1)] = r;
-                __syncthreads();
-                for (int k = tid; k < K0; k += GC_THREADS) {
-                    float v = 0.f;
-                    for (int w = 0; w < GC_THREADS / 64; ++w) v += red[w * K0R + k];
-                    if (k < s) {
-                        gs[k] = A.norm_s ? v / A.obs_std[k] : v;
-                    } else {
-                        const int j = k - s;
-                        float ga = A.norm_a ? v / A.act_std[j] : v;
-                        if (A.has_ac) ga += A.alpha_a * sinhf(acts[t * a + j] / A.alpha_a) / (float)a;
-                        grad[t * a + j] = ga;
-                    }
+            const bool ok = trunk_back(ht, [&](int k, float v) {
+                if (k < s) {
+                    gs[k] = A.norm_s ? v / A.obs_std[k] : v;
+                } else {
+                    const int j = k - s;
+                    float ga = A.norm_a ? v / A.act_std[j] : v;
+                    if (A.has_ac) ga += A.alpha_a * sinhf(acts[t * a + j] / A.alpha_a) / (float)a;
+                    if (A.reward) ga += grad[t * a + j];   // the reward pass's share (above)
+                    grad[t * a + j] = ga;
                 }
-                __syncthreads();
-            }
+            });
+            if (!ok) return;
         }
         // ================= Adam and the stop test (redundant, bit-identical in every workgroup)
         const float kk = (float)(it + 1);
@@ -675,7 +717,7 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
 
 bool gd_coop_supported(const GdArgs& A) {
     const int K0 = A.s + A.a;
-    if (A.reward || A.L < 2 || A.W != A.Wpad || A.Wpad > GC_THREADS || A.Wpad < 64 || K0 > 32 || A.s > 32) return false;
+    if (A.L < 2 || A.W != A.Wpad || A.Wpad > GC_THREADS || A.Wpad < 64 || K0 > 32 || A.s > 32) return false;
     return gc_lds(A.s, A.a, A.W, A.Wpad, A.L, A.H, 32).total <= 160 * 1024;
 }
 

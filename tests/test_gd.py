@@ -96,13 +96,13 @@ def test_gd_fused_kernel_matches_graph_path(cid, over, H, iters, stop):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["single", "abort"])
-def test_gd_cooperative_kernel_and_its_fallback(mode):
-    """mbrl_gd_plan runs the cooperative kernel for W in {64..512}: it must agree with the
-    one-workgroup kernel (MBRL_OPT_GD_SINGLE), and when a hand-off gives up (MBRL_OPT_DEBUG_GD_ABORT)
-    the gated one-workgroup kernel must produce the plan instead."""
+@pytest.mark.parametrize("mode,cid", [("single", 3), ("abort", 3), ("single", 6), ("abort", 6)])
+def test_gd_cooperative_kernel_and_its_fallback(mode, cid):
+    """mbrl_gd_plan runs the cooperative kernel for W in {64..512} (goal-state and reward-head models):
+    it must agree with the one-workgroup kernel (MBRL_OPT_GD_SINGLE), and when a hand-off gives up
+    (MBRL_OPT_DEBUG_GD_ABORT) the gated one-workgroup kernel must produce the plan instead."""
     from mbrl_amd import _lib, gd
-    p, model_fn, cost_fn = closures(3, dict(W=256, L=3))
+    p, model_fn, cost_fn = closures(cid, dict(W=256, L=3))
     mdesc, cdesc = gd.describe(model_fn, cost_fn)
     dev = torch.device("cuda:0")
     H, a = 12, p["cfg"]["a"]
