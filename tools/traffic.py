@@ -25,7 +25,9 @@ def main():
         for r in csv.DictReader(open(f)):
             vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
             kernel = r["Kernel_Name"]
-    out = os.path.join(REPO, "profiles", f"{tag}_rollout_pmc.csv")
+    pdir = os.environ.get("PROFILE_DIR", os.path.join(REPO, "profiles"))   # GPU box: under gpurun_out/
+    os.makedirs(pdir, exist_ok=True)
+    out = os.path.join(pdir, f"{tag}_rollout_pmc.csv")
     with open(out, "w") as fh:
         fh.write("kernel,counter,dispatches,mean_excl_first,min,max\n")
         for k, v in sorted(vals.items()):
@@ -33,7 +35,9 @@ def main():
             fh.write(f"\"{kernel}\",{k},{len(v)},{sum(warm) / len(warm):.1f},{min(v):.1f},{max(v):.1f}\n")
     mean = {k: (sum(v[1:]) / len(v[1:]) if len(v) > 1 else v[0]) for k, v in vals.items()}
     traffic = 2 * mean["FETCH_SIZE"] * 1024 + mean["WRITE_SIZE"] * 1024
-    tj = os.path.join(REPO, "profiles", "rollout_traffic.json")
+    tj = os.path.join(pdir, "rollout_traffic.json")
+    if not os.path.exists(tj) and os.path.exists(os.path.join(REPO, "profiles", "rollout_traffic.json")):
+        json.dump(json.load(open(os.path.join(REPO, "profiles", "rollout_traffic.json"))), open(tj, "w"))
     d = json.load(open(tj)) if os.path.exists(tj) else {}
     d[name] = traffic
     d["_method"] = ("bytes per rollout launch = 2*FETCH_SIZE + WRITE_SIZE (KiB->B), mean over warm dispatches; "
