@@ -984,9 +984,19 @@ __global__ void __launch_bounds__(64 * m8_waves(T, NOT_T), 1) rollout_m8_kernel(
                 if (A.states_out != nullptr && n < A.N)
                     A.states_out[(((size_t)e * A.H + t) * A.N + n) * A.s + d] = sn;
             };
+            if constexpr (SS <= MBRL_EPI_REG_SLOTS) {
 #pragma unroll
-            for (int k = 0; k < SS; ++k)
-                if (j + 16 * k < A.s) slot(j + 16 * k, P.om[k], P.os[k], P.goal[k], P.cw[k], P.bo[k]);
+                for (int k = 0; k < SS; ++k)
+                    if (j + 16 * k < A.s) slot(j + 16 * k, P.om[k], P.os[k], P.goal[k], P.cw[k], P.bo[k]);
+            } else {
+                // wide states: the same values from LDS, in the same order (as the 16-candidate kernel)
+                const float* bout = L.hbias + A.L * A.Wpad;
+#pragma unroll
+                for (int k = 0; k < SS; ++k) {
+                    const int d = j + 16 * k;
+                    if (d < A.s) slot(d, L.obs_mean[d], L.obs_std[d], L.goal[d], L.cw[d], bout[d]);
+                }
+            }
             for (int d = A.s + A.a + j; d < A.s + A.a + A.k0pad_extra; d += 16) actX[m * A.lda + d] = 0.f;
             sc = rowsum16(sc);
             const float ac = acs[(t & 1) * M + m];
