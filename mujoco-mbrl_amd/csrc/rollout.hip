@@ -29,6 +29,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "mbrl_internal.h"
 
 // Waves per workgroup for the rollout: 8 (two per SIMD, T/2 tiles each) for R = 1, 4 for R = 2 (the
@@ -427,8 +429,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
         if constexpr (RING) {
             // a chunk whose 16 inputs are all zero padding (k >= s + a) is skipped: the accumulator starts
             // at +0 and a round-to-nearest sum never turns +0 into -0, so adding exact zero products
-            // leaves it unchanged and the bits match. (Skipping single padded k inside the 8-candidate
-            // kernel's chunks, a branch per 4x4x1 MFMA, measured slower for cartpole: 0.077 -> 0.082 ms.)
+            // leaves it unchanged and the bits match (rollout_m8_kernel's K0L does it per MFMA).
 #pragma unroll
             for (int kc = 0; kc < K0C_T; ++kc) {
                 MBRL_LOAD_CHUNK(ring[((kc % NB) + NB - 1) % NB], g + NB - 1);
@@ -692,7 +693,11 @@ hipError_t launch_rollout(const RolloutArgs& A, int T, int R, hipStream_t stream
 constexpr bool m8_kp(int T, int NOT) { return T == 4 && NOT == 2; }
 constexpr int m8_waves(int T, int NOT) { return m8_kp(T, NOT) ? 8 : T; }
 
-template <int T, int K0C_T, int NOT_T>
+// K0L > 0 (compile time): every real input index k = s + a is below K0L, so layer-0 MFMAs whose k is
+// >= K0L (zero padding: weight and activation both +0) are not issued -- bit-identical, since the
+// accumulator starts at +0 and a round-to-nearest sum never turns +0 into -0. Instantiated for
+// cartpole's KP shape (6 inputs: 8 of 32 dependent layer-0 MFMAs per wave remain).
+template <int T, int K0C_T, int NOT_T, int K0L = 0>
 __global__ void __launch_bounds__(64 * m8_waves(T, NOT_T), 1) rollout_m8_kernel(const RolloutArgs A) {
     constexpr int M = 8;
     constexpr bool KP = m8_kp(T, NOT_T);
@@ -823,6 +828,29 @@ __global__ void __launch_bounds__(64 * m8_waves(T, NOT_T), 1) rollout_m8_kernel(
                 }
         }
     };
+    auto mma_pair_l0 = [&](const f32x4 (&w)[RSL], const f32x4 (&b)[4], auto kcc) {
+        constexpr int kc = decltype(kcc)::value;
+        if constexpr (KP) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const float a = w[i >> 2][i & 3];
+                const int p0 = 2 * i, p1 = 2 * i + 1;    // position p = 4 s + q, k = 16 kc + 4 q + s
+                if (16 * kc + 4 * (p0 & 3) + (p0 >> 2) < K0L)
+                    acc[0] = __builtin_amdgcn_mfma_f32_4x4x1f32(a, b[p0 & 3][p0 >> 2], acc[0], 1, 0, 0);
+                if (16 * kc + 4 * (p1 & 3) + (p1 >> 2) < K0L)
+                    acc[0] = __builtin_amdgcn_mfma_f32_4x4x1f32(a, b[p1 & 3][p1 >> 2], acc[0], 1, 1, 0);
+            }
+        } else {
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (16 * kc + 4 * q + s < K0L) {
+                        acc[0] = __builtin_amdgcn_mfma_f32_4x4x1f32(w[s][q], b[q][s], acc[0], 1, 0, 0);
+                        acc[TPW - 1] = __builtin_amdgcn_mfma_f32_4x4x1f32(w[s][q], b[q][s], acc[TPW - 1], 1, 1, 0);
+                    }
+        }
+    };
     auto store_layer = [&](float* out) {
         const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -858,8 +886,21 @@ __global__ void __launch_bounds__(64 * m8_waves(T, NOT_T), 1) rollout_m8_kernel(
         zero_acc8();
         load_bias8(L.hbias);
         read_b(bb[0], actX, 0);
+        if constexpr (K0L > 0) {
+            static_assert(K0C_T == 2, "K0L instance");
+            M8_LOAD((0 + NB - 1) % NB, g + NB - 1);
+            read_b(bb[1], actX, 16);
+            mma_pair_l0(ring[0], bb[0], std::integral_constant<int, 0>());
+            MBRL_PIN();
+            ++g;
+            M8_LOAD((1 + NB - 1) % NB, g + NB - 1);
+            mma_pair_l0(ring[1], bb[1], std::integral_constant<int, 1>());
+            MBRL_PIN();
+            ++g;
+        } else {
 #pragma unroll
-        for (int kc = 0; kc < K0C_T; ++kc) M8_CHUNK(kc % NB, kc, K0C_T, actX);
+            for (int kc = 0; kc < K0C_T; ++kc) M8_CHUNK(kc % NB, kc, K0C_T, actX);
+        }
         STAMP(0);
         store_layer(actY);
         if (A.L > 1) __syncthreads();
@@ -1042,20 +1083,23 @@ bool rollout_m8_supported(const RolloutArgs& A, int T) {
     return (A.K0C == 2 || A.K0C == 6) && (A.NOT == 2 || A.NOT == 6) && rollout_lds_bytes(A, 8) <= 160 * 1024;
 }
 
-template <int T, int K0C_T, int NOT_T>
+template <int T, int K0C_T, int NOT_T, int K0L = 0>
 static hipError_t launch_m8_tr(const RolloutArgs& A_in, hipStream_t stream) {
     RolloutArgs A = A_in;
     A.nw = 8;   // output partials: the 8-wave kernel's count
     dim3 grid((A.N + 7) / 8, A.E);
     const size_t lds = rollout_lds_bytes(A, 8);
-    hipError_t e = ensure_dynamic_lds(reinterpret_cast<const void*>(&rollout_m8_kernel<T, K0C_T, NOT_T>), 160 * 1024);
+    const auto fn = &rollout_m8_kernel<T, K0C_T, NOT_T, K0L>;
+    hipError_t e = ensure_dynamic_lds(reinterpret_cast<const void*>(fn), 160 * 1024);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((rollout_m8_kernel<T, K0C_T, NOT_T>), grid, dim3(64 * m8_waves(T, NOT_T)), lds, stream, A);
+    hipLaunchKernelGGL(fn, grid, dim3(64 * m8_waves(T, NOT_T)), lds, stream, A);
     return hipGetLastError();
 }
 
 template <int T>
 static hipError_t launch_m8_t(const RolloutArgs& A, hipStream_t stream) {
+    if constexpr (T == 4)   // cartpole-sized inputs in KP mode: padded layer-0 MFMAs not issued
+        if (A.K0C == 2 && A.NOT == 2 && A.s + A.a <= 8) return launch_m8_tr<T, 2, 2, 8>(A, stream);
     if (A.K0C == 2 && A.NOT == 2) return launch_m8_tr<T, 2, 2>(A, stream);
     if (A.K0C == 6 && A.NOT == 6) return launch_m8_tr<T, 6, 6>(A, stream);
     if (A.K0C == 2 && A.NOT == 6) return launch_m8_tr<T, 2, 6>(A, stream);
