@@ -221,6 +221,10 @@ class TransitionsDataset(Dataset):
         """Every (roll_idx, start_idx) the sampler can draw, in the sampler's pre-shuffle order."""
         return [(ri, si) for ri, roll in enumerate(self._rollouts) for si in range(len(roll) - self.horizon)]
 
+    def num_transitions(self):
+        """len(transition_index()) without building the list."""
+        return sum(max(0, len(roll) - self.horizon) for roll in self._rollouts)
+
     def stacked(self, device):
         """(index, inputs, outputs) with inputs/outputs tuples of [T, horizon, dim] tensors on `device`,
         T = len(transition_index()), field order as __getitem__ yields them (flat observations only)."""

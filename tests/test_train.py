@@ -78,6 +78,30 @@ def test_dataset_semantics():
     assert torch.allclose(ds.statistics["rewards"]["mean"], torch.tensor(101.5))
 
 
+@pytest.mark.parametrize("lengths,horizon", [([501] * 20, 1), ([7, 2, 30, 3], 2), ([3], 1), ([5, 5], 3)])
+def test_epoch_order_is_the_samplers_shuffle(lengths, horizon):
+    """train_model's row order (models._epoch_order: shuffle of arange) is the order
+    TransitionsSampler yields (shuffle of the (rollout, start) list), and both leave NumPy's global
+    RNG in the same state."""
+    from mbrl_amd import data, models
+    rolls = [data.Rollout(states=[torch.zeros(2)] * n, observations=[torch.zeros(2)] * n,
+                          actions=[torch.zeros(1)] * (n - 1), rewards=[torch.tensor(0.0)] * (n - 1))
+             for n in lengths]
+    ds = data.TransitionsDataset(rollouts=rolls, horizon=horizon, normalise=False)
+    index = ds.transition_index()
+    pos = {t: i for i, t in enumerate(index)}
+    for seed in (0, 7, 123):
+        np.random.seed(seed)
+        ref = [pos[t] for t in data.TransitionsSampler(ds)]
+        ref_next = np.random.random_sample(3)
+        np.random.seed(seed)
+        got = models._epoch_order(ds)
+        assert got.tolist() == ref and ds.num_transitions() == len(index)
+        assert np.array_equal(np.random.random_sample(3), ref_next)
+    batches = models._epoch_batches(ds, 4)
+    assert [len(b) for b in batches] == [min(4, len(index) - i) for i in range(0, len(index), 4)]
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", list(mg.CASES))
 def test_train_model_on_gpu_matches_reference(golden, name):
