@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MBRL_ABI_VERSION 5
+#define MBRL_ABI_VERSION 6
 
 typedef struct ihipStream_t* mbrl_stream_t; /* == hipStream_t */
 typedef struct ihipEvent_t* mbrl_event_t;   /* == hipEvent_t  */
@@ -153,7 +153,8 @@ enum {
     MBRL_OPT_GD_SINGLE = 3,         /* 1: mbrl_gd_plan runs its one-workgroup kernel                  */
     MBRL_OPT_DEBUG_GD_ABORT = 4,    /* 1: the cooperative gd kernel gives up at once                  */
     MBRL_OPT_UNFUSED_UPDATE = 5,    /* 1: plans run select / refit / proposal draw as separate launches */
-    MBRL_OPT_COUNT = 6
+    MBRL_OPT_ADAM_ARITH = 6,        /* mbrl_adam_step contraction pattern: 0 = torch's; 1 + bits (test) */
+    MBRL_OPT_COUNT = 7
 };
 int mbrl_set_option(int32_t option, int32_t value);
 int mbrl_get_option(int32_t option);
@@ -270,6 +271,69 @@ int mbrl_gd_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_nor
                  const float* s0, float* actions, int32_t H, int32_t num_iterations, float stop_condition,
                  float lr, float* states_out, int32_t* iterations_out, void* workspace, size_t ws_bytes,
                  mbrl_stream_t stream);
+
+/* ---- model training: torch.optim.Adam.step() for one fp32 parameter group
+ * (torch/optim/adam.py _multi_tensor_adam, capturable = False, amsgrad = False, maximize = False),
+ * the optimizer the reference's training loop steps once per batch (models.py:53-93 with the
+ * optimizer of experiment.py:55-62), as one launch over all of the group's tensors. It leaves the
+ * parameters, exp_avg and exp_avg_sq bit-identical to torch's own step; the caller keeps the step
+ * counters (CPU tensors in torch) and computes the per-tensor scalars in double as adam.py does:
+ *   step_size = float(-(lr / (1 - beta1 ** step))),  bc2_sqrt = float((1 - beta2 ** step) ** 0.5)
+ * with `step` already incremented. grad is read only (weight decay does not write it back). */
+typedef struct {
+    float* param;
+    const float* grad;
+    float* exp_avg;
+    float* exp_avg_sq;
+    int64_t numel;
+    float step_size;
+    float bc2_sqrt;
+} mbrl_adam_tensor;
+
+typedef struct {
+    float lerp_weight;      /* float(1 - beta1) */
+    float beta2;            /* float(beta2)     */
+    float one_minus_beta2;  /* float(1 - beta2) */
+    float eps;              /* float(eps)       */
+    float weight_decay;     /* float(weight_decay); 0 = none (L2 added to the gradient, Adam not AdamW) */
+} mbrl_adam_hparams;
+
+int mbrl_adam_step(const mbrl_adam_tensor* tensors, int32_t count, const mbrl_adam_hparams* hparams,
+                   mbrl_stream_t stream);
+
+/* ---- model training: the gradient of one batch's loss for the reference's
+ * MLP dynamics models -- Model (models.py:96-110: n_hidden Linear-ReLU layers and a linear state
+ * head) and ModelWithReward (models.py:125-163: the same trunk, a state head and a reward head) --
+ * under the loss of their train_model (models.py:53-93, 165-217): MSELoss(predicted next state,
+ * next state) (+ MSELoss(predicted reward, reward)) summed over the horizon steps, i.e. what
+ * `loss.backward()` leaves in each Linear's .grad after optimizer.zero_grad(). The batch is
+ * `batch` transitions of the stacked dataset, rows batch_idx[0..batch) (each < transitions, not
+ * checked on the device), every horizon step of each. fp32 throughout; the summation order is not
+ * autograd's, so gradients match torch's to rounding, not bit for bit.
+ * weight / bias: linear1 .. linear{n_hidden} (the trunk, hidden x in), linear{n_hidden+1} (state
+ * head, state_dim x hidden) and, with reward_head, linear{n_hidden+2} (1 x hidden); the *_grad
+ * arrays are overwritten. loss_out: 3 device floats (total, state, reward) or NULL.
+ * workspace >= mbrl_train_workspace_bytes(model, batch). */
+#define MBRL_TRAIN_MAX_LAYERS 10   /* n_hidden + 2 */
+typedef struct {
+    int32_t state_dim, action_dim, hidden, n_hidden, reward_head, horizon;
+    const float* weight[MBRL_TRAIN_MAX_LAYERS];
+    const float* bias[MBRL_TRAIN_MAX_LAYERS];
+    float* weight_grad[MBRL_TRAIN_MAX_LAYERS];
+    float* bias_grad[MBRL_TRAIN_MAX_LAYERS];
+} mbrl_train_model;
+
+typedef struct {
+    const float* states;       /* [transitions][horizon][state_dim]  (TransitionsDataset.stacked) */
+    const float* actions;      /* [transitions][horizon][action_dim] */
+    const float* next_states;  /* [transitions][horizon][state_dim]  */
+    const float* rewards;      /* [transitions][horizon], read with reward_head only */
+    int64_t transitions;
+} mbrl_train_data;
+
+size_t mbrl_train_workspace_bytes(const mbrl_train_model* model, int32_t batch);
+int mbrl_train_grads(const mbrl_train_model* model, const mbrl_train_data* data, const int64_t* batch_idx,
+                     int32_t batch, float* loss_out, void* workspace, size_t ws_bytes, mbrl_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -1246,6 +1246,7 @@ int mbrl_set_option(int32_t option, int32_t value) {
     switch (option) {
         case MBRL_OPT_ROLLOUT_TILE: ok = value == 0 || value == 8 || value == 16; break;
         case MBRL_OPT_SPLIT_TILE: ok = value == 0 || value == 16 || value == 32; break;
+        case MBRL_OPT_ADAM_ARITH: ok = value >= 0 && value <= 16; break;
         default: ok = value == 0 || value == 1; break;
     }
     if (!ok) return fail(MBRL_EINVAL, "option %d: value %d not allowed", option, value);
@@ -1403,6 +1404,57 @@ int mbrl_cem_update(const float* costs, int32_t E, int32_t N, int32_t K, const m
     U.mu_out = mu_out; U.sigma_out = sigma_out;
     U.next_actions = next_actions; U.draw_off = next_actions ? draw_offset : 0; U.draw_n = next_actions ? draw_count : N;
     return update_impl(U, 1, reinterpret_cast<hipStream_t>(stream));
+}
+
+int mbrl_adam_step(const mbrl_adam_tensor* tensors, int32_t count, const mbrl_adam_hparams* hparams,
+                   mbrl_stream_t stream) {
+    if (count < 0 || (count > 0 && !tensors) || !hparams) return fail(MBRL_EINVAL, "adam_step: NULL argument");
+    for (int i = 0; i < count; ++i) {
+        const mbrl_adam_tensor& t = tensors[i];
+        if (t.numel < 0 || (t.numel > 0 && (!t.param || !t.grad || !t.exp_avg || !t.exp_avg_sq)))
+            return fail(MBRL_EINVAL, "adam_step: tensor %d: NULL pointer or negative numel", i);
+    }
+    const int o = g_opt[MBRL_OPT_ADAM_ARITH].load(std::memory_order_relaxed);
+    return hip_check(launch_adam_step(tensors, count, *hparams, o ? o - 1 : ADAM_ARITH_TORCH,
+                                      reinterpret_cast<hipStream_t>(stream)), "adam_step");
+}
+
+static int train_shape(const mbrl_train_model* m, TrainShape* t) {
+    if (!m) return fail(MBRL_EINVAL, "train: NULL model");
+    if (m->state_dim < 1 || m->action_dim < 0 || m->hidden < 1 || m->horizon < 1 || m->n_hidden < 1 ||
+        m->n_hidden + 2 > MBRL_TRAIN_MAX_LAYERS || (m->reward_head != 0 && m->reward_head != 1))
+        return fail(MBRL_EINVAL, "train: bad shape (state %d, action %d, hidden %d x %d, horizon %d, reward %d)",
+                    m->state_dim, m->action_dim, m->hidden, m->n_hidden, m->horizon, m->reward_head);
+    t->s = m->state_dim; t->a = m->action_dim; t->W = m->hidden; t->L = m->n_hidden; t->reward = m->reward_head;
+    t->H = m->horizon;
+    return MBRL_OK;
+}
+
+size_t mbrl_train_workspace_bytes(const mbrl_train_model* model, int32_t batch) {
+    TrainShape t;
+    if (batch < 1 || train_shape(model, &t) != MBRL_OK) return 0;
+    return train_ws_floats(t, batch) * sizeof(float);
+}
+
+int mbrl_train_grads(const mbrl_train_model* model, const mbrl_train_data* data, const int64_t* batch_idx,
+                     int32_t batch, float* loss_out, void* workspace, size_t ws_bytes, mbrl_stream_t stream) {
+    TrainShape t;
+    if (int rc = train_shape(model, &t)) return rc;
+    if (!data || !batch_idx || !workspace || !data->states || !data->next_states || (t.a > 0 && !data->actions) ||
+        (t.reward && !data->rewards))
+        return fail(MBRL_EINVAL, "train_grads: NULL argument");
+    if (batch < 1 || (int64_t)batch > data->transitions)
+        return fail(MBRL_EINVAL, "train_grads: batch %d outside [1, %lld]", batch, (long long)data->transitions);
+    const int layers = t.L + 1 + t.reward;
+    for (int l = 0; l < layers; ++l)
+        if (!model->weight[l] || !model->bias[l] || !model->weight_grad[l] || !model->bias_grad[l])
+            return fail(MBRL_EINVAL, "train_grads: layer %d: NULL weight, bias or gradient", l);
+    const size_t need = train_ws_floats(t, batch) * sizeof(float);
+    if (ws_bytes < need) return fail(MBRL_EWORKSPACE, "train_grads: workspace %zu < %zu bytes", ws_bytes, need);
+    TrainTensors w{model->weight, model->bias, model->weight_grad, model->bias_grad,
+                   data->states, data->actions, data->next_states, data->rewards};
+    return hip_check(launch_train_grads(t, w, batch_idx, batch, loss_out, static_cast<float*>(workspace),
+                                        reinterpret_cast<hipStream_t>(stream)), "train_grads");
 }
 
 // Workspace for mbrl_trajectory: per-member states, exchange granules, status word.

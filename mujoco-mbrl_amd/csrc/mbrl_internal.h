@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
+#include "../../include/mbrl_cem.h"
 
 namespace mbrl {
 
@@ -278,5 +279,29 @@ hipError_t launch_traj_reg(const TrajArgs& A, int E, hipStream_t stream);
 size_t traj_coop_xchg_bytes(const TrajArgs& A, int E);
 hipError_t launch_traj_coop(const TrajArgs& A, int E, unsigned long long* xchg, unsigned* status,
                             hipStream_t stream);
+
+// mbrl_adam_step (train.hip). AdamArith bits: which of torch's element-wise expressions its build
+// contracts to a fused multiply-add; ADAM_ARITH_TORCH is the pattern pinned against torch.optim.Adam
+// on the MI355X (tests/test_gpu_train_adam.py).
+enum { ADAM_FMA_WD = 1, ADAM_FMA_LERP = 2, ADAM_FMA_ADDCMUL = 4, ADAM_FMA_ADDCDIV = 8 };
+constexpr int ADAM_ARITH_TORCH = ADAM_FMA_WD | ADAM_FMA_LERP | ADAM_FMA_ADDCMUL | ADAM_FMA_ADDCDIV;
+constexpr int ADAM_MAX_TENSORS = 32;   // tensors per launch (the table travels in the kernel arguments)
+hipError_t launch_adam_step(const mbrl_adam_tensor* tensors, int count, const mbrl_adam_hparams& hp, int arith,
+                            hipStream_t stream);
+
+// mbrl_train_grads (train.hip): the MLP's loss gradient for one batch, n_hidden + 2 launches.
+struct TrainShape {
+    int s, a, W, L, reward, H;   // state / action dims, hidden width, hidden layers, reward head, horizon
+};
+struct TrainTensors {
+    const float* const* weight;  // L + 1 (+ 1 reward head) nn.Linear weights [out][in]
+    const float* const* bias;
+    float* const* weight_grad;
+    float* const* bias_grad;
+    const float *states, *actions, *next_states, *rewards;   // stacked transitions [T][H][.]
+};
+size_t train_ws_floats(const TrainShape& t, int batch);
+hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const int64_t* idx, int batch,
+                              float* loss_out, float* ws, hipStream_t stream);
 
 }  // namespace mbrl

@@ -21,7 +21,7 @@ MBRL_OK = 0
 MBRL_EUNSUPPORTED = -2
 MBRL_COST_GOAL_STATE = 0
 MBRL_COST_MODEL_REWARD = 1
-ABI_VERSION = 5
+ABI_VERSION = 6
 MBRL_NAN_LAST = 0
 MBRL_NAN_FIRST = 1
 MBRL_PRECISION_F32 = 0
@@ -30,7 +30,7 @@ MBRL_PRECISION_F16X6 = 2
 PRECISIONS = {"f32": MBRL_PRECISION_F32, "f16x3": MBRL_PRECISION_F16X3, "f16x6": MBRL_PRECISION_F16X6}
 # mbrl_set_option switches (include/mbrl_cem.h MBRL_OPT_*): A/B runs and forced fallbacks in tests
 OPTIONS = {"rollout_tile": 0, "split_tile": 1, "debug_traj_abort": 2, "gd_single": 3, "debug_gd_abort": 4,
-           "unfused_update": 5}
+           "unfused_update": 5, "adam_arith": 6}
 
 
 def precision_code(name):
@@ -49,7 +49,7 @@ EXPORTED = (
     "mbrl_refit_workspace_bytes", "mbrl_cem_refit", "mbrl_sample_actions",
     "mbrl_trajectory_workspace_bytes", "mbrl_trajectory", "mbrl_cem_workspace_bytes", "mbrl_cem_plan",
     "mbrl_cem_plan_batch_workspace_bytes", "mbrl_cem_plan_batch", "mbrl_gd_workspace_bytes", "mbrl_gd_plan",
-    "mbrl_cem_update",
+    "mbrl_cem_update", "mbrl_adam_step", "mbrl_train_workspace_bytes", "mbrl_train_grads",
 )
 
 
@@ -80,6 +80,31 @@ class CemParams(ctypes.Structure):
     _fields_ = [("N", c_int32), ("H", c_int32), ("K", c_int32), ("iterations", c_int32),
                 ("alpha", c_float), ("lo", c_float), ("hi", c_float), ("init_mu", c_float),
                 ("init_sigma", c_float), ("_pad", c_int32), ("seed", c_uint64)]
+
+
+class AdamTensor(ctypes.Structure):
+    _fields_ = [("param", c_void_p), ("grad", c_void_p), ("exp_avg", c_void_p), ("exp_avg_sq", c_void_p),
+                ("numel", c_int64), ("step_size", c_float), ("bc2_sqrt", c_float)]
+
+
+class AdamHparams(ctypes.Structure):
+    _fields_ = [("lerp_weight", c_float), ("beta2", c_float), ("one_minus_beta2", c_float), ("eps", c_float),
+                ("weight_decay", c_float)]
+
+
+TRAIN_MAX_LAYERS = 10
+
+
+class TrainModel(ctypes.Structure):
+    _fields_ = [("state_dim", c_int32), ("action_dim", c_int32), ("hidden", c_int32), ("n_hidden", c_int32),
+                ("reward_head", c_int32), ("horizon", c_int32), ("weight", c_void_p * TRAIN_MAX_LAYERS),
+                ("bias", c_void_p * TRAIN_MAX_LAYERS), ("weight_grad", c_void_p * TRAIN_MAX_LAYERS),
+                ("bias_grad", c_void_p * TRAIN_MAX_LAYERS)]
+
+
+class TrainData(ctypes.Structure):
+    _fields_ = [("states", c_void_p), ("actions", c_void_p), ("next_states", c_void_p), ("rewards", c_void_p),
+                ("transitions", c_int64)]
 
 
 _lib = None
@@ -122,6 +147,9 @@ def load():
         "mbrl_gd_workspace_bytes": (c_size_t, [POINTER(MlpShape), c_int32]),
         "mbrl_gd_plan": (c_int32, [POINTER(MlpShape), P, POINTER(Norm), POINTER(Cost), P, P, c_int32, c_int32,
                                    c_float, c_float, P, P, P, c_size_t, P]),
+        "mbrl_adam_step": (c_int32, [POINTER(AdamTensor), c_int32, POINTER(AdamHparams), P]),
+        "mbrl_train_workspace_bytes": (c_size_t, [POINTER(TrainModel), c_int32]),
+        "mbrl_train_grads": (c_int32, [POINTER(TrainModel), POINTER(TrainData), P, c_int32, P, P, c_size_t, P]),
         "mbrl_cem_plan": (c_int32, [POINTER(MlpShape), P, POINTER(Norm), POINTER(Cost), P, POINTER(CemParams),
                                     P, P, P, P, P, P, P, P, P, c_size_t, P]),
     }
@@ -178,4 +206,5 @@ def require_gpu(t):
 __all__ = ["load", "check", "ptr", "stream_handle", "MlpShape", "Norm", "Cost", "Sampler", "CemParams",
            "EXPORTED", "MBRL_NAN_LAST", "MBRL_NAN_FIRST", "MBRL_COST_GOAL_STATE", "MBRL_COST_MODEL_REWARD",
            "ABI_VERSION", "c_int64", "MBRL_PRECISION_F32", "MBRL_PRECISION_F16X3", "MBRL_PRECISION_F16X6",
-           "precision_code", "option", "OPTIONS"]
+           "precision_code", "option", "OPTIONS", "AdamTensor", "AdamHparams",
+           "TrainModel", "TrainData", "TRAIN_MAX_LAYERS"]

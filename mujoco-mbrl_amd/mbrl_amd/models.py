@@ -6,11 +6,14 @@ autograd off it runs the one-step batch through the same HIP rollout kernel the 
 (H = 1, per-row start states); otherwise (training, CPU tensors) it is plain PyTorch, exactly the
 reference's arithmetic.
 """
+import ctypes
 import functools
 
 import numpy as np
 import torch
 import torch.nn as nn
+
+from .optim import AdamStep
 
 
 def _epoch_order(dataset):
@@ -50,10 +53,10 @@ def _batch_loss(dataset, ins, outs, idx, step_loss, n_parts):
 
 
 class _GraphStep:
-    """A full-size batch's gather + forward + loss + backward captured once in a HIP graph (through
-    torch.cuda.CUDAGraph) and replayed per batch; optimizer.step() stays eager so any optimizer
-    works unchanged. The warm-up before capture only touches .grad (zeroed after), never the
-    parameters, so training follows exactly the eager sequence of updates."""
+    """A full-size batch's zero_grad + gather + forward + loss + backward captured once in a HIP
+    graph (through torch.cuda.CUDAGraph) and replayed per batch; optimizer.step() stays outside the
+    graph so any optimizer works unchanged. The warm-up before capture only touches .grad (zeroed
+    after), never the parameters, so training follows exactly the eager sequence of updates."""
 
     def __init__(self, model, dataset, ins, outs, batch_size, step_loss, n_parts):
         dev = _device_of(model)
@@ -67,65 +70,155 @@ class _GraphStep:
                 loss.backward()
             del loss                      # drop the warm-up autograd graph before capturing
         torch.cuda.current_stream(dev).wait_stream(side)
-        self._zero()
+        grads = [p.grad for p in self.params if p.grad is not None]
+        if grads:
+            torch._foreach_zero_(grads)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
+            if grads:                     # zero_grad() as the graph's first node: backward accumulates
+                torch._foreach_zero_(grads)
             self.loss, self.parts = _batch_loss(dataset, ins, outs, self.idx, step_loss, n_parts)
             self.loss.backward()
         # the replay accumulates into exactly these tensors; an eager step in between (the last,
         # partial batch: optimizer.zero_grad() sets .grad to None) must not orphan them
         self.grads = [p.grad for p in self.params]
 
-    def _zero(self):
-        grads = [p.grad for p in self.params if p.grad is not None]
-        if grads:
-            torch._foreach_zero_(grads)
-
     def run(self, rows):
         self.idx.copy_(rows)
         for p, g in zip(self.params, self.grads):
             p.grad = g
-        torch._foreach_zero_(self.grads)
         self.graph.replay()
         return self.loss, self.parts
 
 
-def _train_loop(model, dataset, optimizer, batch_size, num_epochs, step_loss, writer, tags):
+# train_model's device path for the reference's MLP models under the default MSELoss: the batch
+# gradient from mbrl_train_grads (csrc/train.hip) instead of autograd. False: autograd in a HIP graph.
+NATIVE_TRAINING = True
+
+
+class _NativeGrads:
+    """mbrl_train_grads for Model (noise None) / ModelWithReward with MSELoss(reduction='mean'):
+    per batch, one C call that gathers the batch, runs the forward pass and the loss gradient, and
+    overwrites every Linear's .grad (what zero_grad + backward leave). The loss values come back
+    as device scalars (total, state, reward) for the writer."""
+
+    def __init__(self, model, ins, outs, horizon, batch_size, reward):
+        from . import _lib
+        self.lib = _lib.load()
+        dev = _device_of(model)
+        lins = model.linears()
+        self.params = [t for lin in lins for t in (lin.weight, lin.bias)]
+        self.grads = [torch.zeros_like(t) for t in self.params]
+        m = _lib.TrainModel()
+        m.state_dim, m.action_dim, m.hidden = model.state_dim, model.action_dim, model.hidden_units
+        m.n_hidden, m.reward_head, m.horizon = model.n_hidden, int(reward), int(horizon)
+        for i, lin in enumerate(lins):
+            m.weight[i], m.bias[i] = lin.weight.data_ptr(), lin.bias.data_ptr()
+            m.weight_grad[i], m.bias_grad[i] = self.grads[2 * i].data_ptr(), self.grads[2 * i + 1].data_ptr()
+        (states, actions), (rewards, next_states) = ins, outs
+        self.keep = [x.contiguous() for x in (states, actions, next_states, rewards)]
+        d = _lib.TrainData()
+        d.states, d.actions, d.next_states, d.rewards = [x.data_ptr() for x in self.keep]
+        d.transitions = states.shape[0]
+        self.model, self.data = m, d
+        need = self.lib.mbrl_train_workspace_bytes(ctypes.byref(m), int(batch_size))
+        if need == 0:
+            _lib.check(-1, "mbrl_train_workspace_bytes")
+        self.ws = torch.empty(need, dtype=torch.uint8, device=dev)
+        self.loss = torch.zeros(3, dtype=torch.float32, device=dev)
+        self.ptrs = [t.data_ptr() for t in self.params]
+        self.dev = dev
+        self._lib = _lib
+
+    @staticmethod
+    def supported(model, dataset, ins, outs, criterion):
+        if not NATIVE_TRAINING or type(criterion) is not torch.nn.MSELoss or criterion.reduction != "mean":
+            return None
+        if type(model) is Model:
+            if model.noise is not None:
+                return None
+            reward = False
+        elif type(model) is ModelWithReward:
+            reward = True
+        else:
+            return None
+        if model.n_hidden < 1 or model.n_hidden + 2 > 10 or len(ins) != 2 or len(outs) != 2:
+            return None
+        params = list(model.parameters())
+        if len(params) != 2 * len(model.linears()):
+            return None
+        if not all(p.is_cuda and p.dtype == torch.float32 and p.is_contiguous() and p.requires_grad for p in params):
+            return None
+        (states, actions), (rewards, next_states) = ins, outs
+        T, H = states.shape[0], dataset.horizon
+        want = [(states, model.state_dim), (actions, model.action_dim), (next_states, model.state_dim)]
+        if any(tuple(x.shape) != (T, H, w) or x.dtype != torch.float32 for x, w in want):
+            return None
+        if rewards.numel() != T * H:
+            return None
+        return reward
+
+    def run(self, idx):
+        """The batch gradient for the rows `idx` (int64, on the device) into p.grad."""
+        for p, g in zip(self.params, self.grads):
+            if p.grad is not g:
+                p.grad = g
+        if [p.data_ptr() for p in self.params] != self.ptrs:
+            raise RuntimeError("model parameters moved during training")
+        self._lib.check(self.lib.mbrl_train_grads(ctypes.byref(self.model), ctypes.byref(self.data),
+                                                  ctypes.c_void_p(idx.data_ptr()), int(idx.shape[0]),
+                                                  ctypes.c_void_p(self.loss.data_ptr()),
+                                                  ctypes.c_void_p(self.ws.data_ptr()), self.ws.numel(),
+                                                  self._lib.stream_handle(self.dev)), "mbrl_train_grads")
+        return self.loss[0], [self.loss[1], self.loss[2]]
+
+
+def _train_loop(model, dataset, optimizer, batch_size, num_epochs, step_loss, writer, tags, criterion=None):
     """models.py:53-93 / 165-217 on the model's device: per batch, the loss summed over the horizon
     steps, zero_grad, backward, step -- the reference's order of operations. Batches are gathered
     from device-resident transitions (TransitionsDataset.stacked) instead of per-sample collation;
-    on a GPU the full-size batches replay one captured graph (_GraphStep)."""
+    on a GPU the full-size batches replay one captured graph (_GraphStep), and a plain Adam steps
+    through mbrl_adam_step (optim.AdamStep: one launch, torch's arithmetic bit for bit)."""
     dev = _device_of(model)
     _, ins, outs = dataset.stacked(dev)
     n_parts = len(tags)
-    graph = None
-    if dev.type == "cuda" and dataset.num_transitions() >= batch_size:
+    graph = native = None
+    if dev.type == "cuda":
+        reward = _NativeGrads.supported(model, dataset, ins, outs, criterion)
+        if reward is not None:
+            native = _NativeGrads(model, ins, outs, dataset.horizon, batch_size, reward)
+    if native is None and dev.type == "cuda" and dataset.num_transitions() >= batch_size:
         try:
             graph = _GraphStep(model, dataset, ins, outs, batch_size, step_loss, n_parts)
         except RuntimeError:           # capture unsupported for this model / criterion: stay eager
             graph = None
             for p in model.parameters():
                 p.grad = None
+    fast = AdamStep.maybe(optimizer) if dev.type == "cuda" else None
     num_iters = 0
     for _ in range(num_epochs):
         host = _epoch_order(dataset)
         order = torch.from_numpy(host).to(dev)
         for i in range(0, len(host), batch_size):
             idx = order[i:i + batch_size]
-            if graph is not None and idx.shape[0] == batch_size:
+            if native is not None:
+                loss, parts = native.run(idx)
+                parts = parts[:n_parts]
+            elif graph is not None and idx.shape[0] == batch_size:
                 loss, parts = graph.run(idx)
             else:
                 optimizer.zero_grad()
                 loss, parts = _batch_loss(dataset, ins, outs, idx, step_loss, n_parts)
                 loss.backward(retain_graph=True)
-            optimizer.step()
+            if fast is None or not fast.step():
+                optimizer.step()
             num_iters += 1
             if writer is not None:
                 for tag, val in zip(tags, parts if n_parts > 1 else [loss]):
                     writer.add_scalar(tag.format(model.train_iterations), val, num_iters)
                 if n_parts > 1:
                     writer.add_scalar("loss/total/{}".format(model.train_iterations), loss, num_iters)
-    if graph is not None:
+    if graph is not None or native is not None:
         for p in model.parameters():      # release the graph-pool grads; the eager path re-allocates
             p.grad = None
     model.train_iterations += 1
@@ -146,7 +239,8 @@ class DynamicsModel(nn.Module):
             (states, actions), (_, next_states) = inp, out
             return [criterion(self.forward(states, actions, normalize_action=None, normalize_state=None,
                                            unnormalize_state=None), next_states)]
-        _train_loop(self, dataset, optimizer, batch_size, num_epochs, step_loss, writer, ["loss/state/{}"])
+        _train_loop(self, dataset, optimizer, batch_size, num_epochs, step_loss, writer, ["loss/state/{}"],
+                    criterion)
 
     def evaluate_model(self, dataset, batch_size, criterion=None):
         """models.py:30-51: one criterion value per batch and horizon step."""
@@ -275,7 +369,7 @@ class ModelWithReward(nn.Module):
                                         unnormalize_state=None, unnormalize_reward=None)
             return [criterion(s_hat, next_states), criterion(r_hat, rewards.reshape(-1, 1))]
         _train_loop(self, dataset, optimizer, batch_size, num_epochs, step_loss, writer,
-                    ["loss/state/{}", "loss/reward/{}"])
+                    ["loss/state/{}", "loss/reward/{}"], criterion)
 
     def forward(self, state, action, normalize_state=None, unnormalize_state=None, normalize_action=None,
                 unnormalize_reward=None):

@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     assert decl == sorted(_lib.EXPORTED)
     for name in decl:
         assert hasattr(lib, name), name
-    assert lib.mbrl_abi_version() == _lib.ABI_VERSION == 5
+    assert lib.mbrl_abi_version() == _lib.ABI_VERSION == 6
 
 
 def test_no_gpu_needed_for_sizing_calls():
@@ -84,6 +84,11 @@ STRUCTS = {
     "Sampler": ("mbrl_sampler", ["seed", "iteration", "mu", "sigma", "lo", "hi"]),
     "CemParams": ("mbrl_cem_params", ["N", "H", "K", "iterations", "alpha", "lo", "hi", "init_mu", "init_sigma",
                                       "seed"]),
+    "AdamTensor": ("mbrl_adam_tensor", ["param", "grad", "exp_avg", "exp_avg_sq", "numel", "step_size", "bc2_sqrt"]),
+    "AdamHparams": ("mbrl_adam_hparams", ["lerp_weight", "beta2", "one_minus_beta2", "eps", "weight_decay"]),
+    "TrainModel": ("mbrl_train_model", ["state_dim", "action_dim", "hidden", "n_hidden", "reward_head", "horizon",
+                                        "weight", "bias", "weight_grad", "bias_grad"]),
+    "TrainData": ("mbrl_train_data", ["states", "actions", "next_states", "rewards", "transitions"]),
 }
 
 

@@ -1,0 +1,117 @@
+"""Model training on the GPU: mbrl_train_grads (csrc/train.hip) -- the
+batch loss gradient of Model / ModelWithReward under train_model's MSELoss -- against autograd on
+the same batch, in fp32 on the same device.
+
+The native kernels sum in a different order from autograd's GEMMs and reductions, so the bar is
+rounding-level agreement: every gradient within 1e-4 relative of the tensor's largest autograd
+entry (plus 1e-4 elementwise relative), losses within 1e-5 relative. End-to-end training parity
+against the reference's own train_model is tests/test_train.py (1e-4 on the weights after
+training), which runs this path by default."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda", 0)
+
+
+def _dataset(s, a, horizon, T, seed):
+    from mbrl_amd import data
+    rng = np.random.Generator(np.random.PCG64(seed))
+    rolls = []
+    per = T // 3 + horizon
+    for _ in range(3):
+        st = rng.standard_normal((per + 1, s)).astype(np.float32)
+        rolls.append(data.Rollout(states=list(torch.from_numpy(st)), observations=list(torch.from_numpy(st)),
+                                  actions=list(torch.from_numpy(rng.uniform(-1, 1, (per, a)).astype(np.float32))),
+                                  rewards=list(torch.from_numpy(rng.standard_normal(per).astype(np.float32)))))
+    ds = data.TransitionsDataset(rollouts=rolls, horizon=horizon)
+    ds.set_data_mode("state_only")
+    return ds
+
+
+def _model(kind, s, a, W, L, seed):
+    from mbrl_amd import models
+    torch.manual_seed(seed)
+    if kind == "model":
+        return models.Model(s, a, hidden_units=W, n_hidden=L).to(DEV)
+    return models.ModelWithReward(s, a, hidden_units=W, n_hidden=L).to(DEV)
+
+
+def _autograd(m, ds, ins, outs, idx, reward):
+    from mbrl_amd import models
+    crit = torch.nn.MSELoss()
+    for p in m.parameters():
+        p.grad = None
+
+    def step_loss(inp, out):
+        (st, ac), (rw, ns) = inp, out
+        if reward:
+            sh, rh = m.forward(st, ac)
+            return [crit(sh, ns), crit(rh, rw.reshape(-1, 1))]
+        return [crit(m.forward(st, ac), ns)]
+    loss, parts = models._batch_loss(ds, ins, outs, idx, step_loss, 2 if reward else 1)
+    loss.backward()
+    return loss.detach(), [p.grad.clone() for p in m.parameters()], [x.detach() for x in parts]
+
+
+CASES = [("model", 17, 6, 512, 2, 1, 512), ("model", 17, 6, 50, 2, 1, 512), ("model", 5, 1, 64, 1, 2, 37),
+         ("model", 24, 8, 200, 3, 3, 300), ("model", 3, 2, 33, 2, 1, 1), ("reward", 17, 6, 200, 2, 1, 512),
+         ("reward", 11, 3, 96, 2, 2, 129), ("model", 67, 21, 128, 2, 1, 256)]
+
+
+@pytest.mark.parametrize("kind,s,a,W,L,H,B", CASES)
+def test_native_gradients_match_autograd(kind, s, a, W, L, H, B):
+    from mbrl_amd import models
+    ds = _dataset(s, a, H, max(3 * B, 60), seed=s * 7 + W)
+    m = _model(kind, s, a, W, L, seed=W)
+    _, ins, outs = ds.stacked(DEV)
+    reward = kind == "reward"
+    assert models._NativeGrads.supported(m, ds, ins, outs, torch.nn.MSELoss()) == reward
+    g = torch.Generator().manual_seed(B)
+    idx = torch.randperm(ds.num_transitions(), generator=g)[:B].to(DEV)
+    ref_loss, ref_grads, ref_parts = _autograd(m, ds, ins, outs, idx, reward)
+    nat = models._NativeGrads(m, ins, outs, ds.horizon, B, reward)
+    loss, parts = nat.run(idx)
+    torch.cuda.synchronize()
+    got = [p.grad for p in m.parameters()]
+    for i, (x, y) in enumerate(zip(got, ref_grads)):
+        scale = float(y.abs().max())
+        assert torch.allclose(x, y, rtol=1e-4, atol=1e-4 * scale + 1e-12), (i, float((x - y).abs().max()), scale)
+    assert abs(float(loss) - float(ref_loss)) <= 1e-5 * abs(float(ref_loss))
+    for k, rp in enumerate(ref_parts):
+        assert abs(float(parts[k]) - float(rp)) <= 1e-5 * abs(float(rp))
+
+
+def test_native_training_tracks_autograd_training():
+    """Ten epochs of train_model (Adam) through the native gradients and through autograd end within
+    1e-4 of each other (fp32 summation-order differences, amplified by Adam's normalisation)."""
+    from mbrl_amd import models
+    ds = _dataset(17, 6, 2, 900, seed=3)
+    out = {}
+    for native in (True, False):
+        m = _model("model", 17, 6, 64, 2, seed=0)
+        opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+        saved = models.NATIVE_TRAINING
+        models.NATIVE_TRAINING = native
+        try:
+            np.random.seed(4)
+            m.train_model(ds, opt, batch_size=128, num_epochs=10)
+        finally:
+            models.NATIVE_TRAINING = saved
+        out[native] = [p.detach().cpu() for p in m.parameters()]
+    for x, y in zip(out[True], out[False]):
+        assert torch.allclose(x, y, rtol=1e-4, atol=1e-5), float((x - y).abs().max())
+
+
+def test_native_training_declines_other_criteria_and_models():
+    from mbrl_amd import models
+    ds = _dataset(4, 2, 1, 60, seed=1)
+    _, ins, outs = ds.stacked(DEV)
+    m = _model("model", 4, 2, 16, 2, seed=0)
+    assert models._NativeGrads.supported(m, ds, ins, outs, torch.nn.L1Loss()) is None
+    assert models._NativeGrads.supported(m, ds, ins, outs, torch.nn.MSELoss(reduction="sum")) is None
+    noisy = models.Model(4, 2, hidden_units=16, noise=0.1).to(DEV)
+    assert models._NativeGrads.supported(noisy, ds, ins, outs, torch.nn.MSELoss()) is None
+    assert models._NativeGrads.supported(m, ds, ins, outs, torch.nn.MSELoss()) is False
