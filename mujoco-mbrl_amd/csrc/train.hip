@@ -129,14 +129,15 @@ hipError_t launch_adam_step(const mbrl_adam_tensor* tensors, int count, const mb
 // elementwise kernels and reductions.
 //
 // Every launch computes one or two products C = A . B^T over 32 x 32 tiles of C, one tile per
-// workgroup: 4 waves split K, each accumulating a 32 x 32 partial with v_mfma_f32_16x16x4f32
+// workgroup: 4 or 16 waves split K, each accumulating a 32 x 32 partial with v_mfma_f32_16x16x4f32
 // (lane l feeds A(m0 + l%16, k) and B(n0 + l%16, k) for k = kb + 4(l/16) + s, s = 0..3, so a lane's
 // four k are consecutive and one float4 load serves four MFMAs when the operand is k-contiguous).
 // The partials meet in LDS, summed in wave order, and the epilogue fuses what follows the product:
 //   forward        H_l = relu(A W_l^T + b_l)                                  (EPI_ACT)
 //   output layer   Y = H W_out^T + b_out;  dY = (Y - target) * 2 / numel, loss partials (EPI_LOSS)
 //   backward dX    dH_{l-1} = (dH_l W_l) * (H_{l-1} > 0)                        (EPI_MASK)
-//   backward dW    dW_l = dH_l^T H_{l-1}, db_l from a virtual ones column        (EPI_GRAD)
+//   backward dW    dW_l = dH_l^T H_{l-1}, db_l from column sums the dH / dY launch left per
+//                  row tile                                                     (EPI_GRAD)
 // The batch is gathered on the fly from the stacked transitions through the batch's row indices
 // (no materialised input), and the state and reward heads are one output layer of s + 1 rows.
 // Arithmetic is fp32 with fp32 accumulation; the summation order differs from autograd's, so the
@@ -144,10 +145,25 @@ hipError_t launch_adam_step(const mbrl_adam_tensor* tensors, int count, const mb
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// Diagnostic build only (-DMBRL_STAMPS): s_memrealtime (100 MHz) at fixed points of the first and
+// the last workgroup of each launch, 8 slots per launch, into the buffer set by
+// mbrl_diag_set_train_stamps() (tools/train_stamps.py).
+#ifdef MBRL_STAMPS
+__device__ unsigned long long* g_train_stamps;
+#define TSTAMP(k)                                                                                    \
+    do {                                                                                             \
+        if (g_train_stamps && threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1)) \
+            g_train_stamps[L.slot * 8 + (blockIdx.x == 0 ? 0 : 4) + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define TSTAMP(k) \
+    do {          \
+    } while (0)
+#endif
+
 enum { OP_DIRECT = 0, OP_TRANS = 1, OP_GATHER = 2 };
 enum { EPI_ACT = 0, EPI_LOSS = 1, EPI_MASK = 2, EPI_GRAD = 3 };
 constexpr int TT = 32;              // C tile edge
-constexpr int GEMM_THREADS = 256;   // 4 waves
 
 // Logical operand X(i, k), i < rows, k < K, over a row-major storage matrix S whose rows below
 // `split` live at p0 and the rest at p1 (the state and reward heads as one matrix).
@@ -173,9 +189,11 @@ struct Output {
     int relu;
     const float* mask;        // EPI_MASK: C *= (mask[m*ldm + n] > 0)
     int ldm;
-    float* g0;                // EPI_GRAD: column bias_col is the bias gradient, g0[m] / g1[m - split]
+    float* g0;                // EPI_GRAD: the bias gradient, g0[m] / g1[m - split], from colsum_in
     float* g1;
-    int bias_col;
+    const float* colsum_in;   // EPI_GRAD: [colsum_tiles][M] column sums of this layer's output gradient
+    int colsum_tiles;
+    float* colsum_out;        // EPI_MASK / EPI_LOSS: [row tile][N] column sums of the stored C
     float scale_s, scale_r;   // EPI_LOSS: dY scale of the state / reward columns (2 / numel)
     float inv_s, inv_r;       // EPI_LOSS: loss weight of the state / reward columns (1 / numel)
     int s;                    // EPI_LOSS: state columns (n >= s: the reward column)
@@ -198,6 +216,8 @@ struct GemmLaunch {
     const float* gns;   // stacked next states [T][H][s]
     const float* grw;   // stacked rewards     [T][H]
     int H, s, a;
+    float* xstore;      // [rows][s + a]: the gathered input, written by the layer-0 forward launch
+    int slot;           // launch index within the step (diagnostic stamps)
     // loss: one extra workgroup sums the partials (fixed order) into loss_out[0..2]
     const float* loss_part;
     int loss_parts;
@@ -217,6 +237,7 @@ __device__ __forceinline__ const float* storage_row(const Operand& o, int row) {
     return row < o.split ? o.p0 + (int64_t)row * o.ld : o.p1 + (int64_t)(row - o.split) * o.ld;
 }
 
+template <int KIND>
 __device__ __forceinline__ f32x4 load_operand(const GemmLaunch& L, const Operand& o, int i, int k0, int K) {
     f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
     if (i >= o.rows) return v;
@@ -225,13 +246,13 @@ __device__ __forceinline__ f32x4 load_operand(const GemmLaunch& L, const Operand
         for (int e = 0; e < 4; ++e) v[e] = k0 + e < K ? 1.0f : 0.0f;
         return v;
     }
-    if (o.kind == OP_DIRECT) {
+    if constexpr (KIND == OP_DIRECT) {
         const float* row = storage_row(o, i);
         if (o.vec && k0 + 3 < K) return *reinterpret_cast<const f32x4*>(row + k0);
 #pragma unroll
         for (int e = 0; e < 4; ++e)
             if (k0 + e < K) v[e] = row[k0 + e];
-    } else if (o.kind == OP_TRANS) {
+    } else if constexpr (KIND == OP_TRANS) {
 #pragma unroll
         for (int e = 0; e < 4; ++e)
             if (k0 + e < K) v[e] = storage_row(o, k0 + e)[i];
@@ -243,47 +264,77 @@ __device__ __forceinline__ f32x4 load_operand(const GemmLaunch& L, const Operand
     return v;
 }
 
+// The gathered batch input, kept for the layer-0 weight gradient (fwd0 writes it as it loads it).
+__device__ __forceinline__ void stash_input(const GemmLaunch& L, const GemmDesc& D, const f32x4& v, int m, int k0) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+        if (m < D.M && k0 + e < D.K) L.xstore[(int64_t)m * D.K + k0 + e] = v[e];
+}
+
+template <int NW, int AK, int BK>
 __device__ void gemm_tile(const GemmLaunch& L, const GemmDesc& D, int tile, float (*red)[TT][TT + 1]) {
+    constexpr int NT = 64 * NW;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, q = lane >> 4, c = lane & 15;
-    const int m0 = (tile / D.tiles_n) * TT, n0 = (tile % D.tiles_n) * TT;
-    // wave w takes the w-th quarter of K (in 16-deep chunks)
-    const int chunks = (D.K + 15) >> 4, per = (chunks + 3) >> 2;
+    const int tm = tile / D.tiles_n, m0 = tm * TT, n0 = (tile % D.tiles_n) * TT;
+    const bool stash = AK == OP_GATHER && L.xstore != nullptr && n0 == 0;
+    // wave w takes the w-th of NW contiguous K ranges (in 16-deep chunks): a few chunks per wave, so
+    // the loads' latency is paid about once per wave instead of once per chunk
+    const int chunks = (D.K + 15) >> 4, per = (chunks + NW - 1) / NW;
     const int kb0 = wave * per * 16, kb1 = min(D.K, (wave + 1) * per * 16);
     f32x4 acc[2][2];
 #pragma unroll
     for (int x = 0; x < 2; ++x)
 #pragma unroll
         for (int y = 0; y < 2; ++y) acc[x][y] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    f32x4 a[2], b[2];
-    if (kb0 < kb1) {
+    // the epilogue's own operands (bias, ReLU mask, loss targets) are fetched before the K loop so
+    // their latency overlaps the products'
+    const Output& O = D.out;
+    constexpr int EPT = TT * TT / NT;       // C elements per thread in the epilogue
+    float pre[EPT];
 #pragma unroll
-        for (int x = 0; x < 2; ++x) a[x] = load_operand(L, D.A, m0 + 16 * x + c, kb0 + 4 * q, D.K);
-#pragma unroll
-        for (int y = 0; y < 2; ++y) b[y] = load_operand(L, D.B, n0 + 16 * y + c, kb0 + 4 * q, D.K);
-    }
-    for (int kb = kb0; kb < kb1; kb += 16) {
-        f32x4 an[2], bn[2];
-        const bool more = kb + 16 < kb1;
-        if (more) {             // next chunk's operands in flight while this chunk's MFMAs issue
-#pragma unroll
-            for (int x = 0; x < 2; ++x) an[x] = load_operand(L, D.A, m0 + 16 * x + c, kb + 16 + 4 * q, D.K);
-#pragma unroll
-            for (int y = 0; y < 2; ++y) bn[y] = load_operand(L, D.B, n0 + 16 * y + c, kb + 16 + 4 * q, D.K);
-        }
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-            for (int x = 0; x < 2; ++x)
-#pragma unroll
-                for (int y = 0; y < 2; ++y)
-                    acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[x][s], b[y][s], acc[x][y], 0, 0, 0);
-        if (more) {
-#pragma unroll
-            for (int x = 0; x < 2; ++x) a[x] = an[x];
-#pragma unroll
-            for (int y = 0; y < 2; ++y) b[y] = bn[y];
+    for (int j = 0; j < EPT; ++j) {
+        const int e = tid + j * NT, m = m0 + (e >> 5), n = n0 + (e & 31);
+        pre[j] = 0.0f;
+        if (m >= D.M || n >= D.N) continue;
+        if (O.mode == EPI_ACT) pre[j] = n < O.bsplit ? O.b0[n] : O.b1[n - O.bsplit];
+        else if (O.mode == EPI_MASK) pre[j] = O.mask[(int64_t)m * O.ldm + n];
+        else if (O.mode == EPI_LOSS) {
+            const int64_t src = batch_row(L, m);
+            const float t = n < O.s ? L.gns[src * O.s + n] : L.grw[src];
+            pre[j] = t - (n < O.bsplit ? O.b0[n] : O.b1[n - O.bsplit]);   // y - t = acc - (t - bias)
         }
     }
+    TSTAMP(1);
+    // up to GROUP chunks' operands in flight at once, then their MFMAs: with the usual 1-4 chunks
+    // per wave the loads' latency is paid once
+    constexpr int GROUP = NW == 16 ? 2 : 4;
+    for (int g0 = kb0; g0 < kb1; g0 += 16 * GROUP) {
+        f32x4 a[GROUP][2], b[GROUP][2];
+#pragma unroll
+        for (int u = 0; u < GROUP; ++u) {
+            const int kb = g0 + 16 * u;
+            if (kb >= kb1) break;
+#pragma unroll
+            for (int x = 0; x < 2; ++x) {
+                a[u][x] = load_operand<AK>(L, D.A, m0 + 16 * x + c, kb + 4 * q, D.K);
+                if (stash) stash_input(L, D, a[u][x], m0 + 16 * x + c, kb + 4 * q);
+            }
+#pragma unroll
+            for (int y = 0; y < 2; ++y) b[u][y] = load_operand<BK>(L, D.B, n0 + 16 * y + c, kb + 4 * q, D.K);
+        }
+#pragma unroll
+        for (int u = 0; u < GROUP; ++u) {
+            if (g0 + 16 * u >= kb1) break;
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int x = 0; x < 2; ++x)
+#pragma unroll
+                    for (int y = 0; y < 2; ++y)
+                        acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][x][s], b[u][y][s], acc[x][y], 0, 0, 0);
+        }
+    }
+    TSTAMP(2);
     // lane l holds C rows 16x + 4q + v, column 16y + c
 #pragma unroll
     for (int x = 0; x < 2; ++x)
@@ -293,60 +344,92 @@ __device__ void gemm_tile(const GemmLaunch& L, const GemmDesc& D, int tile, floa
             for (int v = 0; v < 4; ++v) red[wave][16 * x + 4 * q + v][16 * y + c] = acc[x][y][v];
     __syncthreads();
 
-    const Output& O = D.out;
-    const int row = tid >> 3, col0 = (tid & 7) * 4, m = m0 + row;
+    // the fused epilogue, EPT C elements per thread; each element sums the waves' partials in wave
+    // order. Elements of this tile that feed the next layer's bias gradient (EPI_MASK, EPI_LOSS)
+    // are kept for the column sums below.
     float loss_s = 0.0f, loss_r = 0.0f;
-    if (m < D.M) {
+    float keep[EPT];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int n = n0 + col0 + e;
-            if (n >= D.N) break;
-            float v = red[0][row][col0 + e];
-            v = v + red[1][row][col0 + e];
-            v = v + red[2][row][col0 + e];
-            v = v + red[3][row][col0 + e];
-            if (O.mode == EPI_GRAD && n == O.bias_col) {
-                (m < O.split ? O.g0[m] : O.g1[m - O.split]) = v;
-                continue;
-            }
-            if (O.mode == EPI_ACT || O.mode == EPI_LOSS) v = v + (n < O.bsplit ? O.b0[n] : O.b1[n - O.bsplit]);
-            if (O.mode == EPI_ACT && O.relu) v = v > 0.0f ? v : 0.0f;
-            if (O.mode == EPI_MASK && !(O.mask[(int64_t)m * O.ldm + n] > 0.0f)) v = 0.0f;
-            if (O.mode == EPI_LOSS) {
-                const int64_t src = batch_row(L, m);
-                const float t = n < O.s ? L.gns[src * O.s + n] : L.grw[src];
-                const float d = v - t;
-                if (n < O.s) loss_s += d * d * O.inv_s;
-                else loss_r += d * d * O.inv_r;
-                v = d * (n < O.s ? O.scale_s : O.scale_r);
-            }
-            float* dst = m < O.split ? O.c0 + (int64_t)m * O.ldc : O.c1 + (int64_t)(m - O.split) * O.ldc;
-            dst[n] = v;
+    for (int j = 0; j < EPT; ++j) {
+        const int e = tid + j * NT, row = e >> 5, col = e & 31, m = m0 + row, n = n0 + col;
+        keep[j] = 0.0f;
+        if (m >= D.M || n >= D.N) continue;
+        float v = red[0][row][col];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) v = v + red[w][row][col];
+        if (O.mode == EPI_ACT) v = v + pre[j];
+        if (O.mode == EPI_ACT && O.relu) v = v > 0.0f ? v : 0.0f;
+        if (O.mode == EPI_MASK && !(pre[j] > 0.0f)) v = 0.0f;
+        if (O.mode == EPI_LOSS) {
+            const float d = v - pre[j];
+            if (n < O.s) loss_s = loss_s + d * d * O.inv_s;
+            else loss_r = loss_r + d * d * O.inv_r;
+            v = d * (n < O.s ? O.scale_s : O.scale_r);
+        }
+        keep[j] = v;
+        float* dst = m < O.split ? O.c0 + (int64_t)m * O.ldc : O.c1 + (int64_t)(m - O.split) * O.ldc;
+        dst[n] = v;
+        // EPI_GRAD: the first column tile also finishes the bias gradient of row m from the column
+        // sums the launch that produced this layer's output gradient left per row tile
+        if (O.mode == EPI_GRAD && n0 == 0 && col == 0) {
+            float g = O.colsum_in[m];
+            for (int i = 1; i < O.colsum_tiles; ++i) g = g + O.colsum_in[(int64_t)i * D.M + m];
+            (m < O.split ? O.g0[m] : O.g1[m - O.split]) = g;
         }
     }
-    if (O.mode == EPI_LOSS) {
-        __syncthreads();        // red is reused for the partial-loss reduction
-        float* sl = &red[0][0][0];
-        sl[tid] = loss_s;
-        sl[GEMM_THREADS + tid] = loss_r;
+    if (O.mode == EPI_MASK || O.mode == EPI_LOSS) {   // per-row-tile column sums (the next bias gradient)
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) {
+            const int e = tid + j * NT;
+            red[0][e >> 5][e & 31] = keep[j];
+        }
+        __syncthreads();
+        if (tid < TT && n0 + tid < D.N) {
+            float t = red[0][0][tid];
+            for (int r = 1; r < TT; ++r) t = t + red[0][r][tid];
+            O.colsum_out[(int64_t)tm * D.N + n0 + tid] = t;
+        }
+    }
+    if (O.mode == EPI_LOSS) {   // the tile's loss: a butterfly per wave, then the waves in order
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            loss_s += __shfl_xor(loss_s, o);
+            loss_r += __shfl_xor(loss_r, o);
+        }
+        __syncthreads();        // red is reused
+        float* sl = &red[1][0][0];
+        if (lane == 0) {
+            sl[2 * wave] = loss_s;
+            sl[2 * wave + 1] = loss_r;
+        }
         __syncthreads();
         if (tid < 2) {
-            float t = 0.0f;
-            for (int i = 0; i < GEMM_THREADS; ++i) t = t + sl[tid * GEMM_THREADS + i];
+            float t = sl[tid];
+            for (int w = 1; w < NW; ++w) t = t + sl[2 * w + tid];
             O.loss_part[tile * 2 + tid] = t;
         }
     }
+    TSTAMP(3);
 }
 
-__global__ __launch_bounds__(GEMM_THREADS) void train_gemm_kernel(const GemmLaunch L) {
-    __shared__ float red[4][TT][TT + 1];
-    int b = blockIdx.x;
-    for (int i = 0; i < L.nd; ++i) {
-        if (b < L.d[i].tiles) {
-            gemm_tile(L, L.d[i], b, red);
+// NW waves per workgroup; A0/B0 (A1/B1): operand kinds of the launch's first (second) product, fixed
+// at compile time so each instantiation carries only its own load paths.
+template <int NW, int A0, int B0, int A1, int B1>
+__global__ __launch_bounds__(64 * NW) void train_gemm_kernel(const GemmLaunch L) {
+    __shared__ float red[NW][TT][TT + 1];
+    TSTAMP(0);
+    // (constant indices only: a dynamic index into the kernel arguments would copy them to scratch)
+    const int b = blockIdx.x;
+    if (b < L.d[0].tiles) {
+        gemm_tile<NW, A0, B0>(L, L.d[0], b, red);
+        return;
+    }
+    if constexpr (A1 >= 0) {
+        if (L.nd > 1 && b - L.d[0].tiles < L.d[1].tiles) {
+            gemm_tile<NW, A1, B1>(L, L.d[1], b - L.d[0].tiles, red);
             return;
         }
-        b -= L.d[i].tiles;
     }
     // the loss workgroup: partials of the output-layer launch, summed in tile order
     if (threadIdx.x < 2 && L.loss_out) {
@@ -382,36 +465,67 @@ static void finish(GemmDesc& D, int M, int N, int K) {
     D.tiles = ((M + TT - 1) / TT) * D.tiles_n;
 }
 
+// 16 waves split a long K (the hidden layers, every weight gradient); 4 suffice for short ones.
+template <int A0, int B0, int A1 = -1, int B1 = -1>
 static hipError_t launch_gemm(GemmLaunch& L, bool loss_wg, hipStream_t stream) {
-    int blocks = loss_wg ? 1 : 0;
-    for (int i = 0; i < L.nd; ++i) blocks += L.d[i].tiles;
+    int blocks = loss_wg ? 1 : 0, kmax = 0;
+    for (int i = 0; i < L.nd; ++i) {
+        blocks += L.d[i].tiles;
+        kmax = max(kmax, L.d[i].K);
+    }
     if (!loss_wg) L.loss_out = nullptr;
-    hipLaunchKernelGGL(train_gemm_kernel, dim3(blocks), dim3(GEMM_THREADS), 0, stream, L);
+    ++L.slot;
+    if (kmax >= 256)
+        hipLaunchKernelGGL((train_gemm_kernel<16, A0, B0, A1, B1>), dim3(blocks), dim3(64 * 16), 0, stream, L);
+    else
+        hipLaunchKernelGGL((train_gemm_kernel<4, A0, B0, A1, B1>), dim3(blocks), dim3(64 * 4), 0, stream, L);
     return hipGetLastError();
 }
 
-size_t train_ws_floats(const TrainShape& t, int batch) {
-    const size_t R = (size_t)batch * t.H, J = t.s + (t.reward ? 1 : 0);
-    const size_t tiles_out = ((R + TT - 1) / TT) * ((J + TT - 1) / TT);
+// Workspace (floats, each piece 256-byte aligned): hidden activations H_0..H_{L-1} [R][W], two
+// backward buffers dH [R][W], dY [R][J], loss partials, the gathered input [R][s + a], and the
+// per-row-tile column sums of dY [tiles][J] and of the two dH [tiles][W].
+struct TrainWs {
+    float* act[MBRL_TRAIN_MAX_LAYERS];
+    float *dh[2], *dy, *loss_part, *xbuf, *cs_dy, *cs_dh[2];
+    size_t floats;
+};
+
+static TrainWs train_ws(const TrainShape& t, int batch, float* base) {
+    const size_t R = (size_t)batch * t.H, J = t.s + (t.reward ? 1 : 0), W = t.W, tiles_r = (R + TT - 1) / TT;
+    const size_t tiles_out = tiles_r * ((J + TT - 1) / TT);
     auto up = [](size_t x) { return (x + 63) & ~(size_t)63; };
-    return up(R * t.W) * (t.L + 2) + up(R * J) + up(tiles_out * 2);
+    TrainWs w{};
+    size_t off = 0;
+    auto take = [&](size_t n) { float* p = base ? base + off : nullptr; off += up(n); return p; };
+    for (int l = 0; l < t.L; ++l) w.act[l] = take(R * W);
+    w.dh[0] = take(R * W);
+    w.dh[1] = take(R * W);
+    w.dy = take(R * J);
+    w.loss_part = take(tiles_out * 2);
+    w.xbuf = take(R * (t.s + t.a));
+    w.cs_dy = take(tiles_r * J);
+    w.cs_dh[0] = take(tiles_r * W);
+    w.cs_dh[1] = take(tiles_r * W);
+    w.floats = off;
+    return w;
 }
+
+size_t train_ws_floats(const TrainShape& t, int batch) { return train_ws(t, batch, nullptr).floats; }
 
 hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const int64_t* idx, int batch,
                               float* loss_out, float* ws, hipStream_t stream) {
     const int R = batch * t.H, W = t.W, K0 = t.s + t.a, J = t.s + (t.reward ? 1 : 0), L = t.L;
-    auto up = [](size_t x) { return (x + 63) & ~(size_t)63; };
-    float* act[MBRL_TRAIN_MAX_LAYERS];
-    for (int l = 0; l < L; ++l) act[l] = ws + up((size_t)R * W) * l;
-    float* dh[2] = {ws + up((size_t)R * W) * L, ws + up((size_t)R * W) * (L + 1)};
-    float* dy = ws + up((size_t)R * W) * (L + 2);
-    float* loss_part = dy + up((size_t)R * J);
+    const int tiles_r = (R + TT - 1) / TT;
+    const TrainWs B = train_ws(t, batch, ws);
     const float* wo_r = t.reward ? w.weight[L + 1] : nullptr;
     const float* bo_r = t.reward ? w.bias[L + 1] : w.bias[L];
 
     GemmLaunch G{};
     G.idx = idx; G.gs = w.states; G.ga = w.actions; G.gns = w.next_states; G.grw = w.rewards;
     G.H = t.H; G.s = t.s; G.a = t.a;
+    G.xstore = B.xbuf;
+    G.slot = -1;
     hipError_t e;
     // forward through the hidden layers
     for (int l = 0; l < L; ++l) {
@@ -421,74 +535,78 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
             D.A = Operand{};
             D.A.kind = OP_GATHER; D.A.rows = R; D.A.ones_row = -1; D.A.gather_trans = 0;
         } else {
-            D.A = direct(act[l - 1], nullptr, 0, W, R);
+            D.A = direct(B.act[l - 1], nullptr, 0, W, R);
         }
         D.B = direct(w.weight[l], nullptr, 0, l == 0 ? K0 : W, W);
-        D.out.mode = EPI_ACT; D.out.c0 = D.out.c1 = act[l]; D.out.split = R; D.out.ldc = W;
+        D.out.mode = EPI_ACT; D.out.c0 = D.out.c1 = B.act[l]; D.out.split = R; D.out.ldc = W;
         D.out.b0 = D.out.b1 = w.bias[l]; D.out.bsplit = W; D.out.relu = 1;
         finish(D, R, W, l == 0 ? K0 : W);
         G.nd = 1;
-        if ((e = launch_gemm(G, false, stream)) != hipSuccess) return e;
+        e = l == 0 ? launch_gemm<OP_GATHER, OP_DIRECT>(G, false, stream) : launch_gemm<OP_DIRECT, OP_DIRECT>(G, false, stream);
+        if (e != hipSuccess) return e;
     }
-    // output layer (state head, reward head) + the loss gradient
+    // output layer (state head, reward head) + the loss gradient dY and its column sums
     {
         GemmDesc& D = G.d[0];
         D = GemmDesc{};
-        D.A = direct(act[L - 1], nullptr, 0, W, R);
+        D.A = direct(B.act[L - 1], nullptr, 0, W, R);
         D.B = direct(w.weight[L], wo_r, t.s, W, J);
         Output& O = D.out;
-        O.mode = EPI_LOSS; O.c0 = O.c1 = dy; O.split = R; O.ldc = J;
+        O.mode = EPI_LOSS; O.c0 = O.c1 = B.dy; O.split = R; O.ldc = J;
         O.b0 = w.bias[L]; O.b1 = bo_r; O.bsplit = t.s;
         O.scale_s = 2.0f / (float)((int64_t)batch * t.s); O.scale_r = 2.0f / (float)batch;
         O.inv_s = 1.0f / (float)((int64_t)batch * t.s); O.inv_r = 1.0f / (float)batch;
-        O.s = t.s; O.loss_part = loss_part;
+        O.s = t.s; O.loss_part = B.loss_part; O.colsum_out = B.cs_dy;
         finish(D, R, J, W);
         G.nd = 1;
-        G.loss_part = loss_part; G.loss_parts = D.tiles;
-        if ((e = launch_gemm(G, false, stream)) != hipSuccess) return e;
+        if ((e = launch_gemm<OP_DIRECT, OP_DIRECT>(G, false, stream)) != hipSuccess) return e;
     }
     const int loss_parts = G.d[0].tiles;
     // backward: layer l = L (output) .. 0; launch l: dH_{l-1} (l >= 1) and dW_l, db_l
     for (int l = L; l >= 0; --l) {
         const bool out_layer = l == L;
-        const float* g_in = out_layer ? dy : dh[l % 2];   // dL/d(pre-activation of layer l), [R][n_out]
+        const float* g_in = out_layer ? B.dy : B.dh[l % 2];   // dL/d(pre-activation of layer l), [R][n_out]
+        const float* cs_in = out_layer ? B.cs_dy : B.cs_dh[l % 2];
         const int n_out = out_layer ? J : W, n_in = l == 0 ? K0 : W;
         G.nd = 0;
-        if (l >= 1) {           // dH_{l-1} = (g_in W_l) * (H_{l-1} > 0)
+        if (l >= 1) {           // dH_{l-1} = (g_in W_l) * (H_{l-1} > 0), and its column sums
             GemmDesc& D = G.d[G.nd++];
             D = GemmDesc{};
             D.A = direct(g_in, nullptr, 0, n_out, R);
             D.B = out_layer ? transposed(w.weight[L], wo_r, t.s, W, W, -1) : transposed(w.weight[l], nullptr, 0, W, W, -1);
-            D.out.mode = EPI_MASK; D.out.c0 = D.out.c1 = dh[(l - 1) % 2]; D.out.split = R; D.out.ldc = W;
-            D.out.mask = act[l - 1]; D.out.ldm = W;
+            D.out.mode = EPI_MASK; D.out.c0 = D.out.c1 = B.dh[(l - 1) % 2]; D.out.split = R; D.out.ldc = W;
+            D.out.mask = B.act[l - 1]; D.out.ldm = W; D.out.colsum_out = B.cs_dh[(l - 1) % 2];
             finish(D, R, W, n_out);
         }
-        {                       // dW_l = g_in^T X_l, db_l = column sums of g_in (the ones column)
+        {                       // dW_l = g_in^T X_l; db_l = the column sums of g_in over the row tiles
             GemmDesc& D = G.d[G.nd++];
             D = GemmDesc{};
             D.A = transposed(g_in, nullptr, 0, n_out, n_out, -1);
-            if (l == 0) {
-                D.B = Operand{};
-                D.B.kind = OP_GATHER; D.B.rows = n_in + 1; D.B.ones_row = n_in; D.B.gather_trans = 1;
-            } else {
-                D.B = transposed(act[l - 1], nullptr, 0, W, n_in + 1, n_in);
-            }
+            D.B = l == 0 ? transposed(B.xbuf, nullptr, 0, K0, n_in, -1) : transposed(B.act[l - 1], nullptr, 0, W, n_in, -1);
             Output& O = D.out;
-            O.mode = EPI_GRAD; O.ldc = n_in; O.bias_col = n_in;
+            O.mode = EPI_GRAD; O.ldc = n_in; O.colsum_in = cs_in; O.colsum_tiles = tiles_r;
             if (out_layer) {
-                O.c0 = w.weight_grad[L]; O.c1 = t.reward ? w.weight_grad[L + 1] : w.weight_grad[L]; O.split = t.s;
+                O.c0 = w.weight_grad[L]; O.c1 = t.reward ? w.weight_grad[L + 1] : w.weight_grad[L];
+                O.split = t.reward ? t.s : J;
                 O.g0 = w.bias_grad[L]; O.g1 = t.reward ? w.bias_grad[L + 1] : w.bias_grad[L];
-                if (!t.reward) O.split = J;
             } else {
                 O.c0 = O.c1 = w.weight_grad[l]; O.split = n_out;
                 O.g0 = O.g1 = w.bias_grad[l];
             }
-            finish(D, n_out, n_in + 1, R);
+            finish(D, n_out, n_in, R);
         }
-        G.loss_part = loss_part; G.loss_parts = loss_parts; G.loss_out = loss_out;
-        if ((e = launch_gemm(G, l == 0 && loss_out != nullptr, stream)) != hipSuccess) return e;
+        G.loss_part = B.loss_part; G.loss_parts = loss_parts; G.loss_out = loss_out;
+        e = l >= 1 ? launch_gemm<OP_DIRECT, OP_TRANS, OP_TRANS, OP_TRANS>(G, false, stream)
+                   : launch_gemm<OP_TRANS, OP_TRANS>(G, loss_out != nullptr, stream);
+        if (e != hipSuccess) return e;
     }
     return hipSuccess;
 }
 
 }  // namespace mbrl
+
+#ifdef MBRL_STAMPS
+extern "C" int mbrl_diag_set_train_stamps(void* buf) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(mbrl::g_train_stamps), &buf, sizeof(buf));
+}
+#endif

@@ -40,6 +40,7 @@ def main():
     m.train_model(ds, opt, batch_size=512, num_epochs=1)
     torch.cuda.synchronize()
     timed(models._GraphStep, "run")
+    timed(models._NativeGrads, "run")
     timed(optim.AdamStep, "step")
     epochs = 10
     t0 = time.perf_counter()
