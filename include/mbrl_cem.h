@@ -335,6 +335,19 @@ size_t mbrl_train_workspace_bytes(const mbrl_train_model* model, int32_t batch);
 int mbrl_train_grads(const mbrl_train_model* model, const mbrl_train_data* data, const int64_t* batch_idx,
                      int32_t batch, float* loss_out, void* workspace, size_t ws_bytes, mbrl_stream_t stream);
 
+/* A whole training epoch with Adam (models.py:63-93 with experiment.py:55-62's optimizer): for each
+ * batch b = 0 .. ceil(rows / batch_size) - 1 of the device row order `order` (the last one short),
+ * mbrl_train_grads on rows order[b * batch_size ..] and then mbrl_adam_step over `tensors` (one
+ * parameter group: every Linear's weight and bias, grad = the model's *_grad buffers) with that
+ * step's scalars step_sizes[b * count + i], bc2_sqrt[b * count + i] (host arrays, computed as for
+ * mbrl_adam_step). The host issues every launch of the epoch in one call. losses: [batches][3]
+ * device floats (total, state, reward per batch) or NULL. workspace as for mbrl_train_grads with
+ * batch = batch_size. */
+int mbrl_train_epoch(const mbrl_train_model* model, const mbrl_train_data* data, const int64_t* order, int64_t rows,
+                     int32_t batch_size, const mbrl_adam_tensor* tensors, int32_t count,
+                     const mbrl_adam_hparams* hparams, const float* step_sizes, const float* bc2_sqrt, float* losses,
+                     void* workspace, size_t ws_bytes, mbrl_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

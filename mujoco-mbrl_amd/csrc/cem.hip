@@ -12,6 +12,8 @@
 #include <set>
 #include <string>
 #include <tuple>
+#include <vector>
+#include <algorithm>
 
 #include "../../include/mbrl_cem.h"
 #include "mbrl_internal.h"
@@ -1455,6 +1457,51 @@ int mbrl_train_grads(const mbrl_train_model* model, const mbrl_train_data* data,
                    data->states, data->actions, data->next_states, data->rewards};
     return hip_check(launch_train_grads(t, w, batch_idx, batch, loss_out, static_cast<float*>(workspace),
                                         reinterpret_cast<hipStream_t>(stream)), "train_grads");
+}
+
+int mbrl_train_epoch(const mbrl_train_model* model, const mbrl_train_data* data, const int64_t* order, int64_t rows,
+                     int32_t batch_size, const mbrl_adam_tensor* tensors, int32_t count,
+                     const mbrl_adam_hparams* hparams, const float* step_sizes, const float* bc2_sqrt, float* losses,
+                     void* workspace, size_t ws_bytes, mbrl_stream_t stream) {
+    TrainShape t;
+    if (int rc = train_shape(model, &t)) return rc;
+    if (!data || !order || !workspace || !data->states || !data->next_states || (t.a > 0 && !data->actions) ||
+        (t.reward && !data->rewards) || !tensors || count < 1 || !hparams || !step_sizes || !bc2_sqrt)
+        return fail(MBRL_EINVAL, "train_epoch: NULL argument");
+    if (batch_size < 1 || rows < 1 || rows > data->transitions)
+        return fail(MBRL_EINVAL, "train_epoch: rows %lld / batch %d outside [1, %lld]", (long long)rows, batch_size,
+                    (long long)data->transitions);
+    const int layers = t.L + 1 + t.reward;
+    for (int l = 0; l < layers; ++l)
+        if (!model->weight[l] || !model->bias[l] || !model->weight_grad[l] || !model->bias_grad[l])
+            return fail(MBRL_EINVAL, "train_epoch: layer %d: NULL weight, bias or gradient", l);
+    for (int i = 0; i < count; ++i)
+        if (tensors[i].numel < 0 || (tensors[i].numel > 0 && (!tensors[i].param || !tensors[i].grad ||
+                                                              !tensors[i].exp_avg || !tensors[i].exp_avg_sq)))
+            return fail(MBRL_EINVAL, "train_epoch: Adam tensor %d: NULL pointer or negative numel", i);
+    const int bs = (int)std::min<int64_t>(batch_size, rows);
+    const size_t need = train_ws_floats(t, bs) * sizeof(float);
+    if (ws_bytes < need) return fail(MBRL_EWORKSPACE, "train_epoch: workspace %zu < %zu bytes", ws_bytes, need);
+    TrainTensors w{model->weight, model->bias, model->weight_grad, model->bias_grad,
+                   data->states, data->actions, data->next_states, data->rewards};
+    const int arith = g_opt[MBRL_OPT_ADAM_ARITH].load(std::memory_order_relaxed);
+    const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    std::vector<mbrl_adam_tensor> table(tensors, tensors + count);
+    const int64_t batches = (rows + batch_size - 1) / batch_size;
+    for (int64_t b = 0; b < batches; ++b) {
+        const int n = (int)std::min<int64_t>(batch_size, rows - b * batch_size);
+        if (int rc = hip_check(launch_train_grads(t, w, order + b * batch_size, n, losses ? losses + 3 * b : nullptr,
+                                                  static_cast<float*>(workspace), st), "train_epoch grads"))
+            return rc;
+        for (int i = 0; i < count; ++i) {
+            table[i].step_size = step_sizes[b * count + i];
+            table[i].bc2_sqrt = bc2_sqrt[b * count + i];
+        }
+        if (int rc = hip_check(launch_adam_step(table.data(), count, *hparams, arith ? arith - 1 : ADAM_ARITH_TORCH, st),
+                               "train_epoch adam"))
+            return rc;
+    }
+    return MBRL_OK;
 }
 
 // Workspace for mbrl_trajectory: per-member states, exchange granules, status word.

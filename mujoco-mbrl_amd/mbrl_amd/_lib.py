@@ -50,6 +50,7 @@ EXPORTED = (
     "mbrl_trajectory_workspace_bytes", "mbrl_trajectory", "mbrl_cem_workspace_bytes", "mbrl_cem_plan",
     "mbrl_cem_plan_batch_workspace_bytes", "mbrl_cem_plan_batch", "mbrl_gd_workspace_bytes", "mbrl_gd_plan",
     "mbrl_cem_update", "mbrl_adam_step", "mbrl_train_workspace_bytes", "mbrl_train_grads",
+    "mbrl_train_epoch",
 )
 
 
@@ -150,6 +151,8 @@ def load():
         "mbrl_adam_step": (c_int32, [POINTER(AdamTensor), c_int32, POINTER(AdamHparams), P]),
         "mbrl_train_workspace_bytes": (c_size_t, [POINTER(TrainModel), c_int32]),
         "mbrl_train_grads": (c_int32, [POINTER(TrainModel), POINTER(TrainData), P, c_int32, P, P, c_size_t, P]),
+        "mbrl_train_epoch": (c_int32, [POINTER(TrainModel), POINTER(TrainData), P, c_int64, c_int32, POINTER(AdamTensor),
+                                       c_int32, POINTER(AdamHparams), P, P, P, P, c_size_t, P]),
         "mbrl_cem_plan": (c_int32, [POINTER(MlpShape), P, POINTER(Norm), POINTER(Cost), P, POINTER(CemParams),
                                     P, P, P, P, P, P, P, P, P, c_size_t, P]),
     }

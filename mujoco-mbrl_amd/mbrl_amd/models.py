@@ -158,6 +158,31 @@ class _NativeGrads:
             return None
         return reward
 
+    def epoch(self, order, batch_size, adam):
+        """One epoch over the device row order `order`: every batch's gradient and Adam step from one
+        mbrl_train_epoch call. Returns the per-batch losses [batches, 3] (device), or None when the
+        optimizer's state does not allow it (the caller then steps per batch)."""
+        for p, g in zip(self.params, self.grads):
+            if p.grad is not g:
+                p.grad = g
+        if [p.data_ptr() for p in self.params] != self.ptrs:
+            raise RuntimeError("model parameters moved during training")
+        rows = int(order.shape[0])
+        steps = (rows + batch_size - 1) // batch_size
+        plan = adam.epoch_plan(self.params, steps)
+        if plan is None:
+            return None
+        table, hp, ss, bc = plan
+        losses = torch.empty((steps, 3), dtype=torch.float32, device=self.dev)
+        self._lib.check(self.lib.mbrl_train_epoch(ctypes.byref(self.model), ctypes.byref(self.data),
+                                                  ctypes.c_void_p(order.data_ptr()), rows, int(batch_size), table,
+                                                  len(self.params), ctypes.byref(hp), ss, bc,
+                                                  ctypes.c_void_p(losses.data_ptr()),
+                                                  ctypes.c_void_p(self.ws.data_ptr()), self.ws.numel(),
+                                                  self._lib.stream_handle(self.dev)), "mbrl_train_epoch")
+        adam.epoch_done(self.params)
+        return losses
+
     def run(self, idx):
         """The batch gradient for the rows `idx` (int64, on the device) into p.grad."""
         for p, g in zip(self.params, self.grads):
@@ -199,6 +224,19 @@ def _train_loop(model, dataset, optimizer, batch_size, num_epochs, step_loss, wr
     for _ in range(num_epochs):
         host = _epoch_order(dataset)
         order = torch.from_numpy(host).to(dev)
+        losses = native.epoch(order, batch_size, fast) if native is not None and fast is not None else None
+        if losses is not None:            # the whole epoch in one call; the writer gets its values after
+            if writer is not None:
+                for row in losses.cpu().tolist():
+                    num_iters += 1
+                    parts = [row[1], row[2]][:n_parts]
+                    for tag, val in zip(tags, parts if n_parts > 1 else [row[0]]):
+                        writer.add_scalar(tag.format(model.train_iterations), val, num_iters)
+                    if n_parts > 1:
+                        writer.add_scalar("loss/total/{}".format(model.train_iterations), row[0], num_iters)
+            else:
+                num_iters += losses.shape[0]
+            continue
         for i in range(0, len(host), batch_size):
             idx = order[i:i + batch_size]
             if native is not None:

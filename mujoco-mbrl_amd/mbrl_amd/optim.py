@@ -117,6 +117,53 @@ class AdamStep:
             increment_version(params + [state[p][k] for p in params for k in ("exp_avg", "exp_avg_sq")])
         return True
 
+    def epoch_plan(self, params, steps):
+        """Inputs of mbrl_train_epoch for `steps` Adam steps over `params` (the optimizer's only
+        group, every parameter with a gradient each step): (table, hparams, step_sizes, bc2_sqrt),
+        with the state created as torch would and the step counters advanced by `steps` -- what
+        `steps` calls of step() leave -- or None when the group does not have that shape."""
+        groups = self.opt.param_groups
+        if len(groups) != 1 or len(groups[0]["params"]) != len(params) or \
+                {id(p) for p in groups[0]["params"]} != {id(p) for p in params}:
+            return None
+        for p in params:
+            gr = p.grad
+            if gr is None or gr.dtype != torch.float32 or gr.shape != p.shape or not gr.is_contiguous():
+                return None
+        g = groups[0]
+        state = self.opt.state
+        scalar_dtype = _optimizer_module._get_scalar_dtype()
+        for p in params:                          # adam.py Adam._init_group: lazy state initialisation
+            st = state[p]
+            if len(st) == 0:
+                st["step"] = torch.tensor(0.0, dtype=scalar_dtype)
+                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        counters = [state[p]["step"] for p in params]
+        k0 = counters[0].item()
+        if any(c.item() != k0 for c in counters) or k0 + steps >= 2 ** 24:
+            return None
+        lr, (b1, b2), eps, wd = g["lr"], g["betas"], g["eps"], g["weight_decay"]
+        n = len(params)
+        ss, bc = (ctypes.c_float * (steps * n))(), (ctypes.c_float * (steps * n))()
+        for s in range(steps):                    # adam.py _multi_tensor_adam, capturable = False
+            k = k0 + s + 1
+            a, b = (lr / (1 - b1 ** k)) * -1, (1 - b2 ** k) ** 0.5
+            for i in range(n):
+                ss[s * n + i], bc[s * n + i] = a, b
+        table = (_lib.AdamTensor * n)()
+        for i, p in enumerate(params):
+            table[i].param, table[i].grad = p.data_ptr(), p.grad.data_ptr()
+            table[i].exp_avg, table[i].exp_avg_sq = state[p]["exp_avg"].data_ptr(), state[p]["exp_avg_sq"].data_ptr()
+            table[i].numel = p.numel()
+        for c in counters:                        # the float32 counters, as `steps` increments by one
+            c.add_(float(steps))
+        return table, _lib.AdamHparams(1 - b1, b2, 1 - b2, eps, wd), ss, bc
+
+    def epoch_done(self, params):
+        state = self.opt.state
+        increment_version(list(params) + [state[p][k] for p in params for k in ("exp_avg", "exp_avg_sq")])
+
     def _table(self, gi, params):
         """The group's mbrl_adam_tensor array, rebuilt when any tensor moved."""
         state = self.opt.state

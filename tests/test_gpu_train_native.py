@@ -115,3 +115,39 @@ def test_native_training_declines_other_criteria_and_models():
     noisy = models.Model(4, 2, hidden_units=16, noise=0.1).to(DEV)
     assert models._NativeGrads.supported(noisy, ds, ins, outs, torch.nn.MSELoss()) is None
     assert models._NativeGrads.supported(m, ds, ins, outs, torch.nn.MSELoss()) is False
+
+
+class _Writer:
+    def __init__(self):
+        self.rows = []
+
+    def add_scalar(self, tag, value, step):
+        self.rows.append((tag, float(value), int(step)))
+
+
+@pytest.mark.parametrize("kind", ["model", "reward"])
+def test_epoch_call_equals_per_batch_calls(kind, monkeypatch):
+    """mbrl_train_epoch (every batch's gradient and Adam step from one host call) trains to the same
+    bits as one mbrl_train_grads + mbrl_adam_step per batch, leaves the same optimizer state and
+    step counters, and hands the writer the same per-batch losses."""
+    from mbrl_amd import models
+    ds = _dataset(17, 6, 2, 700, seed=9)
+    out = {}
+    for epoch_call in (True, False):
+        m = _model(kind, 17, 6, 96, 2, seed=1)
+        opt = torch.optim.Adam(m.parameters(), lr=1e-3, weight_decay=1e-4)
+        w = _Writer()
+        with monkeypatch.context() as mp:
+            if not epoch_call:
+                mp.setattr(models._NativeGrads, "epoch", lambda self, *a: None)
+            np.random.seed(2)
+            m.train_model(ds, opt, batch_size=128, num_epochs=3, writer=w)
+        torch.cuda.synchronize()
+        out[epoch_call] = ([p.detach().cpu() for p in m.parameters()],
+                           [(float(s["step"]), s["exp_avg"].cpu(), s["exp_avg_sq"].cpu()) for s in opt.state.values()],
+                           w.rows)
+    (wa, sa, ra), (wb, sb, rb) = out[True], out[False]
+    assert all(torch.equal(x, y) for x, y in zip(wa, wb))
+    for (ka, ma, va), (kb, mb, vb) in zip(sa, sb):
+        assert ka == kb and torch.equal(ma, mb) and torch.equal(va, vb)
+    assert ra == rb and len(ra) > 0
