@@ -1488,18 +1488,25 @@ int mbrl_train_epoch(const mbrl_train_model* model, const mbrl_train_data* data,
     const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     std::vector<mbrl_adam_tensor> table(tensors, tensors + count);
     const int64_t batches = (rows + batch_size - 1) / batch_size;
+    // the Adam step rides in the backward launches when the table is the model's layers in order
+    // (weight, bias per Linear, gradients = the model's buffers); otherwise a separate launch
+    bool fold = count == 2 * layers;
+    for (int l = 0; fold && l < layers; ++l)
+        fold = tensors[2 * l].param == model->weight[l] && tensors[2 * l].grad == model->weight_grad[l] &&
+               tensors[2 * l + 1].param == model->bias[l] && tensors[2 * l + 1].grad == model->bias_grad[l];
+    const int ar = arith ? arith - 1 : ADAM_ARITH_TORCH;
     for (int64_t b = 0; b < batches; ++b) {
         const int n = (int)std::min<int64_t>(batch_size, rows - b * batch_size);
-        if (int rc = hip_check(launch_train_grads(t, w, order + b * batch_size, n, losses ? losses + 3 * b : nullptr,
-                                                  static_cast<float*>(workspace), st), "train_epoch grads"))
-            return rc;
         for (int i = 0; i < count; ++i) {
             table[i].step_size = step_sizes[b * count + i];
             table[i].bc2_sqrt = bc2_sqrt[b * count + i];
         }
-        if (int rc = hip_check(launch_adam_step(table.data(), count, *hparams, arith ? arith - 1 : ADAM_ARITH_TORCH, st),
-                               "train_epoch adam"))
+        if (int rc = hip_check(launch_train_grads(t, w, order + b * batch_size, n, losses ? losses + 3 * b : nullptr,
+                                                  static_cast<float*>(workspace), st, fold ? table.data() : nullptr,
+                                                  hparams, ar), "train_epoch grads"))
             return rc;
+        if (!fold)
+            if (int rc = hip_check(launch_adam_step(table.data(), count, *hparams, ar, st), "train_epoch adam")) return rc;
     }
     return MBRL_OK;
 }

@@ -301,7 +301,10 @@ struct TrainTensors {
     const float *states, *actions, *next_states, *rewards;   // stacked transitions [T][H][.]
 };
 size_t train_ws_floats(const TrainShape& t, int batch);
+// adam (optional): the step of every layer's weight and bias (linear1.weight, linear1.bias, ...)
+// folded into the backward launches, bit-identical to a separate mbrl_adam_step after the gradient.
 hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const int64_t* idx, int batch,
-                              float* loss_out, float* ws, hipStream_t stream);
+                              float* loss_out, float* ws, hipStream_t stream, const mbrl_adam_tensor* adam = nullptr,
+                              const mbrl_adam_hparams* hp = nullptr, int arith = 0);
 
 }  // namespace mbrl

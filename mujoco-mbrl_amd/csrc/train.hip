@@ -164,6 +164,7 @@ __device__ unsigned long long* g_train_stamps;
 enum { OP_DIRECT = 0, OP_TRANS = 1, OP_GATHER = 2 };
 enum { EPI_ACT = 0, EPI_LOSS = 1, EPI_MASK = 2, EPI_GRAD = 3 };
 constexpr int TT = 32;              // C tile edge
+constexpr int ADAM_FUSED_MAX = 4;   // tensors per fused Adam role (a layer's weight and bias, or both heads')
 
 // Logical operand X(i, k), i < rows, k < K, over a row-major storage matrix S whose rows below
 // `split` live at p0 and the rest at p1 (the state and reward heads as one matrix).
@@ -194,6 +195,9 @@ struct Output {
     const float* colsum_in;   // EPI_GRAD: [colsum_tiles][M] column sums of this layer's output gradient
     int colsum_tiles;
     float* colsum_out;        // EPI_MASK / EPI_LOSS: [row tile][N] column sums of the stored C
+    int adam;                 // EPI_GRAD: also take this layer's Adam step in place (nothing reads it
+                              // in this launch): weight at aw (= c0 layout), bias at ab
+    mbrl_adam_tensor aw, ab;
     float scale_s, scale_r;   // EPI_LOSS: dY scale of the state / reward columns (2 / numel)
     float inv_s, inv_r;       // EPI_LOSS: loss weight of the state / reward columns (1 / numel)
     int s;                    // EPI_LOSS: state columns (n >= s: the reward column)
@@ -222,6 +226,13 @@ struct GemmLaunch {
     const float* loss_part;
     int loss_parts;
     float* loss_out;
+    // fused Adam (mbrl_train_epoch): the step of a layer whose gradient the previous launch finished,
+    // as extra workgroups after the products' tiles (ADAM_FUSED_CHUNK elements each)
+    int adam_count, adam_blocks;
+    mbrl_adam_tensor adam_t[ADAM_FUSED_MAX];
+    int adam_first[ADAM_FUSED_MAX + 1];
+    mbrl_adam_hparams hp;
+    int arith;
 };
 
 __device__ __forceinline__ int64_t batch_row(const GemmLaunch& L, int r) {
@@ -369,12 +380,20 @@ __device__ void gemm_tile(const GemmLaunch& L, const GemmDesc& D, int tile, floa
         keep[j] = v;
         float* dst = m < O.split ? O.c0 + (int64_t)m * O.ldc : O.c1 + (int64_t)(m - O.split) * O.ldc;
         dst[n] = v;
+        if (O.mode == EPI_GRAD && O.adam) {
+            const int64_t i = (int64_t)m * O.ldc + n;
+            adam_element(O.aw.param[i], v, O.aw.exp_avg[i], O.aw.exp_avg_sq[i], O.aw.step_size, O.aw.bc2_sqrt, L.hp,
+                         L.arith);
+        }
         // EPI_GRAD: the first column tile also finishes the bias gradient of row m from the column
         // sums the launch that produced this layer's output gradient left per row tile
         if (O.mode == EPI_GRAD && n0 == 0 && col == 0) {
             float g = O.colsum_in[m];
             for (int i = 1; i < O.colsum_tiles; ++i) g = g + O.colsum_in[(int64_t)i * D.M + m];
             (m < O.split ? O.g0[m] : O.g1[m - O.split]) = g;
+            if (O.adam)
+                adam_element(O.ab.param[m], g, O.ab.exp_avg[m], O.ab.exp_avg_sq[m], O.ab.step_size, O.ab.bc2_sqrt,
+                             L.hp, L.arith);
         }
     }
     if (O.mode == EPI_MASK || O.mode == EPI_LOSS) {   // per-row-tile column sums (the next bias gradient)
@@ -425,11 +444,23 @@ __global__ __launch_bounds__(64 * NW) void train_gemm_kernel(const GemmLaunch L)
         gemm_tile<NW, A0, B0>(L, L.d[0], b, red);
         return;
     }
+    int r = b - L.d[0].tiles;
     if constexpr (A1 >= 0) {
-        if (L.nd > 1 && b - L.d[0].tiles < L.d[1].tiles) {
-            gemm_tile<NW, A1, B1>(L, L.d[1], b - L.d[0].tiles, red);
+        if (L.nd > 1 && r < L.d[1].tiles) {
+            gemm_tile<NW, A1, B1>(L, L.d[1], r, red);
             return;
         }
+        if (L.nd > 1) r -= L.d[1].tiles;
+    }
+    if (r < L.adam_blocks) {    // fused Adam: ADAM_FUSED_CHUNK elements of one tensor per workgroup
+        int ti = 0;
+        while (ti + 1 < L.adam_count && r >= L.adam_first[ti + 1]) ++ti;
+        const mbrl_adam_tensor& T = L.adam_t[ti];
+        const int64_t base = (int64_t)(r - L.adam_first[ti]) * (64 * NW * 4);
+        for (int64_t i = base + threadIdx.x; i < T.numel && i < base + 64 * NW * 4; i += 64 * NW)
+            adam_element(T.param[i], T.grad[i], T.exp_avg[i], T.exp_avg_sq[i], T.step_size, T.bc2_sqrt, L.hp,
+                         L.arith);
+        return;
     }
     // the loss workgroup: partials of the output-layer launch, summed in tile order
     if (threadIdx.x < 2 && L.loss_out) {
@@ -473,6 +504,15 @@ static hipError_t launch_gemm(GemmLaunch& L, bool loss_wg, hipStream_t stream) {
         blocks += L.d[i].tiles;
         kmax = max(kmax, L.d[i].K);
     }
+    // fused Adam blocks: chunks of 4 elements per thread of the launch's workgroup size
+    const int chunk = 64 * (kmax >= 256 ? 16 : 4) * 4;
+    L.adam_blocks = 0;
+    for (int i = 0; i < L.adam_count; ++i) {
+        L.adam_first[i] = L.adam_blocks;
+        L.adam_blocks += (int)((L.adam_t[i].numel + chunk - 1) / chunk);
+    }
+    L.adam_first[L.adam_count] = L.adam_blocks;
+    blocks += L.adam_blocks;
     if (!loss_wg) L.loss_out = nullptr;
     ++L.slot;
     if (kmax >= 256)
@@ -514,7 +554,8 @@ static TrainWs train_ws(const TrainShape& t, int batch, float* base) {
 size_t train_ws_floats(const TrainShape& t, int batch) { return train_ws(t, batch, nullptr).floats; }
 
 hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const int64_t* idx, int batch,
-                              float* loss_out, float* ws, hipStream_t stream) {
+                              float* loss_out, float* ws, hipStream_t stream, const mbrl_adam_tensor* adam,
+                              const mbrl_adam_hparams* hp, int arith) {
     const int R = batch * t.H, W = t.W, K0 = t.s + t.a, J = t.s + (t.reward ? 1 : 0), L = t.L;
     const int tiles_r = (R + TT - 1) / TT;
     const TrainWs B = train_ws(t, batch, ws);
@@ -526,6 +567,10 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
     G.H = t.H; G.s = t.s; G.a = t.a;
     G.xstore = B.xbuf;
     G.slot = -1;
+    if (adam) {
+        G.hp = *hp;
+        G.arith = arith;
+    }
     hipError_t e;
     // forward through the hidden layers
     for (int l = 0; l < L; ++l) {
@@ -594,6 +639,18 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
                 O.g0 = O.g1 = w.bias_grad[l];
             }
             finish(D, n_out, n_in, R);
+        }
+        if (adam && l == 0) {   // nothing in this launch reads layer 0's parameters: step them in place
+            G.d[G.nd - 1].out.adam = 1;
+            G.d[G.nd - 1].out.aw = adam[0];
+            G.d[G.nd - 1].out.ab = adam[1];
+        }
+        // layer l + 1's gradient is complete (previous launch) and this launch does not read its
+        // parameters: its Adam step rides along (with the reward head when l + 1 is the output layer)
+        G.adam_count = 0;
+        if (adam && l + 1 <= L) {
+            const int first = 2 * (l + 1), n = (l + 1 == L && t.reward) ? 4 : 2;
+            for (int i = 0; i < n; ++i) G.adam_t[G.adam_count++] = adam[first + i];
         }
         G.loss_part = B.loss_part; G.loss_parts = loss_parts; G.loss_out = loss_out;
         e = l >= 1 ? launch_gemm<OP_DIRECT, OP_TRANS, OP_TRANS, OP_TRANS>(G, false, stream)
