@@ -267,10 +267,20 @@ int mbrl_cem_update(const float* costs, int32_t E, int32_t N, int32_t K, const m
  * (reward_head == 0) or a MODEL_REWARD cost (reward_head == 1), else MBRL_EUNSUPPORTED.
  * workspace >= mbrl_gd_workspace_bytes(shape, H). */
 size_t mbrl_gd_workspace_bytes(const mbrl_mlp_shape* shape, int32_t H);
+size_t mbrl_gd_batch_workspace_bytes(const mbrl_mlp_shape* shape, int32_t H, int32_t B);
 int mbrl_gd_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_norm* norm, const mbrl_cost* cost,
                  const float* s0, float* actions, int32_t H, int32_t num_iterations, float stop_condition,
                  float lr, float* states_out, int32_t* iterations_out, void* workspace, size_t ws_bytes,
                  mbrl_stream_t stream);
+/* B independent gradient-descent plans in shared launches (parallel environments: one start state
+ * each, SURVEY.md §8f rank 3 "batching over restarts"): s0 [B][s], actions [B][H][a] (in: the initial
+ * sequences, out: the optimised ones), states_out [B][H+1][s], iterations_out [B] or NULL. Each plan
+ * is exactly mbrl_gd_plan's (same arithmetic, its own stop test); the cooperative grids of as many
+ * plans as fit the device together run in one launch. workspace >= mbrl_gd_batch_workspace_bytes. */
+int mbrl_gd_plan_batch(const mbrl_mlp_shape* shape, const void* packed, const mbrl_norm* norm, const mbrl_cost* cost,
+                       const float* s0, float* actions, int32_t B, int32_t H, int32_t num_iterations,
+                       float stop_condition, float lr, float* states_out, int32_t* iterations_out, void* workspace,
+                       size_t ws_bytes, mbrl_stream_t stream);
 
 /* ---- model training: torch.optim.Adam.step() for one fp32 parameter group
  * (torch/optim/adam.py _multi_tensor_adam, capturable = False, amsgrad = False, maximize = False),

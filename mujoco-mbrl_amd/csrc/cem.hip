@@ -1795,39 +1795,53 @@ int mbrl_cem_plan_batch(const mbrl_mlp_shape* shape, const void* packed, const m
 
 
 // ---- fused gradient-descent planner (gd.hip)
+// Workspace of B gradient-descent plans: the hand-off blocks of every plan first (2 Wpad granules,
+// then the status word; one memset clears them all), then per plan its Adam moments and saved
+// hidden vectors, plan_ws bytes apart.
 struct GdWs {
     float *m, *v, *hist;
     unsigned long long* xchg;
     unsigned* status;
-    size_t bytes;
+    size_t xchg_stride, plan_ws, bytes;
 };
 
-static GdWs gd_ws(const Geometry& g, int H, void* base) {
+static GdWs gd_ws(const Geometry& g, int H, int B, void* base) {
     GdWs w{};
     char* b = static_cast<char*>(base);
-    size_t o = 0;
-    auto take = [&](size_t n) { void* r = b ? b + o : nullptr; o += align256(n); return r; };
     const size_t ha = (size_t)H * g.a;
     const size_t row = ((size_t)((g.s + g.a + 3) & ~3) + (size_t)g.L * g.Wpad) * (g.reward ? 2 : 1);
     const size_t coop = (size_t)(g.Wpad / 16) * H * g.L * g.Wpad * (g.reward ? 2 : 1);   // per-workgroup hidden-vector copies
-    w.xchg = (unsigned long long*)take((size_t)2 * g.Wpad * 8 + 16);   // granules, then the status word
+    w.xchg_stride = (size_t)2 * g.Wpad + 2;                                  // granules, then the status word
+    const size_t xbytes = align256((size_t)B * w.xchg_stride * 8);
+    w.plan_ws = align256(ha * 4) * 2 + align256((H * row > coop ? H * row : coop) * 4);
+    w.xchg = b ? reinterpret_cast<unsigned long long*>(b) : nullptr;
     w.status = w.xchg ? reinterpret_cast<unsigned*>(w.xchg + 2 * g.Wpad) : nullptr;
-    w.m = (float*)take(ha * 4);
-    w.v = (float*)take(ha * 4);
-    w.hist = (float*)take((H * row > coop ? H * row : coop) * 4);
-    w.bytes = o;
+    w.m = b ? reinterpret_cast<float*>(b + xbytes) : nullptr;
+    w.v = b ? reinterpret_cast<float*>(b + xbytes + align256(ha * 4)) : nullptr;
+    w.hist = b ? reinterpret_cast<float*>(b + xbytes + 2 * align256(ha * 4)) : nullptr;
+    w.bytes = xbytes + (size_t)B * w.plan_ws;
     return w;
 }
 
-size_t mbrl_gd_workspace_bytes(const mbrl_mlp_shape* shape, int32_t H) {
+size_t mbrl_gd_workspace_bytes(const mbrl_mlp_shape* shape, int32_t H) { return mbrl_gd_batch_workspace_bytes(shape, H, 1); }
+
+size_t mbrl_gd_batch_workspace_bytes(const mbrl_mlp_shape* shape, int32_t H, int32_t B) {
     Geometry g;
-    if (shape_geometry(shape, &g) != MBRL_OK || H < 1) return 0;
-    return gd_ws(g, H, nullptr).bytes;
+    if (shape_geometry(shape, &g) != MBRL_OK || H < 1 || B < 1) return 0;
+    return gd_ws(g, H, B, nullptr).bytes;
 }
 
 int mbrl_gd_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_norm* norm, const mbrl_cost* cost,
                  const float* s0, float* actions, int32_t H, int32_t num_iterations, float stop_condition, float lr,
                  float* states_out, int32_t* iterations_out, void* workspace, size_t ws_bytes, mbrl_stream_t stream) {
+    return mbrl_gd_plan_batch(shape, packed, norm, cost, s0, actions, 1, H, num_iterations, stop_condition, lr,
+                              states_out, iterations_out, workspace, ws_bytes, stream);
+}
+
+int mbrl_gd_plan_batch(const mbrl_mlp_shape* shape, const void* packed, const mbrl_norm* norm, const mbrl_cost* cost,
+                       const float* s0, float* actions, int32_t B, int32_t H, int32_t num_iterations,
+                       float stop_condition, float lr, float* states_out, int32_t* iterations_out, void* workspace,
+                       size_t ws_bytes, mbrl_stream_t stream) {
     Geometry g;
     int rc = shape_geometry(shape, &g);
     if (rc) return rc;
@@ -1835,14 +1849,14 @@ int mbrl_gd_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_nor
     if (!cost || cost->kind != (g.reward ? MBRL_COST_MODEL_REWARD : MBRL_COST_GOAL_STATE))
         return fail(MBRL_EUNSUPPORTED, "gd_plan: needs a GOAL_STATE cost, or MODEL_REWARD with a reward-head model");
     if (!packed || !s0 || !actions || !states_out || !workspace) return fail(MBRL_EINVAL, "gd_plan: NULL argument");
-    if (H < 1 || num_iterations < 0) return fail(MBRL_EINVAL, "gd_plan: H=%d iterations=%d", H, num_iterations);
+    if (H < 1 || num_iterations < 0 || B < 1)
+        return fail(MBRL_EINVAL, "gd_plan: H=%d iterations=%d B=%d", H, num_iterations, B);
     if (gd_lds_bytes(g.s, g.a, g.Wpad, H) > 160 * 1024) return fail(MBRL_EUNSUPPORTED, "gd_plan: H * a too large");
     if (!g.reward && cost->has_state_cost && (!cost->weights || !cost->goal))
         return fail(MBRL_EINVAL, "gd_plan: state cost without weights/goal");
     GdArgs A{};
-    const GdWs w = gd_ws(g, H, workspace);
+    const GdWs w = gd_ws(g, H, B, workspace);
     if (ws_bytes < w.bytes) return fail(MBRL_EWORKSPACE, "gd workspace %zu < %zu", ws_bytes, w.bytes);
-    A.m = w.m; A.v = w.v; A.hist = w.hist;
     A.packed = static_cast<const float*>(packed);
     A.bias_off = g.stream_floats;
     A.tw_base = g.stream_floats + g.bias_floats;
@@ -1866,24 +1880,47 @@ int mbrl_gd_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_nor
         A.alpha_s = cost->alpha_state; A.alpha_a = cost->alpha_action;
         A.has_sc = cost->has_state_cost; A.has_ac = cost->has_action_cost;
     }
-    A.s0 = s0; A.actions = actions; A.states_out = states_out;
     A.hist_row = (((g.s + g.a + 3) & ~3) + g.L * g.Wpad) * (g.reward ? 2 : 1);
     A.iterations = num_iterations; A.stop = stop_condition; A.lr = lr;
-    A.iterations_out = iterations_out;
+    A.plan_ws = w.plan_ws;
+    A.xchg_stride = w.xchg_stride;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     // MBRL_OPT_GD_SINGLE (A/B and tests): the one-workgroup kernel
-    if (gd_coop_supported(A) && g_opt[MBRL_OPT_GD_SINGLE].load(std::memory_order_relaxed) == 0) {
-        A.debug_abort = g_opt[MBRL_OPT_DEBUG_GD_ABORT].load(std::memory_order_relaxed) != 0;
-        const hipError_t err = launch_gd_coop(A, w.xchg, w.status, st);
-        if (err != hipErrorCooperativeLaunchTooLarge) {   // too large: the grid cannot be co-resident
-            rc = hip_check(err, "gd_plan coop launch");
-            if (rc) return rc;
-            // the one-workgroup kernel redoes the plan only if a cooperative hand-off timed out
-            A.gate = w.status;
+    const bool coop = gd_coop_supported(A) && g_opt[MBRL_OPT_GD_SINGLE].load(std::memory_order_relaxed) == 0;
+    // plans run in groups whose cooperative grids fit the device together (Wpad / 16 workgroups each)
+    int group = B;
+    for (int i = 0; i < B; i += group) {
+        const int n = std::min(group, B - i);
+        A.batch = n;
+        A.s0 = s0 + (size_t)i * g.s;
+        A.actions = actions + (size_t)i * H * g.a;
+        A.states_out = states_out + (size_t)i * (H + 1) * g.s;
+        A.iterations_out = iterations_out ? iterations_out + i : nullptr;
+        A.m = reinterpret_cast<float*>(reinterpret_cast<char*>(w.m) + i * w.plan_ws);
+        A.v = reinterpret_cast<float*>(reinterpret_cast<char*>(w.v) + i * w.plan_ws);
+        A.hist = reinterpret_cast<float*>(reinterpret_cast<char*>(w.hist) + i * w.plan_ws);
+        unsigned long long* xchg = w.xchg + (size_t)i * w.xchg_stride;
+        unsigned* status = reinterpret_cast<unsigned*>(xchg + 2 * g.Wpad);
+        A.gate = nullptr;
+        if (coop) {
+            A.debug_abort = g_opt[MBRL_OPT_DEBUG_GD_ABORT].load(std::memory_order_relaxed) != 0;
+            const hipError_t err = launch_gd_coop(A, xchg, status, st);
+            if (err == hipErrorCooperativeLaunchTooLarge && n > 1) {   // fewer plans per group, same start
+                group = std::max(1, n / 2);
+                i -= group;
+                continue;
+            }
+            if (err != hipErrorCooperativeLaunchTooLarge) {   // too large for even one plan: one workgroup each
+                rc = hip_check(err, "gd_plan coop launch");
+                if (rc) return rc;
+                // the one-workgroup kernel redoes a plan only if its cooperative hand-offs timed out
+                A.gate = status;
+            }
+            A.debug_abort = 0;
         }
-        A.debug_abort = 0;
+        if ((rc = hip_check(launch_gd_plan(A, st), "gd_plan launch"))) return rc;
     }
-    return hip_check(launch_gd_plan(A, st), "gd_plan launch");
+    return MBRL_OK;
 }
 
 }  // extern "C"

@@ -128,12 +128,22 @@ __device__ float gd_block_sum(float v, float* red) {
 
 __global__ void __launch_bounds__(GD_THREADS) gd_plan_kernel(const GdArgs A) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
+    // plan blockIdx.y of a batch: its own start state, actions, states, workspace block and gate
+    const int pb = blockIdx.y;
+    const float* s0 = A.s0 + (size_t)pb * A.s;
+    float* actions = A.actions + (size_t)pb * A.H * A.a;
+    float* states_out = A.states_out + (size_t)pb * (A.H + 1) * A.s;
+    float* am = reinterpret_cast<float*>(reinterpret_cast<char*>(A.m) + pb * A.plan_ws);
+    float* av = reinterpret_cast<float*>(reinterpret_cast<char*>(A.v) + pb * A.plan_ws);
+    float* ahist = reinterpret_cast<float*>(reinterpret_cast<char*>(A.hist) + pb * A.plan_ws);
+    int* iterations_out = A.iterations_out ? A.iterations_out + pb : nullptr;
+    const unsigned* gate = A.gate ? A.gate + (size_t)pb * A.xchg_stride * 2 : nullptr;
     // behind the cooperative kernel: only when that one gave up (its status word set)
-    if (A.gate != nullptr && *A.gate == 0u) return;
+    if (gate != nullptr && *gate == 0u) return;
     const GdLds m = gd_lds(A.s, A.a, A.Wpad, A.H, smem);
     const int tid = threadIdx.x;
     const int s = A.s, a = A.a, Wp = A.Wpad, K0 = s + a, L = A.L, H = A.H;
-    const int rowf = A.hist_row;                       // floats per step in hist: K0p + L * Wpad
+    const int rowf = A.hist_row;                      // floats per step in hist: K0p + L * Wpad
     const int K0p = (K0 + 3) & ~3;
     const float* bias = A.packed + A.bias_off;
     const float* tw = A.packed + A.tw_base;
@@ -149,25 +159,25 @@ __global__ void __launch_bounds__(GD_THREADS) gd_plan_kernel(const GdArgs A) {
     const float* bout = bias + (size_t)L * Wp;
     const float b1 = 0.9f, b2 = 0.999f, eps = 1e-8f;
 
-    for (int i = tid; i < H * a; i += GD_THREADS) { A.m[i] = 0.f; A.v[i] = 0.f; }
+    for (int i = tid; i < H * a; i += GD_THREADS) { am[i] = 0.f; av[i] = 0.f; }
     // the reference's states tensor before any iteration: s0, then zeros (returned as is when
     // num_iterations == 0)
-    for (int i = tid; i < (H + 1) * s; i += GD_THREADS) A.states_out[i] = i < s ? A.s0[i] : 0.f;
+    for (int i = tid; i < (H + 1) * s; i += GD_THREADS) states_out[i] = i < s ? s0[i] : 0.f;
     __syncthreads();
     int done = 0;
     for (int it = 0; it < A.iterations; ++it) {
         // ---------------- forward: the rollout of the current actions (states_out rows 0..H)
-        for (int d = tid; d < s; d += GD_THREADS) A.states_out[d] = A.s0[d];
+        for (int d = tid; d < s; d += GD_THREADS) states_out[d] = s0[d];
         __syncthreads();
         for (int t = 0; t < H; ++t) {
-            float* hist = A.hist + (size_t)t * rowf;
+            float* hist = ahist + (size_t)t * rowf;
             for (int d = tid; d < K0; d += GD_THREADS) {
                 float v;
                 if (d < s) {
-                    const float sv = A.states_out[(size_t)t * s + d];
+                    const float sv = states_out[(size_t)t * s + d];
                     v = A.norm_s ? (sv - A.obs_mean[d]) / A.obs_std[d] : sv;
                 } else {
-                    const float av = A.actions[t * a + d - s];
+                    const float av = actions[t * a + d - s];
                     v = A.norm_a ? (av - A.act_mean[d - s]) / A.act_std[d - s] : av;
                 }
                 m.x[d] = v;
@@ -188,7 +198,7 @@ __global__ void __launch_bounds__(GD_THREADS) gd_plan_kernel(const GdArgs A) {
                 v = gd_wave_sum(v);
                 if (lane == 0) {
                     const float o = v + bout[n];
-                    A.states_out[(size_t)(t + 1) * s + n] = A.unnorm_s ? o * A.obs_std[n] + A.obs_mean[n] : o;
+                    states_out[(size_t)(t + 1) * s + n] = A.unnorm_s ? o * A.obs_std[n] + A.obs_mean[n] : o;
                 }
             }
             __threadfence_block();
@@ -200,7 +210,7 @@ __global__ void __launch_bounds__(GD_THREADS) gd_plan_kernel(const GdArgs A) {
                 for (int d = tid; d < K0; d += GD_THREADS) {
                     float v;
                     if (d < s) {
-                        const float sv = A.states_out[(size_t)(t + 1) * s + d];
+                        const float sv = states_out[(size_t)(t + 1) * s + d];
                         v = A.norm_s ? (sv - A.obs_mean[d]) / A.obs_std[d] : sv;
                     } else {
                         v = hist[d];   // norm(a_t), as the state pass
@@ -222,7 +232,7 @@ __global__ void __launch_bounds__(GD_THREADS) gd_plan_kernel(const GdArgs A) {
         for (int d = tid; d < s; d += GD_THREADS) m.gs[d] = 0.f;
         __syncthreads();
         for (int t = H - 1; t >= 0; --t) {
-            const float* hist = A.hist + (size_t)t * rowf;
+            const float* hist = ahist + (size_t)t * rowf;
             if (A.reward) {
                 // reward pass backward: d r_t / d head = rew_std (unnormalise_reward), through the
                 // reward row of the output block and the pass's saved ReLU masks to its input
@@ -255,7 +265,7 @@ __global__ void __launch_bounds__(GD_THREADS) gd_plan_kernel(const GdArgs A) {
             for (int d = tid; d < s; d += GD_THREADS) {
                 float g = m.gs[d];
                 if (A.has_sc) {
-                    const float x = A.states_out[(size_t)(t + 1) * s + d] - A.goal[d];
+                    const float x = states_out[(size_t)(t + 1) * s + d] - A.goal[d];
                     const float wx = x * A.cw[d];
                     g += wx * A.cw[d] / sqrtf(wx * wx + A.alpha_s * A.alpha_s);
                 }
@@ -287,7 +297,7 @@ __global__ void __launch_bounds__(GD_THREADS) gd_plan_kernel(const GdArgs A) {
                     const int j = d - s;
                     float ga = A.norm_a ? g / A.act_std[j] : g;
                     if (A.has_ac)
-                        ga += A.alpha_a * sinhf(A.actions[t * a + j] / A.alpha_a) / (float)a;
+                        ga += A.alpha_a * sinhf(actions[t * a + j] / A.alpha_a) / (float)a;
                     if (A.reward) ga += m.ga[t * a + j];   // the reward pass's share (above)
                     m.ga[t * a + j] = ga;
                 }
@@ -301,14 +311,14 @@ __global__ void __launch_bounds__(GD_THREADS) gd_plan_kernel(const GdArgs A) {
         float change = 0.f;
         for (int i = tid; i < H * a; i += GD_THREADS) {
             const float g = m.ga[i];
-            float mm = A.m[i];
+            float mm = am[i];
             mm = mm + (1.0f - b1) * (g - mm);
-            const float vv = b2 * A.v[i] + (1.0f - b2) * g * g;
-            A.m[i] = mm;
-            A.v[i] = vv;
-            const float old = A.actions[i];
+            const float vv = b2 * av[i] + (1.0f - b2) * g * g;
+            am[i] = mm;
+            av[i] = vv;
+            const float old = actions[i];
             const float nw = old - step * (mm / (sqrtf(vv) / bc2s + eps));
-            A.actions[i] = nw;
+            actions[i] = nw;
             change += fabsf(old - nw);
         }
         __threadfence_block();
@@ -316,7 +326,7 @@ __global__ void __launch_bounds__(GD_THREADS) gd_plan_kernel(const GdArgs A) {
         done = it + 1;
         if (change / (float)(H * a) < A.stop) break;
     }
-    if (tid == 0 && A.iterations_out != nullptr) *A.iterations_out = done;
+    if (tid == 0 && iterations_out != nullptr) *iterations_out = done;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -455,6 +465,14 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
                                                              unsigned* __restrict__ status) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int p = blockIdx.x;
+    // plan blockIdx.y of a batch: its own start state, actions, states, hand-off block and workspace
+    const int pb = blockIdx.y;
+    const float* s0 = A.s0 + (size_t)pb * A.s;
+    float* actions = A.actions + (size_t)pb * A.H * A.a;
+    float* states_out = A.states_out + (size_t)pb * (A.H + 1) * A.s;
+    int* iterations_out = A.iterations_out ? A.iterations_out + pb : nullptr;
+    xchg_all += (size_t)pb * A.xchg_stride;
+    status += (size_t)pb * A.xchg_stride * 2;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = tid >> 5, c = tid & 31;
     const int s = A.s, a = A.a, W = A.W, Wp = A.Wpad, K0 = s + a, L = A.L, H = A.H;
     const GcLds m = gc_lds(s, a, W, Wp, L, H, K0R);
@@ -475,7 +493,8 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
     gc_gu64* xchg = (gc_gu64*)xchg_all;
     // this workgroup's copy of the hidden vectors: [H][L][Wp] per pass (state pass, then the reward
     // pass of a reward-head model at rows H..2H-1)
-    float* hist = A.hist + (size_t)p * (A.reward ? 2 : 1) * H * L * Wp;
+    float* hist = reinterpret_cast<float*>(reinterpret_cast<char*>(A.hist) + pb * A.plan_ws) +
+                  (size_t)p * (A.reward ? 2 : 1) * H * L * Wp;
 
     if (A.debug_abort) {                       // test hook: behave as a timed-out hand-off
         if (tid == 0) atomicOr(status, 1u);
@@ -497,8 +516,8 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
             b[o * m.rs + n] = wt[(size_t)(p * GC_ROWS + o) * Wp + n];  // W_l[n][16p + o]
         }
     }
-    for (int i = tid; i < H * a; i += GC_THREADS) { acts[i] = A.actions[i]; m1[i] = 0.f; m2[i] = 0.f; }
-    for (int i = tid; i < (H + 1) * s; i += GC_THREADS) st[i] = i < s ? A.s0[i] : 0.f;
+    for (int i = tid; i < H * a; i += GC_THREADS) { acts[i] = actions[i]; m1[i] = 0.f; m2[i] = 0.f; }
+    for (int i = tid; i < (H + 1) * s; i += GC_THREADS) st[i] = i < s ? s0[i] : 0.f;
     for (int d = tid; d < 32; d += GC_THREADS) gout[d] = 0.f;   // entries >= s stay zero
     const bool has_unit = tid < Wp;
     const float b0 = has_unit ? bias[tid] : 0.0f;
@@ -707,9 +726,9 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
         if (change / (float)(H * a) < A.stop) break;
     }
     if (p == 0) {
-        for (int i = tid; i < H * a; i += GC_THREADS) A.actions[i] = acts[i];
-        for (int i = tid; i < (H + 1) * s; i += GC_THREADS) A.states_out[i] = st[i];
-        if (tid == 0 && A.iterations_out != nullptr) *A.iterations_out = done;
+        for (int i = tid; i < H * a; i += GC_THREADS) actions[i] = acts[i];
+        for (int i = tid; i < (H + 1) * s; i += GC_THREADS) states_out[i] = st[i];
+        if (tid == 0 && iterations_out != nullptr) *iterations_out = done;
     }
 }
 
@@ -727,15 +746,15 @@ static hipError_t launch_gd_coop_w(const GdArgs& A, gc_u64* xchg, unsigned* stat
     hipError_t err = ensure_dynamic_lds(reinterpret_cast<const void*>(fn), 160 * 1024);
     if (err != hipSuccess) return err;
     const size_t lds = gc_lds(A.s, A.a, A.W, A.Wpad, A.L, A.H, 32).total;
-    if (!grid_fits(reinterpret_cast<const void*>(fn), GC_THREADS, lds, A.Wpad / GC_ROWS))
+    if (!grid_fits(reinterpret_cast<const void*>(fn), GC_THREADS, lds, A.Wpad / GC_ROWS * A.batch))
         return hipErrorCooperativeLaunchTooLarge;
-    hipLaunchKernelGGL(fn, dim3(A.Wpad / GC_ROWS), dim3(GC_THREADS), lds, stream, A, xchg, status);
+    hipLaunchKernelGGL(fn, dim3(A.Wpad / GC_ROWS, A.batch), dim3(GC_THREADS), lds, stream, A, xchg, status);
     return hipGetLastError();
 }
 
 hipError_t launch_gd_coop(const GdArgs& A, unsigned long long* xchg, unsigned* status, hipStream_t stream) {
-    // zero the granules and the status word (adjacent: one memset)
-    hipError_t err = hipMemsetAsync(xchg, 0, (size_t)2 * A.Wpad * 8 + 16, stream);
+    // zero the granules and the status words (each plan's block: granules, then its status word)
+    hipError_t err = hipMemsetAsync(xchg, 0, (size_t)A.batch * A.xchg_stride * 8, stream);
     if (err != hipSuccess) return err;
     switch (A.Wpad) {
         case 64: return launch_gd_coop_w<2>(A, xchg, status, stream);
@@ -753,7 +772,7 @@ hipError_t launch_gd_plan(const GdArgs& A, hipStream_t stream) {
     // the kernel also has a few bytes of static LDS: raise the dynamic limit to what it needs, not 160 KiB
     hipError_t err = ensure_dynamic_lds(reinterpret_cast<const void*>(&gd_plan_kernel), (int)lds);
     if (err != hipSuccess) return err;
-    hipLaunchKernelGGL(gd_plan_kernel, dim3(1), dim3(GD_THREADS), lds, stream, A);
+    hipLaunchKernelGGL(gd_plan_kernel, dim3(1, A.batch), dim3(GD_THREADS), lds, stream, A);
     return hipGetLastError();
 }
 

@@ -258,6 +258,11 @@ struct GdArgs {
     int* iterations_out;                   // device int or NULL
     const unsigned* gate;                  // gd_plan_kernel: when non-NULL, run only if *gate != 0
     int debug_abort;                       // gd_coop_kernel: give up at once (MBRL_DEBUG_GD_ABORT)
+    // batched plans (grid.y = batch): plan b reads s0 + b s, actions + b H a, writes states_out +
+    // b (H+1) s and iterations_out + b; its m / v / hist lie plan_ws bytes after plan b-1's, its
+    // hand-off block (2 Wpad granules, then the status word) xchg_stride granules after
+    int batch;
+    size_t plan_ws, xchg_stride;
 };
 size_t gd_lds_bytes(int s, int a, int Wpad, int H);
 hipError_t launch_gd_plan(const GdArgs& A, hipStream_t stream);

@@ -50,7 +50,7 @@ EXPORTED = (
     "mbrl_trajectory_workspace_bytes", "mbrl_trajectory", "mbrl_cem_workspace_bytes", "mbrl_cem_plan",
     "mbrl_cem_plan_batch_workspace_bytes", "mbrl_cem_plan_batch", "mbrl_gd_workspace_bytes", "mbrl_gd_plan",
     "mbrl_cem_update", "mbrl_adam_step", "mbrl_train_workspace_bytes", "mbrl_train_grads",
-    "mbrl_train_epoch",
+    "mbrl_train_epoch", "mbrl_gd_batch_workspace_bytes", "mbrl_gd_plan_batch",
 )
 
 
@@ -146,6 +146,9 @@ def load():
                                           POINTER(CemParams), P, P, P, P, P, c_size_t, P]),
         "mbrl_cem_workspace_bytes": (c_size_t, [POINTER(MlpShape), POINTER(CemParams)]),
         "mbrl_gd_workspace_bytes": (c_size_t, [POINTER(MlpShape), c_int32]),
+        "mbrl_gd_batch_workspace_bytes": (c_size_t, [POINTER(MlpShape), c_int32, c_int32]),
+        "mbrl_gd_plan_batch": (c_int32, [POINTER(MlpShape), P, POINTER(Norm), POINTER(Cost), P, P, c_int32, c_int32,
+                                         c_int32, c_float, c_float, P, P, P, c_size_t, P]),
         "mbrl_gd_plan": (c_int32, [POINTER(MlpShape), P, POINTER(Norm), POINTER(Cost), P, P, c_int32, c_int32,
                                    c_float, c_float, P, P, P, c_size_t, P]),
         "mbrl_adam_step": (c_int32, [POINTER(AdamTensor), c_int32, POINTER(AdamHparams), P]),

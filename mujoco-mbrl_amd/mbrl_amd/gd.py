@@ -10,7 +10,8 @@ Recognised closures (the same introspection as the CEM path: GoalStateAgent's an
 wiring) run on the device:
   * a single model with the goal-state cost, or a reward-head model with RewardAgent's reward cost
     -> mbrl_gd_plan (csrc/gd.hip): one launch runs every iteration's rollout, backward pass, Adam
-    step and stop test; the host waits once per plan;
+    step and stop test; the host waits once per plan. GradientDescentPlanner.plan_batch runs B
+    such plans (parallel environments) in shared launches (mbrl_gd_plan_batch);
   * ensembles -> a device restatement as differentiable torch ops: the MLP,
     normalisers and cost rebuilt from the described nn.Linear weights and statistics; the
     forward + loss + backward of one iteration (a chain of H x (L + 1) batch-1 layers) is captured
@@ -155,6 +156,26 @@ def plan_fused(initial_state, mdesc, cdesc, action_list, horizon, num_iterations
                                 float(stop_condition), float(lr), _lib.ptr(states), _lib.ptr(iters), _lib.ptr(ws),
                                 need, _lib.stream_handle(dev)), "mbrl_gd_plan")
     return states, actions, iters
+
+
+def plan_fused_batch(initial_states, mdesc, cdesc, actions, horizon, num_iterations, stop_condition, dev, lr=0.01):
+    """mbrl_gd_plan_batch: B plans (initial_states [B, s], initial actions [B, H, a]) in shared
+    launches, each exactly plan_fused's. Returns (states [B, H+1, s], actions [B, H, a], iterations [B])."""
+    lib = _lib.load()
+    prob = fused.device_problem(mdesc, cdesc, dev)
+    H, B = int(horizon), int(initial_states.shape[0])
+    s0 = initial_states.to(device=dev, dtype=torch.float32).reshape(B, -1).contiguous()
+    acts = actions.to(device=dev, dtype=torch.float32).reshape(B, H, -1).contiguous().clone()
+    states = torch.empty((B, H + 1, mdesc["s"]), dtype=torch.float32, device=dev)
+    iters = torch.zeros(B, dtype=torch.int32, device=dev)
+    need = lib.mbrl_gd_batch_workspace_bytes(fused.ctypes_ref(prob.shape), H, B)
+    ws = torch.empty(need, dtype=torch.uint8, device=dev)
+    _lib.check(lib.mbrl_gd_plan_batch(fused.ctypes_ref(prob.shape), _lib.ptr(prob.packed), fused.ctypes_ref(prob.norm),
+                                      fused.ctypes_ref(prob.cost), _lib.ptr(s0), _lib.ptr(acts), B, H,
+                                      int(num_iterations), float(stop_condition), float(lr), _lib.ptr(states),
+                                      _lib.ptr(iters), _lib.ptr(ws), need, _lib.stream_handle(dev)),
+               "mbrl_gd_plan_batch")
+    return states, acts, iters
 
 
 def plan_device(initial_state, mdesc, cdesc, action_list, horizon, num_iterations, stop_condition, dev,

@@ -109,6 +109,40 @@ class GradientDescentPlanner(ModelPlanner):
         states, actions = _to_host(states, keep), _to_host(actions, keep)
         return list(states.split(1, 0)), list(actions.split(1, 0))
 
+    @staticmethod
+    def plan_batch(initial_states, model, cost, sample_action, horizon, initial_trajectories=None, **kwargs):
+        """B independent plans, one per row of initial_states [B, s] (parallel environments), each
+        what plan() returns for that row. Row b starts from initial_trajectories[b][1] or, without
+        them, from sample_action(batch_size=horizon) drawn for b = 0, 1, ... in order (as B plan()
+        calls would draw). Recognised closures run in shared launches (mbrl_gd_plan_batch: the
+        cooperative grids of up to 256 / (Wpad / 16) plans at once); others run plan() per row.
+        Returns (states [B, H+1, s], actions [B, H, a])."""
+        from . import gd
+        num_iterations = int(kwargs.get("num_iterations", GradientDescentPlanner.defaults["num_iterations"]))
+        stop_condition = float(kwargs.get("stop_condition", GradientDescentPlanner.defaults["stop_condition"]))
+        H, B = int(horizon), int(initial_states.shape[0])
+        starts = []
+        for b in range(B):
+            if initial_trajectories is None:
+                starts.append(torch.cat(list(sample_action(batch_size=H).split(1, dim=0)), 0))
+            else:
+                starts.append(torch.cat([x.reshape(1, -1) for x in initial_trajectories[b][1]], 0))
+        mdesc, cdesc = gd.describe(model, cost)
+        keep = kwargs.get("return_device", False)
+        if mdesc is not None and torch.cuda.is_available():
+            dev = _device(kwargs)
+            if gd.fused_supported(mdesc, cdesc, dev) and num_iterations > 0:
+                with torch.cuda.device(dev):
+                    states, actions, _ = gd.plan_fused_batch(initial_states, mdesc, cdesc, torch.stack(starts), H,
+                                                             num_iterations, stop_condition, dev)
+                return _to_host(states, keep), _to_host(actions, keep)
+        outs = [GradientDescentPlanner.plan(initial_states[b], model, cost, sample_action, H,
+                                            initial_trajectory=(None, list(starts[b].split(1, 0))),
+                                            **dict(kwargs, return_device=True)) for b in range(B)]
+        states = torch.stack([torch.cat(o[0], 0).reshape(H + 1, -1) for o in outs])
+        actions = torch.stack([torch.cat(o[1], 0).reshape(H, -1) for o in outs])
+        return _to_host(states, keep), _to_host(actions, keep)
+
 
 class RandomShootingPlanner(ModelPlanner):
     """planners.py:140-216 on the GPU."""

@@ -139,3 +139,52 @@ def test_gd_reference_toy_known_answer(golden):
     assert np.allclose(ac, g["actions"], rtol=1e-6, atol=1e-6)
     total = float(mgd.toy_cost(torch.stack(states), torch.cat(actions)).sum())
     assert abs(total - float(g["total_cost"])) < 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cid,over,H,B,mode", [(3, {}, 12, 11, None), (3, dict(W=64, L=2), 8, 5, None),
+                                                (6, dict(W=256, L=3), 8, 9, None), (2, {}, 6, 3, "gd_single"),
+                                                (3, dict(W=128, L=3), 6, 4, "debug_gd_abort")])
+def test_gd_plan_batch_equals_single_plans(cid, over, H, B, mode):
+    """mbrl_gd_plan_batch: B plans from different start states and initial sequences, in groups of
+    co-resident cooperative grids (B = 11 at Wpad 512 needs two groups), are bit for bit the B plans
+    mbrl_gd_plan makes one at a time -- through the cooperative kernel, the one-workgroup kernel, and
+    the gated fallback after a forced hand-off timeout. Each plan keeps its own stop test."""
+    from mbrl_amd import _lib, gd
+    p, model_fn, cost_fn = closures(cid, over)
+    mdesc, cdesc = gd.describe(model_fn, cost_fn)
+    dev = torch.device("cuda:0")
+    s, a = p["cfg"]["s"], p["cfg"]["a"]
+    rng = np.random.default_rng(cid * 10 + B)
+    S0 = torch.from_numpy(np.stack([p["s0"]] + [rng.standard_normal(s).astype(np.float32) for _ in range(B - 1)]))
+    A0 = torch.from_numpy(rng.uniform(-1, 1, (B, H, a)).astype(np.float32))
+    iters, stop = 25, 0.002
+    ctx = _lib.option(mode, 1) if mode else _lib.option("gd_single", 0)
+    with ctx:
+        sb, ab, nb = gd.plan_fused_batch(S0, mdesc, cdesc, A0, H, iters, stop, dev)
+        singles = [gd.plan_fused(S0[b], mdesc, cdesc, list(A0[b].split(1, 0)), H, iters, stop, dev) for b in range(B)]
+    torch.cuda.synchronize()
+    for b, (s1, a1, n1) in enumerate(singles):
+        assert torch.equal(sb[b], s1) and torch.equal(ab[b], a1), b
+        assert int(nb[b]) == int(n1.item()), b
+    assert len({int(x) for x in nb.tolist()}) >= 1
+
+
+@pytest.mark.gpu
+def test_gd_planner_plan_batch_api():
+    """GradientDescentPlanner.plan_batch returns what B plan() calls return for the same start
+    states and the same sampler draws (the sampler is called in row order)."""
+    from mbrl_amd import GradientDescentPlanner
+    p, model_fn, cost_fn = closures(3, dict(W=64, L=2))
+    s, a, H, B = p["cfg"]["s"], p["cfg"]["a"], 6, 4
+    S0 = torch.from_numpy(np.random.default_rng(0).standard_normal((B, s)).astype(np.float32))
+
+    def sampler(batch_size):
+        return torch.rand((batch_size, a)) * 2 - 1
+    torch.manual_seed(7)
+    st, ac = GradientDescentPlanner.plan_batch(S0, model_fn, cost_fn, sampler, H, num_iterations=20, device="cuda:0")
+    torch.manual_seed(7)
+    for b in range(B):
+        s1, a1 = GradientDescentPlanner.plan(S0[b], model_fn, cost_fn, sampler, H, num_iterations=20, device="cuda:0")
+        assert torch.equal(st[b], torch.cat(s1, 0)) and torch.equal(ac[b], torch.cat(a1, 0)), b
+    assert st.shape == (B, H + 1, s) and ac.shape == (B, H, a)

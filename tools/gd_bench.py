@@ -41,6 +41,22 @@ def main():
             torch.cuda.synchronize()
             out[key] = (time.perf_counter() - t0) * 1e3 / reps
         out["gpu_ms_per_plan"] = out["gpu_fused_ms_per_plan"]
+        # B plans in shared launches (mbrl_gd_plan_batch): parallel environments, one start state each
+        rng = np.random.Generator(np.random.PCG64(7))
+        s0 = torch.as_tensor(np.asarray(prob["s0"], np.float32))
+        for B in (1, 4, 8, 16):
+            S0 = torch.stack([s0] + [s0 + torch.from_numpy(rng.normal(0, 0.1, s0.shape[0]).astype(np.float32))
+                                     for _ in range(B - 1)])
+            AB = torch.from_numpy(np.stack([A0] * B))
+            gd.plan_fused_batch(S0, md, cd, AB, H, iters, 0.0, dev)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(3):
+                gd.plan_fused_batch(S0, md, cd, AB, H, iters, 0.0, dev)
+            torch.cuda.synchronize()
+            ms = (time.perf_counter() - t0) * 1e3 / 3
+            out[f"gpu_batch{B}_ms"] = ms
+            out[f"gpu_batch{B}_plans_per_s"] = B / ms * 1e3
         out["speedup"] = out["cpu_ms_per_plan"] / out["gpu_ms_per_plan"]
     print(json.dumps(out))
 
