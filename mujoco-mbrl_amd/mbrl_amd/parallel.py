@@ -173,10 +173,11 @@ def _serve(policy, procs, req_q, conns, num_rollouts, on_batch, timeout):
     pending = {}                  # worker -> (rollout index, timestep, state, observation)
     results = [None] * num_rollouts
     copies = {}                   # rollout index -> its policy copy (planners without plan_batch)
+    last = {}                     # rollout index -> its previous plan (warm-starting planners)
     waited = 0.0
     while active:
         if pending and len(pending) == len(active):
-            _answer(policy, pending, conns, copies, on_batch)
+            _answer(policy, pending, conns, copies, on_batch, last)
             pending.clear()
             continue
         try:
@@ -203,15 +204,29 @@ def _serve(policy, procs, req_q, conns, num_rollouts, on_batch, timeout):
     return results
 
 
-def _answer(policy, pending, conns, copies, on_batch):
+def _answer(policy, pending, conns, copies, on_batch, last):
     """One planning round: every waiting worker's request, ordered by rollout index."""
     order = sorted(pending, key=lambda w: pending[w][0])
     indices = [pending[w][0] for w in order]
     obs = [torch.from_numpy(np.asarray(pending[w][3])) for w in order]
     plan_batch = getattr(policy.planner, "plan_batch", None)
     if plan_batch is not None:
-        _, actions = plan_batch(torch.stack(obs), policy.model, policy.cost, policy.sample_action, policy.horizon,
-                                **getattr(policy, "plan_kwargs", {}))
+        kw = dict(getattr(policy, "plan_kwargs", {}))
+        warm = getattr(policy.planner, "warm_starts", False)
+        if warm:
+            # what each rollout's own MPCPolicy.get_action would pass (agents.py:40-55): nothing at
+            # timestep 0, else (previous states[1:], previous actions[0:]) of the same rollout
+            inits = []
+            for w in order:
+                i, t = pending[w][0], pending[w][1]
+                prev = None if t == 0 else last.get(i)
+                inits.append(None if prev is None else (prev[0][1:], prev[1][0:]))
+            kw["initial_trajectories"] = inits
+        states, actions = plan_batch(torch.stack(obs), policy.model, policy.cost, policy.sample_action,
+                                     policy.horizon, **kw)
+        if warm:
+            for b, i in enumerate(indices):
+                last[i] = (list(states[b].split(1, 0)), list(actions[b].split(1, 0)))
         acts = [actions[b][0].flatten().detach().cpu() for b in range(len(order))]
     else:
         acts = []

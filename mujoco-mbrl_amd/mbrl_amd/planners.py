@@ -84,6 +84,9 @@ class GradientDescentPlanner(ModelPlanner):
     GPU for recognised closures (mbrl_amd/gd.py), else the reference's loop on the given callables.
     Returns lists of H+1 states [1, s] and H actions [1, a], as the reference does."""
     defaults = dict(num_iterations=40, stop_condition=0.002)
+    # plans start from the previous plan of the same episode (MPCPolicy's initial_trajectory,
+    # agents.py:40-55): the planner service passes those to plan_batch (parallel._answer)
+    warm_starts = True
 
     @staticmethod
     def plan(initial_state, model, cost, sample_action, horizon, initial_trajectory=None, **kwargs):
@@ -112,9 +115,9 @@ class GradientDescentPlanner(ModelPlanner):
     @staticmethod
     def plan_batch(initial_states, model, cost, sample_action, horizon, initial_trajectories=None, **kwargs):
         """B independent plans, one per row of initial_states [B, s] (parallel environments), each
-        what plan() returns for that row. Row b starts from initial_trajectories[b][1] or, without
-        them, from sample_action(batch_size=horizon) drawn for b = 0, 1, ... in order (as B plan()
-        calls would draw). Recognised closures run in shared launches (mbrl_gd_plan_batch: the
+        what plan() returns for that row. Row b starts from initial_trajectories[b][1] or, where that
+        (or the whole list) is None, from sample_action(batch_size=horizon), drawn in row order (as
+        B plan() calls would draw). Recognised closures run in shared launches (mbrl_gd_plan_batch: the
         cooperative grids of up to 256 / (Wpad / 16) plans at once); others run plan() per row.
         Returns (states [B, H+1, s], actions [B, H, a])."""
         from . import gd
@@ -123,10 +126,11 @@ class GradientDescentPlanner(ModelPlanner):
         H, B = int(horizon), int(initial_states.shape[0])
         starts = []
         for b in range(B):
-            if initial_trajectories is None:
+            init = None if initial_trajectories is None else initial_trajectories[b]
+            if init is None:
                 starts.append(torch.cat(list(sample_action(batch_size=H).split(1, dim=0)), 0))
             else:
-                starts.append(torch.cat([x.reshape(1, -1) for x in initial_trajectories[b][1]], 0))
+                starts.append(torch.cat([x.reshape(1, -1) for x in init[1]], 0))
         mdesc, cdesc = gd.describe(model, cost)
         keep = kwargs.get("return_device", False)
         if mdesc is not None and torch.cuda.is_available():

@@ -127,3 +127,27 @@ def test_a_dead_worker_is_reported():
     with pytest.raises(RuntimeError, match="died"):
         parallel.get_rollouts_parallel("linear", "run", True, 2, dict(num_steps=3), num_workers=2,
                                        env_factory=se.dying_env)
+
+
+@pytest.mark.gpu
+def test_gpu_planner_service_serves_gradient_descent_batches_with_warm_starts():
+    """GradientDescentPlanner through the service: one plan_batch (mbrl_gd_plan_batch) per lockstep
+    round, each row warm-started from its own rollout's previous plan exactly as its MPCPolicy would
+    (agents.py:40-55) -- the rollouts equal in-process rollouts with per-rollout MPCPolicy copies."""
+    from mbrl_amd import GradientDescentPlanner, data, fused, models
+    torch.manual_seed(0)
+    m = models.Model(5, 1, hidden_units=64, n_hidden=2)
+    ds = data.TransitionsDataset.from_statistics({"observations": {"mean": torch.zeros(5), "std": torch.ones(5)},
+                                                  "actions": {"mean": torch.zeros(1), "std": torch.ones(1)}})
+    cost = models.goal_state_cost(models.SmoothAbsLoss(torch.ones(5), torch.zeros(5)), models.CoshLoss())
+    model_fn = functools.partial(m, **ds.normalizers())
+    assert fused.describe_model(model_fn) is not None
+
+    def sample_action(batch_size):           # deterministic: the worker processes and the parent agree
+        return torch.linspace(-0.5, 0.5, batch_size).reshape(batch_size, 1)
+    pol = MPCPolicy(model_fn, cost, GradientDescentPlanner, sample_action, 6, num_iterations=15, device="cuda:0")
+    rs = parallel.get_rollouts_parallel("linear", "run", True, 3, dict(num_steps=4, get_action=pol.get_action),
+                                        num_workers=3, env_factory=se.make_env)
+    ref = _sequential("run", 3, pol, num_steps=4)
+    for r, q in zip(rs, ref):
+        _same(r, q)
