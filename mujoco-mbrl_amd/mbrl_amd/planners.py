@@ -186,6 +186,46 @@ class RandomShootingPlanner(ModelPlanner):
             return _to_host(out_states, keep), _to_host(out_actions, keep)
 
 
+    @staticmethod
+    def plan_batch(initial_states, model, cost, sample_action, horizon, **kwargs):
+        """B plans, one per row of initial_states [B, s] (parallel environments), each what plan()
+        returns for that row: row b's N x H proposals are the b-th sample_action(batch_size=N*H)
+        draw (row order, as B plan() calls would draw). Recognised closures roll all B*N candidates
+        out in one launch (per-candidate start states), then take each row's np.argmin.
+        Returns (states [B, H, s], actions [B, H, a])."""
+        kw = dict(kwargs)
+        N = int(kw.pop("num_trajectories", RandomShootingPlanner.defaults["num_trajectories"]))
+        H, B = int(horizon), int(initial_states.shape[0])
+        keep = kw.get("return_device", False)
+        dev = _device(kw)
+        draws = [sample_action(batch_size=N * H) for _ in range(B)]
+        a = draws[0].shape[1]
+        with torch.cuda.device(dev):
+            mdesc = fused.describe_model(model)
+            cdesc = fused.describe_cost(cost, mdesc["s"], mdesc) if mdesc is not None else None
+            if mdesc is None or cdesc is None or mdesc["E"] != 1 or mdesc["a"] != a:
+                outs = []
+                for b in range(B):
+                    it = iter([draws[b]])
+                    outs.append(RandomShootingPlanner._plan(initial_states[b], model, cost,
+                                                            lambda batch_size: next(it), H, None, N,
+                                                            **dict(kw, return_device=True)))
+                return (_to_host(torch.stack([o[0] for o in outs]), keep),
+                        _to_host(torch.stack([o[1] for o in outs]), keep))
+            prob = fused.device_problem(mdesc, cdesc, dev, _lib.precision_code(kw.get("precision", "f32")))
+            acts = torch.cat([d.to(device=dev, dtype=torch.float32).reshape(H, N, a) for d in draws], 1).contiguous()
+            s0 = initial_states.to(device=dev, dtype=torch.float32).reshape(B, 1, -1).expand(B, N, -1)
+            s0 = s0.reshape(B * N, -1).contiguous()
+            states = torch.empty((1, H, B * N, mdesc["s"]), dtype=torch.float32, device=dev)
+            costs = fused.rollout(prob, s0, B * N, H, actions=acts, s0_per_candidate=True, states_out=states)
+            best = torch.stack([fused.select(costs[:, b * N:(b + 1) * N].contiguous(), 1,
+                                             nan_policy=_lib.MBRL_NAN_FIRST)[0] for b in range(B)])  # np.argmin
+            cols = best + torch.arange(B, device=dev) * N
+            out_states = states[0][:, cols].transpose(0, 1)
+            out_actions = acts[:, cols].transpose(0, 1)
+            return _to_host(out_states.contiguous(), keep), _to_host(out_actions.contiguous(), keep)
+
+
 class CEMPlanner(ModelPlanner):
     """Cross-entropy method over action sequences (not in the reference).
 

@@ -188,3 +188,4 @@ def test_gd_planner_plan_batch_api():
         s1, a1 = GradientDescentPlanner.plan(S0[b], model_fn, cost_fn, sampler, H, num_iterations=20, device="cuda:0")
         assert torch.equal(st[b], torch.cat(s1, 0)) and torch.equal(ac[b], torch.cat(a1, 0)), b
     assert st.shape == (B, H + 1, s) and ac.shape == (B, H, a)
+
