@@ -256,9 +256,10 @@ def _train_loop(model, dataset, optimizer, batch_size, num_epochs, step_loss, wr
                     writer.add_scalar(tag.format(model.train_iterations), val, num_iters)
                 if n_parts > 1:
                     writer.add_scalar("loss/total/{}".format(model.train_iterations), loss, num_iters)
-    if graph is not None or native is not None:
+    if graph is not None:
         for p in model.parameters():      # release the graph-pool grads; the eager path re-allocates
             p.grad = None
+    # (the native path leaves the last batch's gradients in .grad, as the reference's loop does)
     model.train_iterations += 1
 
 

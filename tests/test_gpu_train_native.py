@@ -151,3 +151,22 @@ def test_epoch_call_equals_per_batch_calls(kind, monkeypatch):
     for (ka, ma, va), (kb, mb, vb) in zip(sa, sb):
         assert ka == kb and torch.equal(ma, mb) and torch.equal(va, vb)
     assert ra == rb and len(ra) > 0
+
+
+def test_native_training_leaves_the_last_batch_gradient():
+    """After train_model, every .grad holds the last batch's gradient, as after the reference's loop
+    (zero_grad, backward, step per batch)."""
+    from mbrl_amd import models
+    ds = _dataset(7, 2, 1, 300, seed=4)
+    m = _model("model", 7, 2, 32, 2, seed=2)
+    opt = torch.optim.SGD(m.parameters(), lr=0.0)          # lr 0: the weights stay put
+    np.random.seed(6)
+    m.train_model(ds, opt, batch_size=64, num_epochs=1)
+    got = [p.grad.clone() for p in m.parameters()]
+    np.random.seed(6)
+    order = models._epoch_order(ds)
+    last = torch.from_numpy(order[(len(order) - 1) // 64 * 64:]).to(DEV)
+    _, ins, outs = ds.stacked(DEV)
+    _, ref, _ = _autograd(m, ds, ins, outs, last, False)
+    for x, y in zip(got, ref):
+        assert torch.allclose(x, y, rtol=1e-4, atol=1e-4 * float(y.abs().max()) + 1e-12)
