@@ -7,8 +7,8 @@ include/mbrl_cem.h). See DESIGN.md and INTEGRATION.md at the repository root.
 from . import agents, data, env, env_wrappers, gd, models, parallel, planners  # noqa: F401
 from .agents import MPCPolicy  # noqa: F401
 from .env_wrappers import EnvWrapper  # noqa: F401
-from .models import (CoshLoss, DynamicsModel, EnsembleModel, Model, ModelWithReward, SmoothAbsLoss,  # noqa: F401
-                     compose, goal_state_cost, state_action_cost)
+from .models import (CoshLoss, CostModel, DynamicsModel, EnsembleModel, LinearModel, Model,  # noqa: F401
+                     ModelWithReward, QuadraticCost, SmoothAbsLoss, compose, goal_state_cost, state_action_cost)
 from .planners import CEMPlanner, GradientDescentPlanner, ModelPlanner, RandomShootingPlanner  # noqa: F401
 
 

@@ -81,7 +81,7 @@ def _linear_layers(module):
         m0 = module.members[0]
         return members, m0.n_hidden, m0.hidden_units, m0.state_dim, m0.action_dim
     if isinstance(module, Model):
-        if module.noise is not None:
+        if module.noise is not None or module.n_hidden < 1:
             return None
         return [module.linears()], module.n_hidden, module.hidden_units, module.state_dim, module.action_dim
     names = [n for n in ("linear1", "linear2", "linear3") if isinstance(getattr(module, n, None), torch.nn.Linear)]

@@ -343,6 +343,22 @@ class Model(DynamicsModel):
         return x if self.noise is None else x + torch.randn_like(x) * self.noise
 
 
+class LinearModel(DynamicsModel):
+    """models.py:113-122: one Linear from (s, a) to s, plus optional Gaussian noise (experiment.py:41's
+    "lin" model). The fused kernels need a hidden layer, so the planners run this model through its
+    callable and train_model through autograd."""
+
+    def __init__(self, state_dim, action_dim, noise=None):
+        super().__init__()
+        self.state_dim, self.action_dim = state_dim, action_dim
+        self.linear1 = nn.Linear(state_dim + action_dim, state_dim)
+        self.noise = noise
+
+    def _forward(self, x):
+        x = self.linear1(x)
+        return x if self.noise is None else x + torch.randn_like(x) * self.noise
+
+
 class EnsembleModel(DynamicsModel):
     """PETS-style ensemble of E `Model`s (not in the reference; BASELINE.json config 5).
 
@@ -425,6 +441,23 @@ class ModelWithReward(nn.Module):
         return state, reward
 
 
+class CostModel(nn.Module):
+    """models.py:220-234: a learned cost of (state, action), two ReLU layers and a scalar head."""
+
+    def __init__(self, state_dim, action_dim, hidden_units=70):
+        super().__init__()
+        self.linear1 = nn.Linear(state_dim + action_dim, hidden_units)
+        self.linear2 = nn.Linear(hidden_units, hidden_units)
+        self.linear3 = nn.Linear(hidden_units, 1)
+        self.activation_fn = nn.ReLU()
+
+    def forward(self, state, action):
+        x = torch.cat((state, action), -1)
+        x = self.activation_fn(self.linear1(x))
+        x = self.activation_fn(self.linear2(x))
+        return self.linear3(x)
+
+
 class StateCost(nn.Module):
     goal_state = None
 
@@ -444,6 +477,21 @@ class SmoothAbsLoss(StateCost):
     def forward(self, x):
         x = x - self.goal_state
         return torch.sum(torch.sqrt((x * self.weights) ** 2 + self.alpha ** 2) - self.alpha, dim=-1)
+
+
+class QuadraticCost(StateCost):
+    """models.py:275-288: (x - g) . L(x - g) with a learned Linear L on the state. The reference's
+    forward reads `self.goalState`, an attribute it never sets, so it raises AttributeError; this
+    restatement computes what the code spells out with the goal it stores (`goal_state`)."""
+
+    def __init__(self, dim, goal_state):
+        super().__init__()
+        self.linear = nn.Linear(dim, dim)
+        self.goal_state = goal_state
+
+    def forward(self, x):
+        d = x - self.goal_state
+        return torch.dot(d, self.linear(d))
 
 
 class CoshLoss(nn.Module):
