@@ -538,6 +538,54 @@ def test_sharded_plan_two_processes_on_one_gpu():
         assert np.allclose(g["states"], ref["states"].numpy(), rtol=1e-5, atol=1e-5)
 
 
+def _rccl_worker(rank, world, init_file, out_dir):
+    import os
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [repo, os.path.join(repo, "mujoco-mbrl_amd")]
+    import torch.distributed as dist
+    from mbrl_amd import CEMPlanner, fused, planners
+    from oracle import cem as oc
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    try:
+        assert dist.get_backend() == "nccl"
+        p = oc.synth_problem(3, N=1024, H=8)
+        _, model_fn, cost_fn, sample_action = build(p)
+        dev = torch.device("cuda", 0)
+        md = fused.describe_model(model_fn)
+        prob = fused.device_problem(md, fused.describe_cost(cost_fn, md["s"], md), dev)
+        st = CEMPlanner._settings(sample_action, 8, dict(num_candidates=1024, num_iterations=3, seed=p["rng_seed"],
+                                                         record=True))
+        s0 = torch.from_numpy(p["s0"]).to(dev)
+        res = planners._cem_fused_sharded(prob, s0, st, world)   # every iteration all-gathers over RCCL
+        np.savez(os.path.join(out_dir, f"r{rank}.npz"), mu=res["mu"].cpu().numpy(), sigma=res["sigma"].cpu().numpy(),
+                 elites=torch.stack(list(res["elites"])).cpu().numpy(), actions=res["actions"].cpu().numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_plan_over_rccl():
+    """The sharded plan's device-memory all-gather through RCCL (torch.distributed backend "nccl", the
+    multi-GPU path's collective) with a one-rank process group on this GPU -- RCCL refuses two ranks
+    on one device, so the 2-8 rank runs are the driver's 8-GPU node's -- bit-identical to the
+    single-process plan."""
+    import tempfile
+    import torch.multiprocessing as mp
+    from mbrl_amd import CEMPlanner
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_rccl_worker, args=(1, os.path.join(d, "pg"), d), nprocs=1, join=True,
+                           start_method="spawn")
+        g = dict(np.load(os.path.join(d, "r0.npz")))
+    p = ocem.synth_problem(3, N=1024, H=8)
+    _, model_fn, cost_fn, sample_action = build(p)
+    ref = CEMPlanner.plan_detailed(torch.from_numpy(p["s0"]), model_fn, cost_fn, sample_action, 8,
+                                   num_candidates=1024, num_iterations=3, seed=p["rng_seed"], record=True)
+    assert np.array_equal(g["elites"], torch.stack(list(ref["elites"])).cpu().numpy())
+    assert np.array_equal(g["mu"], ref["mu"].cpu().numpy()) and np.array_equal(g["sigma"], ref["sigma"].cpu().numpy())
+    assert np.array_equal(g["actions"], ref["actions"].numpy())
+
+
 @pytest.mark.parametrize("cid,N,H,B", [(2, 1024, 20, 4), (3, 512, 6, 3), (6, 256, 5, 2), (5, 128, 4, 2)])
 def test_batched_plans_match_per_problem_oracle(cid, N, H, B):
     """mbrl_cem_plan_batch: problem b == a single CEM plan whose proposals are candidates
