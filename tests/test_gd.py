@@ -189,3 +189,30 @@ def test_gd_planner_plan_batch_api():
         assert torch.equal(st[b], torch.cat(s1, 0)) and torch.equal(ac[b], torch.cat(a1, 0)), b
     assert st.shape == (B, H + 1, s) and ac.shape == (B, H, a)
 
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", range(12))
+def test_gd_fused_random_shapes_match_graph_path(case):
+    """mbrl_gd_plan at random shapes (the cooperative kernel where it applies, the one-workgroup kernel
+    elsewhere) against the graph-replayed torch restatement, within the float tolerance."""
+    from mbrl_amd import gd
+    rng = np.random.default_rng(9000 + case)
+    reward = case % 3 == 2
+    over = dict(s=int(rng.integers(1, 24)), a=int(rng.integers(1, 8)),
+                W=int(rng.choice([16, 50, 64, 100, 128, 256, 512])), L=int(rng.integers(1, 4)))
+    p = ocem.synth_problem(6 if reward else 3, **over)
+    import test_gpu_parity as tg
+    _, model_fn, cost_fn, _ = tg.build(p)
+    mdesc, cdesc = gd.describe(model_fn, cost_fn)
+    dev = torch.device("cuda:0")
+    assert gd.fused_supported(mdesc, cdesc, dev)
+    H, iters = int(rng.integers(1, 16)), int(rng.integers(0, 30))
+    A0 = rng.uniform(-0.5, 0.5, (H, over["a"])).astype(np.float32)
+    acts = [torch.from_numpy(A0[i:i + 1].copy()) for i in range(H)]
+    s0 = torch.from_numpy(p["s0"])
+    s1, a1, _ = gd.plan_fused(s0, mdesc, cdesc, acts, H, iters, 0.0, dev)
+    s2, a2 = gd.plan_device(s0, mdesc, cdesc, acts, H, iters, 0.0, dev, use_fused=False)
+    torch.cuda.synchronize()
+    assert torch.allclose(a1, a2, rtol=1e-4, atol=1e-5), (over, H, iters, float((a1 - a2).abs().max()))
+    assert torch.allclose(s1, s2, rtol=1e-4, atol=1e-4), (over, H, iters, float((s1 - s2).abs().max()))

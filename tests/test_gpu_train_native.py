@@ -170,3 +170,31 @@ def test_native_training_leaves_the_last_batch_gradient():
     _, ref, _ = _autograd(m, ds, ins, outs, last, False)
     for x, y in zip(got, ref):
         assert torch.allclose(x, y, rtol=1e-4, atol=1e-4 * float(y.abs().max()) + 1e-12)
+
+
+@pytest.mark.parametrize("case", range(24))
+def test_native_gradients_random_shapes(case):
+    """mbrl_train_grads at random shapes (dims, widths off the tile grid, depth, horizon, batch sizes
+    that leave partial row tiles, both model kinds) against autograd on the same batch."""
+    from mbrl_amd import models
+    rng = np.random.default_rng(5000 + case)
+    kind = "reward" if case % 4 == 3 else "model"
+    s, a = int(rng.integers(1, 40)), int(rng.integers(1, 12))
+    W = int(rng.choice([1, 7, 16, 31, 64, 97, 128, 200, 256, 333]))
+    L = int(rng.integers(1, 5))
+    H = int(rng.integers(1, 4))
+    B = int(rng.choice([1, 3, 32, 33, 100, 257]))
+    ds = _dataset(s, a, H, max(3 * B, 40), seed=case)
+    m = _model(kind, s, a, W, L, seed=case)
+    _, ins, outs = ds.stacked(DEV)
+    reward = kind == "reward"
+    g = torch.Generator().manual_seed(case)
+    idx = torch.randperm(ds.num_transitions(), generator=g)[:B].to(DEV)
+    ref_loss, ref_grads, _ = _autograd(m, ds, ins, outs, idx, reward)
+    nat = models._NativeGrads(m, ins, outs, ds.horizon, B, reward)
+    loss, _ = nat.run(idx)
+    torch.cuda.synchronize()
+    for i, (x, y) in enumerate(zip([p.grad for p in m.parameters()], ref_grads)):
+        scale = float(y.abs().max())
+        assert torch.allclose(x, y, rtol=1e-4, atol=1e-4 * scale + 1e-12), (i, s, a, W, L, H, B)
+    assert abs(float(loss) - float(ref_loss)) <= 1e-5 * abs(float(ref_loss)) + 1e-12
