@@ -205,6 +205,14 @@ def _train_loop(model, dataset, optimizer, batch_size, num_epochs, step_loss, wr
     on a GPU the full-size batches replay one captured graph (_GraphStep), and a plain Adam steps
     through mbrl_adam_step (optim.AdamStep: one launch, torch's arithmetic bit for bit)."""
     dev = _device_of(model)
+    if dev.type == "cuda":
+        with torch.cuda.device(dev):       # launches and workspaces on the model's GPU
+            return _train_loop_on(dev, model, dataset, optimizer, batch_size, num_epochs, step_loss, writer, tags,
+                                  criterion)
+    return _train_loop_on(dev, model, dataset, optimizer, batch_size, num_epochs, step_loss, writer, tags, criterion)
+
+
+def _train_loop_on(dev, model, dataset, optimizer, batch_size, num_epochs, step_loss, writer, tags, criterion):
     _, ins, outs = dataset.stacked(dev)
     n_parts = len(tags)
     graph = native = None
