@@ -213,6 +213,9 @@ def _train_loop(model, dataset, optimizer, batch_size, num_epochs, step_loss, wr
 
 
 def _train_loop_on(dev, model, dataset, optimizer, batch_size, num_epochs, step_loss, writer, tags, criterion):
+    if dataset.num_transitions() == 0:    # the reference's DataLoader yields no batch
+        model.train_iterations += 1
+        return
     _, ins, outs = dataset.stacked(dev)
     n_parts = len(tags)
     graph = native = None
@@ -293,6 +296,8 @@ class DynamicsModel(nn.Module):
         """models.py:30-51: one criterion value per batch and horizon step."""
         criterion = criterion or torch.nn.MSELoss()
         dev = _device_of(self)
+        if dataset.num_transitions() == 0:
+            return []
         _, ins, outs = dataset.stacked(dev)
         evals = []
         with torch.no_grad():

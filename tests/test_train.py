@@ -110,3 +110,19 @@ def test_train_model_on_gpu_matches_reference(golden, name):
         assert np.allclose(w, rw, rtol=1e-4, atol=1e-5) and np.allclose(b, rb, rtol=1e-4, atol=1e-5)
     if before is not None:
         assert abs(before - g["eval_before"]) < 1e-5 and abs(after - g["eval_after"]) < 1e-5
+
+
+def test_train_model_on_an_empty_dataset_takes_no_step():
+    """Rollouts shorter than the horizon leave no transition: the reference's DataLoader yields no
+    batch, so the weights stay put and train_iterations still counts the call."""
+    from mbrl_amd import data, models
+    rolls = [data.Rollout(states=[torch.zeros(3)] * 2, observations=[torch.zeros(3)] * 2,
+                          actions=[torch.zeros(1)], rewards=[torch.tensor(0.0)])]
+    ds = data.TransitionsDataset(rollouts=rolls, horizon=2, normalise=False)
+    ds.set_data_mode("state_only")
+    assert ds.num_transitions() == 0
+    m = models.Model(3, 1, hidden_units=8)
+    before = [p.detach().clone() for p in m.parameters()]
+    m.train_model(ds, torch.optim.Adam(m.parameters()), batch_size=4, num_epochs=2)
+    assert all(torch.equal(a, b) for a, b in zip(before, m.parameters())) and m.train_iterations == 1
+    assert m.evaluate_model(ds, batch_size=4) == []
