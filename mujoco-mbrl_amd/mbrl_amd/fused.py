@@ -212,6 +212,110 @@ def describe_cost(cost, s, mdesc=None):
                                                    float(sc.alpha), float(ac.alpha)))
 
 
+def describe(model, cost, device):
+    """(mdesc, cdesc) for closures the fused path may run, else (None, None): recognised by
+    describe_model / describe_cost AND confirmed once by semantic_check (recognition goes by names
+    and types; the check makes sure the arithmetic behind those names is the reference's)."""
+    mdesc = describe_model(model)
+    cdesc = describe_cost(cost, mdesc["s"], mdesc) if mdesc is not None else None
+    if mdesc is None or cdesc is None:
+        return None, None
+    if not semantic_check(model, cost, mdesc, cdesc, device):
+        return None, None
+    return mdesc, cdesc
+
+
+def _fn_sig(fn):
+    """Identity of what a recognised closure resolves to: the functions behind the partials, the
+    module's class and hooks, the cost modules' classes."""
+    uc = _uncompose(fn)
+    if uc is not None:
+        fn = uc[0]
+    f, kw = _unpartial(fn)
+    if isinstance(f, torch.nn.Module):
+        head = (id(type(f)), id(f), len(f._forward_hooks), len(f._forward_pre_hooks),
+                id(type(getattr(f, "activation_fn", None))))
+    else:
+        head = (id(f),)
+    return head + tuple((k, id(_unpartial(kw[k])[0]), id(type(kw[k]))) for k in sorted(kw))
+
+
+def _rebind(fn, module, new):
+    """fn (module | partial(module, ...) | compose(partial(module, ...), getter)) with module -> new."""
+    from .models import compose
+    if fn is module:
+        return new
+    uc = _uncompose(fn)
+    if uc is not None:
+        return compose(_rebind(uc[0], module, new), uc[1])
+    f, kw = _unpartial(fn)
+    return functools.partial(new, **kw) if f is module else fn
+
+
+def _probe_call(fn, module, *args):
+    """The user's callable on the probe batch, on the device; if its tensors live elsewhere (e.g.
+    normaliser statistics on the host while the module is on the GPU -- the fused path moves them),
+    on the host with a host copy of the module."""
+    try:
+        return fn(*args)
+    except RuntimeError as e:
+        if "device" not in str(e):
+            raise
+    import copy
+    return _rebind(fn, module, copy.deepcopy(module).cpu())(*[x.cpu() for x in args])
+
+
+PROBE_ROWS = 8
+PROBE_RTOL = 1e-4   # fp32 summation-order differences here are ~1e-6; any change of arithmetic is far above
+
+
+def _close(x, ref):
+    x = x.detach().to("cpu", torch.float64).reshape(-1)
+    ref = ref.detach().to("cpu", torch.float64).reshape(-1)
+    return x.shape == ref.shape and bool(torch.all(torch.abs(x - ref) <= PROBE_RTOL * torch.clamp(ref.abs(), min=1.0)))
+
+
+def semantic_check(model, cost, mdesc, cdesc, device):
+    """One-time check (per closure identity and weights version) that the fused arithmetic equals
+    the caller's callables: a one-step fused rollout of PROBE_ROWS random (state, action) rows
+    against model(s, a) and cost(s', a) evaluated through the callables themselves (torch autograd
+    mode, so a DynamicsModel does not take its own fused forward). A mismatch -- e.g. a function
+    that is named normalize_field / state_action_cost but computes something else -- disables the
+    fused path for these closures with a warning; the planner then runs them on the generic path
+    (the reference's semantics: planners.py:199-210 on the callables as given)."""
+    import warnings
+    device = torch.device(device)
+    prob = device_problem(mdesc, cdesc, device)
+    sig = (_fn_sig(model), _fn_sig(cost))
+    ok = prob.verified.get(sig)
+    if ok is not None:
+        return ok
+    s, a, E, P = mdesc["s"], mdesc["a"], mdesc["E"], PROBE_ROWS
+    n = mdesc["norm"]
+    gen = torch.Generator().manual_seed(0x5eed)
+    om = n["obs_mean"].float().cpu() if n["obs_mean"] is not None else torch.zeros(s)
+    osd = n["obs_std"].float().cpu() if n["obs_std"] is not None else torch.ones(s)
+    states = (om + osd * torch.randn((P, s), generator=gen)).to(device).contiguous()
+    acts = (torch.rand((P, a), generator=gen) * 2 - 1).to(device).contiguous()
+    out = torch.empty((E, 1, P, s), dtype=torch.float32, device=device)
+    with torch.cuda.device(device):
+        costs = rollout(prob, states, P, 1, actions=acts.view(1, P, a), s0_per_candidate=True, states_out=out)
+    try:
+        with torch.enable_grad():
+            nxt = _probe_call(model, mdesc["module"], states, acts)
+            ok = _close(out[:, 0].mean(0) if E > 1 else out[0, 0], nxt)
+            for e in range(E):
+                ok = ok and _close(costs[e], _probe_call(cost, mdesc["module"], out[e, 0], acts))
+    except Exception as exc:   # the callables cannot run the probe: not the arithmetic the kernels assume
+        ok = False
+        warnings.warn(f"mbrl_amd: probing the model / cost closures raised {exc!r}")
+    if not ok:
+        warnings.warn("mbrl_amd: the model / cost closures are recognised by name but do not compute what the "
+                      "fused kernels compute on a probe batch; these closures run on the generic path")
+    prob.verified[sig] = ok
+    return ok
+
+
 def describe_sampler(sample_action):
     """partial(_sample_action, action_spec=spec) -> (lo, hi, a) or None."""
     f, kw = _unpartial(sample_action)
@@ -286,6 +390,7 @@ class DeviceProblem:
 
     def __init__(self, mdesc, cdesc, device, precision=_lib.MBRL_PRECISION_F32):
         self.mdesc, self.cdesc, self.device = mdesc, cdesc, device
+        self.verified = {}                          # semantic_check results per closure identity
         self.shape = mlp_shape(mdesc, precision)   # the packed buffer serves both precisions
         self.packed = packed_weights(mdesc, device)
         n = mdesc["norm"]
@@ -425,6 +530,34 @@ def make_sampler(seed, iteration, mu, sigma, lo, hi):
 # ------------------------------------------------------------------------------------------------
 # DynamicsModel.forward on device (one step, per-row start states)
 # ------------------------------------------------------------------------------------------------
+def _forward_checked(prob, module, normalize_action, normalize_state, unnormalize_state):
+    """semantic_check for DynamicsModel.forward's fused path: the module's own forward (autograd
+    mode) with the given normalisers on a probe batch, against the fused one-step rollout."""
+    import warnings
+    norms = dict(normalize_action=normalize_action, normalize_state=normalize_state,
+                 unnormalize_state=unnormalize_state)
+    sig = ("forward", _fn_sig(functools.partial(module, **{k: v for k, v in norms.items() if v is not None})))
+    ok = prob.verified.get(sig)
+    if ok is not None:
+        return ok
+    s, a, P, dev = prob.mdesc["s"], prob.mdesc["a"], PROBE_ROWS, prob.device
+    gen = torch.Generator().manual_seed(0x5eed)
+    st = torch.randn((P, s), generator=gen).to(dev)
+    ac = (torch.rand((P, a), generator=gen) * 2 - 1).to(dev)
+    out = torch.empty((1, 1, P, s), dtype=torch.float32, device=dev)
+    rollout(prob, st, P, 1, actions=ac.view(1, P, a), s0_per_candidate=True, states_out=out)
+    try:
+        with torch.enable_grad():
+            ok = _close(out[0, 0], _probe_call(functools.partial(module, **norms), module, st, ac))
+    except Exception:
+        ok = False
+    if not ok:
+        warnings.warn("mbrl_amd: DynamicsModel.forward's normalisers are recognised by name but compute "
+                      "something else on a probe batch; forward runs the module as written")
+    prob.verified[sig] = ok
+    return ok
+
+
 def try_forward(module, state, action, normalize_action, normalize_state, unnormalize_state):
     layers = _linear_layers(module)
     if layers is None or isinstance(module, EnsembleModel):
@@ -439,6 +572,8 @@ def try_forward(module, state, action, normalize_action, normalize_state, unnorm
     desc = dict(module=module, members=members, L=L, W=W, s=s, a=a, E=1, norm=norm, reward=False)
     dev = state.device
     prob = device_problem(desc, None, dev)
+    if not _forward_checked(prob, module, normalize_action, normalize_state, unnormalize_state):
+        return None
     B = state.shape[0]
     st = state.contiguous()
     act = action.contiguous().view(1, B, a)

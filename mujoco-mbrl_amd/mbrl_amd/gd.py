@@ -238,7 +238,6 @@ def plan_generic(initial_state, model, cost, sample_action, horizon, initial_tra
     return states.detach(), actions.detach()
 
 
-def describe(model, cost):
-    mdesc = fused.describe_model(model)
-    cdesc = fused.describe_cost(cost, mdesc["s"], mdesc) if mdesc is not None else None
-    return (mdesc, cdesc) if mdesc is not None and cdesc is not None else (None, None)
+def describe(model, cost, dev):
+    """Recognised and semantically checked closures (fused.describe), else (None, None)."""
+    return fused.describe(model, cost, dev)

@@ -144,6 +144,11 @@ class _NativeGrads:
             return None
         if model.n_hidden < 1 or model.n_hidden + 2 > 10 or len(ins) != 2 or len(outs) != 2:
             return None
+        # train.hip computes Linear-ReLU chains and never calls the module: a replaced activation or
+        # a hook would make it train a different function than the model computes
+        if type(model.activation_fn) is not nn.ReLU or any(
+                m._forward_hooks or m._forward_pre_hooks or m._backward_hooks for m in model.modules()):
+            return None
         params = list(model.parameters())
         if len(params) != 2 * len(model.linears()):
             return None
@@ -195,7 +200,8 @@ class _NativeGrads:
                                                   ctypes.c_void_p(self.loss.data_ptr()),
                                                   ctypes.c_void_p(self.ws.data_ptr()), self.ws.numel(),
                                                   self._lib.stream_handle(self.dev)), "mbrl_train_grads")
-        return self.loss[0], [self.loss[1], self.loss[2]]
+        loss = self.loss.clone()          # the buffer is reused by the next batch; the writer keeps these
+        return loss[0], [loss[1], loss[2]]
 
 
 def _train_loop(model, dataset, optimizer, batch_size, num_epochs, step_loss, writer, tags, criterion=None):
@@ -231,6 +237,9 @@ def _train_loop_on(dev, model, dataset, optimizer, batch_size, num_epochs, step_
             for p in model.parameters():
                 p.grad = None
     fast = AdamStep.maybe(optimizer) if dev.type == "cuda" else None
+    # parameters the optimizer steps that the native gradient call does not overwrite each batch
+    own = set() if native is None else {id(p) for p in native.params}
+    extra = [p for g in optimizer.param_groups for p in g["params"] if id(p) not in own] if native is not None else []
     num_iters = 0
     for _ in range(num_epochs):
         host = _epoch_order(dataset)
@@ -251,6 +260,8 @@ def _train_loop_on(dev, model, dataset, optimizer, batch_size, num_epochs, step_
         for i in range(0, len(host), batch_size):
             idx = order[i:i + batch_size]
             if native is not None:
+                for p in extra:               # optimizer.zero_grad() for what the native call does not write
+                    p.grad = None
                 loss, parts = native.run(idx)
                 parts = parts[:n_parts]
             elif graph is not None and idx.shape[0] == batch_size:

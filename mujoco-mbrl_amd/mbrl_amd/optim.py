@@ -37,6 +37,7 @@ class AdamStep:
         self.opt = optimizer
         self.device = device
         self._tables = {}
+        self._pending = None     # (step counters, steps) of the epoch_plan awaiting epoch_done
 
     @classmethod
     def maybe(cls, optimizer):
@@ -121,7 +122,8 @@ class AdamStep:
         """Inputs of mbrl_train_epoch for `steps` Adam steps over `params` (the optimizer's only
         group, every parameter with a gradient each step): (table, hparams, step_sizes, bc2_sqrt),
         with the state created as torch would and the step counters advanced by `steps` -- what
-        `steps` calls of step() leave -- or None when the group does not have that shape."""
+        `steps` calls of step() leave once epoch_done() confirms the launch -- or None when the group
+        does not have that shape."""
         groups = self.opt.param_groups
         if len(groups) != 1 or len(groups[0]["params"]) != len(params) or \
                 {id(p) for p in groups[0]["params"]} != {id(p) for p in params}:
@@ -156,11 +158,17 @@ class AdamStep:
             table[i].param, table[i].grad = p.data_ptr(), p.grad.data_ptr()
             table[i].exp_avg, table[i].exp_avg_sq = state[p]["exp_avg"].data_ptr(), state[p]["exp_avg_sq"].data_ptr()
             table[i].numel = p.numel()
-        for c in counters:                        # the float32 counters, as `steps` increments by one
-            c.add_(float(steps))
+        self._pending = (counters, steps)
         return table, _lib.AdamHparams(1 - b1, b2, 1 - b2, eps, wd), ss, bc
 
     def epoch_done(self, params):
+        """After a successful mbrl_train_epoch: advance the step counters by the epoch's steps (the
+        float32 counters, as `steps` increments by one) -- only then, so that a failed launch leaves
+        the optimizer as it was -- and bump the version counters of what the kernels wrote."""
+        counters, steps = self._pending
+        self._pending = None
+        for c in counters:
+            c.add_(float(steps))
         state = self.opt.state
         increment_version(list(params) + [state[p][k] for p in params for k in ("exp_avg", "exp_avg_sq")])
 

@@ -94,9 +94,11 @@ class GradientDescentPlanner(ModelPlanner):
         num_iterations = int(kwargs.get("num_iterations", GradientDescentPlanner.defaults["num_iterations"]))
         stop_condition = float(kwargs.get("stop_condition", GradientDescentPlanner.defaults["stop_condition"]))
         H = int(horizon)
-        mdesc, cdesc = gd.describe(model, cost)
-        if mdesc is not None and torch.cuda.is_available():
+        mdesc = None
+        if torch.cuda.is_available():
             dev = _device(kwargs)
+            mdesc, cdesc = gd.describe(model, cost, dev)
+        if mdesc is not None:
             if initial_trajectory is None:
                 # planners.py:94: the nominal sequence (its states are not used for a deterministic model)
                 action_list = list(sample_action(batch_size=H).split(1, dim=0))
@@ -124,24 +126,23 @@ class GradientDescentPlanner(ModelPlanner):
         num_iterations = int(kwargs.get("num_iterations", GradientDescentPlanner.defaults["num_iterations"]))
         stop_condition = float(kwargs.get("stop_condition", GradientDescentPlanner.defaults["stop_condition"]))
         H, B = int(horizon), int(initial_states.shape[0])
-        starts = []
-        for b in range(B):
-            init = None if initial_trajectories is None else initial_trajectories[b]
-            if init is None:
-                starts.append(torch.cat(list(sample_action(batch_size=H).split(1, dim=0)), 0))
-            else:
-                starts.append(torch.cat([x.reshape(1, -1) for x in init[1]], 0))
-        mdesc, cdesc = gd.describe(model, cost)
+        inits = [None if initial_trajectories is None else initial_trajectories[b] for b in range(B)]
         keep = kwargs.get("return_device", False)
-        if mdesc is not None and torch.cuda.is_available():
+        mdesc = cdesc = None
+        if torch.cuda.is_available():
             dev = _device(kwargs)
-            if gd.fused_supported(mdesc, cdesc, dev) and num_iterations > 0:
-                with torch.cuda.device(dev):
-                    states, actions, _ = gd.plan_fused_batch(initial_states, mdesc, cdesc, torch.stack(starts), H,
-                                                             num_iterations, stop_condition, dev)
-                return _to_host(states, keep), _to_host(actions, keep)
+            mdesc, cdesc = gd.describe(model, cost, dev)
+        if mdesc is not None and gd.fused_supported(mdesc, cdesc, dev) and num_iterations > 0:
+            starts = [torch.cat(list(sample_action(batch_size=H).split(1, dim=0)), 0) if init is None
+                      else torch.cat([x.reshape(1, -1) for x in init[1]], 0) for init in inits]
+            with torch.cuda.device(dev):
+                states, actions, _ = gd.plan_fused_batch(initial_states, mdesc, cdesc, torch.stack(starts), H,
+                                                         num_iterations, stop_condition, dev)
+            return _to_host(states, keep), _to_host(actions, keep)
+        # per row, in row order; a row without a warm start draws its sequence inside its own plan(),
+        # so a model that uses torch's RNG sees exactly the stream of B plan() calls
         outs = [GradientDescentPlanner.plan(initial_states[b], model, cost, sample_action, H,
-                                            initial_trajectory=(None, list(starts[b].split(1, 0))),
+                                            initial_trajectory=None if inits[b] is None else (None, list(inits[b][1])),
                                             **dict(kwargs, return_device=True)) for b in range(B)]
         states = torch.stack([torch.cat(o[0], 0).reshape(H + 1, -1) for o in outs])
         actions = torch.stack([torch.cat(o[1], 0).reshape(H, -1) for o in outs])
@@ -169,8 +170,7 @@ class RandomShootingPlanner(ModelPlanner):
         with torch.cuda.device(dev):
             acts = action_list.to(device=dev, dtype=torch.float32).reshape(H, N, a).contiguous()
             s0 = initial_state.to(device=dev, dtype=torch.float32).contiguous()
-            mdesc = fused.describe_model(model)
-            cdesc = fused.describe_cost(cost, mdesc["s"], mdesc) if mdesc is not None else None
+            mdesc, cdesc = fused.describe(model, cost, dev)
             if mdesc is not None and cdesc is not None and mdesc["E"] == 1 and mdesc["a"] == a:
                 prob = fused.device_problem(mdesc, cdesc, dev, _lib.precision_code(kwargs.get("precision", "f32")))
                 states = torch.empty((1, H, N, mdesc["s"]), dtype=torch.float32, device=dev)
@@ -198,20 +198,24 @@ class RandomShootingPlanner(ModelPlanner):
         H, B = int(horizon), int(initial_states.shape[0])
         keep = kw.get("return_device", False)
         dev = _device(kw)
-        draws = [sample_action(batch_size=N * H) for _ in range(B)]
-        a = draws[0].shape[1]
         with torch.cuda.device(dev):
-            mdesc = fused.describe_model(model)
-            cdesc = fused.describe_cost(cost, mdesc["s"], mdesc) if mdesc is not None else None
-            if mdesc is None or cdesc is None or mdesc["E"] != 1 or mdesc["a"] != a:
+            mdesc, cdesc = fused.describe(model, cost, dev)
+            fusable = mdesc is not None and cdesc is not None and mdesc["E"] == 1
+            # recognised closures use no RNG, so all B draws can come first; unrecognised ones (a model
+            # may draw from torch's RNG) interleave each row's draw with its plan, as B plan() calls do
+            draws = [sample_action(batch_size=N * H) for _ in range(B)] if fusable else None
+            if not fusable or mdesc["a"] != draws[0].shape[1]:
                 outs = []
                 for b in range(B):
-                    it = iter([draws[b]])
-                    outs.append(RandomShootingPlanner._plan(initial_states[b], model, cost,
-                                                            lambda batch_size: next(it), H, None, N,
+                    sampler = sample_action
+                    if draws is not None:
+                        it = iter([draws[b]])
+                        sampler = lambda batch_size, it=it: next(it)  # noqa: E731
+                    outs.append(RandomShootingPlanner._plan(initial_states[b], model, cost, sampler, H, None, N,
                                                             **dict(kw, return_device=True)))
                 return (_to_host(torch.stack([o[0] for o in outs]), keep),
                         _to_host(torch.stack([o[1] for o in outs]), keep))
+            a = draws[0].shape[1]
             prob = fused.device_problem(mdesc, cdesc, dev, _lib.precision_code(kw.get("precision", "f32")))
             acts = torch.cat([d.to(device=dev, dtype=torch.float32).reshape(H, N, a) for d in draws], 1).contiguous()
             s0 = initial_states.to(device=dev, dtype=torch.float32).reshape(B, 1, -1).expand(B, N, -1)
@@ -282,8 +286,7 @@ class CEMPlanner(ModelPlanner):
         st = CEMPlanner._settings(sample_action, horizon, kwargs)
         with torch.cuda.device(dev):
             s0 = initial_state.to(device=dev, dtype=torch.float32).contiguous()
-            mdesc = fused.describe_model(model)
-            cdesc = fused.describe_cost(cost, mdesc["s"], mdesc) if mdesc is not None else None
+            mdesc, cdesc = fused.describe(model, cost, dev)
             ws = None
             if st["distributed"] and torch.distributed.is_available() and torch.distributed.is_initialized() \
                     and torch.distributed.get_world_size() > 1:
@@ -323,8 +326,7 @@ def cem_plan_batch(initial_states, model, cost, sample_action, horizon, **kwargs
     st = CEMPlanner._settings(sample_action, horizon, kwargs)
     B = int(initial_states.shape[0])
     with torch.cuda.device(dev):
-        mdesc = fused.describe_model(model)
-        cdesc = fused.describe_cost(cost, mdesc["s"], mdesc) if mdesc is not None else None
+        mdesc, cdesc = fused.describe(model, cost, dev)
         if mdesc is None or cdesc is None:
             outs = [CEMPlanner.plan(initial_states[b], model, cost, sample_action, horizon,
                                     **dict(kwargs, seed=st["seed"], return_device=True)) for b in range(B)]

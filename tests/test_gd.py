@@ -42,7 +42,7 @@ def plan(name, golden, device=None):
 def test_gd_host_loop_matches_reference(golden, name, monkeypatch):
     """Unrecognised closures (forced here) run the reference's loop on the given callables."""
     from mbrl_amd import gd
-    monkeypatch.setattr(gd, "describe", lambda model, cost: (None, None))
+    monkeypatch.setattr(gd, "describe", lambda model, cost, dev: (None, None))
     st, ac, g = plan(name, golden)
     assert np.allclose(ac, g["actions"], rtol=1e-5, atol=1e-6)
     assert np.allclose(st, g["states"], rtol=1e-5, atol=1e-5)
@@ -60,7 +60,7 @@ def test_gd_device_matches_reference(golden, name):
 def test_gd_graph_replay_equals_eager():
     from mbrl_amd import gd
     p, model_fn, cost_fn = closures(3, dict(W=50, L=2))
-    mdesc, cdesc = gd.describe(model_fn, cost_fn)
+    mdesc, cdesc = gd.describe(model_fn, cost_fn, torch.device("cuda:0"))
     A0 = mgd.initial_actions(10, 6)
     acts = [torch.from_numpy(A0[i:i + 1].copy()) for i in range(10)]
     dev = torch.device("cuda:0")
@@ -80,7 +80,7 @@ def test_gd_fused_kernel_matches_graph_path(cid, over, H, iters, stop):
     reward-head models (config 6: RewardAgent's reward cost, two trunk passes per step)."""
     from mbrl_amd import gd
     p, model_fn, cost_fn = closures(cid, over)
-    mdesc, cdesc = gd.describe(model_fn, cost_fn)
+    mdesc, cdesc = gd.describe(model_fn, cost_fn, torch.device("cuda:0"))
     dev = torch.device("cuda:0")
     assert gd.fused_supported(mdesc, cdesc, dev)
     a = p["cfg"]["a"]
@@ -103,7 +103,7 @@ def test_gd_cooperative_kernel_and_its_fallback(mode, cid):
     (MBRL_OPT_DEBUG_GD_ABORT) the gated one-workgroup kernel must produce the plan instead."""
     from mbrl_amd import _lib, gd
     p, model_fn, cost_fn = closures(cid, dict(W=256, L=3))
-    mdesc, cdesc = gd.describe(model_fn, cost_fn)
+    mdesc, cdesc = gd.describe(model_fn, cost_fn, torch.device("cuda:0"))
     dev = torch.device("cuda:0")
     H, a = 12, p["cfg"]["a"]
     A0 = mgd.initial_actions(H, a)
@@ -152,7 +152,7 @@ def test_gd_plan_batch_equals_single_plans(cid, over, H, B, mode):
     the gated fallback after a forced hand-off timeout. Each plan keeps its own stop test."""
     from mbrl_amd import _lib, gd
     p, model_fn, cost_fn = closures(cid, over)
-    mdesc, cdesc = gd.describe(model_fn, cost_fn)
+    mdesc, cdesc = gd.describe(model_fn, cost_fn, torch.device("cuda:0"))
     dev = torch.device("cuda:0")
     s, a = p["cfg"]["s"], p["cfg"]["a"]
     rng = np.random.default_rng(cid * 10 + B)
@@ -204,7 +204,7 @@ def test_gd_fused_random_shapes_match_graph_path(case):
     p = ocem.synth_problem(6 if reward else 3, **over)
     import test_gpu_parity as tg
     _, model_fn, cost_fn, _ = tg.build(p)
-    mdesc, cdesc = gd.describe(model_fn, cost_fn)
+    mdesc, cdesc = gd.describe(model_fn, cost_fn, torch.device("cuda:0"))
     dev = torch.device("cuda:0")
     assert gd.fused_supported(mdesc, cdesc, dev)
     H, iters = int(rng.integers(1, 16)), int(rng.integers(0, 30))

@@ -247,6 +247,71 @@ def test_random_shooting_toy_known_answer(golden):
     assert float(torch.abs(states - 9).sum()) == 18.0
 
 
+def _impostors():
+    """Functions that carry the names closure recognition goes by (fused._field_stats,
+    describe_cost) but compute something else (VERDICT r02 weak #8)."""
+    def normalize_field(field_value, field_name, stats):
+        return (field_value - stats[field_name]["mean"]) / stats[field_name]["std"] * 0.5
+
+    def state_action_cost(state, action, state_cost, action_cost):
+        return state_cost(state) + 2.0 * action_cost(action)
+    return normalize_field, state_action_cost
+
+
+def test_semantic_check_sends_impostor_closures_to_the_generic_path():
+    """A one-time probe (fused.semantic_check) compares the fused arithmetic with the callables; a
+    same-named impostor normaliser or cost is caught and the planner runs the callables as given
+    (the reference's semantics), with a warning. Genuine closures keep the fused path."""
+    from mbrl_amd import CEMPlanner, fused
+    p = ocem.synth_problem(2, N=256, H=6)
+    module, model_fn, cost_fn, sample_action = build(p)
+    assert fused.describe(model_fn, cost_fn, torch.device(DEV))[0] is not None
+    imp_norm, imp_cost = _impostors()
+    kw = dict(model_fn.keywords)
+    kw["normalize_state"] = functools.partial(imp_norm, **kw["normalize_state"].keywords)
+    bad_model = functools.partial(model_fn.func, **kw)
+    bad_cost = functools.partial(imp_cost, **cost_fn.keywords)
+    for m, c in ((bad_model, cost_fn), (model_fn, bad_cost)):
+        assert fused.describe_model(m) is not None and fused.describe_cost(c, 5, fused.describe_model(m)) is not None
+        with pytest.warns(UserWarning, match="generic path"):
+            md, cd = fused.describe(m, c, torch.device(DEV))
+        assert md is None and cd is None
+        opts = dict(num_candidates=256, num_iterations=2, seed=9, record=True)
+        got = CEMPlanner.plan_detailed(torch.from_numpy(p["s0"]), m, c, sample_action, 6, **opts)
+        opaque = CEMPlanner.plan_detailed(torch.from_numpy(p["s0"]), lambda s, a: m(s, a), lambda s, a: c(s, a),
+                                          sample_action, 6, **opts)
+        assert torch.equal(got["returns"], opaque["returns"]) and torch.equal(got["elites"], opaque["elites"])
+    # the verdict is cached per closure identity and weights version: no second probe
+    assert fused.describe(bad_model, cost_fn, torch.device(DEV))[0] is None
+    assert fused.describe(model_fn, cost_fn, torch.device(DEV))[0] is not None
+
+
+def test_semantic_check_guards_dynamics_forward():
+    """DynamicsModel.forward's fused path runs only after its normalisers pass the probe."""
+    from mbrl_amd import fused
+    p = ocem.synth_problem(4)
+    module, model_fn, _, _ = build(p)
+    imp_norm, _ = _impostors()
+    kw = dict(model_fn.keywords)
+    st = kw["normalize_action"].keywords["stats"]
+    dev_stats = {k: {q: torch.as_tensor(v[q]).to(DEV) for q in ("mean", "std")} for k, v in st.items()}
+    kw["normalize_action"] = functools.partial(imp_norm, field_name="actions", stats=dev_stats)
+    rng = np.random.default_rng(3)
+    s = torch.from_numpy(rng.standard_normal((64, 24)).astype(np.float32)).to(DEV)
+    a = torch.from_numpy(rng.uniform(-1, 1, (64, 6)).astype(np.float32)).to(DEV)
+    with pytest.warns(UserWarning, match="normalisers"):
+        with torch.no_grad():
+            got = module(s, a, **kw)
+    with torch.enable_grad():
+        want = module(s, a, **kw).detach()
+    assert torch.equal(got, want)
+    with torch.no_grad():
+        ok = model_fn(s, a)
+    assert fused._PACKED.get(module) is not None
+    assert np.allclose(ok.cpu().numpy(), ocem.dynamics_step(p["model"][0], p["norm"], s.cpu().numpy(), a.cpu().numpy()),
+                       rtol=1e-5, atol=1e-5)
+
+
 def test_cem_generic_path_matches_fused():
     """Opaque callables (generic path) and recognised closures (fused path) agree on the elite sets."""
     from mbrl_amd import CEMPlanner
@@ -296,7 +361,7 @@ def test_full_size_plan_sampled_candidates(cid):
 
 
 # ------------------------------------------------------------------------------------------------ full sizes vs the reference
-FULL_CASES = [("config4_cem_full", 4), ("config5_cem_full", 5)]
+FULL_CASES = [("config4_cem_full", 4), ("config5_cem_full", 5), ("config6_cem_full", 6)]
 
 
 def elite_diff_at_ties(got, ref_elites, ref_returns, K, tie_rel):
@@ -354,9 +419,104 @@ def test_full_size_iterations_against_reference_golden(golden, name, cid, capsys
     _, model_fn, cost_fn, sample_action = build(p)
     res = CEMPlanner.plan_detailed(torch.from_numpy(p["s0"]), model_fn, cost_fn, sample_action, H,
                                    num_candidates=N, num_iterations=I, seed=p["rng_seed"], record=True)
-    same = [bool(np.array_equal(res["elites"][it].cpu().numpy(), g["elites"][it])) for it in range(I)]
+    fr = free_running_against_reference(prob, s0, p, g, res, acts)
     with capsys.disabled():
-        print(f"\n{name}: " + "; ".join(lines) + f"; free-running plan elites identical per iteration: {same}")
+        print(f"\n{name}: " + "; ".join(lines))
+        for ln in fr["lines"]:
+            print(f"  free-running {ln}")
+    if cid in (4, 6):
+        # walker, and the cheetah reward head: the reference's K-boundary gaps exceed the GEMM-order
+        # error at every iteration, so the free-running plan is the reference's plan bit for bit
+        assert fr["swaps"] == [0] * I
+        assert np.array_equal(res["mu"].cpu().numpy(), g["mu"][-1])
+        assert np.array_equal(res["sigma"].cpu().numpy(), g["sigma"][-1])
+        assert np.array_equal(res["actions"].numpy(), g["final_actions"])
+
+
+def free_running_against_reference(prob, s0, p, g, res, acts):
+    """The free-running plan (no teacher forcing) against the reference's, with the drift that
+    boundary swaps can cause derived and ASSERTED (the one relaxation of bit-exact
+    elites). Iteration i starts from the plan's own mu^G, sigma^G and the reference's mu^R, sigma^R,
+    with measured drifts Dmu = |mu^G - mu^R| and Dsigma (per element [t, j]):
+      * proposals share their normal draws eps (same Philox counters), and clip is 1-Lipschitz, so
+        |a^G_n - a^R_n| <= Dmu + Dsigma |eps_n|;
+      * elites: both sets are exact stable top-K, so with delta = max_n |r^G_n - r^R_n| every
+        candidate in exactly one set has a reference return within 2 delta (+ 5e-7 relative ties)
+        of the reference's K-th return -- asserted; s = |G xor R| / 2 swaps;
+      * elite mean over K: |Dmean| <= Dmu + Dsigma e + s (hi - lo) / K, e = the mean |eps| over the
+        candidates in both sets; mu' = alpha mu + (1 - alpha) mean, so
+        |Dmu'| <= alpha Dmu + (1 - alpha) Dmean;
+      * population variance (E a^2 - mean^2, |a| <= M = max(|lo|, |hi|)):
+        |Dvar| <= 2 M (Dmu + Dsigma e) + s M^2 / K + 2 M Dmean; sigma'^2 = alpha sigma^2 + (1 - alpha) var,
+        so X := |D sigma'^2| <= alpha |D sigma^2| + (1 - alpha) Dvar, and
+        |Dsigma'| <= min(sqrt(X), X / (sigma'^G + sigma'^R));
+      * fp32 rounding: nothing when every input is bit-identical (then so are the outputs), else
+        2 (32 + K / 32 + 8) ulp(M) for the chunked refit sums.
+    Each iteration's measured drift is asserted against the bound from its measured inputs; the same
+    recurrences fed with the swap counts alone give an a-priori bound, compounded over the I
+    iterations, that the final actions clip(mu) must respect (|Daction| <= |Dmu_I|)."""
+    from mbrl_amd import fused
+    N, H, K, I = int(g["N"]), int(g["H"]), int(g["K"]), int(g["I"])
+    a = p["cfg"]["a"]
+    alpha, lo, hi = 0.1, -1.0, 1.0
+    M = max(abs(lo), abs(hi))
+    ulp = float(np.finfo(np.float32).eps) * M
+    zero = torch.zeros((H, a), dtype=torch.float32, device=DEV)
+    one = torch.ones((H, a), dtype=torch.float32, device=DEV)
+    mu = np.zeros((H, a), np.float32)
+    sg = np.full((H, a), 0.5, np.float32)
+    mu_r, sg_r = mu.astype(np.float64), sg.astype(np.float64)     # the reference's, entering iteration it
+    c_mu, c_sq, c_sg = np.zeros((H, a)), np.zeros((H, a)), np.zeros((H, a))   # a-priori (swaps only)
+    swaps, lines = [], []
+
+    def step_bound(dmu, dsg, dsq, e, s, any_diff, sg_new_sum):
+        rnd = 2 * (32 + K / 32 + 8) * ulp if any_diff else 0.0
+        dmean = dmu + dsg * e + s * (hi - lo) / K
+        dvar = 2 * M * (dmu + dsg * e) + s * M * M / K + 2 * M * dmean
+        b_mu = alpha * dmu + (1 - alpha) * dmean + rnd
+        x = alpha * dsq + (1 - alpha) * dvar + rnd
+        b_sg = np.minimum(np.sqrt(x), x / sg_new_sum) + rnd
+        return b_mu, x, b_sg
+
+    for it in range(I):
+        mu_d, sg_d = torch.from_numpy(mu).to(DEV), torch.from_numpy(sg).to(DEV)   # the sampler holds their pointers
+        sp = fused.make_sampler(p["rng_seed"], it, mu_d, sg_d, lo, hi)
+        costs = fused.rollout(prob, s0, N, H, sampler=sp, actions_out=acts)
+        ret = torch.empty(N, dtype=torch.float32, device=DEV)
+        el = fused.select(costs, K, returns_out=ret).cpu().numpy()
+        assert np.array_equal(el, res["elites"][it].cpu().numpy()), "step-by-step plan != CEMPlanner plan"
+        mo = torch.empty((H, a), dtype=torch.float32, device=DEV)
+        so = torch.empty((H, a), dtype=torch.float32, device=DEV)
+        fused.refit(sp, H, a, torch.from_numpy(el).to(DEV), alpha, mo, so)
+        ref_el = g["elites"][it].astype(np.int64)
+        rG, rR = ret.cpu().numpy().astype(np.float64), g["returns"][it].astype(np.float64)
+        delta = float(np.max(np.abs(rG - rR)))
+        kth = float(rR[np.argsort(g["returns"][it], kind="stable")[K - 1]])
+        diff = np.setxor1d(el, ref_el)
+        assert np.all(np.abs(rR[diff] - kth) <= 2 * delta + 5e-7 * max(abs(kth), 1.0)), \
+            f"iteration {it}: elite swaps away from the K boundary"
+        s = len(diff) // 2
+        swaps.append(s)
+        common = torch.from_numpy(np.intersect1d(el, ref_el)).to(DEV)
+        fused.sample_actions(fused.make_sampler(p["rng_seed"], it, zero, one, -3.0e38, 3.0e38), H, a, N, 0, acts)
+        e = acts.index_select(1, common).abs().double().mean(dim=1).cpu().numpy()      # [H, a]
+        mu_g, sg_g = mu.astype(np.float64), sg.astype(np.float64)
+        dmu, dsg, dsq = np.abs(mu_g - mu_r), np.abs(sg_g - sg_r), np.abs(sg_g ** 2 - sg_r ** 2)
+        mu, sg = mo.cpu().numpy(), so.cpu().numpy()
+        mu_r, sg_r = g["mu"][it].astype(np.float64), g["sigma"][it].astype(np.float64)
+        sg_sum = sg.astype(np.float64) + sg_r
+        b_mu, _, b_sg = step_bound(dmu, dsg, dsq, e, s, bool(dmu.any() or dsg.any() or s), sg_sum)
+        got_mu, got_sg = np.abs(mu - mu_r), np.abs(sg - sg_r)
+        assert np.all(got_mu <= b_mu), f"iteration {it}: |Dmu| {got_mu.max():.3e} above its bound"
+        assert np.all(got_sg <= b_sg), f"iteration {it}: |Dsigma| {got_sg.max():.3e} above its bound"
+        c_mu, c_sq, c_sg = step_bound(c_mu, c_sg, c_sq, e, s, bool(c_mu.any() or c_sg.any() or s), sg_sum)
+        lines.append(f"it {it}: swaps {s}, max|r^G - r^R| {delta:.2e}, |Dmu| {got_mu.max():.2e} "
+                     f"(bound {b_mu.max():.2e}), |Dsigma| {got_sg.max():.2e} (bound {b_sg.max():.2e})")
+    assert np.array_equal(mu, res["mu"].cpu().numpy()) and np.array_equal(sg, res["sigma"].cpu().numpy())
+    d_act = np.abs(res["actions"].numpy().astype(np.float64) - g["final_actions"])
+    assert np.all(d_act <= c_mu), f"final actions drift {d_act.max():.3e} beyond the a-priori bound"
+    lines.append(f"final: max|Daction| {d_act.max():.3e} <= a-priori bound {c_mu.max():.3e} from swaps {swaps}")
+    return dict(swaps=swaps, lines=lines)
 
 
 # ------------------------------------------------------------------------------------------------ trajectory / sharding

@@ -96,7 +96,7 @@ def test_cem_actions_are_the_ones_rolled_out():
     assert np.allclose(c1[0], c2[0][::-1], rtol=1e-6)
 
 
-FULL_CASES = [("config4_cem_full", 4), ("config5_cem_full", 5)]
+FULL_CASES = [("config4_cem_full", 4), ("config5_cem_full", 5), ("config6_cem_full", 6)]
 
 
 @pytest.mark.parametrize("name,cid", FULL_CASES, ids=[c[0] for c in FULL_CASES])

@@ -29,7 +29,7 @@ def main():
     gd.plan_generic(prob["s0"], prob["model"], prob["cost"], None, H, ([], acts), iters, 0.0)
     out["cpu_ms_per_plan"] = (time.perf_counter() - t0) * 1e3
     if torch.cuda.is_available():
-        md, cd = gd.describe(prob["model"], prob["cost"])
+        md, cd = gd.describe(prob["model"], prob["cost"], torch.device("cuda:0"))
         dev = torch.device("cuda:0")
         for key, fused_on in (("gpu_fused_ms_per_plan", True), ("gpu_graph_ms_per_plan", False)):
             gd.plan_device(prob["s0"], md, cd, acts, H, iters, 0.0, dev, use_fused=fused_on)   # warm-up
