@@ -1068,6 +1068,9 @@ static int rollout_impl(const Geometry& g, const void* packed, const mbrl_norm* 
             return hip_check(launch_rollout(X, g.T, RS, stream), "split redo launch");
         }
     }
+    // ensembles: member-major workgroup order per XCD (mbrl_internal.h xcd_unit), so that an XCD's
+    // L2 streams the weights of one or two members (humanoid: 5 x 2.4 MB would not fit its 4 MB)
+    A.xcd_map = (g.E > 1 && g_opt[MBRL_OPT_NO_XCD_MAP].load(std::memory_order_relaxed) == 0) ? 1 : 0;
     // 8-candidate tiles (rollout_m8_kernel, bit-identical sums) when 16-candidate tiles would leave
     // at least half the CUs idle: the shard of a strong-scaled plan, small plans.
     // MBRL_OPT_ROLLOUT_TILE = 8 / 16 forces a choice (tests, A/B).

@@ -135,7 +135,27 @@ struct RolloutArgs {
     // 16-candidate kernel, L odd >= 3, no reward head: the output partials live in the activation
     // buffer the last hidden layer does not read (act2), so 32-candidate tiles of wide states fit LDS
     int part_alias;
+    // ensembles (E > 1): a 1-D grid of ntiles * E workgroups whose ids map member-major onto the 8
+    // XCDs (xcd_unit), so each XCD's L2 holds the weights of one or two members instead of all E
+    int xcd_map;
 };
+
+// Workgroup -> (tile, member). Dispatch places workgroup w on XCD w % 8 (round robin), so XCD k runs
+// ids k, k + 8, k + 16, ... in that order; xcd_map hands XCD k the contiguous unit range
+// [k q + min(k, r), ...) of the member-major order unit = e * ntiles + tile (q = total / 8,
+// r = total % 8): a bijection, and every XCD streams at most ceil(E / 8) + 1 members' weights.
+__device__ __forceinline__ void xcd_unit(int xcd_map, int ntiles, int& tile, int& e) {
+    if (!xcd_map) {
+        tile = blockIdx.x;
+        e = blockIdx.y;
+        return;
+    }
+    const int total = gridDim.x, q = total >> 3, r = total & 7;
+    const int k = blockIdx.x & 7, slot = blockIdx.x >> 3;
+    const int unit = k * q + (k < r ? k : r) + slot;
+    e = unit / ntiles;
+    tile = unit - e * ntiles;
+}
 
 // F16X3 operand scales (exact powers of two): activations and weights are scaled before the f16
 // split so that their residual pieces stay normal; products carry X_SCALE * W_SCALE.

@@ -306,7 +306,9 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const LdsMap L = lds_map(A, smem, M);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int tile = blockIdx.x, e = blockIdx.y;
+    const int ntiles = (A.N + M - 1) / M;
+    int tile, e;
+    xcd_unit(A.xcd_map, ntiles, tile, e);
     if (A.redo) {
         // F16X3 redo pass (rollout_f16x3.hip): run only where the split kernel left MBRL_REDO_MARK
         bool any = false;
@@ -604,7 +606,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
 #ifdef MBRL_STAMPS
     seg[NSEG - 1] = __builtin_amdgcn_s_memrealtime() - rt0;
     if (lane == 0 && g_mbrl_stamps != nullptr) {
-        unsigned long long* dst = g_mbrl_stamps + (((size_t)e * gridDim.x + tile) * NW + wave) * NSEG;
+        unsigned long long* dst = g_mbrl_stamps + (((size_t)e * ntiles + tile) * NW + wave) * NSEG;
 #pragma unroll
         for (int k = 0; k < NSEG; ++k) dst[k] = seg[k];
     }
@@ -623,7 +625,8 @@ static hipError_t launch_rollout_tr(const RolloutArgs& A_in, hipStream_t stream)
     RolloutArgs A = A_in;
     A.nw = NW;
     const int M = 16 * R;
-    dim3 grid((A.N + M - 1) / M, A.E);
+    const int ntiles = (A.N + M - 1) / M;
+    const dim3 grid = A.xcd_map ? dim3(ntiles * A.E) : dim3(ntiles, A.E);
     const size_t lds = rollout_lds_bytes(A, M);
     hipError_t e = ensure_dynamic_lds(reinterpret_cast<const void*>(&rollout_kernel<T, R, K0C_T, NOT_T, NW>),
                                       160 * 1024);
@@ -726,7 +729,9 @@ __global__ void __launch_bounds__(64 * m8_waves(T, NOT_T), 1) rollout_m8_kernel(
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const LdsMap L = lds_map(A, smem, M);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int tile = blockIdx.x, e = blockIdx.y;
+    const int ntiles = (A.N + M - 1) / M;
+    int tile, e;
+    xcd_unit(A.xcd_map, ntiles, tile, e);
     const float* member = A.packed + (size_t)e * A.member_stride;
     float* const actX = L.act;
     float* const actY = L.act2;
@@ -1064,7 +1069,7 @@ __global__ void __launch_bounds__(64 * m8_waves(T, NOT_T), 1) rollout_m8_kernel(
 #ifdef MBRL_STAMPS
     seg[NSEG - 1] = __builtin_amdgcn_s_memrealtime() - rt0;
     if (lane == 0 && g_mbrl_stamps != nullptr) {
-        unsigned long long* dst = g_mbrl_stamps + (((size_t)e * gridDim.x + tile) * 8 + wave) * NSEG;
+        unsigned long long* dst = g_mbrl_stamps + (((size_t)e * ntiles + tile) * 8 + wave) * NSEG;
 #pragma unroll
         for (int k = 0; k < NSEG; ++k) dst[k] = seg[k];
     }
@@ -1087,7 +1092,7 @@ template <int T, int K0C_T, int NOT_T, int K0L = 0>
 static hipError_t launch_m8_tr(const RolloutArgs& A_in, hipStream_t stream) {
     RolloutArgs A = A_in;
     A.nw = 8;   // output partials: the 8-wave kernel's count
-    dim3 grid((A.N + 7) / 8, A.E);
+    const dim3 grid = A.xcd_map ? dim3((A.N + 7) / 8 * A.E) : dim3((A.N + 7) / 8, A.E);
     const size_t lds = rollout_lds_bytes(A, 8);
     const auto fn = &rollout_m8_kernel<T, K0C_T, NOT_T, K0L>;
     hipError_t e = ensure_dynamic_lds(reinterpret_cast<const void*>(fn), 160 * 1024);

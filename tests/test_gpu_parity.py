@@ -291,11 +291,15 @@ def test_semantic_check_guards_dynamics_forward():
     from mbrl_amd import fused
     p = ocem.synth_problem(4)
     module, model_fn, _, _ = build(p)
+    module.to(DEV)                      # the module's own forward runs once the probe fails
     imp_norm, _ = _impostors()
-    kw = dict(model_fn.keywords)
-    st = kw["normalize_action"].keywords["stats"]
-    dev_stats = {k: {q: torch.as_tensor(v[q]).to(DEV) for q in ("mean", "std")} for k, v in st.items()}
-    kw["normalize_action"] = functools.partial(imp_norm, field_name="actions", stats=dev_stats)
+    # every normaliser on device statistics (the module's own forward runs once the probe fails)
+    kw = {}
+    for k, f in model_fn.keywords.items():
+        st = f.keywords["stats"]
+        dev_stats = {n: {q: torch.as_tensor(v[q]).to(DEV) for q in ("mean", "std")} for n, v in st.items()}
+        kw[k] = functools.partial(imp_norm if k == "normalize_action" else f.func, field_name=f.keywords["field_name"],
+                                  stats=dev_stats)
     rng = np.random.default_rng(3)
     s = torch.from_numpy(rng.standard_normal((64, 24)).astype(np.float32)).to(DEV)
     a = torch.from_numpy(rng.uniform(-1, 1, (64, 6)).astype(np.float32)).to(DEV)

@@ -36,7 +36,8 @@ def main():
     for _ in range(10):
         CEMPlanner.plan(p["s0"], p["model"], p["cost"], p["sample_action"], cfg["H"], **kw)
     torch.cuda.synchronize()
-    for mod, name in ((fused, "describe_model"), (fused, "describe_cost"), (fused, "device_problem"),
+    for mod, name in ((fused, "describe"), (fused, "semantic_check"), (fused, "describe_model"),
+                      (fused, "describe_cost"), (fused, "device_problem"),
                       (fused, "describe_sampler"), (planners, "_cem_fused_single")):
         timed(mod, name)
     lib = _lib.load()
