@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MBRL_ABI_VERSION 6
+#define MBRL_ABI_VERSION 7
 
 typedef struct ihipStream_t* mbrl_stream_t; /* == hipStream_t */
 typedef struct ihipEvent_t* mbrl_event_t;   /* == hipEvent_t  */
@@ -147,7 +147,7 @@ const char* mbrl_last_error(void);
  * cannot be redirected by a stray variable. mbrl_set_option returns the previous value, or
  * MBRL_EINVAL for an unknown option or value. Not part of any reference interface. */
 enum {
-    MBRL_OPT_ROLLOUT_TILE = 0,      /* fp32 rollout candidates per workgroup: 0 auto, 8, 16 (16 R)   */
+    MBRL_OPT_ROLLOUT_TILE = 0,      /* fp32 rollout candidates per workgroup: 0 auto, 4, 8, 16 (16 R) */
     MBRL_OPT_SPLIT_TILE = 1,        /* F16X3 / F16X6 rollout candidates per workgroup: 0 auto, 16, 32 */
     MBRL_OPT_DEBUG_TRAJ_ABORT = 2,  /* 1: the cooperative trajectory kernel gives up at once          */
     MBRL_OPT_GD_SINGLE = 3,         /* 1: mbrl_gd_plan runs its one-workgroup kernel                  */
@@ -159,6 +159,14 @@ enum {
 };
 int mbrl_set_option(int32_t option, int32_t value);
 int mbrl_get_option(int32_t option);
+
+/* ---- host staging: mapped, coherent pinned host memory (hipHostMalloc Mapped | Coherent) that the
+ * kernels read and write directly. plan() (planners.py:14-25) takes its initial state from the host and
+ * returns host tensors; passing mbrl_cem_plan a staged s0 and staged outputs replaces the two
+ * host<->device copies around the plan with the plan's own first and last launches. *device_ptr is
+ * the address kernels use (the same as *host_ptr under unified addressing). */
+int mbrl_host_alloc(size_t bytes, void** host_ptr, void** device_ptr);
+int mbrl_host_free(void* host_ptr);
 
 /* ---- model upload: replaces the per-call nn.Linear weight reads of Model._forward (models.py:106-110) */
 size_t mbrl_mlp_packed_bytes(const mbrl_mlp_shape* shape);

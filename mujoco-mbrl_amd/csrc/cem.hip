@@ -207,6 +207,25 @@ __global__ void pack_m8_out_kernel(const float* __restrict__ w, int in_real, int
     }
 }
 
+// 4-candidate output chunks (rollout_m4_kernel): chunk kc of wave w's own 64 features; float4 s =
+// output group g, element q: row n = 16 g + 4 (l >> 4) + (l & 3), k = 64 w + 16 kc + 4 q + chain,
+// chain = (l >> 2) & 3 -- the canonical output chains of the 16-candidate kernel (mma_out).
+__global__ void pack_m4_out_kernel(const float* __restrict__ w, int in_real, int out_real, int T,
+                                   float* __restrict__ dst) {
+    const size_t total = (size_t)4 * T * 1024;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const int q = (int)(i & 3);
+        const int lane = (int)((i >> 2) & 63);
+        const int grp = (int)((i >> 8) & 3);
+        const size_t cw = i >> 10;            // kc * T + wave
+        const int wave = (int)(cw % T);
+        const int kc = (int)(cw / T);
+        const int n = 16 * grp + 4 * (lane >> 4) + (lane & 3);
+        const int k = 64 * wave + 16 * kc + 4 * q + ((lane >> 2) & 3);
+        dst[i] = (n < out_real && k < in_real) ? w[(size_t)n * in_real + k] : 0.0f;
+    }
+}
+
 // Split streams (rollout_f16x3.hip): chunk = 32 K rows; per chunk 8 waves x (T/2 tiles x P pieces)
 // fragments of 64 lanes x 8 halves. Fragment f of a hidden-type chunk = tile f / P, piece f % P.
 // Lane l, element q: row n = 16 (wave T/2 + tile) + (l & 15), k = 32 kc + 8 (l >> 4) + q.
@@ -874,12 +893,18 @@ __global__ void __launch_bounds__(1024) cem_update_kernel(const UpdateArgs U) {
 // The plan's first launch: workgroup (t * S + j, b) sets row t of problem b's distribution to
 // (init_mu, init_sigma) and, with `actions`, draws row t of iteration 0's proposals for candidate
 // slice j (fill2_kernel + sample_kernel, bit-identical: the same floats go into cem_action).
+// s0_src (optional): the plan's start state, device or mapped host memory, copied once into the
+// workspace (s0_dst) so that every later launch reads device memory.
 __global__ void __launch_bounds__(1024) cem_init_kernel(uint64_t seed, float init_mu, float init_sigma, float lo,
                                                         float hi, int H, int a, int N, float* __restrict__ mu,
-                                                        float* __restrict__ sigma, float* __restrict__ actions) {
+                                                        float* __restrict__ sigma, float* __restrict__ actions,
+                                                        const float* __restrict__ s0_src, int s,
+                                                        float* __restrict__ s0_dst) {
     const int S = gridDim.x / H;
     const int t = blockIdx.x / S, j = blockIdx.x - (blockIdx.x / S) * S, b = blockIdx.y;
     const size_t ro = ((size_t)b * H + t) * a;
+    if (s0_src && blockIdx.x == 0 && b == 0)
+        for (int d = threadIdx.x; d < s; d += blockDim.x) s0_dst[d] = s0_src[d];
     if (j == 0)
         for (int d = threadIdx.x; d < a; d += blockDim.x) { mu[ro + d] = init_mu; sigma[ro + d] = init_sigma; }
     if (!actions) return;
@@ -1077,9 +1102,18 @@ static int rollout_impl(const Geometry& g, const void* packed, const mbrl_norm* 
     if (g.m8_ok) {
         A.m8_off = g.m8_off;
         A.C8 = g.C8;
+        A.m4_off = g.m4_off;
+        A.C4 = g.C4;
+        const int o = g_opt[MBRL_OPT_ROLLOUT_TILE].load(std::memory_order_relaxed);
+        // 4-candidate tiles (rollout_m4_kernel) once 8-candidate tiles would still leave at least half
+        // the CUs idle (cartpole's N = 1024, shards of <= 1024 candidates); both bit-identical
+        bool use4 = (size_t)((N + 7) / 8) * g.E * 2 <= (size_t)device_cus();
         bool use8 = (size_t)((N + 15) / 16) * g.E * 2 <= (size_t)device_cus();
-        if (const int o = g_opt[MBRL_OPT_ROLLOUT_TILE].load(std::memory_order_relaxed)) use8 = o == 8;
-        if (use8 && rollout_m8_supported(A, g.T)) return hip_check(launch_rollout_m8(A, g.T, stream), "rollout m8 launch");
+        if (o) { use4 = o == 4; use8 = o == 8; }
+        if (use4 && g.m4_ok && rollout_m4_supported(A, g.T, g.NG4))
+            return hip_check(launch_rollout_m4(A, g.T, g.NG4, stream), "rollout m4 launch");
+        if ((use8 || use4) && rollout_m8_supported(A, g.T))
+            return hip_check(launch_rollout_m8(A, g.T, stream), "rollout m8 launch");
     }
     // partials in the activation buffer the last hidden layer does not read (rollout.hip): layer 0
     // writes act2, hidden layer l reads act2 for odd l, so with L odd the last one reads act and act2
@@ -1249,13 +1283,35 @@ int mbrl_set_option(int32_t option, int32_t value) {
     if (option < 0 || option >= MBRL_OPT_COUNT) return fail(MBRL_EINVAL, "unknown option %d", option);
     bool ok = false;
     switch (option) {
-        case MBRL_OPT_ROLLOUT_TILE: ok = value == 0 || value == 8 || value == 16; break;
+        case MBRL_OPT_ROLLOUT_TILE: ok = value == 0 || value == 4 || value == 8 || value == 16; break;
         case MBRL_OPT_SPLIT_TILE: ok = value == 0 || value == 16 || value == 32; break;
         case MBRL_OPT_ADAM_ARITH: ok = value >= 0 && value <= 16; break;
         default: ok = value == 0 || value == 1; break;
     }
     if (!ok) return fail(MBRL_EINVAL, "option %d: value %d not allowed", option, value);
     return g_opt[option].exchange(value);
+}
+
+int mbrl_host_alloc(size_t bytes, void** host_ptr, void** device_ptr) {
+    if (!host_ptr || !device_ptr || bytes == 0) return fail(MBRL_EINVAL, "mbrl_host_alloc: bad arguments");
+    *host_ptr = nullptr;
+    *device_ptr = nullptr;
+    void* h = nullptr;
+    int rc = hip_check(hipHostMalloc(&h, bytes, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc");
+    if (rc) return rc;
+    void* d = nullptr;
+    rc = hip_check(hipHostGetDevicePointer(&d, h, 0), "hipHostGetDevicePointer");
+    if (rc) {
+        (void)hipHostFree(h);
+        return rc;
+    }
+    *host_ptr = h;
+    *device_ptr = d;
+    return MBRL_OK;
+}
+
+int mbrl_host_free(void* host_ptr) {
+    return host_ptr ? hip_check(hipHostFree(host_ptr), "hipHostFree") : MBRL_OK;
 }
 
 int mbrl_get_option(int32_t option) {
@@ -1289,6 +1345,7 @@ int mbrl_mlp_pack(const mbrl_mlp_shape* shape, const float* const* weights, cons
         size_t split_chunk = 0;
         float* m8_base = base + g.m8_off;
         size_t m8_chunk = 0;
+        float* m4_base = base + g.m4_off;
         if (g.split_ok)
             for (int q = 0; q < 2; ++q) {
                 hipError_t err = hipMemsetAsync(split_bad[q], 0, 4, stream);
@@ -1317,6 +1374,9 @@ int mbrl_mlp_pack(const mbrl_mlp_shape* shape, const float* const* weights, cons
                 if (g.m8_ok) {
                     hipLaunchKernelGGL(pack_m8_hidden_kernel, dim3(256), dim3(256), 0, stream, w, in_real, g.W, nkc,
                                        g.T, (int)(g.T == 4 && g.NOT == 2), m8_base + m8_chunk * 1024 * (size_t)g.T);
+                    if (g.m4_ok)   // the same chunks without KP pairing (the m8 chunk index = the m4 one here)
+                        hipLaunchKernelGGL(pack_m8_hidden_kernel, dim3(256), dim3(256), 0, stream, w, in_real, g.W, nkc,
+                                           g.T, 0, m4_base + m8_chunk * 1024 * (size_t)g.T);
                     m8_chunk += nkc;
                 }
                 chunk += nkc;
@@ -1334,6 +1394,9 @@ int mbrl_mlp_pack(const mbrl_mlp_shape* shape, const float* const* weights, cons
                     hipLaunchKernelGGL(pack_m8_out_kernel, dim3(256), dim3(256), 0, stream, w, g.W, g.s, g.NOP8, g.NOC8 == 2, g.T,
                                        (int)(g.T == 4 && g.NOT == 2),
                                        m8_base + m8_chunk * 1024 * (size_t)g.T);
+                if (g.m4_ok)
+                    hipLaunchKernelGGL(pack_m4_out_kernel, dim3(256), dim3(256), 0, stream, w, g.W, g.s, g.T,
+                                       m4_base + m8_chunk * 1024 * (size_t)g.T);
                 float* ob = bias_base + (size_t)g.L * g.Wpad;
                 hipLaunchKernelGGL(pack_bias_kernel, dim3(1), dim3(256), 0, stream, b, g.s, 16 * g.NOT, ob);
                 hipLaunchKernelGGL(copy_kernel, dim3(64), dim3(256), 0, stream, w, (size_t)g.s * g.W, plain);
@@ -1565,7 +1628,7 @@ int mbrl_trajectory(const mbrl_mlp_shape* shape, const void* packed, const mbrl_
 
 // Workspace layout for mbrl_cem_plan.
 struct PlanWs {
-    float *costs, *mu[2], *sigma[2], *aelite, *states, *tmp_cost, *actions;
+    float *costs, *mu[2], *sigma[2], *aelite, *states, *tmp_cost, *actions, *s0;
     unsigned long long* xchg;
     unsigned* status;
     size_t xchg_bytes;
@@ -1592,6 +1655,7 @@ static PlanWs plan_ws(const Geometry& g, const mbrl_cem_params* p, void* base) {
     w.xchg_bytes = (size_t)g.E * 2 * g.Wpad * 8;
     w.xchg = (unsigned long long*)take(w.xchg_bytes);
     w.status = (unsigned*)take(16);
+    w.s0 = (float*)take((size_t)g.s * 4);
     w.bytes = o;
     return w;
 }
@@ -1603,7 +1667,7 @@ size_t mbrl_cem_workspace_bytes(const mbrl_mlp_shape* shape, const mbrl_cem_para
 }
 
 int mbrl_cem_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_norm* norm, const mbrl_cost* cost,
-                  const float* s0, const mbrl_cem_params* p, float* mu, float* sigma, float* actions_out,
+                  const float* s0_in, const mbrl_cem_params* p, float* mu, float* sigma, float* actions_out,
                   float* states_out, float* cost_hist, float* returns_hist, int64_t* elite_hist,
                   mbrl_event_t* rollout_events, void* workspace, size_t ws_bytes, mbrl_stream_t stream_) {
     hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
@@ -1614,6 +1678,7 @@ int mbrl_cem_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_no
     if (p->N < 1 || p->H < 1 || p->K < 1 || p->K > p->N || p->iterations < 1)
         return fail(MBRL_EINVAL, "bad CEM params N=%d H=%d K=%d I=%d", p->N, p->H, p->K, p->iterations);
     if (!actions_out || !states_out || !workspace) return fail(MBRL_EINVAL, "actions_out/states_out/workspace NULL");
+    if (!s0_in) return fail(MBRL_EINVAL, "s0 is NULL");
     PlanWs w = plan_ws(g, p, workspace);
     if (ws_bytes < w.bytes) return fail(MBRL_EWORKSPACE, "workspace %zu < %zu", ws_bytes, w.bytes);
     const int Ha = p->H * g.a;
@@ -1624,10 +1689,13 @@ int mbrl_cem_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_no
     if (fuse_draw)
         hipLaunchKernelGGL(cem_init_kernel, dim3(p->H * draw_slices(p->H, 1, p->N, g.a), 1), dim3(1024), 0, stream,
                            p->seed, p->init_mu, p->init_sigma, p->lo, p->hi, p->H, g.a, p->N, w.mu[0], w.sigma[0],
-                           w.actions);
-    else
+                           w.actions, s0_in, g.s, w.s0);
+    else {
         hipLaunchKernelGGL(fill2_kernel, dim3((Ha + 255) / 256), dim3(256), 0, stream, w.mu[0], p->init_mu, w.sigma[0],
                            p->init_sigma, Ha);
+        hipLaunchKernelGGL(copy_kernel, dim3(1), dim3(64), 0, stream, s0_in, (size_t)g.s, w.s0);
+    }
+    const float* s0 = w.s0;   // the workspace copy (s0_in may be mapped host memory)
     int cur = 0;
     for (int it = 0; it < p->iterations; ++it) {
         mbrl_sampler sp{};
@@ -1745,7 +1813,7 @@ int mbrl_cem_plan_batch(const mbrl_mlp_shape* shape, const void* packed, const m
     if (fuse_draw)
         hipLaunchKernelGGL(cem_init_kernel, dim3(p->H * draw_slices(p->H, B, p->N, g.a), B), dim3(1024), 0, stream,
                            p->seed, p->init_mu, p->init_sigma, p->lo, p->hi, p->H, g.a, p->N, w.mu[0], w.sigma[0],
-                           w.actions);
+                           w.actions, nullptr, 0, nullptr);
     else
         hipLaunchKernelGGL(fill2_kernel, dim3((BHa + 255) / 256), dim3(256), 0, stream, w.mu[0], p->init_mu,
                            w.sigma[0], p->init_sigma, BHa);

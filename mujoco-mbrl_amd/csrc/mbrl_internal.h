@@ -49,6 +49,16 @@ struct Geometry {
     int C8;                // chunks per step
     size_t m8_off;         // floats from the member base (0: absent)
     size_t m8_floats;      // C8 * 1024 * T
+    // 4-candidate fp32 stream (rollout.hip rollout_m4_kernel): layer-0 and hidden chunks in the m8
+    // layout without KP pairing (wave w: row 64 w + 32 ((l >> 2) & 1) + 4 (l >> 3) + (l & 3)), then 4
+    // output chunks, one per 16-feature chunk kc of the wave's own 64: float4 s = output group g,
+    // element q = W[16 g + 4 (l >> 4) + (l & 3)][64 w + 16 kc + 4 q + ((l >> 2) & 3)]. Present when
+    // m4_ok (m8_ok and s <= 64: NG4 <= 4 groups of 16 output rows).
+    int m4_ok;
+    int NG4;               // output row groups of 16
+    int C4;                // chunks per step = K0C + (L-1)*4T + 4
+    size_t m4_off;
+    size_t m4_floats;      // C4 * 1024 * T
     size_t member_stride;  // floats per ensemble member (64-float aligned)
 };
 
@@ -100,6 +110,12 @@ inline bool make_geometry(int s, int a, int W, int L, int E, int reward, Geometr
     g->m8_off = g->m8_ok ? (end + 63) / 64 * 64 : 0;
     g->m8_floats = g->m8_ok ? (size_t)g->C8 * 1024 * T : 0;
     if (g->m8_ok) end = g->m8_off + g->m8_floats;
+    g->NG4 = (g->so + 15) / 16;
+    g->m4_ok = (g->m8_ok && g->NG4 <= 4) ? 1 : 0;
+    g->C4 = g->K0C + (L - 1) * 4 * T + 4;
+    g->m4_off = g->m4_ok ? (end + 63) / 64 * 64 : 0;
+    g->m4_floats = g->m4_ok ? (size_t)g->C4 * 1024 * T : 0;
+    if (g->m4_ok) end = g->m4_off + g->m4_floats;
     g->member_stride = (end + 63) / 64 * 64;
     return true;
 }
@@ -132,6 +148,9 @@ struct RolloutArgs {
     // 8-candidate kernel (rollout_m8_kernel)
     size_t m8_off;         // 0: no 8-candidate stream in the pack
     int C8;
+    // 4-candidate kernel (rollout_m4_kernel)
+    size_t m4_off;         // 0: no 4-candidate stream in the pack
+    int C4;
     // 16-candidate kernel, L odd >= 3, no reward head: the output partials live in the activation
     // buffer the last hidden layer does not read (act2), so 32-candidate tiles of wide states fit LDS
     int part_alias;
@@ -226,6 +245,8 @@ bool grid_fits(const void* fn, int threads, size_t lds, int blocks);
 hipError_t launch_rollout(const RolloutArgs& A, int T, int R, hipStream_t stream);
 bool rollout_m8_supported(const RolloutArgs& A, int T);
 hipError_t launch_rollout_m8(const RolloutArgs& A, int T, hipStream_t stream);
+bool rollout_m4_supported(const RolloutArgs& A, int T, int NG);
+hipError_t launch_rollout_m4(const RolloutArgs& A, int T, int NG, hipStream_t stream);
 
 // F16X3 rollout (8 waves, 16 R candidates per workgroup, goal-state cost). Supported for
 // geometry.split_ok; the caller follows it with launch_rollout(redo = 1) at the same R.

@@ -1118,6 +1118,317 @@ hipError_t launch_rollout_m8(const RolloutArgs& A, int T, hipStream_t stream) {
     return hipErrorInvalidValue;
 }
 
+// ------------------------------------------------------------------------------------------------
+// 4-candidate tiles (DESIGN.md §3 "rollout_m4_kernel"): v_mfma_f32_4x4x1_16b_f32 without A broadcast.
+//
+// A plan of N <= 1024 candidates fills at most 128 CUs with 8-candidate tiles. Here each workgroup
+// owns 4 candidates and every 4x4x1 block a distinct 4-row group: wave w (T waves, T = Wpad / 64)
+// owns hidden rows [64 w, 64 w + 64) of every layer as ONE accumulator chain, fed by the 8-candidate
+// weight stream without KP pairing (lane l: row 64 w + 32 ((l >> 2) & 1) + 4 (l >> 3) + (l & 3)):
+//   A (lane l): W[row(l)][k]   B (lane l): X[k][cand l & 3]   D (lane l, v): row(4 (l >> 2) + v), cand l & 3
+// Every accumulator consumes its k in the canonical order (16-deep chunk kc, step s, then q: k =
+// 16 kc + 4 q + s), so sums equal the 8/16/32-candidate kernels' bit for bit
+// (tools/ubench/mfma4x4_chain.hip: one chain per SIMD issues every 12.3 cycles against 8 for two;
+// at Wpad 256 that single chain still beats two waves x two 32-row tiles of 8 candidates).
+// Output layer: the canonical chains of mma_out -- per half of T/2 16-feature tiles, four chains
+// c (k = 16 kc + 4 q + c) -- as 4x4x1 blocks: block b = 4 (l >> 4) + chain, rows 16 g + 4 (l >> 4) + v
+// of output group g, B = the chain's own k of the wave's own features (from LDS), then the chains
+// close as (c0 + c1) + (c2 + c3) through two lane swaps (exactly commutative) and each half's partial
+// goes to LDS for the canonical 8-partial sum of the epilogue (sum_partials<8>).
+template <int T, int K0C_T, int NG, int K0L = 0>
+__global__ void __launch_bounds__(64 * T, 1) rollout_m4_kernel(const RolloutArgs A) {
+    constexpr int M = 4;
+    constexpr int NW = T;
+    constexpr int NT = 64 * NW;
+    constexpr int KH = 4 * T;
+    constexpr int NB = 4;                    // ring slots of 4 float4 per lane, 3 chunks ahead
+    constexpr int NOC = 4;                   // output chunks: the wave's own 4 K chunks
+    constexpr int DUM = (NB - (K0C_T + NOC) % NB) % NB;
+    constexpr int NHW = 8 / T;               // canonical output halves per wave (T / 2 tiles each)
+    constexpr int KPH = 4 / NHW;             // own K chunks per half
+    constexpr int SS = NG;                   // state slots per epilogue lane (ceil(s / 16) <= NG)
+    static_assert((T == 4 || T == 8) && NG >= 1 && NG <= 4 && KH % NB == 0, "m4 geometry");
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const LdsMap L = lds_map(A, smem, M);
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int ntiles = (A.N + M - 1) / M;
+    int tile, e;
+    xcd_unit(A.xcd_map, ntiles, tile, e);
+    const float* member = A.packed + (size_t)e * A.member_stride;
+    float* const actX = L.act;
+    float* const actY = L.act2;
+    // epilogue roles: wave 0 the state rows of the 4 candidates, wave 1 their actions
+    const bool epi = wave == 0;
+    const bool actw = wave == 1;
+    const int awave = 0;
+    float* acs = L.aterm;
+    const int cand = lane & 3;
+    float av[1][MAX_A_PER_LANE];
+    float acp[1];
+    auto fetch_a = [&](int t) {
+        const int n = min(tile * M + epi_row(0, awave, lane), A.N - 1);
+        const float* src = A.actions + ((size_t)t * A.N + n) * A.a;
+#pragma unroll
+        for (int k = 0; k < MAX_A_PER_LANE; ++k) av[0][k] = src[min((lane & 15) + 16 * k, A.a - 1)];
+    };
+    if (actw) fetch_a(0);
+    for (int i = tid; i < A.s; i += NT) {
+        L.obs_mean[i] = A.obs_mean ? A.obs_mean[i] : 0.f;
+        L.obs_std[i] = A.obs_std ? A.obs_std[i] : 1.f;
+        L.goal[i] = A.goal ? A.goal[i] : 0.f;
+        L.cw[i] = A.cw ? A.cw[i] : 0.f;
+    }
+    for (int i = tid; i < A.a; i += NT) {
+        L.act_mean[i] = A.act_mean ? A.act_mean[i] : 0.f;
+        L.act_std[i] = A.act_std ? A.act_std[i] : 1.f;
+    }
+    const float* bias_src = member + A.stream_floats;
+    for (int i = tid; i < A.L * A.Wpad + 16 * A.NOT; i += NT) L.hbias[i] = bias_src[i];
+    __syncthreads();
+    for (int i = tid; i < M * A.s; i += NT) {
+        const int m = i / A.s, d = i - (i / A.s) * A.s;
+        const int n = min(tile * M + m, A.N - 1);
+        const float sv = A.s0_per_cand ? A.s0[(size_t)n * A.s + d] : A.s0[d];
+        actX[m * A.lda + d] = A.norm_s ? (sv - L.obs_mean[d]) / L.obs_std[d] : sv;
+    }
+    for (int i = tid; i < M * A.k0pad_extra; i += NT) {
+        const int m = i / A.k0pad_extra, j = i - (i / A.k0pad_extra) * A.k0pad_extra;
+        actX[m * A.lda + A.s + A.a + j] = 0.f;
+    }
+    EpiParams<SS> P;
+    load_epi_params<SS>(A, L, lane, P);
+    if (actw) {
+        stage_actions<1, SS>(A, P, L, actX, awave, lane, av, acp);
+        const float v = rowsum16(acp[0]);
+        if ((lane & 15) == 0) acs[epi_row(0, awave, lane)] = v;
+    }
+    __syncthreads();
+
+    // ---- weight stream: chunk g of this wave at byte (g T + wave) 4096 + slot 1024 + lane 16
+    const int C4 = A.C4;
+    const int CSQ = C4 + DUM;
+    const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(member + A.m4_off), 0, (int)((size_t)C4 * 4096 * T), 0x00020000);
+    const unsigned lane_off = (unsigned)(wave * 4 * 1024 + lane * 16);
+    f32x4 ring[NB][4];
+#define M4_LOAD(SLOT, G)                                                                          \
+    do {                                                                                          \
+        int gg_ = (G);                                                                            \
+        if (gg_ >= CSQ) gg_ -= CSQ;                                                               \
+        gg_ = gg_ < C4 ? gg_ : C4 - 1;                                                            \
+        const int so_ = gg_ * (4096 * T);                                                         \
+        _Pragma("unroll") for (int s_ = 0; s_ < 4; ++s_) ring[SLOT][s_] = __builtin_bit_cast(     \
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, lane_off + s_ * 1024, so_, 0));   \
+    } while (0)
+#pragma unroll
+    for (int q = 0; q < NB - 1; ++q) M4_LOAD(q, q);
+    f32x4 bb[2][4];     // B: X[cand][16 kc + 4 q' .. +3], double-buffered over chunks
+    f32x4 acc;
+    f32x4 bias;
+    float total = 0.f;
+    const int row0 = 64 * wave + 32 * ((lane >> 2) & 1) + 4 * (lane >> 3);   // this lane's 4 D rows
+    auto read_b = [&](f32x4 (&b)[4], const float* in, int col) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) b[q] = *reinterpret_cast<const f32x4*>(in + cand * A.lda + col + 4 * q);
+    };
+    auto mma_chunk = [&](const f32x4 (&w)[4], const f32x4 (&b)[4]) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc = __builtin_amdgcn_mfma_f32_4x4x1f32(w[s][q], b[q][s], acc, 0, 0, 0);
+    };
+    auto mma_chunk_l0 = [&](const f32x4 (&w)[4], const f32x4 (&b)[4], auto kcc) {
+        constexpr int kc = decltype(kcc)::value;
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (16 * kc + 4 * q + s < K0L) acc = __builtin_amdgcn_mfma_f32_4x4x1f32(w[s][q], b[q][s], acc, 0, 0, 0);
+    };
+    auto store_layer = [&](float* out) {
+        f32x4 v = acc + bias;
+        v = __builtin_elementwise_max(v, f32x4{0.f, 0.f, 0.f, 0.f});
+        *reinterpret_cast<f32x4*>(out + cand * A.lda + row0) = v;
+    };
+#define M4_CHUNK(SLOT, KC, NK, IN)                                          \
+    do {                                                                    \
+        M4_LOAD(((SLOT) + NB - 1) % NB, g + NB - 1);                         \
+        if ((KC) + 1 < (NK)) read_b(bb[((KC) + 1) & 1], IN, 16 * ((KC) + 1)); \
+        mma_chunk(ring[SLOT], bb[(KC) & 1]);                                \
+        MBRL_PIN();                                                         \
+        ++g;                                                                \
+    } while (0)
+
+    for (int t = 0; t < A.H; ++t) {
+        int g = 0;
+        if (actw && t + 1 < A.H) fetch_a(t + 1);
+        // ---- layer 0: actX [s | a | 0-pad] -> actY
+        acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        bias = *reinterpret_cast<const f32x4*>(L.hbias + row0);
+        read_b(bb[0], actX, 0);
+        if constexpr (K0L > 0) {
+            static_assert(K0C_T == 2, "K0L instance");
+            M4_LOAD((0 + NB - 1) % NB, g + NB - 1);
+            read_b(bb[1], actX, 16);
+            mma_chunk_l0(ring[0], bb[0], std::integral_constant<int, 0>());
+            MBRL_PIN();
+            ++g;
+            M4_LOAD((1 + NB - 1) % NB, g + NB - 1);
+            mma_chunk_l0(ring[1], bb[1], std::integral_constant<int, 1>());
+            MBRL_PIN();
+            ++g;
+        } else {
+#pragma unroll
+            for (int kc = 0; kc < K0C_T; ++kc) M4_CHUNK(kc % NB, kc, K0C_T, actX);
+        }
+        store_layer(actY);
+        if (A.L > 1) __syncthreads();
+        float* in = actY;
+        float* out = actX;
+        for (int l = 1; l < A.L; ++l) {
+            acc = f32x4{0.f, 0.f, 0.f, 0.f};
+            bias = *reinterpret_cast<const f32x4*>(L.hbias + l * A.Wpad + row0);
+            read_b(bb[0], in, 0);
+#pragma unroll
+            for (int kc = 0; kc < KH; ++kc) M4_CHUNK((K0C_T + kc) % NB, kc, KH, in);
+            store_layer(out);
+            if (l + 1 < A.L) __syncthreads();   // the last hidden layer is read back by its own wave only
+            float* tmp = in; in = out; out = tmp;
+        }
+        // ---- output layer over this wave's own 64 features (its own LDS stores, in order)
+        {
+            const int chain = (lane >> 2) & 3;
+            f32x4 ch[NHW][NG];
+#pragma unroll
+            for (int h = 0; h < NHW; ++h)
+#pragma unroll
+                for (int gr = 0; gr < NG; ++gr) ch[h][gr] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int o = 0; o < NOC; ++o) {
+                f32x4 hq[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    hq[q] = *reinterpret_cast<const f32x4*>(in + cand * A.lda + 64 * wave + 16 * o + 4 * q);
+                constexpr int base = K0C_T;   // output chunk o sits in slot (K0C + KH + o) % NB
+                M4_LOAD(((base + o) + NB - 1) % NB, g + NB - 1);
+                const int h = o / KPH;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float b = chain == 0 ? hq[q][0] : chain == 1 ? hq[q][1] : chain == 2 ? hq[q][2] : hq[q][3];
+#pragma unroll
+                    for (int gr = 0; gr < NG; ++gr)
+                        ch[h][gr] = __builtin_amdgcn_mfma_f32_4x4x1f32(ring[(base + o) % NB][gr][q], b, ch[h][gr], 0, 0, 0);
+                }
+                MBRL_PIN();
+                ++g;
+            }
+#pragma unroll
+            for (int d = 0; d < DUM; ++d) {
+                M4_LOAD((K0C_T + NOC + d + NB - 1) % NB, g + NB - 1);
+                ++g;
+            }
+            // (c0 + c1) + (c2 + c3): chains c ^ 1 / c ^ 2 sit 4 / 8 lanes away
+#pragma unroll
+            for (int h = 0; h < NHW; ++h)
+#pragma unroll
+                for (int gr = 0; gr < NG; ++gr) {
+                    f32x4 x, y;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) x[i] = ch[h][gr][i] + __shfl_xor(ch[h][gr][i], 4);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) y[i] = x[i] + __shfl_xor(x[i], 8);
+                    if (chain == 0)
+                        *reinterpret_cast<f32x4*>(L.part + (wave * NHW + h) * (M * A.pw) + cand * A.pw + 16 * gr +
+                                                  4 * (lane >> 4)) = y;
+                }
+        }
+        __syncthreads();
+        // ---- epilogue: the 8-wave kernel's split-mode goal-state epilogue for rows 0..3
+        if (epi) {
+            const int ws = M * A.pw;
+            const int j = lane & 15;
+            const int m = epi_row(0, 0, lane);
+            const int n = tile * M + m;
+            float sc = 0.f;
+            auto slot = [&](int d, float om, float os, float goal, float cw, float bo) {
+                const int ro = m * A.pw + d;
+                float o = sum_partials<8>(L.part, ws, ro);
+                o = o + bo;
+                const float sn = A.unnorm_s ? o * os + om : o;
+                if (A.has_sc) {
+                    const float x = (sn - goal) * cw;
+                    sc += sqrtf(x * x + A.alpha_s2) - A.alpha_s;
+                }
+                actX[m * A.lda + d] = A.norm_s ? (sn - om) / os : sn;
+                if (A.states_out != nullptr && n < A.N)
+                    A.states_out[(((size_t)e * A.H + t) * A.N + n) * A.s + d] = sn;
+            };
+            if constexpr (SS <= MBRL_EPI_REG_SLOTS) {
+#pragma unroll
+                for (int k = 0; k < SS; ++k)
+                    if (j + 16 * k < A.s) slot(j + 16 * k, P.om[k], P.os[k], P.goal[k], P.cw[k], P.bo[k]);
+            } else {
+                const float* bout = L.hbias + A.L * A.Wpad;
+#pragma unroll
+                for (int k = 0; k < SS; ++k) {
+                    const int d = j + 16 * k;
+                    if (d < A.s) slot(d, L.obs_mean[d], L.obs_std[d], L.goal[d], L.cw[d], bout[d]);
+                }
+            }
+            for (int d = A.s + A.a + j; d < A.s + A.a + A.k0pad_extra; d += 16) actX[m * A.lda + d] = 0.f;
+            sc = rowsum16(sc);
+            const float ac = acs[(t & 1) * M + m];
+            total += sc + A.alpha_a2 * (ac / (float)A.a);
+        } else if (actw && t + 1 < A.H) {
+            stage_actions<1, SS>(A, P, L, actX, awave, lane, av, acp);
+            const float v = rowsum16(acp[0]);
+            if ((lane & 15) == 0) acs[((t + 1) & 1) * M + epi_row(0, awave, lane)] = v;
+        }
+        __syncthreads();
+    }
+#undef M4_CHUNK
+#undef M4_LOAD
+    if (epi && (lane & 15) == 0) {
+        const int n = tile * M + epi_row(0, 0, lane);
+        if (n < A.N) A.costs[(size_t)e * A.N + n] = total;
+    }
+}
+
+bool rollout_m4_supported(const RolloutArgs& A, int T, int NG) {
+    if (A.reward || A.redo || A.m4_off == 0) return false;
+    if ((T != 4 && T != 8) || NG < 1 || NG > 4) return false;
+    return (A.K0C == 2 || A.K0C == 6) && rollout_lds_bytes(A, 4) <= 160 * 1024;
+}
+
+template <int T, int K0C_T, int NG, int K0L = 0>
+static hipError_t launch_m4_tr(const RolloutArgs& A_in, hipStream_t stream) {
+    RolloutArgs A = A_in;
+    A.nw = 8;   // output partials: the canonical 8
+    const int ntiles = (A.N + 3) / 4;
+    const dim3 grid = A.xcd_map ? dim3(ntiles * A.E) : dim3(ntiles, A.E);
+    const size_t lds = rollout_lds_bytes(A, 4);
+    const auto fn = &rollout_m4_kernel<T, K0C_T, NG, K0L>;
+    hipError_t e = ensure_dynamic_lds(reinterpret_cast<const void*>(fn), 160 * 1024);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(fn, grid, dim3(64 * T), lds, stream, A);
+    return hipGetLastError();
+}
+
+template <int T, int K0C_T>
+static hipError_t launch_m4_tk(const RolloutArgs& A, int NG, hipStream_t stream) {
+    if (NG == 1) return launch_m4_tr<T, K0C_T, 1>(A, stream);
+    if (NG == 2) return launch_m4_tr<T, K0C_T, 2>(A, stream);
+    return launch_m4_tr<T, K0C_T, 4>(A, stream);   // NG 3: one all-zero group more
+}
+
+hipError_t launch_rollout_m4(const RolloutArgs& A, int T, int NG, hipStream_t stream) {
+    if (T == 4 && A.K0C == 2 && NG == 1 && A.s + A.a <= 8)   // cartpole-sized inputs: padded MFMAs skipped
+        return launch_m4_tr<4, 2, 1, 8>(A, stream);
+    if (T == 4) return A.K0C == 2 ? launch_m4_tk<4, 2>(A, NG, stream) : launch_m4_tk<4, 6>(A, NG, stream);
+    if (T == 8) return A.K0C == 2 ? launch_m4_tk<8, 2>(A, NG, stream) : launch_m4_tk<8, 6>(A, NG, stream);
+    return hipErrorInvalidValue;
+}
+
 }  // namespace mbrl
 
 #ifdef MBRL_STAMPS

@@ -12,6 +12,7 @@ import ctypes
 import os
 from ctypes import POINTER, c_float, c_int32, c_int64, c_size_t, c_uint64, c_void_p
 
+import numpy as np
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 LIB_PATH = os.environ.get("MBRL_AMD_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
@@ -21,7 +22,7 @@ MBRL_OK = 0
 MBRL_EUNSUPPORTED = -2
 MBRL_COST_GOAL_STATE = 0
 MBRL_COST_MODEL_REWARD = 1
-ABI_VERSION = 6
+ABI_VERSION = 7
 MBRL_NAN_LAST = 0
 MBRL_NAN_FIRST = 1
 MBRL_PRECISION_F32 = 0
@@ -50,7 +51,8 @@ EXPORTED = (
     "mbrl_trajectory_workspace_bytes", "mbrl_trajectory", "mbrl_cem_workspace_bytes", "mbrl_cem_plan",
     "mbrl_cem_plan_batch_workspace_bytes", "mbrl_cem_plan_batch", "mbrl_gd_workspace_bytes", "mbrl_gd_plan",
     "mbrl_cem_update", "mbrl_adam_step", "mbrl_train_workspace_bytes", "mbrl_train_grads",
-    "mbrl_train_epoch", "mbrl_gd_batch_workspace_bytes", "mbrl_gd_plan_batch",
+    "mbrl_train_epoch", "mbrl_gd_batch_workspace_bytes", "mbrl_gd_plan_batch", "mbrl_host_alloc",
+    "mbrl_host_free",
 )
 
 
@@ -127,6 +129,8 @@ def load():
         "mbrl_last_error": (ctypes.c_char_p, []),
         "mbrl_set_option": (c_int32, [c_int32, c_int32]),
         "mbrl_get_option": (c_int32, [c_int32]),
+        "mbrl_host_alloc": (c_int32, [c_size_t, POINTER(c_void_p), POINTER(c_void_p)]),
+        "mbrl_host_free": (c_int32, [c_void_p]),
         "mbrl_mlp_packed_bytes": (c_size_t, [POINTER(MlpShape)]),
         "mbrl_mlp_pack": (c_int32, [POINTER(MlpShape), POINTER(c_void_p), POINTER(c_void_p), P, P]),
         "mbrl_rollout_cost": (c_int32, [POINTER(MlpShape), P, POINTER(Norm), POINTER(Cost), P, c_int32, P,
@@ -195,6 +199,28 @@ class option:
         return False
 
 
+class HostStaging:
+    """Mapped, coherent pinned host memory (mbrl_host_alloc) as `n` float32s: `.array` is the host's
+    NumPy view, `.device` the address kernels read and write. Freed with the object."""
+
+    def __init__(self, n):
+        lib = load()
+        h, d = c_void_p(), c_void_p()
+        check(lib.mbrl_host_alloc(4 * int(n), ctypes.byref(h), ctypes.byref(d)), "mbrl_host_alloc")
+        self._lib, self.host, self.n = lib, h.value, int(n)
+        self.device = c_void_p(d.value)
+        self.array = np.ctypeslib.as_array((ctypes.c_float * self.n).from_address(self.host))
+
+    def at(self, offset):
+        """Device address of element `offset`."""
+        return c_void_p(self.device.value + 4 * int(offset))
+
+    def __del__(self):
+        if getattr(self, "host", None):
+            self._lib.mbrl_host_free(c_void_p(self.host))
+            self.host = None
+
+
 def ptr(t):
     """Device pointer of a tensor (None -> NULL)."""
     return None if t is None else c_void_p(t.data_ptr())
@@ -213,4 +239,4 @@ __all__ = ["load", "check", "ptr", "stream_handle", "MlpShape", "Norm", "Cost", 
            "EXPORTED", "MBRL_NAN_LAST", "MBRL_NAN_FIRST", "MBRL_COST_GOAL_STATE", "MBRL_COST_MODEL_REWARD",
            "ABI_VERSION", "c_int64", "MBRL_PRECISION_F32", "MBRL_PRECISION_F16X3", "MBRL_PRECISION_F16X6",
            "precision_code", "option", "OPTIONS", "AdamTensor", "AdamHparams",
-           "TrainModel", "TrainData", "TRAIN_MAX_LAYERS"]
+           "TrainModel", "TrainData", "TRAIN_MAX_LAYERS", "HostStaging"]

@@ -21,6 +21,8 @@ Both take the fused path when fused.describe_* recognise the model / cost closur
 user's callables run on device tensors (reference semantics, planners.py:199-210) and selection /
 refit still run in the HIP extension.
 """
+import threading
+
 import numpy as np
 import torch
 
@@ -285,7 +287,6 @@ class CEMPlanner(ModelPlanner):
         dev = _device(kwargs)
         st = CEMPlanner._settings(sample_action, horizon, kwargs)
         with torch.cuda.device(dev):
-            s0 = initial_state.to(device=dev, dtype=torch.float32).contiguous()
             mdesc, cdesc = fused.describe(model, cost, dev)
             ws = None
             if st["distributed"] and torch.distributed.is_available() and torch.distributed.is_initialized() \
@@ -294,14 +295,18 @@ class CEMPlanner(ModelPlanner):
             if mdesc is not None and cdesc is not None:
                 prob = fused.device_problem(mdesc, cdesc, dev, st["precision"])
                 if ws is None:
-                    res = _cem_fused_single(prob, s0, st)
+                    res = _cem_fused_single(prob, initial_state, st)
+                    if res.pop("_host", False):
+                        return res
                 else:
-                    res = _cem_fused_sharded(prob, s0, st, ws)
+                    res = _cem_fused_sharded(prob, initial_state.to(device=dev, dtype=torch.float32).contiguous(),
+                                             st, ws)
             else:
                 a = st["adim"]
                 if a is None:
                     a = sample_action(batch_size=1).shape[1]
-                res = _cem_generic(model, cost, s0, st, a, dev)
+                res = _cem_generic(model, cost, initial_state.to(device=dev, dtype=torch.float32).contiguous(), st,
+                                   a, dev)
             both = res.pop("_both", None)
             if both is not None and not st["keep"]:
                 host = both.cpu()              # one device-to-host copy for states and actions
@@ -363,7 +368,52 @@ def _workspace(key, nbytes, device):
     return buf
 
 
-def _cem_fused_single(prob, s0, st):
+_STAGING = threading.local()
+
+
+def _staging(dev, n):
+    """This thread's mapped pinned host buffer of >= n floats for plans on `dev` (_lib.HostStaging)."""
+    bufs = getattr(_STAGING, "bufs", None)
+    if bufs is None:
+        bufs = _STAGING.bufs = {}
+    buf = bufs.get(str(dev))
+    if buf is None or buf.n < n:
+        buf = bufs[str(dev)] = _lib.HostStaging(max(n, 256))
+    return buf
+
+
+def _cem_plan_host(lib, prob, initial_state, st, params, ws):
+    """mbrl_cem_plan with host staging (_lib.HostStaging): the plan's first launch reads the initial
+    state from mapped host memory and its last launches write states, actions, mu and sigma there, so
+    no copy launch precedes or follows the plan; one stream sync, then host tensors."""
+    dev = prob.device
+    md = prob.mdesc
+    H, a, s = st["H"], md["a"], md["s"]
+    stage = _staging(dev, H * (s + 3 * a) + s)
+    arr = stage.array
+    o_s0 = H * (s + 3 * a)
+    arr[o_s0:o_s0 + s] = initial_state.detach().reshape(-1).to(torch.float32).numpy()
+    o_act, o_mu, o_sg = H * s, H * (s + a), H * (s + 2 * a)
+    _lib.check(lib.mbrl_cem_plan(fused.ctypes_ref(prob.shape), _lib.ptr(prob.packed), fused.ctypes_ref(prob.norm),
+                                 fused.ctypes_ref(prob.cost), stage.at(o_s0), fused.ctypes_ref(params), stage.at(o_mu),
+                                 stage.at(o_sg), stage.at(o_act), stage.at(0), None, None, None,
+                                 _events(st, params.iterations), _lib.ptr(ws), ws.numel(), _lib.stream_handle(dev)),
+               "mbrl_cem_plan")
+    torch.cuda.current_stream(dev).synchronize()
+    out = torch.from_numpy(arr[:o_s0].copy())
+    return dict(states=out[:o_act].view(H, s), actions=out[o_act:o_mu].view(H, a), mu=out[o_mu:o_sg].view(H, a),
+                sigma=out[o_sg:].view(H, a), _host=True)
+
+
+def _events(st, I):
+    events = st["events"]
+    if events is None:
+        return None
+    return (_lib.c_void_p * (2 * I))(*[(e.cuda_event if pair is not None else None)
+                                       for pair in events for e in (pair or (None, None))])
+
+
+def _cem_fused_single(prob, initial_state, st):
     """One C-ABI call: mbrl_cem_plan (every iteration stream-ordered, no host sync)."""
     lib = _lib.load()
     dev = prob.device
@@ -374,6 +424,9 @@ def _cem_fused_single(prob, s0, st):
                             int(st["seed"]) & 0xFFFFFFFFFFFFFFFF)
     need = lib.mbrl_cem_workspace_bytes(fused.ctypes_ref(prob.shape), fused.ctypes_ref(params))
     ws = _workspace(("cem", str(dev)), need, dev)
+    if not st["keep"] and not st["record"] and not initial_state.is_cuda:
+        return _cem_plan_host(lib, prob, initial_state, st, params, ws)
+    s0 = initial_state.to(device=dev, dtype=torch.float32).contiguous()
     # one allocation for the outputs; states and actions side by side, so that plan() hands both
     # back to the host in ONE copy
     buf = torch.empty(H * (s + 3 * a), dtype=torch.float32, device=dev)
@@ -386,11 +439,7 @@ def _cem_fused_single(prob, s0, st):
     cost_hist = torch.empty((I, E, N), dtype=torch.float32, device=dev) if rec else None
     ret_hist = torch.empty((I, N), dtype=torch.float32, device=dev) if rec else None
     elite_hist = torch.empty((I, K), dtype=torch.int64, device=dev) if rec else None
-    events = st["events"]
-    ev_arr = None
-    if events is not None:
-        ev_arr = (_lib.c_void_p * (2 * I))(*[(e.cuda_event if pair is not None else None)
-                                             for pair in events for e in (pair or (None, None))])
+    ev_arr = _events(st, I)
     _lib.check(lib.mbrl_cem_plan(fused.ctypes_ref(prob.shape), _lib.ptr(prob.packed), fused.ctypes_ref(prob.norm),
                                  fused.ctypes_ref(prob.cost), _lib.ptr(s0), fused.ctypes_ref(params), _lib.ptr(mu),
                                  _lib.ptr(sigma), _lib.ptr(actions), _lib.ptr(states), _lib.ptr(cost_hist),

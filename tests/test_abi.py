@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     assert decl == sorted(_lib.EXPORTED)
     for name in decl:
         assert hasattr(lib, name), name
-    assert lib.mbrl_abi_version() == _lib.ABI_VERSION == 6
+    assert lib.mbrl_abi_version() == _lib.ABI_VERSION == 7
 
 
 def test_no_gpu_needed_for_sizing_calls():
@@ -42,7 +42,10 @@ def test_no_gpu_needed_for_sizing_calls():
     split = 34 * 2048 * 8 + 64 + 34 * 3072 * 8 + 64
     # then the 8-candidate stream: 2 + 2 x 32 + 2 chunks of 16 K rows x 8 waves x 4 KiB
     m8 = 68 * 8192
-    assert lib.mbrl_mlp_packed_bytes(ctypes.byref(sh)) == a64(a64(68 * 8192 + 3 * 512 + 32 + plain) + split + m8) * 4
+    # then the 4-candidate stream: 2 + 2 x 32 layer-0 / hidden chunks + 4 output chunks x 8 waves x 4 KiB
+    m4 = 70 * 8192
+    assert lib.mbrl_mlp_packed_bytes(ctypes.byref(sh)) == \
+        a64(a64(68 * 8192 + 3 * 512 + 32 + plain) + split + m8) * 4 + m4 * 4
     # precision does not change the packed layout; an unknown precision is rejected
     assert lib.mbrl_mlp_packed_bytes(ctypes.byref(_lib.MlpShape(17, 6, 512, 3, 1, 0, 1))) == \
         lib.mbrl_mlp_packed_bytes(ctypes.byref(sh))

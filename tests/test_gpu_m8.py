@@ -99,3 +99,42 @@ def test_ensemble_xcd_order_is_bitwise_neutral(cid, N, H, m):
     assert torch.equal(c_map, c_plain) and torch.equal(s_map, s_plain)
     ref = ocem.ensemble_returns(ocem.rollout(p["model"], p["norm"], p["cost"], p["s0"], A[:, :48]))
     assert rel_err(c_map.mean(0)[:48] if p["cfg"]["E"] > 1 else c_map[0, :48], ref) < RTOL
+
+
+@pytest.mark.parametrize("cid,N,H,over", [(2, 1000, 20, {}), (2, 9, 5, {}), (3, 1024, 6, {}), (3, 300, 30, {}),
+                                          (3, 1, 3, {}), (4, 517, 7, {}), (5, 40, 6, {}), (3, 33, 1, {}),
+                                          (2, 300, 5, dict(L=1)), (3, 100, 4, dict(W=200)),
+                                          (4, 64, 3, dict(W=256, L=4)), (2, 64, 4, dict(W=512)),
+                                          (4, 90, 3, dict(W=200, L=1))])
+def test_m4_matches_m16_bitwise_and_the_oracle(cid, N, H, over):
+    """The 4-candidate tile (rollout_m4_kernel: one 64-row chain per wave, the output layer's
+    canonical chains as 4x4x1 blocks closed by lane swaps) against the 16-candidate kernel: the same
+    bits, costs and states, and the oracle bars. Humanoid (s = 67 > 64) has no 4-candidate stream and
+    falls back to 8-candidate tiles -- also bit-identical."""
+    p = ocem.synth_problem(cid, N=N, H=H, **over)
+    a = p["cfg"]["a"]
+    A = cem_actions(np.zeros((H, a), np.float32), np.full((H, a), 0.5, np.float32), -1, 1, 5, 0, np.arange(N))
+    prob = device_problem(p)
+    c4, s4 = _rollout(prob, p, N, H, 4, A)
+    c16, s16 = _rollout(prob, p, N, H, 16, A)
+    assert torch.equal(c4, c16), float((c4 - c16).abs().max())
+    assert torch.equal(s4, s16)
+    ref_costs, ref_states = ocem.rollout(p["model"], p["norm"], p["cost"], p["s0"], A, store_states=True)
+    assert rel_err(c4, ref_costs) < RTOL
+    assert np.allclose(s4.cpu().numpy(), ref_states, rtol=1e-4, atol=1e-4)
+
+
+def test_cartpole_plan_equal_for_every_tile_height():
+    """BASELINE config 2 (cartpole N=1024, H=20) picks 4-candidate tiles; the whole plan is the same
+    with 4, 8 and 16 candidates per workgroup."""
+    from mbrl_amd import CEMPlanner, _lib
+    p = ocem.synth_problem(2)
+    _, model_fn, cost_fn, sample_action = build(p)
+    out = {}
+    for m in (4, 8, 16):
+        with _lib.option("rollout_tile", m):
+            out[m] = CEMPlanner.plan_detailed(torch.from_numpy(p["s0"]), model_fn, cost_fn, sample_action, 20,
+                                              num_candidates=1024, num_iterations=5, seed=p["rng_seed"], record=True)
+    for m in (8, 16):
+        for k in ("returns", "elites", "mu", "sigma", "actions", "states"):
+            assert torch.equal(out[4][k], out[m][k]), (m, k)

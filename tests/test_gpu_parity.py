@@ -796,3 +796,25 @@ def test_cem_plan_edge_sizes_against_oracle(cid, N, H, K, I):
     assert np.array_equal(res["mu"].cpu().numpy(), ref["mu"][-1])
     assert np.array_equal(res["sigma"].cpu().numpy(), ref["sigma"][-1])
     assert np.array_equal(res["actions"].numpy(), ref["final_actions"])
+
+
+@pytest.mark.parametrize("cid,over", [(2, {}), (3, dict(N=512, H=8)), (5, dict(N=256, H=6)), (6, dict(N=256, H=5))])
+def test_staged_host_plan_equals_device_plan(cid, over):
+    """plan() with a host initial state and host results runs mbrl_cem_plan on mapped pinned staging
+    (planners._cem_plan_host: the first launch reads s0 from host memory, the last ones write the
+    results there): bit-identical to the device-buffer path (record=True / return_device=True / a
+    device initial state), for single models, ensembles (member-mean states) and reward heads."""
+    from mbrl_amd import CEMPlanner
+    p = ocem.synth_problem(cid, **over)
+    _, model_fn, cost_fn, sample_action = build(p)
+    H, N = p["cfg"]["H"], p["cfg"]["N"]
+    kw = dict(num_candidates=N, num_iterations=3, seed=p["rng_seed"])
+    s0 = torch.from_numpy(p["s0"])
+    st_h, act_h = CEMPlanner.plan(s0, model_fn, cost_fn, sample_action, H, **kw)
+    assert not st_h.is_cuda and not act_h.is_cuda
+    ref = CEMPlanner.plan_detailed(s0, model_fn, cost_fn, sample_action, H, record=True, **kw)
+    st_d, act_d = CEMPlanner.plan(s0.to(DEV), model_fn, cost_fn, sample_action, H, return_device=True, **kw)
+    for st, act in ((ref["states"], ref["actions"]), (st_d.cpu(), act_d.cpu())):
+        assert torch.equal(st_h, st) and torch.equal(act_h, act)
+    st2, act2 = CEMPlanner.plan(s0.double(), model_fn, cost_fn, sample_action, H, **kw)   # dtype conversion
+    assert torch.equal(st2, st_h) and torch.equal(act2, act_h)
