@@ -154,7 +154,7 @@ enum {
     MBRL_OPT_DEBUG_GD_ABORT = 4,    /* 1: the cooperative gd kernel gives up at once                  */
     MBRL_OPT_UNFUSED_UPDATE = 5,    /* 1: plans run select / refit / proposal draw as separate launches */
     MBRL_OPT_ADAM_ARITH = 6,        /* mbrl_adam_step contraction pattern: 0 = torch's; 1 + bits (test) */
-    MBRL_OPT_NO_XCD_MAP = 7,        /* 1: ensemble rollouts keep the plain (tile, member) workgroup order */
+    MBRL_OPT_XCD_MAP = 7,           /* 1: ensemble rollouts map workgroups member-major per XCD (A/B) */
     MBRL_OPT_COUNT = 8
 };
 int mbrl_set_option(int32_t option, int32_t value);

@@ -1093,9 +1093,10 @@ static int rollout_impl(const Geometry& g, const void* packed, const mbrl_norm* 
             return hip_check(launch_rollout(X, g.T, RS, stream), "split redo launch");
         }
     }
-    // ensembles: member-major workgroup order per XCD (mbrl_internal.h xcd_unit), so that an XCD's
-    // L2 streams the weights of one or two members (humanoid: 5 x 2.4 MB would not fit its 4 MB)
-    A.xcd_map = (g.E > 1 && g_opt[MBRL_OPT_NO_XCD_MAP].load(std::memory_order_relaxed) == 0) ? 1 : 0;
+    // ensembles: member-major workgroup order per XCD (mbrl_internal.h xcd_unit), opt-in. The plain
+    // (tile, member) grid already keeps each XCD on one member at a time (consecutive ids of one member
+    // round-robin over the XCDs), so it measured the same (humanoid 75.5 ms either way)
+    A.xcd_map = (g.E > 1 && g_opt[MBRL_OPT_XCD_MAP].load(std::memory_order_relaxed) == 1) ? 1 : 0;
     // 8-candidate tiles (rollout_m8_kernel, bit-identical sums) when 16-candidate tiles would leave
     // at least half the CUs idle: the shard of a strong-scaled plan, small plans.
     // MBRL_OPT_ROLLOUT_TILE = 8 / 16 forces a choice (tests, A/B).
@@ -1107,7 +1108,7 @@ static int rollout_impl(const Geometry& g, const void* packed, const mbrl_norm* 
         const int o = g_opt[MBRL_OPT_ROLLOUT_TILE].load(std::memory_order_relaxed);
         // 4-candidate tiles (rollout_m4_kernel) once 8-candidate tiles would still leave at least half
         // the CUs idle (cartpole's N = 1024, shards of <= 1024 candidates); both bit-identical
-        bool use4 = (size_t)((N + 7) / 8) * g.E * 2 <= (size_t)device_cus();
+        bool use4 = false;   // opt-in: slower than 8-candidate tiles at cartpole size
         bool use8 = (size_t)((N + 15) / 16) * g.E * 2 <= (size_t)device_cus();
         if (o) { use4 = o == 4; use8 = o == 8; }
         if (use4 && g.m4_ok && rollout_m4_supported(A, g.T, g.NG4))

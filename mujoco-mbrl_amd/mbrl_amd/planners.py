@@ -369,6 +369,9 @@ def _workspace(key, nbytes, device):
 
 
 _STAGING = threading.local()
+# plan() with host inputs / outputs goes through mapped pinned staging (_cem_plan_host); False: the
+# device-buffer path with a host-to-device copy of s0 and a device-to-host copy of the results (A/B)
+HOST_STAGING = True
 
 
 def _staging(dev, n):
@@ -424,7 +427,7 @@ def _cem_fused_single(prob, initial_state, st):
                             int(st["seed"]) & 0xFFFFFFFFFFFFFFFF)
     need = lib.mbrl_cem_workspace_bytes(fused.ctypes_ref(prob.shape), fused.ctypes_ref(params))
     ws = _workspace(("cem", str(dev)), need, dev)
-    if not st["keep"] and not st["record"] and not initial_state.is_cuda:
+    if HOST_STAGING and not st["keep"] and not st["record"] and not initial_state.is_cuda:
         return _cem_plan_host(lib, prob, initial_state, st, params, ws)
     s0 = initial_state.to(device=dev, dtype=torch.float32).contiguous()
     # one allocation for the outputs; states and actions side by side, so that plan() hands both

@@ -84,18 +84,18 @@ def test_32_candidate_tiles_match_smaller_shards_bitwise(cid, N, H):
 @pytest.mark.parametrize("cid,N,H,m", [(5, 8192, 3, 16), (5, 1000, 4, 16), (5, 1000, 4, 8), (5, 33, 2, 16),
                                        (3, 600, 3, 16)])
 def test_ensemble_xcd_order_is_bitwise_neutral(cid, N, H, m):
-    """Ensembles launch a 1-D grid whose workgroups map member-major onto the XCDs (xcd_unit,
-    DESIGN.md §3): every (tile, member) is still computed exactly once, so costs and states equal the
-    plain (tile, member) grid (MBRL_OPT_NO_XCD_MAP) bit for bit -- including grids whose size is not
-    a multiple of 8 and single-member models (which never remap)."""
+    """MBRL_OPT_XCD_MAP: ensembles launch a 1-D grid whose workgroups map member-major onto the XCDs
+    (xcd_unit): every (tile, member) is still computed exactly once, so costs and states
+    equal the plain (tile, member) grid bit for bit -- including grids whose size is not a multiple of
+    8 and single-member models (which never remap)."""
     from mbrl_amd import _lib
     p = ocem.synth_problem(cid, N=N, H=H)
     a = p["cfg"]["a"]
     A = cem_actions(np.zeros((H, a), np.float32), np.full((H, a), 0.5, np.float32), -1, 1, 7, 0, np.arange(N))
     prob = device_problem(p)
-    c_map, s_map = _rollout(prob, p, N, H, m, A)
-    with _lib.option("no_xcd_map", 1):
-        c_plain, s_plain = _rollout(prob, p, N, H, m, A)
+    c_plain, s_plain = _rollout(prob, p, N, H, m, A)
+    with _lib.option("xcd_map", 1):
+        c_map, s_map = _rollout(prob, p, N, H, m, A)
     assert torch.equal(c_map, c_plain) and torch.equal(s_map, s_plain)
     ref = ocem.ensemble_returns(ocem.rollout(p["model"], p["norm"], p["cost"], p["s0"], A[:, :48]))
     assert rel_err(c_map.mean(0)[:48] if p["cfg"]["E"] > 1 else c_map[0, :48], ref) < RTOL
@@ -125,8 +125,8 @@ def test_m4_matches_m16_bitwise_and_the_oracle(cid, N, H, over):
 
 
 def test_cartpole_plan_equal_for_every_tile_height():
-    """BASELINE config 2 (cartpole N=1024, H=20) picks 4-candidate tiles; the whole plan is the same
-    with 4, 8 and 16 candidates per workgroup."""
+    """BASELINE config 2 (cartpole N=1024, H=20): the whole plan is the same with 4, 8 and 16
+    candidates per workgroup."""
     from mbrl_amd import CEMPlanner, _lib
     p = ocem.synth_problem(2)
     _, model_fn, cost_fn, sample_action = build(p)

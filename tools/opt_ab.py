@@ -1,5 +1,7 @@
 """A/B of one mbrl_set_option switch on a BASELINE config: plan wall time and the rollout kernel's
-HIP-event time, option off vs on, interleaved. Usage: python tools/opt_ab.py <option> <config_id> [reps]"""
+HIP-event time for each value, interleaved over three rounds.
+Usage: python tools/opt_ab.py <option> <config_id> [reps] [values, default "1,0"]
+<option> "staging" toggles planners.HOST_STAGING (the plan's mapped pinned host staging) instead."""
 import json
 import os
 import sys
@@ -10,12 +12,29 @@ sys.path[:0] = [REPO, os.path.join(REPO, "mujoco-mbrl_amd")]
 
 import torch  # noqa: E402
 
-from mbrl_amd import CEMPlanner, _lib, fused, synthetic  # noqa: E402
+import contextlib  # noqa: E402
+
+from mbrl_amd import CEMPlanner, _lib, fused, planners, synthetic  # noqa: E402
+
+
+@contextlib.contextmanager
+def setting(opt, val):
+    if opt == "staging":
+        prev = planners.HOST_STAGING
+        planners.HOST_STAGING = bool(val)
+        try:
+            yield
+        finally:
+            planners.HOST_STAGING = prev
+    else:
+        with _lib.option(opt, val):
+            yield
 
 
 def main():
     opt, cid = sys.argv[1], int(sys.argv[2])
     reps = int(sys.argv[3]) if len(sys.argv) > 3 else 40
+    values = [int(v) for v in (sys.argv[4] if len(sys.argv) > 4 else "1,0").split(",")]
     p = synthetic.make_problem(cid)
     cfg = p["cfg"]
     kw = dict(num_candidates=cfg["N"], num_iterations=5, seed=p["rng_seed"], device="cuda:0")
@@ -25,8 +44,8 @@ def main():
     s0 = torch.as_tensor(p["s0"], dtype=torch.float32, device="cuda:0")
     out = {}
     for rnd in range(3):
-        for val in (1, 0):
-            with _lib.option(opt, val):
+        for val in values:
+            with setting(opt, val):
                 for _ in range(3):
                     CEMPlanner.plan(p["s0"], p["model"], p["cost"], p["sample_action"], cfg["H"], **kw)
                 torch.cuda.synchronize()
