@@ -228,7 +228,10 @@ int mbrl_trajectory(const mbrl_mlp_shape* shape, const void* packed, const mbrl_
  * states_out: [H][s] rollout of actions_out (ensemble mean over members).
  * cost_hist [I][E][N], returns_hist [I][N], elite_hist [I][K]: optional per-iteration records (NULL = off).
  * rollout_events: NULL or 2*I events; pair i brackets iteration i's rollout launch on `stream`
- * (a NULL pair skips iteration i: each record leaves the GPU idle a few microseconds). */
+ * (a NULL pair skips iteration i: each record leaves the GPU idle a few microseconds).
+ * s0 [s] is read once, by the plan's first launch (into the workspace), and mu / sigma / actions_out /
+ * states_out are written by its last launches only: all five may be device memory or mapped host
+ * memory from mbrl_host_alloc (ABI v7; plan() on host tensors with no copy launch around it). */
 size_t mbrl_cem_workspace_bytes(const mbrl_mlp_shape* shape, const mbrl_cem_params* params);
 int mbrl_cem_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_norm* norm,
                   const mbrl_cost* cost, const float* s0, const mbrl_cem_params* params,
