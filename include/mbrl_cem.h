@@ -155,7 +155,8 @@ enum {
     MBRL_OPT_UNFUSED_UPDATE = 5,    /* 1: plans run select / refit / proposal draw as separate launches */
     MBRL_OPT_ADAM_ARITH = 6,        /* mbrl_adam_step contraction pattern: 0 = torch's; 1 + bits (test) */
     MBRL_OPT_XCD_MAP = 7,           /* 1: ensemble rollouts map workgroups member-major per XCD (A/B) */
-    MBRL_OPT_COUNT = 8
+    MBRL_OPT_TRAIN_TILE = 8,        /* training backward C tile height: 0 auto, 32, 64 (bit-identical) */
+    MBRL_OPT_COUNT = 9
 };
 int mbrl_set_option(int32_t option, int32_t value);
 int mbrl_get_option(int32_t option);

@@ -57,6 +57,8 @@ static int device_cus() {
     return n;
 }
 
+int device_cu_count() { return device_cus(); }
+
 hipError_t ensure_dynamic_lds(const void* fn, int bytes) {
     static std::mutex mu;
     static std::set<std::tuple<const void*, int, int>> done;
@@ -1287,6 +1289,7 @@ int mbrl_set_option(int32_t option, int32_t value) {
         case MBRL_OPT_ROLLOUT_TILE: ok = value == 0 || value == 4 || value == 8 || value == 16; break;
         case MBRL_OPT_SPLIT_TILE: ok = value == 0 || value == 16 || value == 32; break;
         case MBRL_OPT_ADAM_ARITH: ok = value >= 0 && value <= 16; break;
+        case MBRL_OPT_TRAIN_TILE: ok = value == 0 || value == 32 || value == 64; break;
         default: ok = value == 0 || value == 1; break;
     }
     if (!ok) return fail(MBRL_EINVAL, "option %d: value %d not allowed", option, value);
@@ -1496,6 +1499,7 @@ static int train_shape(const mbrl_train_model* m, TrainShape* t) {
                     m->state_dim, m->action_dim, m->hidden, m->n_hidden, m->horizon, m->reward_head);
     t->s = m->state_dim; t->a = m->action_dim; t->W = m->hidden; t->L = m->n_hidden; t->reward = m->reward_head;
     t->H = m->horizon;
+    t->tile = g_opt[MBRL_OPT_TRAIN_TILE].load(std::memory_order_relaxed);
     return MBRL_OK;
 }
 

@@ -233,6 +233,9 @@ inline size_t rollout_lds_bytes(const RolloutArgs& A, int M) {
     return need > floor_bytes ? need : floor_bytes;
 }
 
+// Compute units of the current device (cached; cem.hip).
+int device_cu_count();
+
 // Raise `fn`'s dynamic-LDS limit to `bytes` on the current device, once per (kernel, device,
 // bytes); thread-safe (cem.hip).
 hipError_t ensure_dynamic_lds(const void* fn, int bytes);
@@ -338,6 +341,7 @@ hipError_t launch_adam_step(const mbrl_adam_tensor* tensors, int count, const mb
 // mbrl_train_grads (train.hip): the MLP's loss gradient for one batch, n_hidden + 2 launches.
 struct TrainShape {
     int s, a, W, L, reward, H;   // state / action dims, hidden width, hidden layers, reward head, horizon
+    int tile;                    // backward C tile height: 0 auto, 32, 64 (MBRL_OPT_TRAIN_TILE; same bits)
 };
 struct TrainTensors {
     const float* const* weight;  // L + 1 (+ 1 reward head) nn.Linear weights [out][in]

@@ -282,25 +282,29 @@ __device__ __forceinline__ void stash_input(const GemmLaunch& L, const GemmDesc&
         if (m < D.M && k0 + e < D.K) L.xstore[(int64_t)m * D.K + k0 + e] = v[e];
 }
 
-template <int NW, int AK, int BK>
-__device__ void gemm_tile(const GemmLaunch& L, const GemmDesc& D, int tile, float (*red)[TT][TT + 1]) {
+// TMX = 1: 32 x 32 C tiles; TMX = 2: 64 x 32 (the W x W backward products, so that a launch's tiles
+// fit one round of the CUs). Each element's K order is the same for both (the K split over the waves
+// depends on K and NW only), so the tile height never changes a bit of the result.
+template <int NW, int AK, int BK, int TMX>
+__device__ void gemm_tile(const GemmLaunch& L, const GemmDesc& D, int tile, float (*red)[TT * TMX][TT + 1]) {
     constexpr int NT = 64 * NW;
+    constexpr int TM = TT * TMX;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, q = lane >> 4, c = lane & 15;
-    const int tm = tile / D.tiles_n, m0 = tm * TT, n0 = (tile % D.tiles_n) * TT;
+    const int tm = tile / D.tiles_n, m0 = tm * TM, n0 = (tile % D.tiles_n) * TT;
     const bool stash = AK == OP_GATHER && L.xstore != nullptr && n0 == 0;
     // wave w takes the w-th of NW contiguous K ranges (in 16-deep chunks): a few chunks per wave, so
     // the loads' latency is paid about once per wave instead of once per chunk
     const int chunks = (D.K + 15) >> 4, per = (chunks + NW - 1) / NW;
     const int kb0 = wave * per * 16, kb1 = min(D.K, (wave + 1) * per * 16);
-    f32x4 acc[2][2];
+    f32x4 acc[2 * TMX][2];
 #pragma unroll
-    for (int x = 0; x < 2; ++x)
+    for (int x = 0; x < 2 * TMX; ++x)
 #pragma unroll
         for (int y = 0; y < 2; ++y) acc[x][y] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     // the epilogue's own operands (bias, ReLU mask, loss targets) are fetched before the K loop so
     // their latency overlaps the products'
     const Output& O = D.out;
-    constexpr int EPT = TT * TT / NT;       // C elements per thread in the epilogue
+    constexpr int EPT = TM * TT / NT;       // C elements per thread in the epilogue
     float pre[EPT];
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
@@ -318,15 +322,15 @@ __device__ void gemm_tile(const GemmLaunch& L, const GemmDesc& D, int tile, floa
     TSTAMP(1);
     // up to GROUP chunks' operands in flight at once, then their MFMAs: with the usual 1-4 chunks
     // per wave the loads' latency is paid once
-    constexpr int GROUP = NW == 16 ? 2 : 4;
+    constexpr int GROUP = NW == 16 ? (TMX == 2 ? 1 : 2) : 4;   // TMX 2 at 16 waves: the 128-VGPR budget
     for (int g0 = kb0; g0 < kb1; g0 += 16 * GROUP) {
-        f32x4 a[GROUP][2], b[GROUP][2];
+        f32x4 a[GROUP][2 * TMX], b[GROUP][2];
 #pragma unroll
         for (int u = 0; u < GROUP; ++u) {
             const int kb = g0 + 16 * u;
             if (kb >= kb1) break;
 #pragma unroll
-            for (int x = 0; x < 2; ++x) {
+            for (int x = 0; x < 2 * TMX; ++x) {
                 a[u][x] = load_operand<AK>(L, D.A, m0 + 16 * x + c, kb + 4 * q, D.K);
                 if (stash) stash_input(L, D, a[u][x], m0 + 16 * x + c, kb + 4 * q);
             }
@@ -339,7 +343,7 @@ __device__ void gemm_tile(const GemmLaunch& L, const GemmDesc& D, int tile, floa
 #pragma unroll
             for (int s = 0; s < 4; ++s)
 #pragma unroll
-                for (int x = 0; x < 2; ++x)
+                for (int x = 0; x < 2 * TMX; ++x)
 #pragma unroll
                     for (int y = 0; y < 2; ++y)
                         acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][x][s], b[u][y][s], acc[x][y], 0, 0, 0);
@@ -348,7 +352,7 @@ __device__ void gemm_tile(const GemmLaunch& L, const GemmDesc& D, int tile, floa
     TSTAMP(2);
     // lane l holds C rows 16x + 4q + v, column 16y + c
 #pragma unroll
-    for (int x = 0; x < 2; ++x)
+    for (int x = 0; x < 2 * TMX; ++x)
 #pragma unroll
         for (int y = 0; y < 2; ++y)
 #pragma unroll
@@ -396,7 +400,7 @@ __device__ void gemm_tile(const GemmLaunch& L, const GemmDesc& D, int tile, floa
                              L.hp, L.arith);
         }
     }
-    if (O.mode == EPI_MASK || O.mode == EPI_LOSS) {   // per-row-tile column sums (the next bias gradient)
+    if (O.mode == EPI_MASK || O.mode == EPI_LOSS) {   // per-32-row-tile column sums (the next bias gradient)
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < EPT; ++j) {
@@ -404,10 +408,11 @@ __device__ void gemm_tile(const GemmLaunch& L, const GemmDesc& D, int tile, floa
             red[0][e >> 5][e & 31] = keep[j];
         }
         __syncthreads();
-        if (tid < TT && n0 + tid < D.N) {
-            float t = red[0][0][tid];
-            for (int r = 1; r < TT; ++r) t = t + red[0][r][tid];
-            O.colsum_out[(int64_t)tm * D.N + n0 + tid] = t;
+        const int sub = tid / TT, col = tid - (tid / TT) * TT;
+        if (tid < TM && n0 + col < D.N && m0 + TT * sub < D.M) {
+            float t = red[0][TT * sub][col];
+            for (int r = 1; r < TT; ++r) t = t + red[0][TT * sub + r][col];
+            O.colsum_out[(int64_t)(tm * TMX + sub) * D.N + n0 + col] = t;
         }
     }
     if (O.mode == EPI_LOSS) {   // the tile's loss: a butterfly per wave, then the waves in order
@@ -434,20 +439,20 @@ __device__ void gemm_tile(const GemmLaunch& L, const GemmDesc& D, int tile, floa
 
 // NW waves per workgroup; A0/B0 (A1/B1): operand kinds of the launch's first (second) product, fixed
 // at compile time so each instantiation carries only its own load paths.
-template <int NW, int A0, int B0, int A1, int B1>
+template <int NW, int A0, int B0, int A1, int B1, int TMX>
 __global__ __launch_bounds__(64 * NW) void train_gemm_kernel(const GemmLaunch L) {
-    __shared__ float red[NW][TT][TT + 1];
+    __shared__ float red[NW][TT * TMX][TT + 1];
     TSTAMP(0);
     // (constant indices only: a dynamic index into the kernel arguments would copy them to scratch)
     const int b = blockIdx.x;
     if (b < L.d[0].tiles) {
-        gemm_tile<NW, A0, B0>(L, L.d[0], b, red);
+        gemm_tile<NW, A0, B0, TMX>(L, L.d[0], b, red);
         return;
     }
     int r = b - L.d[0].tiles;
     if constexpr (A1 >= 0) {
         if (L.nd > 1 && r < L.d[1].tiles) {
-            gemm_tile<NW, A1, B1>(L, L.d[1], r, red);
+            gemm_tile<NW, A1, B1, TMX>(L, L.d[1], r, red);
             return;
         }
         if (L.nd > 1) r -= L.d[1].tiles;
@@ -490,14 +495,15 @@ static Operand transposed(const float* p0, const float* p1, int split, int ld, i
     return o;
 }
 
-static void finish(GemmDesc& D, int M, int N, int K) {
+static void finish(GemmDesc& D, int M, int N, int K, int tmx = 1) {
     D.M = M; D.N = N; D.K = K;
     D.tiles_n = (N + TT - 1) / TT;
-    D.tiles = ((M + TT - 1) / TT) * D.tiles_n;
+    D.tiles = ((M + TT * tmx - 1) / (TT * tmx)) * D.tiles_n;
 }
 
 // 16 waves split a long K (the hidden layers, every weight gradient); 4 suffice for short ones.
-template <int A0, int B0, int A1 = -1, int B1 = -1>
+// TMX: the C tile height of every product of the launch (finish() with the same tmx).
+template <int A0, int B0, int A1 = -1, int B1 = -1, int TMX = 1>
 static hipError_t launch_gemm(GemmLaunch& L, bool loss_wg, hipStream_t stream) {
     int blocks = loss_wg ? 1 : 0, kmax = 0;
     for (int i = 0; i < L.nd; ++i) {
@@ -515,10 +521,14 @@ static hipError_t launch_gemm(GemmLaunch& L, bool loss_wg, hipStream_t stream) {
     blocks += L.adam_blocks;
     if (!loss_wg) L.loss_out = nullptr;
     ++L.slot;
-    if (kmax >= 256)
-        hipLaunchKernelGGL((train_gemm_kernel<16, A0, B0, A1, B1>), dim3(blocks), dim3(64 * 16), 0, stream, L);
-    else
-        hipLaunchKernelGGL((train_gemm_kernel<4, A0, B0, A1, B1>), dim3(blocks), dim3(64 * 4), 0, stream, L);
+    if constexpr (TMX == 2) {   // chosen only for long K (launch_train_grads): 16 waves
+        if (kmax < 256) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((train_gemm_kernel<16, A0, B0, A1, B1, TMX>), dim3(blocks), dim3(64 * 16), 0, stream, L);
+    } else if (kmax >= 256) {
+        hipLaunchKernelGGL((train_gemm_kernel<16, A0, B0, A1, B1, TMX>), dim3(blocks), dim3(64 * 16), 0, stream, L);
+    } else {
+        hipLaunchKernelGGL((train_gemm_kernel<4, A0, B0, A1, B1, TMX>), dim3(blocks), dim3(64 * 4), 0, stream, L);
+    }
     return hipGetLastError();
 }
 
@@ -613,6 +623,12 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
         const float* g_in = out_layer ? B.dy : B.dh[l % 2];   // dL/d(pre-activation of layer l), [R][n_out]
         const float* cs_in = out_layer ? B.cs_dy : B.cs_dh[l % 2];
         const int n_out = out_layer ? J : W, n_in = l == 0 ? K0 : W;
+        // 64-row tiles when the launch's 32 x 32 tiles would need a second round of the CUs
+        // (2 x 512: dH_0 and dW_1 are 256 tiles each); the tile height changes no bit
+        const int tiles32 = (l >= 1 ? tiles_r * ((W + TT - 1) / TT) : 0) +
+                            ((n_out + TT - 1) / TT) * ((n_in + TT - 1) / TT);
+        int tmx = (l >= 1 && tiles32 > device_cu_count() && (n_out >= 256 || R >= 256)) ? 2 : 1;
+        if (t.tile == 32 || (t.tile == 64 && l >= 1 && (n_out >= 256 || R >= 256))) tmx = t.tile / 32;
         G.nd = 0;
         if (l >= 1) {           // dH_{l-1} = (g_in W_l) * (H_{l-1} > 0), and its column sums
             GemmDesc& D = G.d[G.nd++];
@@ -621,7 +637,7 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
             D.B = out_layer ? transposed(w.weight[L], wo_r, t.s, W, W, -1) : transposed(w.weight[l], nullptr, 0, W, W, -1);
             D.out.mode = EPI_MASK; D.out.c0 = D.out.c1 = B.dh[(l - 1) % 2]; D.out.split = R; D.out.ldc = W;
             D.out.mask = B.act[l - 1]; D.out.ldm = W; D.out.colsum_out = B.cs_dh[(l - 1) % 2];
-            finish(D, R, W, n_out);
+            finish(D, R, W, n_out, tmx);
         }
         {                       // dW_l = g_in^T X_l; db_l = the column sums of g_in over the row tiles
             GemmDesc& D = G.d[G.nd++];
@@ -638,7 +654,7 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
                 O.c0 = O.c1 = w.weight_grad[l]; O.split = n_out;
                 O.g0 = O.g1 = w.bias_grad[l];
             }
-            finish(D, n_out, n_in, R);
+            finish(D, n_out, n_in, R, tmx);
         }
         if (adam && l == 0) {   // nothing in this launch reads layer 0's parameters: step them in place
             G.d[G.nd - 1].out.adam = 1;
@@ -653,8 +669,9 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
             for (int i = 0; i < n; ++i) G.adam_t[G.adam_count++] = adam[first + i];
         }
         G.loss_part = B.loss_part; G.loss_parts = loss_parts; G.loss_out = loss_out;
-        e = l >= 1 ? launch_gemm<OP_DIRECT, OP_TRANS, OP_TRANS, OP_TRANS>(G, false, stream)
-                   : launch_gemm<OP_TRANS, OP_TRANS>(G, loss_out != nullptr, stream);
+        e = l == 0    ? launch_gemm<OP_TRANS, OP_TRANS>(G, loss_out != nullptr, stream)
+            : tmx == 2 ? launch_gemm<OP_DIRECT, OP_TRANS, OP_TRANS, OP_TRANS, 2>(G, false, stream)
+                       : launch_gemm<OP_DIRECT, OP_TRANS, OP_TRANS, OP_TRANS>(G, false, stream);
         if (e != hipSuccess) return e;
     }
     return hipSuccess;

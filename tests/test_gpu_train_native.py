@@ -198,3 +198,28 @@ def test_native_gradients_random_shapes(case):
         scale = float(y.abs().max())
         assert torch.allclose(x, y, rtol=1e-4, atol=1e-4 * scale + 1e-12), (i, s, a, W, L, H, B)
     assert abs(float(loss) - float(ref_loss)) <= 1e-5 * abs(float(ref_loss)) + 1e-12
+
+
+@pytest.mark.parametrize("kind,s,a,W,L,H,B", [("model", 17, 6, 512, 2, 1, 512), ("model", 24, 8, 512, 3, 2, 300),
+                                             ("reward", 17, 6, 512, 2, 1, 512), ("model", 5, 1, 256, 2, 1, 1000)])
+def test_backward_tile_height_is_bitwise_neutral(kind, s, a, W, L, H, B):
+    """The W x W backward products run on 64 x 32 C tiles when 32 x 32 tiles would need a second round
+    of the CUs (2 x 512 at batch 512: dH_0 and dW_1 are 256 tiles each). Every element keeps its K
+    order (the K split over the 16 waves does not depend on the tile), so gradients and losses equal
+    the 32-row path (MBRL_OPT_TRAIN_TILE = 32) bit for bit, as do the epoch's fused Adam steps."""
+    from mbrl_amd import _lib, models
+    ds = _dataset(s, a, H, max(3 * B, 60), seed=s * 7 + W)
+    m = _model(kind, s, a, W, L, seed=W)
+    _, ins, outs = ds.stacked(DEV)
+    reward = kind == "reward"
+    idx = torch.randperm(ds.num_transitions(), generator=torch.Generator().manual_seed(B))[:B].to(DEV)
+    res = {}
+    for tile in (32, 64, 0):
+        with _lib.option("train_tile", tile):
+            nat = models._NativeGrads(m, ins, outs, ds.horizon, B, reward)
+            loss, parts = nat.run(idx)
+            torch.cuda.synchronize()
+            res[tile] = [loss.clone()] + [p.grad.clone() for p in m.parameters()]
+    for tile in (64, 0):
+        for x, y in zip(res[tile], res[32]):
+            assert torch.equal(x, y), tile
