@@ -161,6 +161,16 @@ enum {
 int mbrl_set_option(int32_t option, int32_t value);
 int mbrl_get_option(int32_t option);
 
+/* ---- multi-GPU (the reference has no distributed code): an RCCL communicator the
+ * library owns. mbrl_comm_unique_id on one rank, the MBRL_COMM_ID_BYTES broadcast to the others by the
+ * caller (torch.distributed), then mbrl_comm_init on every rank at once (collective), with the rank's
+ * GPU current. */
+#define MBRL_COMM_ID_BYTES 128
+typedef void* mbrl_comm_t;
+int mbrl_comm_unique_id(void* id_out);
+int mbrl_comm_init(const void* id, int32_t nranks, int32_t rank, mbrl_comm_t* comm_out);
+int mbrl_comm_destroy(mbrl_comm_t comm);
+
 /* ---- host staging: mapped, coherent pinned host memory (hipHostMalloc Mapped | Coherent) that the
  * kernels read and write directly. plan() (planners.py:14-25) takes its initial state from the host and
  * returns host tensors; passing mbrl_cem_plan a staged s0 and staged outputs replaces the two
@@ -240,6 +250,20 @@ int mbrl_cem_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_no
                   float* cost_hist, float* returns_hist, int64_t* elite_hist,
                   mbrl_event_t* rollout_events, void* workspace, size_t ws_bytes,
                   mbrl_stream_t stream);
+
+/* ---- the same plan sharded over `nranks` GPUs, one call per rank: rank r rolls out global candidates
+ * [r N / nranks, (r + 1) N / nranks) (proposals keyed by the global index), every iteration all-gathers
+ * the [E][N / nranks] costs over `comm` as a step on `stream` (ncclAllGather), then every rank runs the
+ * same selection over all N, the same refit and draws its own shard of the next proposals. Outputs are
+ * bit-identical on every rank and to mbrl_cem_plan's for any nranks (records as mbrl_cem_plan's, over
+ * all N). Replaces planners.cem_sharded_protocol's per-iteration Python loop. N % nranks == 0. */
+size_t mbrl_cem_plan_sharded_workspace_bytes(const mbrl_mlp_shape* shape, const mbrl_cem_params* params,
+                                             int32_t nranks);
+int mbrl_cem_plan_sharded(const mbrl_mlp_shape* shape, const void* packed, const mbrl_norm* norm,
+                          const mbrl_cost* cost, const float* s0, const mbrl_cem_params* params, mbrl_comm_t comm,
+                          int32_t nranks, int32_t rank, float* mu, float* sigma, float* actions_out,
+                          float* states_out, float* cost_hist, float* returns_hist, int64_t* elite_hist,
+                          mbrl_event_t* rollout_events, void* workspace, size_t ws_bytes, mbrl_stream_t stream);
 
 /* ---- batched planning: B independent CEM plans, one per initial state s0[b] (parallel environments
  * feeding one GPU planner), in shared launches: one proposal draw, one rollout

@@ -5,6 +5,7 @@
 #include <stdint.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <string.h>
 
 #include <atomic>
 #include <map>
@@ -17,6 +18,7 @@
 
 #include "../../include/mbrl_cem.h"
 #include "mbrl_internal.h"
+#include <rccl/rccl.h>
 #include "mbrl_rng.h"
 
 namespace mbrl {
@@ -965,6 +967,16 @@ __global__ void finalize_kernel(const float* __restrict__ mu_src, const float* _
     }
 }
 
+// Sharded plans: the all-gathered costs arrive rank-major [G][E][Nl]; the selection reads [E][N] with
+// candidate r * Nl + j of member e at e * N + r * Nl + j.
+__global__ void shard_costs_kernel(const float* __restrict__ gathered, int G, int E, int Nl, float* __restrict__ costs) {
+    const size_t total = (size_t)G * E * Nl;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t r = i / ((size_t)E * Nl), rem = i - r * E * Nl, e = rem / Nl, j = rem - e * Nl;
+        costs[e * (size_t)G * Nl + r * Nl + j] = gathered[i];
+    }
+}
+
 __global__ void member_mean_kernel(const float* __restrict__ src, int E, int n, float* __restrict__ dst) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) {
@@ -1750,6 +1762,173 @@ int mbrl_cem_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_no
                            states_out);
     }
     return hip_check(hipGetLastError(), "plan launch");
+}
+
+// ---- multi-GPU: an RCCL communicator owned by the library, and the sharded plan as
+// one call with the all-gather as a stream-ordered step.
+static int nccl_check(ncclResult_t r, const char* what) {
+    if (r == ncclSuccess) return MBRL_OK;
+    return fail(MBRL_EHIP, "%s: %s", what, ncclGetErrorString(r));
+}
+
+int mbrl_comm_unique_id(void* id_out) {
+    static_assert(sizeof(ncclUniqueId) == MBRL_COMM_ID_BYTES, "ncclUniqueId size");
+    if (!id_out) return fail(MBRL_EINVAL, "comm_unique_id: NULL");
+    ncclUniqueId id;
+    if (int rc = nccl_check(ncclGetUniqueId(&id), "ncclGetUniqueId")) return rc;
+    memcpy(id_out, &id, sizeof(id));
+    return MBRL_OK;
+}
+
+int mbrl_comm_init(const void* id, int32_t nranks, int32_t rank, mbrl_comm_t* comm_out) {
+    if (!id || !comm_out || nranks < 1 || rank < 0 || rank >= nranks)
+        return fail(MBRL_EINVAL, "comm_init: bad arguments (nranks %d, rank %d)", nranks, rank);
+    ncclUniqueId u;
+    memcpy(&u, id, sizeof(u));
+    ncclComm_t c = nullptr;
+    if (int rc = nccl_check(ncclCommInitRank(&c, nranks, u, rank), "ncclCommInitRank")) return rc;
+    *comm_out = reinterpret_cast<mbrl_comm_t>(c);
+    return MBRL_OK;
+}
+
+int mbrl_comm_destroy(mbrl_comm_t comm) {
+    return comm ? nccl_check(ncclCommDestroy(reinterpret_cast<ncclComm_t>(comm)), "ncclCommDestroy") : MBRL_OK;
+}
+
+struct ShardWs {
+    float *local, *gathered, *costs, *actions, *mu[2], *sigma[2], *aelite, *states, *s0;
+    unsigned long long* xchg;
+    unsigned* status;
+    size_t xchg_bytes;
+    int64_t* elites;
+    uint32_t* keys;
+    size_t bytes;
+};
+
+static ShardWs shard_ws(const Geometry& g, const mbrl_cem_params* p, int G, void* base) {
+    ShardWs w{};
+    char* b = static_cast<char*>(base);
+    size_t o = 0;
+    auto take = [&](size_t n) { void* r = b ? b + o : nullptr; o += align256(n); return r; };
+    const int Nl = p->N / G;
+    const size_t Ha = (size_t)p->H * g.a;
+    w.xchg_bytes = (size_t)g.E * 2 * g.Wpad * 8;
+    w.xchg = (unsigned long long*)take(w.xchg_bytes);   // the trajectory hand-off block, status right behind
+    w.status = (unsigned*)take(16);
+    w.local = (float*)take((size_t)g.E * Nl * 4);
+    w.gathered = (float*)take((size_t)g.E * p->N * 4);
+    w.costs = (float*)take((size_t)g.E * p->N * 4);
+    w.actions = (float*)take((size_t)p->H * Nl * g.a * 4);
+    w.mu[0] = (float*)take(Ha * 4); w.mu[1] = (float*)take(Ha * 4);
+    w.sigma[0] = (float*)take(Ha * 4); w.sigma[1] = (float*)take(Ha * 4);
+    w.aelite = (float*)take((size_t)p->H * p->K * g.a * 4);
+    w.states = (float*)take((size_t)g.E * p->H * g.s * 4);
+    w.elites = (int64_t*)take((size_t)p->K * 8);
+    w.keys = (uint32_t*)take((size_t)p->N * 4);
+    w.s0 = (float*)take((size_t)g.s * 4);
+    w.bytes = o;
+    return w;
+}
+
+size_t mbrl_cem_plan_sharded_workspace_bytes(const mbrl_mlp_shape* shape, const mbrl_cem_params* params,
+                                             int32_t nranks) {
+    Geometry g;
+    if (shape_geometry(shape, &g) != MBRL_OK || !params || nranks < 1 || params->N % nranks) return 0;
+    return shard_ws(g, params, nranks, nullptr).bytes;
+}
+
+int mbrl_cem_plan_sharded(const mbrl_mlp_shape* shape, const void* packed, const mbrl_norm* norm,
+                          const mbrl_cost* cost, const float* s0_in, const mbrl_cem_params* p, mbrl_comm_t comm,
+                          int32_t nranks, int32_t rank, float* mu, float* sigma, float* actions_out,
+                          float* states_out, float* cost_hist, float* returns_hist, int64_t* elite_hist,
+                          mbrl_event_t* rollout_events, void* workspace, size_t ws_bytes, mbrl_stream_t stream_) {
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
+    Geometry g;
+    int rc = shape_geometry(shape, &g);
+    if (rc) return rc;
+    if (!p || !comm) return fail(MBRL_EINVAL, "plan_sharded: NULL params or comm");
+    if (p->N < 1 || p->H < 1 || p->K < 1 || p->K > p->N || p->iterations < 1)
+        return fail(MBRL_EINVAL, "bad CEM params N=%d H=%d K=%d I=%d", p->N, p->H, p->K, p->iterations);
+    if (nranks < 1 || rank < 0 || rank >= nranks || p->N % nranks)
+        return fail(MBRL_EINVAL, "plan_sharded: N=%d over %d ranks (rank %d)", p->N, nranks, rank);
+    if (!actions_out || !states_out || !workspace || !s0_in)
+        return fail(MBRL_EINVAL, "plan_sharded: s0/actions_out/states_out/workspace NULL");
+    const ShardWs w = shard_ws(g, p, nranks, workspace);
+    if (ws_bytes < w.bytes) return fail(MBRL_EWORKSPACE, "workspace %zu < %zu", ws_bytes, w.bytes);
+    const int N = p->N, Nl = N / nranks, H = p->H, a = g.a, E = g.E, Ha = H * a;
+    const int off = rank * Nl;   // this rank's global candidates [off, off + Nl)
+    const bool fuse = update_kpt(N, p->K, a) != 0 && g_opt[MBRL_OPT_UNFUSED_UPDATE].load(std::memory_order_relaxed) == 0;
+    const bool fuse_draw = fuse && update_samples(Nl, a);
+    // distribution rows, the workspace copy of s0, iteration 0's proposals of this shard
+    hipLaunchKernelGGL(fill2_kernel, dim3((Ha + 255) / 256), dim3(256), 0, stream, w.mu[0], p->init_mu, w.sigma[0],
+                       p->init_sigma, Ha);
+    hipLaunchKernelGGL(copy_kernel, dim3(1), dim3(64), 0, stream, s0_in, (size_t)g.s, w.s0);
+    mbrl_sampler sp0{};
+    sp0.seed = p->seed; sp0.iteration = 0; sp0.mu = w.mu[0]; sp0.sigma = w.sigma[0]; sp0.lo = p->lo; sp0.hi = p->hi;
+    if ((rc = sample_impl(&sp0, H, a, Nl, off, w.actions, stream))) return rc;
+    int cur = 0;
+    for (int it = 0; it < p->iterations; ++it) {
+        mbrl_sampler sp{};
+        sp.seed = p->seed; sp.iteration = it; sp.mu = w.mu[cur]; sp.sigma = w.sigma[cur]; sp.lo = p->lo; sp.hi = p->hi;
+        if (rollout_events && rollout_events[2 * it] &&
+            (rc = hip_check(hipEventRecord(reinterpret_cast<hipEvent_t>(rollout_events[2 * it]), stream), "event")))
+            return rc;
+        rc = rollout_impl(g, packed, norm, cost, w.s0, 0, w.actions, nullptr, Nl, H, 0, w.local, nullptr, nullptr,
+                          stream);
+        if (rc) return rc;
+        if (rollout_events && rollout_events[2 * it + 1] &&
+            (rc = hip_check(hipEventRecord(reinterpret_cast<hipEvent_t>(rollout_events[2 * it + 1]), stream), "event")))
+            return rc;
+        // the one collective of an iteration: every rank's [E][Nl] costs, rank-major
+        if ((rc = nccl_check(ncclAllGather(w.local, w.gathered, (size_t)E * Nl, ncclFloat,
+                                           reinterpret_cast<ncclComm_t>(comm), stream), "ncclAllGather")))
+            return rc;
+        float* costs = w.gathered;
+        if (E > 1) {   // (one rank: the identity)
+            hipLaunchKernelGGL(shard_costs_kernel, dim3(256), dim3(256), 0, stream, w.gathered, nranks, E, Nl, w.costs);
+            costs = w.costs;
+        }
+        if (cost_hist && (rc = hip_check(hipMemcpyAsync(cost_hist + (size_t)it * E * N, costs, (size_t)E * N * 4,
+                                                        hipMemcpyDeviceToDevice, stream), "cost record")))
+            return rc;
+        int64_t* elites = elite_hist ? elite_hist + (size_t)it * p->K : w.elites;
+        float* rets = returns_hist ? returns_hist + (size_t)it * N : nullptr;
+        const bool last = it + 1 == p->iterations;
+        if (fuse) {
+            UpdateArgs U{};
+            U.costs = costs; U.E = E; U.N = N; U.K = p->K; U.member_stride = N; U.H = H; U.a = a;
+            U.elite_out = elites; U.returns_out = rets;
+            U.seed = p->seed; U.iteration = it; U.mu = w.mu[cur]; U.sigma = w.sigma[cur];
+            U.lo = p->lo; U.hi = p->hi; U.alpha = p->alpha; U.oma = 1.0f - p->alpha;
+            U.mu_out = w.mu[cur ^ 1]; U.sigma_out = w.sigma[cur ^ 1];
+            U.fin_mu = last ? mu : nullptr; U.fin_sigma = last ? sigma : nullptr; U.fin_actions = last ? actions_out : nullptr;
+            U.next_actions = (fuse_draw && !last) ? w.actions : nullptr;   // this rank's shard of iteration it + 1
+            U.draw_off = off; U.draw_n = Nl;
+            rc = update_impl(U, 1, stream);
+        } else {
+            rc = select_impl(costs, E, N, p->K, MBRL_NAN_LAST, elites, rets, w.keys, align256((size_t)N * 4), stream);
+            if (rc) return rc;
+            rc = refit_impl(&sp, H, a, elites, p->K, p->alpha, w.aelite, w.mu[cur ^ 1], w.sigma[cur ^ 1], stream,
+                            last ? mu : nullptr, last ? sigma : nullptr, last ? actions_out : nullptr);
+        }
+        if (rc) return rc;
+        cur ^= 1;
+        if (!last && !fuse_draw) {
+            mbrl_sampler sn = sp;
+            sn.iteration = it + 1; sn.mu = w.mu[cur]; sn.sigma = w.sigma[cur];
+            if ((rc = sample_impl(&sn, H, a, Nl, off, w.actions, stream))) return rc;
+        }
+    }
+    // the final mean's states, on every rank (the same on each)
+    float* per_member = E == 1 ? states_out : w.states;
+    rc = traj_impl(g, packed, norm, w.s0, actions_out, H, per_member, w.xchg, w.xchg_bytes, w.status, stream);
+    if (rc) return rc;
+    if (E > 1) {
+        const int Hs = H * g.s;
+        hipLaunchKernelGGL(member_mean_kernel, dim3((Hs + 255) / 256), dim3(256), 0, stream, w.states, E, Hs,
+                           states_out);
+    }
+    return hip_check(hipGetLastError(), "sharded plan launch");
 }
 
 #ifdef MBRL_STAMPS

@@ -19,6 +19,7 @@ LIB_PATH = os.environ.get("MBRL_AMD_LIB") or os.path.join(os.path.dirname(os.pat
                                                           "libmbrl_cem.so")
 
 MBRL_OK = 0
+MBRL_COMM_ID_BYTES = 128
 MBRL_EUNSUPPORTED = -2
 MBRL_COST_GOAL_STATE = 0
 MBRL_COST_MODEL_REWARD = 1
@@ -52,7 +53,8 @@ EXPORTED = (
     "mbrl_cem_plan_batch_workspace_bytes", "mbrl_cem_plan_batch", "mbrl_gd_workspace_bytes", "mbrl_gd_plan",
     "mbrl_cem_update", "mbrl_adam_step", "mbrl_train_workspace_bytes", "mbrl_train_grads",
     "mbrl_train_epoch", "mbrl_gd_batch_workspace_bytes", "mbrl_gd_plan_batch", "mbrl_host_alloc",
-    "mbrl_host_free",
+    "mbrl_host_free", "mbrl_comm_unique_id", "mbrl_comm_init", "mbrl_comm_destroy",
+    "mbrl_cem_plan_sharded_workspace_bytes", "mbrl_cem_plan_sharded",
 )
 
 
@@ -162,6 +164,13 @@ def load():
                                        c_int32, POINTER(AdamHparams), P, P, P, P, c_size_t, P]),
         "mbrl_cem_plan": (c_int32, [POINTER(MlpShape), P, POINTER(Norm), POINTER(Cost), P, POINTER(CemParams),
                                     P, P, P, P, P, P, P, P, P, c_size_t, P]),
+        "mbrl_comm_unique_id": (c_int32, [P]),
+        "mbrl_comm_init": (c_int32, [P, c_int32, c_int32, POINTER(c_void_p)]),
+        "mbrl_comm_destroy": (c_int32, [P]),
+        "mbrl_cem_plan_sharded_workspace_bytes": (c_size_t, [POINTER(MlpShape), POINTER(CemParams), c_int32]),
+        "mbrl_cem_plan_sharded": (c_int32, [POINTER(MlpShape), P, POINTER(Norm), POINTER(Cost), P,
+                                            POINTER(CemParams), P, c_int32, c_int32, P, P, P, P, P, P, P, P, P,
+                                            c_size_t, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

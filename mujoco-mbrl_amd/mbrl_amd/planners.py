@@ -581,8 +581,73 @@ class _FusedShardOps:
         return fused.trajectory(self.prob, self.s0, actions, self.st["H"], workspace=self._traj_ws)
 
 
+# RCCL process groups run the sharded plan as ONE C call per plan (mbrl_cem_plan_sharded: the
+# all-gather is a step on the plan's stream); False, or a gloo group, runs cem_sharded_protocol's
+# per-iteration Python loop (the same plan bit for bit)
+SHARDED_NATIVE = True
+_COMMS = {}
+
+
+def _rccl_comm(dev, world, rank):
+    """The library's RCCL communicator for this process group (created once, collectively: rank 0's
+    unique id is broadcast through torch.distributed, then every rank joins)."""
+    import ctypes
+    import torch.distributed as dist
+    key = (str(dev), world, rank, id(dist.distributed_c10d._get_default_group()))
+    comm = _COMMS.get(key)
+    if comm is None:
+        lib = _lib.load()
+        obj = [None]
+        if rank == 0:
+            buf = ctypes.create_string_buffer(_lib.MBRL_COMM_ID_BYTES)
+            _lib.check(lib.mbrl_comm_unique_id(buf), "mbrl_comm_unique_id")
+            obj[0] = buf.raw
+        dist.broadcast_object_list(obj, src=0)
+        comm = ctypes.c_void_p()
+        _lib.check(lib.mbrl_comm_init(ctypes.c_char_p(obj[0]), world, rank, ctypes.byref(comm)), "mbrl_comm_init")
+        _COMMS[key] = comm
+    return comm
+
+
+def _cem_sharded_native(prob, s0, st, world, rank):
+    """mbrl_cem_plan_sharded: this rank's shard of the plan, every iteration's all-gather included, in
+    one C-ABI call on the current stream (the result is the single-GPU plan's, on every rank)."""
+    lib = _lib.load()
+    dev = prob.device
+    md = prob.mdesc
+    N, K, H, I = st["N"], st["K"], st["H"], st["I"]
+    a, s, E = md["a"], md["s"], md["E"]
+    params = _lib.CemParams(N, H, K, I, st["alpha"], st["lo"], st["hi"], 0.0, st["init_std"], 0,
+                            int(st["seed"]) & 0xFFFFFFFFFFFFFFFF)
+    need = lib.mbrl_cem_plan_sharded_workspace_bytes(fused.ctypes_ref(prob.shape), fused.ctypes_ref(params), world)
+    if need == 0:
+        raise ValueError(f"num_candidates {N} must divide evenly over {world} ranks")
+    ws = _workspace(("cem_sharded", str(dev)), need, dev)
+    comm = _rccl_comm(dev, world, rank)
+    buf = torch.empty(H * (s + 3 * a), dtype=torch.float32, device=dev)
+    both = buf[:H * (s + a)]
+    states, actions = both[:H * s].view(H, s), both[H * s:].view(H, a)
+    mu, sigma = buf[H * (s + a):H * (s + 2 * a)].view(H, a), buf[H * (s + 2 * a):].view(H, a)
+    rec = st["record"]
+    cost_hist = torch.empty((I, E, N), dtype=torch.float32, device=dev) if rec else None
+    ret_hist = torch.empty((I, N), dtype=torch.float32, device=dev) if rec else None
+    elite_hist = torch.empty((I, K), dtype=torch.int64, device=dev) if rec else None
+    _lib.check(lib.mbrl_cem_plan_sharded(fused.ctypes_ref(prob.shape), _lib.ptr(prob.packed),
+                                         fused.ctypes_ref(prob.norm), fused.ctypes_ref(prob.cost), _lib.ptr(s0),
+                                         fused.ctypes_ref(params), comm, world, rank, _lib.ptr(mu), _lib.ptr(sigma),
+                                         _lib.ptr(actions), _lib.ptr(states), _lib.ptr(cost_hist), _lib.ptr(ret_hist),
+                                         _lib.ptr(elite_hist), _events(st, I), _lib.ptr(ws), ws.numel(),
+                                         _lib.stream_handle(dev)), "mbrl_cem_plan_sharded")
+    out = dict(states=states, actions=actions, mu=mu, sigma=sigma, _both=both)
+    if rec:
+        out.update(costs=cost_hist, returns=ret_hist, elites=elite_hist)
+    return out
+
+
 def _cem_fused_sharded(prob, s0, st, world):
     import torch.distributed as dist
+    if SHARDED_NATIVE and dist.get_backend() == "nccl":
+        return _cem_sharded_native(prob, s0, st, world, dist.get_rank())
     st = dict(st, E=prob.mdesc["E"], a=prob.mdesc["a"])
     return cem_sharded_protocol(_FusedShardOps(prob, s0, st), st, world, dist.get_rank())
 

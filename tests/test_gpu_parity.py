@@ -702,6 +702,9 @@ def test_sharded_plan_two_processes_on_one_gpu():
         assert np.allclose(g["states"], ref["states"].numpy(), rtol=1e-5, atol=1e-5)
 
 
+RCCL_CASES = [(3, dict(N=1024, H=8)), (5, dict(N=256, H=6))]
+
+
 def _rccl_worker(rank, world, init_file, out_dir):
     import os
     import sys
@@ -714,40 +717,56 @@ def _rccl_worker(rank, world, init_file, out_dir):
     dist.init_process_group("nccl", init_method=f"file://{init_file}", rank=rank, world_size=world)
     try:
         assert dist.get_backend() == "nccl"
-        p = oc.synth_problem(3, N=1024, H=8)
-        _, model_fn, cost_fn, sample_action = build(p)
         dev = torch.device("cuda", 0)
-        md = fused.describe_model(model_fn)
-        prob = fused.device_problem(md, fused.describe_cost(cost_fn, md["s"], md), dev)
-        st = CEMPlanner._settings(sample_action, 8, dict(num_candidates=1024, num_iterations=3, seed=p["rng_seed"],
-                                                         record=True))
-        s0 = torch.from_numpy(p["s0"]).to(dev)
-        res = planners._cem_fused_sharded(prob, s0, st, world)   # every iteration all-gathers over RCCL
-        np.savez(os.path.join(out_dir, f"r{rank}.npz"), mu=res["mu"].cpu().numpy(), sigma=res["sigma"].cpu().numpy(),
-                 elites=torch.stack(list(res["elites"])).cpu().numpy(), actions=res["actions"].cpu().numpy())
+        for cid, over in RCCL_CASES:
+            p = oc.synth_problem(cid, **over)
+            _, model_fn, cost_fn, sample_action = build(p)
+            md = fused.describe_model(model_fn)
+            prob = fused.device_problem(md, fused.describe_cost(cost_fn, md["s"], md), dev)
+            st = CEMPlanner._settings(sample_action, over["H"], dict(num_candidates=over["N"], num_iterations=3,
+                                                                     seed=p["rng_seed"], record=True))
+            s0 = torch.from_numpy(p["s0"]).to(dev)
+            for native in (True, False):
+                # native: mbrl_cem_plan_sharded (ncclAllGather on the plan's stream, the library's own
+                # communicator); else cem_sharded_protocol (torch.distributed all_gather_into_tensor)
+                planners.SHARDED_NATIVE = native
+                res = planners._cem_fused_sharded(prob, s0, st, world)
+                np.savez(os.path.join(out_dir, f"c{cid}_n{int(native)}_r{rank}.npz"), mu=res["mu"].cpu().numpy(),
+                         sigma=res["sigma"].cpu().numpy(), elites=torch.stack(list(res["elites"])).cpu().numpy(),
+                         returns=torch.stack(list(res["returns"])).cpu().numpy(),
+                         costs=torch.stack(list(res["costs"])).cpu().numpy(),
+                         actions=res["actions"].cpu().numpy(), states=res["states"].cpu().numpy())
     finally:
+        planners.SHARDED_NATIVE = True
         dist.destroy_process_group()
 
 
 def test_sharded_plan_over_rccl():
-    """The sharded plan's device-memory all-gather through RCCL (torch.distributed backend "nccl", the
-    multi-GPU path's collective) with a one-rank process group on this GPU -- RCCL refuses two ranks
-    on one device, so the 2-8 rank runs are the driver's 8-GPU node's -- bit-identical to the
-    single-process plan."""
+    """The multi-GPU plan over RCCL (torch.distributed backend "nccl") with a one-rank process group
+    on this GPU -- RCCL refuses two ranks on one device, so the 2-8 rank runs are the driver's 8-GPU
+    node's: both the one-call C path (mbrl_cem_plan_sharded: the library's RCCL communicator, the
+    all-gather a step on the plan's stream, the ensemble's rank-major cost permutation) and the
+    per-iteration protocol (cem_sharded_protocol over all_gather_into_tensor) are bit-identical to the
+    single-process plan, for a single model and a 5-member ensemble."""
     import tempfile
     import torch.multiprocessing as mp
     from mbrl_amd import CEMPlanner
     with tempfile.TemporaryDirectory() as d:
         mp.start_processes(_rccl_worker, args=(1, os.path.join(d, "pg"), d), nprocs=1, join=True,
                            start_method="spawn")
-        g = dict(np.load(os.path.join(d, "r0.npz")))
-    p = ocem.synth_problem(3, N=1024, H=8)
-    _, model_fn, cost_fn, sample_action = build(p)
-    ref = CEMPlanner.plan_detailed(torch.from_numpy(p["s0"]), model_fn, cost_fn, sample_action, 8,
-                                   num_candidates=1024, num_iterations=3, seed=p["rng_seed"], record=True)
-    assert np.array_equal(g["elites"], torch.stack(list(ref["elites"])).cpu().numpy())
-    assert np.array_equal(g["mu"], ref["mu"].cpu().numpy()) and np.array_equal(g["sigma"], ref["sigma"].cpu().numpy())
-    assert np.array_equal(g["actions"], ref["actions"].numpy())
+        got = {(cid, n): dict(np.load(os.path.join(d, f"c{cid}_n{n}_r0.npz"))) for cid, _ in RCCL_CASES for n in (0, 1)}
+    for cid, over in RCCL_CASES:
+        p = ocem.synth_problem(cid, **over)
+        _, model_fn, cost_fn, sample_action = build(p)
+        ref = CEMPlanner.plan_detailed(torch.from_numpy(p["s0"]), model_fn, cost_fn, sample_action, over["H"],
+                                       num_candidates=over["N"], num_iterations=3, seed=p["rng_seed"], record=True)
+        for n in (0, 1):
+            g = got[(cid, n)]
+            assert np.array_equal(g["elites"], ref["elites"].cpu().numpy()), (cid, n)
+            assert np.array_equal(g["returns"], ref["returns"].cpu().numpy()), (cid, n)
+            assert np.array_equal(g["costs"], ref["costs"].cpu().numpy()), (cid, n)
+            assert np.array_equal(g["mu"], ref["mu"].cpu().numpy()) and np.array_equal(g["sigma"], ref["sigma"].cpu().numpy())
+            assert np.array_equal(g["actions"], ref["actions"].numpy()) and np.array_equal(g["states"], ref["states"].numpy())
 
 
 @pytest.mark.parametrize("cid,N,H,B", [(2, 1024, 20, 4), (3, 512, 6, 3), (6, 256, 5, 2), (5, 128, 4, 2)])

@@ -1,5 +1,6 @@
-"""What the per-iteration sharded protocol (planners.cem_sharded_protocol: rollout, RCCL all-gather,
-update, issued from Python each iteration) costs over the one-call single-GPU plan (mbrl_cem_plan),
+"""What the sharded plan costs over the one-call single-GPU plan (mbrl_cem_plan): the one-call C path
+(mbrl_cem_plan_sharded, the all-gather a step on the plan's stream) and the per-iteration protocol
+(planners.cem_sharded_protocol: rollout, RCCL all-gather, update, issued from Python each iteration),
 on one GPU with a one-rank RCCL process group (the collective really runs; RCCL refuses two ranks on
 one device). Per plan: wall time with a stream sync, and the host time spent issuing it.
 Usage: python tools/shard_host_cost.py [config_id] [candidates] [plans]"""
@@ -41,12 +42,16 @@ def main():
             def single():
                 return planners._cem_fused_single(prob, s0, st)
 
-            def sharded():
+            def native():
+                planners.SHARDED_NATIVE = True
+                return planners._cem_fused_sharded(prob, s0, st, 1)
+
+            def protocol():
+                planners.SHARDED_NATIVE = False
                 return planners._cem_fused_sharded(prob, s0, st, 1)
 
             out = dict(config=cfg["name"], candidates=N)
-            for label, fn in (("single", single), ("sharded_protocol", sharded), ("single", single),
-                              ("sharded_protocol", sharded)):
+            for label, fn in (("single", single), ("sharded_native", native), ("sharded_protocol", protocol)) * 2:
                 for _ in range(5):
                     fn()
                 stream.synchronize()
