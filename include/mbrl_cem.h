@@ -156,7 +156,8 @@ enum {
     MBRL_OPT_ADAM_ARITH = 6,        /* mbrl_adam_step contraction pattern: 0 = torch's; 1 + bits (test) */
     MBRL_OPT_XCD_MAP = 7,           /* 1: ensemble rollouts map workgroups member-major per XCD (A/B) */
     MBRL_OPT_TRAIN_TILE = 8,        /* training backward C tile height: 0 auto, 32, 64 (bit-identical) */
-    MBRL_OPT_COUNT = 9
+    MBRL_OPT_TRAIN_NO_FOLD = 9,     /* 1: the layer-0 weight gradient in its own launch (bit-identical) */
+    MBRL_OPT_COUNT = 10
 };
 int mbrl_set_option(int32_t option, int32_t value);
 int mbrl_get_option(int32_t option);

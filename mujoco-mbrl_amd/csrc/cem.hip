@@ -1512,6 +1512,7 @@ static int train_shape(const mbrl_train_model* m, TrainShape* t) {
     t->s = m->state_dim; t->a = m->action_dim; t->W = m->hidden; t->L = m->n_hidden; t->reward = m->reward_head;
     t->H = m->horizon;
     t->tile = g_opt[MBRL_OPT_TRAIN_TILE].load(std::memory_order_relaxed);
+    t->fold = g_opt[MBRL_OPT_TRAIN_NO_FOLD].load(std::memory_order_relaxed) == 0 ? 1 : 0;
     return MBRL_OK;
 }
 
@@ -1578,19 +1579,30 @@ int mbrl_train_epoch(const mbrl_train_model* model, const mbrl_train_data* data,
         fold = tensors[2 * l].param == model->weight[l] && tensors[2 * l].grad == model->weight_grad[l] &&
                tensors[2 * l + 1].param == model->bias[l] && tensors[2 * l + 1].grad == model->bias_grad[l];
     const int ar = arith ? arith - 1 : ADAM_ARITH_TORCH;
+    // a layer's step the layer-0 fold defers: carried by the next batch's first launch, or launched
+    // after the last batch
+    mbrl_adam_tensor carry[2][4];
+    int carry_n = 0;
     for (int64_t b = 0; b < batches; ++b) {
         const int n = (int)std::min<int64_t>(batch_size, rows - b * batch_size);
         for (int i = 0; i < count; ++i) {
             table[i].step_size = step_sizes[b * count + i];
             table[i].bc2_sqrt = bc2_sqrt[b * count + i];
         }
+        mbrl_adam_tensor* next = carry[(b + 1) & 1];
+        int next_n = 0;
         if (int rc = hip_check(launch_train_grads(t, w, order + b * batch_size, n, losses ? losses + 3 * b : nullptr,
                                                   static_cast<float*>(workspace), st, fold ? table.data() : nullptr,
-                                                  hparams, ar), "train_epoch grads"))
+                                                  hparams, ar, carry[b & 1], carry_n, next, &next_n),
+                               "train_epoch grads"))
             return rc;
+        carry_n = next_n;
         if (!fold)
             if (int rc = hip_check(launch_adam_step(table.data(), count, *hparams, ar, st), "train_epoch adam")) return rc;
     }
+    if (carry_n > 0)
+        if (int rc = hip_check(launch_adam_step(carry[batches & 1], carry_n, *hparams, ar, st), "train_epoch adam tail"))
+            return rc;
     return MBRL_OK;
 }
 

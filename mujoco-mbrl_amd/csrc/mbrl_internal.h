@@ -342,6 +342,7 @@ hipError_t launch_adam_step(const mbrl_adam_tensor* tensors, int count, const mb
 struct TrainShape {
     int s, a, W, L, reward, H;   // state / action dims, hidden width, hidden layers, reward head, horizon
     int tile;                    // backward C tile height: 0 auto, 32, 64 (MBRL_OPT_TRAIN_TILE; same bits)
+    int fold;                    // 1: the layer-0 weight gradient folds into the dH_0 launch (same bits)
 };
 struct TrainTensors {
     const float* const* weight;  // L + 1 (+ 1 reward head) nn.Linear weights [out][in]
@@ -353,8 +354,13 @@ struct TrainTensors {
 size_t train_ws_floats(const TrainShape& t, int batch);
 // adam (optional): the step of every layer's weight and bias (linear1.weight, linear1.bias, ...)
 // folded into the backward launches, bit-identical to a separate mbrl_adam_step after the gradient.
+// With the layer-0 fold one layer's step cannot ride in this step's launches: it comes back in
+// pending[0 .. *pending_n) (then required with adam) for the caller to pass as the next step's
+// `prior` (taken by its first launch) or to run with launch_adam_step.
 hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const int64_t* idx, int batch,
                               float* loss_out, float* ws, hipStream_t stream, const mbrl_adam_tensor* adam = nullptr,
-                              const mbrl_adam_hparams* hp = nullptr, int arith = 0);
+                              const mbrl_adam_hparams* hp = nullptr, int arith = 0,
+                              const mbrl_adam_tensor* prior = nullptr, int prior_n = 0,
+                              mbrl_adam_tensor* pending = nullptr, int* pending_n = nullptr);
 
 }  // namespace mbrl

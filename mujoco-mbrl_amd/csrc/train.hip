@@ -198,6 +198,18 @@ struct Output {
     int adam;                 // EPI_GRAD: also take this layer's Adam step in place (nothing reads it
                               // in this launch): weight at aw (= c0 layout), bias at ab
     mbrl_adam_tensor aw, ab;
+    // EPI_MASK of dH_0 with fold (launch_train_grads): the tile also yields the layer-0 weight
+    // gradient's partial over each of its 32-row blocks -- exactly what wave tr of the separate dW_0
+    // launch summed -- into fold_part[tr][W][K0]; the last of a column block's tiles to finish (a
+    // ticket per column block) adds them in wave order into dW_0 / db_0 and takes layer 0's Adam step
+    int fold, fold_k0, fold_nw;         // input columns K0, the separate launch's wave count
+    const float* fold_x;                // the gathered input [R][K0] (xbuf, written by the forward)
+    float* fold_part;
+    unsigned* fold_ticket;              // [ceil(W / 32)], zeroed by the forward launch
+    float *fold_dw, *fold_db;           // dW_0 [W][K0], db_0 [W]
+    int fold_cs_tiles;                  // 32-row tiles of the column sums (colsum_out of this product)
+    int fold_adam;
+    mbrl_adam_tensor fold_aw, fold_ab;
     float scale_s, scale_r;   // EPI_LOSS: dY scale of the state / reward columns (2 / numel)
     float inv_s, inv_r;       // EPI_LOSS: loss weight of the state / reward columns (1 / numel)
     int s;                    // EPI_LOSS: state columns (n >= s: the reward column)
@@ -228,8 +240,11 @@ struct GemmLaunch {
     float* loss_out;
     // fused Adam (mbrl_train_epoch): the step of a layer whose gradient the previous launch finished,
     // as extra workgroups after the products' tiles (ADAM_FUSED_CHUNK elements each)
-    int adam_count, adam_blocks;
+    int adam_count, adam_blocks, adam_chunk;   // adam_chunk: elements per Adam workgroup
+    int adam_long;                             // 16 elements per thread instead of 4
     mbrl_adam_tensor adam_t[ADAM_FUSED_MAX];
+    unsigned* zero_words;   // workgroup 0 zeroes zero_n words first (the fold's tickets; forward launch)
+    int zero_n;
     int adam_first[ADAM_FUSED_MAX + 1];
     mbrl_adam_hparams hp;
     int arith;
@@ -281,6 +296,9 @@ __device__ __forceinline__ void stash_input(const GemmLaunch& L, const GemmDesc&
     for (int e = 0; e < 4; ++e)
         if (m < D.M && k0 + e < D.K) L.xstore[(int64_t)m * D.K + k0 + e] = v[e];
 }
+
+template <int NW, int TMX>
+__device__ void fold_dw0(const GemmLaunch& L, const GemmDesc& D, int tm, int n0, float (*red)[TT * TMX][TT + 1]);
 
 // TMX = 1: 32 x 32 C tiles; TMX = 2: 64 x 32 (the W x W backward products, so that a launch's tiles
 // fit one round of the CUs). Each element's K order is the same for both (the K split over the waves
@@ -412,8 +430,13 @@ __device__ void gemm_tile(const GemmLaunch& L, const GemmDesc& D, int tile, floa
         if (tid < TM && n0 + col < D.N && m0 + TT * sub < D.M) {
             float t = red[0][TT * sub][col];
             for (int r = 1; r < TT; ++r) t = t + red[0][TT * sub + r][col];
-            O.colsum_out[(int64_t)(tm * TMX + sub) * D.N + n0 + col] = t;
+            float* dst = O.colsum_out + (int64_t)(tm * TMX + sub) * D.N + n0 + col;
+            if (O.fold)   // read back by the fold's last arriver (sc1 hand-off)
+                __hip_atomic_store(dst, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else
+                *dst = t;
         }
+        if (O.mode == EPI_MASK && O.fold) fold_dw0<NW, TMX>(L, D, tm, n0, red);
     }
     if (O.mode == EPI_LOSS) {   // the tile's loss: a butterfly per wave, then the waves in order
 #pragma unroll
@@ -437,6 +460,122 @@ __device__ void gemm_tile(const GemmLaunch& L, const GemmDesc& D, int tile, floa
     TSTAMP(3);
 }
 
+// The layer-0 weight gradient folded into the dH_0 launch (Output.fold). red[0] holds this tile's
+// dH_0 rows [m0, m0 + TM) x columns [n0, n0 + 32) (the EPI_MASK column-sum staging). The separate
+// dW_0 launch (M = W, N = K0, K = R, fold_nw waves of 32 rows each) computed, per wave tr, one 32 x 32
+// block of dW_0 over rows [32 tr, 32 tr + 32) with acc[x][y] over 16-row chunks u, k = 4 q + s: the
+// same loads and MFMAs in the same order run here per 32-row half of the tile, so every partial is
+// the same float, and the last arriver sums them in wave order with the empty waves' +0 -- the
+// separate launch's result bit for bit.
+template <int NW, int TMX>
+__device__ void fold_dw0(const GemmLaunch& L, const GemmDesc& D, int tm, int n0, float (*red)[TT * TMX][TT + 1]) {
+    constexpr int TM = TT * TMX;
+    const Output& O = D.out;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, q = lane >> 4, c = lane & 15;
+    const int R = D.M, W = D.N, K0 = O.fold_k0, m0 = tm * TM;
+    const int kt = (K0 + TT - 1) / TT;
+    for (int task = wave; task < TMX * kt; task += NW) {
+        const int h = task / kt, kb = task - (task / kt) * kt;
+        const int r0 = m0 + TT * h;
+        if (r0 >= R) continue;
+        const int r1 = min(R, r0 + TT);
+        f32x4 acc[2][2];
+#pragma unroll
+        for (int x = 0; x < 2; ++x)
+#pragma unroll
+            for (int y = 0; y < 2; ++y) acc[x][y] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int k0 = r0 + 16 * u;
+            if (k0 >= r1) break;
+            f32x4 a[2], b[2];
+#pragma unroll
+            for (int x = 0; x < 2; ++x) {          // A(i = j, k = r) = dH_0[r][j]
+                const int j = 16 * x + c;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int r = k0 + 4 * q + e;
+                    a[x][e] = (n0 + j < W && r < R) ? red[0][r - m0][j] : 0.0f;
+                }
+            }
+#pragma unroll
+            for (int y = 0; y < 2; ++y) {          // B(i = k, k = r) = X[r][k]
+                const int kk = TT * kb + 16 * y + c;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int r = k0 + 4 * q + e;
+                    b[y][e] = (kk < K0 && r < R) ? O.fold_x[(int64_t)r * K0 + kk] : 0.0f;
+                }
+            }
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int x = 0; x < 2; ++x)
+#pragma unroll
+                    for (int y = 0; y < 2; ++y)
+                        acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[x][s], b[y][s], acc[x][y], 0, 0, 0);
+        }
+        const int tr = r0 / TT;
+#pragma unroll
+        for (int x = 0; x < 2; ++x)
+#pragma unroll
+            for (int y = 0; y < 2; ++y)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const int j = n0 + 16 * x + 4 * q + v, kk = TT * kb + 16 * y + c;
+                    if (j < W && kk < K0)    // sc1 (write-through) stores: no release fence needed
+                        __hip_atomic_store(O.fold_part + ((int64_t)tr * W + j) * K0 + kk, acc[x][y][v],
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+    }
+    // ticket: the last tile of column block n0 / 32 to arrive finishes dW_0 / db_0 of its 32 rows.
+    // Hand-off (MI355X_MICROARCH.md, the sc1 table's first row): every partial and column sum is an sc1
+    // store, every storing wave waits for its stores, one lane adds to the block's ticket after a
+    // barrier, and the workgroup whose add returns the last count reads them back with sc1 loads.
+    __shared__ unsigned last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int tiles_m = (R + TM - 1) / TM;
+    if (tid == 0) {
+        const unsigned t = __hip_atomic_fetch_add(&O.fold_ticket[n0 / TT], 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+        last = (t + 1 == (unsigned)tiles_m) ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!last) return;
+    const int ntr = (R + TT - 1) / TT;      // non-empty waves of the separate launch
+    for (int e = tid; e < TT * K0; e += 64 * NW) {
+        const int j = n0 + e / K0, kk = e - (e / K0) * K0;
+        if (j >= W) continue;
+        float p[16];                         // fold_nw <= 16: every load in flight before the sum
+#pragma unroll
+        for (int w = 0; w < 16; ++w)
+            p[w] = (w < ntr && w < O.fold_nw)
+                       ? __hip_atomic_load(O.fold_part + ((int64_t)w * W + j) * K0 + kk, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT)
+                       : 0.0f;
+        float v = p[0];
+#pragma unroll
+        for (int w = 1; w < 16; ++w)
+            if (w < O.fold_nw) v = v + p[w];
+        const int64_t i = (int64_t)j * K0 + kk;
+        O.fold_dw[i] = v;
+        if (O.fold_adam)
+            adam_element(O.fold_aw.param[i], v, O.fold_aw.exp_avg[i], O.fold_aw.exp_avg_sq[i], O.fold_aw.step_size,
+                         O.fold_aw.bc2_sqrt, L.hp, L.arith);
+    }
+    if (tid < TT && n0 + tid < W) {          // db_0: the column sums of dH_0 over the 32-row tiles
+        const int j = n0 + tid;
+        float g = __hip_atomic_load(O.colsum_out + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int i = 1; i < O.fold_cs_tiles; ++i)
+            g = g + __hip_atomic_load(O.colsum_out + (int64_t)i * W + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        O.fold_db[j] = g;
+        if (O.fold_adam)
+            adam_element(O.fold_ab.param[j], g, O.fold_ab.exp_avg[j], O.fold_ab.exp_avg_sq[j], O.fold_ab.step_size,
+                         O.fold_ab.bc2_sqrt, L.hp, L.arith);
+    }
+}
+
 // NW waves per workgroup; A0/B0 (A1/B1): operand kinds of the launch's first (second) product, fixed
 // at compile time so each instantiation carries only its own load paths.
 template <int NW, int A0, int B0, int A1, int B1, int TMX>
@@ -445,6 +584,8 @@ __global__ __launch_bounds__(64 * NW) void train_gemm_kernel(const GemmLaunch L)
     TSTAMP(0);
     // (constant indices only: a dynamic index into the kernel arguments would copy them to scratch)
     const int b = blockIdx.x;
+    if (b == 0 && L.zero_words)
+        for (int i = threadIdx.x; i < L.zero_n; i += 64 * NW) L.zero_words[i] = 0u;
     if (b < L.d[0].tiles) {
         gemm_tile<NW, A0, B0, TMX>(L, L.d[0], b, red);
         return;
@@ -461,8 +602,8 @@ __global__ __launch_bounds__(64 * NW) void train_gemm_kernel(const GemmLaunch L)
         int ti = 0;
         while (ti + 1 < L.adam_count && r >= L.adam_first[ti + 1]) ++ti;
         const mbrl_adam_tensor& T = L.adam_t[ti];
-        const int64_t base = (int64_t)(r - L.adam_first[ti]) * (64 * NW * 4);
-        for (int64_t i = base + threadIdx.x; i < T.numel && i < base + 64 * NW * 4; i += 64 * NW)
+        const int64_t base = (int64_t)(r - L.adam_first[ti]) * L.adam_chunk;
+        for (int64_t i = base + threadIdx.x; i < T.numel && i < base + L.adam_chunk; i += 64 * NW)
             adam_element(T.param[i], T.grad[i], T.exp_avg[i], T.exp_avg_sq[i], T.step_size, T.bc2_sqrt, L.hp,
                          L.arith);
         return;
@@ -510,8 +651,10 @@ static hipError_t launch_gemm(GemmLaunch& L, bool loss_wg, hipStream_t stream) {
         blocks += L.d[i].tiles;
         kmax = max(kmax, L.d[i].K);
     }
-    // fused Adam blocks: chunks of 4 elements per thread of the launch's workgroup size
-    const int chunk = 64 * (kmax >= 256 ? 16 : 4) * 4;
+    // fused Adam blocks: chunks of 4 elements per thread of the launch's workgroup size (16 in a
+    // forward launch, which carries the previous step's deferred layer: fewer, longer workgroups)
+    const int chunk = 64 * (kmax >= 256 ? 16 : 4) * (L.adam_long ? 16 : 4);
+    L.adam_chunk = chunk;
     L.adam_blocks = 0;
     for (int i = 0; i < L.adam_count; ++i) {
         L.adam_first[i] = L.adam_blocks;
@@ -537,7 +680,8 @@ static hipError_t launch_gemm(GemmLaunch& L, bool loss_wg, hipStream_t stream) {
 // per-row-tile column sums of dY [tiles][J] and of the two dH [tiles][W].
 struct TrainWs {
     float* act[MBRL_TRAIN_MAX_LAYERS];
-    float *dh[2], *dy, *loss_part, *xbuf, *cs_dy, *cs_dh[2];
+    float *dh[2], *dy, *loss_part, *xbuf, *cs_dy, *cs_dh[2], *fold_part;
+    unsigned* tickets;
     size_t floats;
 };
 
@@ -557,17 +701,32 @@ static TrainWs train_ws(const TrainShape& t, int batch, float* base) {
     w.cs_dy = take(tiles_r * J);
     w.cs_dh[0] = take(tiles_r * W);
     w.cs_dh[1] = take(tiles_r * W);
+    w.fold_part = take(tiles_r * W * (size_t)(t.s + t.a));   // the folded dW_0's per-32-row partials
+    w.tickets = reinterpret_cast<unsigned*>(take((W + TT - 1) / TT));
     w.floats = off;
     return w;
 }
 
 size_t train_ws_floats(const TrainShape& t, int batch) { return train_ws(t, batch, nullptr).floats; }
 
+// Whether the layer-0 weight gradient folds into the dH_0 launch bit-identically: its separate launch
+// (M = W, K = R) gives each of its waves one 32-row block of the batch (16 waves at R >= 256, else 4).
+static int fold_waves(const TrainShape& t, int R) {
+    if (t.fold == 0 || t.L < 1) return 0;
+    const int nw = R >= 256 ? 16 : 4, chunks = (R + 15) / 16, per = (chunks + nw - 1) / nw;
+    return per == 2 ? nw : 0;
+}
+
 hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const int64_t* idx, int batch,
                               float* loss_out, float* ws, hipStream_t stream, const mbrl_adam_tensor* adam,
-                              const mbrl_adam_hparams* hp, int arith) {
+                              const mbrl_adam_hparams* hp, int arith, const mbrl_adam_tensor* prior, int prior_n,
+                              mbrl_adam_tensor* pending, int* pending_n) {
     const int R = batch * t.H, W = t.W, K0 = t.s + t.a, J = t.s + (t.reward ? 1 : 0), L = t.L;
     const int tiles_r = (R + TT - 1) / TT;
+    const int fold_nw = fold_waves(t, R);
+    if (pending_n) *pending_n = 0;
+    if ((prior_n > 0 && !prior) || prior_n > ADAM_FUSED_MAX || (adam && fold_nw && (!pending || !pending_n)))
+        return hipErrorInvalidValue;
     const TrainWs B = train_ws(t, batch, ws);
     const float* wo_r = t.reward ? w.weight[L + 1] : nullptr;
     const float* bo_r = t.reward ? w.bias[L + 1] : w.bias[L];
@@ -597,7 +756,18 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
         D.out.b0 = D.out.b1 = w.bias[l]; D.out.bsplit = W; D.out.relu = 1;
         finish(D, R, W, l == 0 ? K0 : W);
         G.nd = 1;
+        if (l == 0) {
+            // the forward launch zeroes the fold's tickets and takes the previous step's deferred
+            // Adam step (a layer nothing before this step's second forward launch reads)
+            G.zero_words = fold_nw ? B.tickets : nullptr;
+            G.zero_n = (W + TT - 1) / TT;
+            G.adam_count = 0;
+            for (int i = 0; i < prior_n; ++i) G.adam_t[G.adam_count++] = prior[i];
+        }
         e = l == 0 ? launch_gemm<OP_GATHER, OP_DIRECT>(G, false, stream) : launch_gemm<OP_DIRECT, OP_DIRECT>(G, false, stream);
+        G.zero_words = nullptr;
+        G.adam_count = 0;
+        G.adam_long = 0;
         if (e != hipSuccess) return e;
     }
     // output layer (state head, reward head) + the loss gradient dY and its column sums
@@ -617,8 +787,10 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
         if ((e = launch_gemm<OP_DIRECT, OP_DIRECT>(G, false, stream)) != hipSuccess) return e;
     }
     const int loss_parts = G.d[0].tiles;
-    // backward: layer l = L (output) .. 0; launch l: dH_{l-1} (l >= 1) and dW_l, db_l
-    for (int l = L; l >= 0; --l) {
+    // backward: layer l = L (output) .. 0; launch l: dH_{l-1} (l >= 1) and dW_l, db_l. With the fold
+    // (fold_waves) launch 1 also finishes dW_0 / db_0 and launch 0 does not exist.
+    const int l_end = fold_nw ? 1 : 0;
+    for (int l = L; l >= l_end; --l) {
         const bool out_layer = l == L;
         const float* g_in = out_layer ? B.dy : B.dh[l % 2];   // dL/d(pre-activation of layer l), [R][n_out]
         const float* cs_in = out_layer ? B.cs_dy : B.cs_dh[l % 2];
@@ -638,6 +810,15 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
             D.out.mode = EPI_MASK; D.out.c0 = D.out.c1 = B.dh[(l - 1) % 2]; D.out.split = R; D.out.ldc = W;
             D.out.mask = B.act[l - 1]; D.out.ldm = W; D.out.colsum_out = B.cs_dh[(l - 1) % 2];
             finish(D, R, W, n_out, tmx);
+            if (l == 1 && fold_nw) {
+                Output& O = D.out;
+                O.fold = 1; O.fold_k0 = K0; O.fold_nw = fold_nw; O.fold_x = B.xbuf; O.fold_part = B.fold_part;
+                O.fold_ticket = B.tickets; O.fold_dw = w.weight_grad[0]; O.fold_db = w.bias_grad[0];
+                O.fold_cs_tiles = tiles_r;
+                if (adam) {          // nothing in this launch reads layer 0's parameters
+                    O.fold_adam = 1; O.fold_aw = adam[0]; O.fold_ab = adam[1];
+                }
+            }
         }
         {                       // dW_l = g_in^T X_l; db_l = the column sums of g_in over the row tiles
             GemmDesc& D = G.d[G.nd++];
@@ -669,10 +850,16 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
             for (int i = 0; i < n; ++i) G.adam_t[G.adam_count++] = adam[first + i];
         }
         G.loss_part = B.loss_part; G.loss_parts = loss_parts; G.loss_out = loss_out;
-        e = l == 0    ? launch_gemm<OP_TRANS, OP_TRANS>(G, loss_out != nullptr, stream)
-            : tmx == 2 ? launch_gemm<OP_DIRECT, OP_TRANS, OP_TRANS, OP_TRANS, 2>(G, false, stream)
-                       : launch_gemm<OP_DIRECT, OP_TRANS, OP_TRANS, OP_TRANS>(G, false, stream);
+        const bool loss_wg = l == l_end && loss_out != nullptr;
+        e = l == 0    ? launch_gemm<OP_TRANS, OP_TRANS>(G, loss_wg, stream)
+            : tmx == 2 ? launch_gemm<OP_DIRECT, OP_TRANS, OP_TRANS, OP_TRANS, 2>(G, loss_wg, stream)
+                       : launch_gemm<OP_DIRECT, OP_TRANS, OP_TRANS, OP_TRANS>(G, loss_wg, stream);
         if (e != hipSuccess) return e;
+    }
+    if (adam && fold_nw) {   // layer 1's step (launch 0's passenger before the fold): the next forward launch's
+        const int n = (L == 1 && t.reward) ? 4 : 2;
+        for (int i = 0; i < n; ++i) pending[i] = adam[2 + i];
+        *pending_n = n;
     }
     return hipSuccess;
 }

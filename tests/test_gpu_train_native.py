@@ -223,3 +223,42 @@ def test_backward_tile_height_is_bitwise_neutral(kind, s, a, W, L, H, B):
     for tile in (64, 0):
         for x, y in zip(res[tile], res[32]):
             assert torch.equal(x, y), tile
+
+
+@pytest.mark.parametrize("kind,W,L,H,B", [("model", 512, 2, 1, 512), ("model", 96, 2, 1, 300), ("model", 64, 3, 2, 50),
+                                         ("reward", 200, 2, 1, 400), ("reward", 64, 1, 1, 500),
+                                         ("model", 128, 1, 2, 60)])
+def test_layer0_gradient_fold_is_bitwise_neutral(kind, W, L, H, B):
+    """The layer-0 weight gradient folded into the dH_0 launch (per-32-row partials of each dH_0 tile,
+    summed in wave order by the last tile of a column block; layer 0's Adam step there, layer 1's in the
+    next batch's first launch) against its own launch (MBRL_OPT_TRAIN_NO_FOLD): the same gradients and
+    losses from mbrl_train_grads, and the same parameters, optimizer state and losses after three epochs
+    of mbrl_train_epoch with the last batch partial."""
+    from mbrl_amd import _lib, models
+    ds = _dataset(17, 6, H, 3 * B + 37, seed=W + L)
+    _, ins, outs = ds.stacked(DEV)
+    reward = kind == "reward"
+    idx = torch.randperm(ds.num_transitions(), generator=torch.Generator().manual_seed(B))[:B].to(DEV)
+    grads, trained = {}, {}
+    for no_fold in (1, 0):
+        with _lib.option("train_no_fold", no_fold):
+            m = _model(kind, 17, 6, W, L, seed=W)
+            nat = models._NativeGrads(m, ins, outs, ds.horizon, B, reward)
+            loss, parts = nat.run(idx)
+            torch.cuda.synchronize()
+            grads[no_fold] = [loss.clone()] + [p.grad.clone() for p in m.parameters()]
+            m = _model(kind, 17, 6, W, L, seed=W)
+            opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+            w = _Writer()
+            np.random.seed(3)
+            m.train_model(ds, opt, batch_size=B, num_epochs=3, writer=w)
+            torch.cuda.synchronize()
+            trained[no_fold] = ([p.detach().clone() for p in m.parameters()],
+                                [(float(s["step"]), s["exp_avg"].clone(), s["exp_avg_sq"].clone())
+                                 for s in opt.state.values()], w.rows)
+    assert all(torch.equal(x, y) for x, y in zip(grads[0], grads[1]))
+    (pa, sa, ra), (pb, sb, rb) = trained[0], trained[1]
+    assert all(torch.equal(x, y) for x, y in zip(pa, pb))
+    for (ka, ma, va), (kb, mb, vb) in zip(sa, sb):
+        assert ka == kb and torch.equal(ma, mb) and torch.equal(va, vb)
+    assert ra == rb and len(ra) > 0
