@@ -187,6 +187,7 @@ constexpr uint32_t MBRL_REDO_MARK = 0x7FC0DEADu;
 
 struct LdsMap {
     float *act, *act2, *part, *sterm, *aterm, *obs_mean, *obs_std, *act_mean, *act_std, *goal, *cw, *hbias;
+    uint32_t* lflag;   // per-wave hidden-layer store counters (rollout.hip hidden_store_flag), 16 words
     size_t total_floats;
 };
 
@@ -208,6 +209,7 @@ __host__ __device__ inline LdsMap lds_map(const RolloutArgs& A, float* base, int
     L.goal = take(A.s);
     L.cw = take(A.s);
     L.hbias = take((size_t)A.L * A.Wpad + 16 * (size_t)A.NOT);
+    L.lflag = reinterpret_cast<uint32_t*>(take(16));
     L.total_floats = o;
     return L;
 }

@@ -49,6 +49,12 @@
 #ifndef MBRL_EPI_REG_SLOTS
 #define MBRL_EPI_REG_SLOTS 2
 #endif
+// Hidden-layer hand-offs by per-wave LDS flags instead of workgroup barriers.
+// Off: parity-green but 3-35 % slower than the barriers (profiles/r03_ab_layer_flags.txt) -- every
+// flag poll is an LDS load the wave must drain its prefetched B reads for (s_waitcnt lgkmcnt(0)).
+#ifndef MBRL_LAYER_FLAGS
+#define MBRL_LAYER_FLAGS 0
+#endif
 
 namespace mbrl {
 
@@ -187,6 +193,31 @@ __device__ __forceinline__ void hidden_store(const f32x4 (&acc)[R][T], const f32
     __syncthreads();
 }
 
+// hidden_store without the barrier; then this wave's count of finished layer stores is published
+// in LDS (lflag[wave]) once its own ds_writes have completed (s_waitcnt lgkmcnt(0)).
+template <int T, int R>
+__device__ __forceinline__ void hidden_store_flag(const f32x4 (&acc)[R][T], const f32x4 (&bias)[T], float* out,
+                                                  int lda, int wave, int lane, uint32_t* lflag, uint32_t count) {
+    const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int j = 0; j < T; ++j) {
+            f32x4 v = acc[r][j] + bias[j];
+            v = __builtin_elementwise_max(v, zero);
+            *reinterpret_cast<f32x4*>(out + (16 * r + (lane & 15)) * lda + wave * 16 * T + 16 * j + 4 * (lane >> 4)) = v;
+        }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) *reinterpret_cast<volatile uint32_t*>(lflag + wave) = count;
+    asm volatile("" ::: "memory");
+}
+
+// Block until wave p has published at least `need` layer stores (its columns of the layer input).
+__device__ __forceinline__ void wait_layer(const uint32_t* lflag, int p, uint32_t need) {
+    while (*reinterpret_cast<const volatile uint32_t*>(lflag + p) < need) __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+}
+
 template <int T>
 __device__ __forceinline__ void load_bias(f32x4 (&bias)[T], const float* hb, int wave, int lane) {
 #pragma unroll
@@ -303,8 +334,17 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
     // candidates x 8 waves, whose MFMA loop already takes the whole 256-VGPR budget
     constexpr bool EREG = SS <= MBRL_EPI_REG_SLOTS && !(R == 2 && NW == 8);
     static_assert(!RING || ((K0C_T + NOT_T) % NB == 0 && K0C_T % 2 == 0 && NOT_T % 2 == 0), "ring layout");
+    // hidden-layer hand-offs by per-wave flags (hidden_store_flag / wait_layer): a wave starts layer
+    // l + 1 as soon as the producers of its first K chunks have stored layer l, so the waves that win
+    // the MFMA arbitration run ahead instead of idling at a barrier. Layer l + 1 consumes every wave's
+    // layer-l columns before it stores, and a wave stores layer l only after reading all of layer l's
+    // input, so no buffer is overwritten while another wave still reads it (the ping-pong invariant
+    // the barriers kept).
+    constexpr bool LFLAGS = RING && MBRL_LAYER_FLAGS;
+    uint32_t nstore = 0;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const LdsMap L = lds_map(A, smem, M);
+    uint32_t* const lflag = L.lflag;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int ntiles = (A.N + M - 1) / M;
     int tile, e;
@@ -373,6 +413,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
     const int npass = A.reward ? 2 : 1;
     const float rmean = (A.reward && A.unnorm_r) ? A.rew_mean[0] : 0.f;
     const float rstd = (A.reward && A.unnorm_r) ? A.rew_std[0] : 1.f;
+    if (tid < NW) lflag[tid] = 0;
     __syncthreads();
 
     // ---- weight stream: this wave's slice of chunk g is at wb + g * cs (f32x4 units)
@@ -411,6 +452,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
 #define MBRL_HIDDEN_CHUNK(SLOT, KC, NK, IN)                                          \
     do {                                                                             \
         MBRL_LOAD_CHUNK(ring[((SLOT) + NB - 1) % NB], g + NB - 1);                   \
+        if (LFLAGS && (KC) + 1 < (NK) && ((KC) + 1) % TW == 0) wait_layer(lflag, ((KC) + 1) / TW, nstore); \
         if ((KC) + 1 < (NK)) read_a<R>(aAB[((KC) + 1) & 1], IN, A.lda, (KC) + 1, lane); \
         mma_hidden<TW, R>(acc, aAB[(KC) & 1], ring[SLOT]);                           \
         interleave_loads<TW, R>();                                                   \
@@ -452,7 +494,10 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
         // The last hidden layer's activations stay in registers: the output layer splits K by wave,
         // so wave w only needs the columns it produced itself, in exactly the accumulator layout
         // (lane: 4 consecutive units of candidate lane & 15). No LDS store, barrier or re-read.
-        if (A.L > 1) hidden_store<TW, R>(acc, bias, actY, A.lda, wave, lane);
+        if (A.L > 1) {
+            if constexpr (LFLAGS) hidden_store_flag<TW, R>(acc, bias, actY, A.lda, wave, lane, lflag, ++nstore);
+            else hidden_store<TW, R>(acc, bias, actY, A.lda, wave, lane);
+        }
         STAMP(1);
         // ---- hidden layers 1..L-1 (W -> W), alternating Y->X->Y...
         float* in = actY;
@@ -460,13 +505,17 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
         for (int l = 1; l < A.L; ++l) {
             zero_acc<TW, R>(acc);
             load_bias<TW>(bias, L.hbias + l * A.Wpad, wave, lane);
+            if constexpr (LFLAGS) wait_layer(lflag, 0, nstore);
             read_a<R>(aAB[0], in, A.lda, 0, lane);
             constexpr int KH = 4 * T;  // 4T % NB == 0: every hidden layer starts on the same slot
             constexpr int S0 = RING ? K0C_T % NB : 0;
 #pragma unroll
             for (int kc = 0; kc < KH; ++kc) MBRL_HIDDEN_CHUNK((S0 + kc) % NB, kc, KH, in);
             STAMP(2);
-            if (l + 1 < A.L) hidden_store<TW, R>(acc, bias, out, A.lda, wave, lane);
+            if (l + 1 < A.L) {
+                if constexpr (LFLAGS) hidden_store_flag<TW, R>(acc, bias, out, A.lda, wave, lane, lflag, ++nstore);
+                else hidden_store<TW, R>(acc, bias, out, A.lda, wave, lane);
+            }
             STAMP(3);
             float* tmp = in; in = out; out = tmp;
         }
@@ -726,8 +775,14 @@ __global__ void __launch_bounds__(64 * m8_waves(T, NOT_T), 1) rollout_m8_kernel(
     constexpr int NPW = (FPW / 16) / TW16;   // its partials inside this wave's own chunks
     constexpr int SS = NOT_T;
     static_assert(KH % NB == 0 && (T == 4 || T == 8), "m8 geometry");
+    // hidden-layer hand-offs by per-wave flags, as in rollout_kernel (wave w produces K chunks
+    // [CPW w, CPW (w + 1)) of the next layer)
+    constexpr bool LFLAGS = MBRL_LAYER_FLAGS;
+    constexpr int CPW = FPW / 16;
+    uint32_t nstore = 0;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const LdsMap L = lds_map(A, smem, M);
+    uint32_t* const lflag = L.lflag;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int ntiles = (A.N + M - 1) / M;
     int tile, e;
@@ -781,6 +836,7 @@ __global__ void __launch_bounds__(64 * m8_waves(T, NOT_T), 1) rollout_m8_kernel(
         const float v = rowsum16(acp[0]);
         if ((lane & 15) == 0) acs[epi_row(0, awave, lane)] = v;
     }
+    if (tid < NW) lflag[tid] = 0;
     __syncthreads();
 
     // ---- weight stream: chunk g of this wave at byte (g T + wave) 4096 + s 1024 + lane 16
@@ -865,6 +921,17 @@ __global__ void __launch_bounds__(64 * m8_waves(T, NOT_T), 1) rollout_m8_kernel(
             *reinterpret_cast<f32x4*>(out + cand * A.lda + FPW * wave + 32 * u + 4 * (lane >> 3)) = v;
         }
     };
+    // a stored layer another wave reads: publish it (flags) or wait for every wave (barrier)
+    auto publish_layer = [&]() {
+        if constexpr (LFLAGS) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            ++nstore;
+            if (lane == 0) *reinterpret_cast<volatile uint32_t*>(lflag + wave) = nstore;
+            asm volatile("" ::: "memory");
+        } else {
+            __syncthreads();
+        }
+    };
     auto load_bias8 = [&](const float* hb) {
 #pragma unroll
         for (int u = 0; u < TPW; ++u)
@@ -875,9 +942,10 @@ __global__ void __launch_bounds__(64 * m8_waves(T, NOT_T), 1) rollout_m8_kernel(
         for (int u = 0; u < TPW; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
     };
 // one hidden-type chunk: refill the slot chunk c-1 vacated, read the next chunk's B, MFMAs of chunk c
-#define M8_CHUNK(SLOT, KC, NK, IN)                                          \
+#define M8_CHUNK(SLOT, KC, NK, IN, FL)                                      \
     do {                                                                    \
         M8_LOAD(((SLOT) + NB - 1) % NB, g + NB - 1);                         \
+        if (LFLAGS && (FL) && (KC) + 1 < (NK) && ((KC) + 1) % CPW == 0) wait_layer(lflag, ((KC) + 1) / CPW, nstore); \
         if ((KC) + 1 < (NK)) read_b(bb[((KC) + 1) & 1], IN, 16 * ((KC) + 1)); \
         mma_pair(ring[SLOT], bb[(KC) & 1]);                                 \
         MBRL_PIN();                                                         \
@@ -904,23 +972,24 @@ __global__ void __launch_bounds__(64 * m8_waves(T, NOT_T), 1) rollout_m8_kernel(
             ++g;
         } else {
 #pragma unroll
-            for (int kc = 0; kc < K0C_T; ++kc) M8_CHUNK(kc % NB, kc, K0C_T, actX);
+            for (int kc = 0; kc < K0C_T; ++kc) M8_CHUNK(kc % NB, kc, K0C_T, actX, false);
         }
         STAMP(0);
         store_layer(actY);
-        if (A.L > 1) __syncthreads();
+        if (A.L > 1) publish_layer();
         STAMP(1);
         float* in = actY;
         float* out = actX;
         for (int l = 1; l < A.L; ++l) {
             zero_acc8();
             load_bias8(L.hbias + l * A.Wpad);
+            if constexpr (LFLAGS) wait_layer(lflag, 0, nstore);
             read_b(bb[0], in, 0);
 #pragma unroll
-            for (int kc = 0; kc < KH; ++kc) M8_CHUNK((K0C_T + kc) % NB, kc, KH, in);
+            for (int kc = 0; kc < KH; ++kc) M8_CHUNK((K0C_T + kc) % NB, kc, KH, in, true);
             STAMP(2);
             store_layer(out);
-            if (l + 1 < A.L) __syncthreads();   // the last hidden layer is read back by its own wave only
+            if (l + 1 < A.L) publish_layer();   // the last hidden layer is read back by its own wave only
             STAMP(3);
             float* tmp = in; in = out; out = tmp;
         }
