@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MBRL_ABI_VERSION 7
+#define MBRL_ABI_VERSION 8
 
 typedef struct ihipStream_t* mbrl_stream_t; /* == hipStream_t */
 typedef struct ihipEvent_t* mbrl_event_t;   /* == hipEvent_t  */
@@ -157,7 +157,9 @@ enum {
     MBRL_OPT_XCD_MAP = 7,           /* 1: ensemble rollouts map workgroups member-major per XCD (A/B) */
     MBRL_OPT_TRAIN_TILE = 8,        /* training backward C tile height: 0 auto, 32, 64 (bit-identical) */
     MBRL_OPT_TRAIN_NO_FOLD = 9,     /* 1: the layer-0 weight gradient in its own launch (bit-identical) */
-    MBRL_OPT_COUNT = 10
+    MBRL_OPT_ROLLOUT_PAIR = 10,     /* column-split pairs in plans: 0 auto, 1 forced (MBRL_EUNSUPPORTED where
+                                       they cannot run), 2 never; standalone rollouts never use them  */
+    MBRL_OPT_COUNT = 11
 };
 int mbrl_set_option(int32_t option, int32_t value);
 int mbrl_get_option(int32_t option);

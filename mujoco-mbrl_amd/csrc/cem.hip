@@ -27,6 +27,11 @@ static thread_local std::string g_err;
 
 // mbrl_set_option switches (include/mbrl_cem.h MBRL_OPT_*); 0 = automatic.
 static std::atomic<int> g_opt[MBRL_OPT_COUNT];
+// MBRL_OPT_ROLLOUT_PAIR = 0 (auto) takes column-split pairs for small plans when this is set
+#ifndef MBRL_PAIR_AUTO
+#define MBRL_PAIR_AUTO 0
+#endif
+static constexpr bool kPairAuto = MBRL_PAIR_AUTO;
 
 static int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 static int fail(int code, const char* fmt, ...) {
@@ -1021,10 +1026,26 @@ static int sample_impl(const mbrl_sampler* sp, int H, int a, int N, int n_offset
     return hip_check(hipGetLastError(), "sample launch");
 }
 
+// Column-split pair exchange area a plan workspace reserves for N candidates (0: pairs not offered:
+// Wpad != 512, or more than 256 workgroups, the co-resident count of the 256-CU MI355X).
+static size_t pair_area_bytes(const Geometry& g, int N) {
+    const int ntiles = (N + 15) / 16;
+    if (g.T != 8 || (size_t)2 * ntiles * g.E > 256) return 0;
+    return pair_layout(g.Wpad, g.pw, ntiles, g.E).bytes;
+}
+
+// MBRL_OPT_ROLLOUT_PAIR = 1 on a plan whose shape or size has no pair area: an error, not a fallback.
+static int pair_forced_check(const Geometry& g, int N) {
+    if (g_opt[MBRL_OPT_ROLLOUT_PAIR].load(std::memory_order_relaxed) == 1 && pair_area_bytes(g, N) == 0)
+        return fail(MBRL_EUNSUPPORTED, "rollout_pair forced: no pair kernel for N=%d (Wpad %d, E %d)", N, g.Wpad, g.E);
+    return MBRL_OK;
+}
+
+// pair_area: a pair_area_bytes(g, N) block of the caller's workspace, or NULL (no column-split pairs).
 static int rollout_impl(const Geometry& g, const void* packed, const mbrl_norm* norm, const mbrl_cost* cost,
                         const float* s0, int s0_per_cand, const float* actions, const mbrl_sampler* sampler,
                         int N, int H, int n_offset, float* costs, float* actions_out, float* states_out,
-                        hipStream_t stream) {
+                        hipStream_t stream, void* pair_area = nullptr) {
     if (!packed || !s0 || !costs) return fail(MBRL_EINVAL, "packed, s0 and costs must be non-NULL");
     if (N < 1 || H < 1) return fail(MBRL_EINVAL, "N=%d H=%d must be >= 1", N, H);
     if (!actions && !sampler) return fail(MBRL_EINVAL, "need either actions or a sampler");
@@ -1114,6 +1135,28 @@ static int rollout_impl(const Geometry& g, const void* packed, const mbrl_norm* 
     // 8-candidate tiles (rollout_m8_kernel, bit-identical sums) when 16-candidate tiles would leave
     // at least half the CUs idle: the shard of a strong-scaled plan, small plans.
     // MBRL_OPT_ROLLOUT_TILE = 8 / 16 forces a choice (tests, A/B).
+    // column-split pairs: each 16-candidate tile on two workgroups of half the columns (16x16x4 MFMA at
+    // full clock, half the weight stream per workgroup) where 16-candidate tiles would leave at least
+    // half the CUs idle; opt-in until measured (MBRL_OPT_ROLLOUT_PAIR)
+    if (pair_area && !A.reward && g_opt[MBRL_OPT_ROLLOUT_TILE].load(std::memory_order_relaxed) == 0) {
+        const int po = g_opt[MBRL_OPT_ROLLOUT_PAIR].load(std::memory_order_relaxed);
+        const int ntiles = (N + 15) / 16;
+        const bool want = po == 1 || (po == 0 && kPairAuto && (size_t)ntiles * g.E * 2 <= (size_t)device_cus());
+        if (want && pair_area_bytes(g, N) != 0) {
+            RolloutArgs P = A;
+            P.pair_flags = static_cast<unsigned*>(pair_area);
+            P.pair_data = reinterpret_cast<float*>(static_cast<char*>(pair_area) +
+                                                   pair_layout(g.Wpad, g.pw, ntiles, g.E).flags_bytes);
+            if (rollout_pair_supported(P, g.T)) {
+                const hipError_t err = launch_rollout_pair(P, g.T, stream);
+                if (err != hipErrorCooperativeLaunchTooLarge || po == 1) return hip_check(err, "rollout pair launch");
+            } else if (po == 1) {
+                return fail(MBRL_EUNSUPPORTED, "rollout_pair forced: shape not supported by the pair kernel");
+            }
+        } else if (po == 1) {
+            return fail(MBRL_EUNSUPPORTED, "rollout_pair forced: no pair area for N=%d (Wpad %d, E %d)", N, g.Wpad, g.E);
+        }
+    }
     if (g.m8_ok) {
         A.m8_off = g.m8_off;
         A.C8 = g.C8;
@@ -1302,6 +1345,7 @@ int mbrl_set_option(int32_t option, int32_t value) {
         case MBRL_OPT_SPLIT_TILE: ok = value == 0 || value == 16 || value == 32; break;
         case MBRL_OPT_ADAM_ARITH: ok = value >= 0 && value <= 16; break;
         case MBRL_OPT_TRAIN_TILE: ok = value == 0 || value == 32 || value == 64; break;
+        case MBRL_OPT_ROLLOUT_PAIR: ok = value >= 0 && value <= 2; break;
         default: ok = value == 0 || value == 1; break;
     }
     if (!ok) return fail(MBRL_EINVAL, "option %d: value %d not allowed", option, value);
@@ -1658,6 +1702,7 @@ int mbrl_trajectory(const mbrl_mlp_shape* shape, const void* packed, const mbrl_
 // Workspace layout for mbrl_cem_plan.
 struct PlanWs {
     float *costs, *mu[2], *sigma[2], *aelite, *states, *tmp_cost, *actions, *s0;
+    void* pair;   // column-split pair exchange area (NULL-sized when pairs are not offered)
     unsigned long long* xchg;
     unsigned* status;
     size_t xchg_bytes;
@@ -1685,6 +1730,7 @@ static PlanWs plan_ws(const Geometry& g, const mbrl_cem_params* p, void* base) {
     w.xchg = (unsigned long long*)take(w.xchg_bytes);
     w.status = (unsigned*)take(16);
     w.s0 = (float*)take((size_t)g.s * 4);
+    w.pair = take(pair_area_bytes(g, p->N));
     w.bytes = o;
     return w;
 }
@@ -1710,6 +1756,7 @@ int mbrl_cem_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_no
     if (!s0_in) return fail(MBRL_EINVAL, "s0 is NULL");
     PlanWs w = plan_ws(g, p, workspace);
     if (ws_bytes < w.bytes) return fail(MBRL_EWORKSPACE, "workspace %zu < %zu", ws_bytes, w.bytes);
+    if ((rc = pair_forced_check(g, p->N))) return rc;
     const int Ha = p->H * g.a;
     // Launches per iteration: rollout + one fused update (select, refit, next proposals) where it fits;
     // else the proposal draw, rollout, select and refit as separate launches.
@@ -1737,7 +1784,7 @@ int mbrl_cem_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_no
             if (rc) return rc;
         }
         rc = rollout_impl(g, packed, norm, cost, s0, 0, fuse_draw ? w.actions : nullptr, fuse_draw ? nullptr : &sp, p->N,
-                          p->H, 0, costs, w.actions, nullptr, stream);
+                          p->H, 0, costs, w.actions, nullptr, stream, pair_area_bytes(g, p->N) ? w.pair : nullptr);
         if (rc) return rc;
         if (rollout_events && rollout_events[2 * it + 1]) {
             rc = hip_check(hipEventRecord(reinterpret_cast<hipEvent_t>(rollout_events[2 * it + 1]), stream), "event");
@@ -1809,6 +1856,7 @@ int mbrl_comm_destroy(mbrl_comm_t comm) {
 
 struct ShardWs {
     float *local, *gathered, *costs, *actions, *mu[2], *sigma[2], *aelite, *states, *s0;
+    void* pair;
     unsigned long long* xchg;
     unsigned* status;
     size_t xchg_bytes;
@@ -1838,6 +1886,7 @@ static ShardWs shard_ws(const Geometry& g, const mbrl_cem_params* p, int G, void
     w.elites = (int64_t*)take((size_t)p->K * 8);
     w.keys = (uint32_t*)take((size_t)p->N * 4);
     w.s0 = (float*)take((size_t)g.s * 4);
+    w.pair = take(pair_area_bytes(g, Nl));
     w.bytes = o;
     return w;
 }
@@ -1867,6 +1916,7 @@ int mbrl_cem_plan_sharded(const mbrl_mlp_shape* shape, const void* packed, const
         return fail(MBRL_EINVAL, "plan_sharded: s0/actions_out/states_out/workspace NULL");
     const ShardWs w = shard_ws(g, p, nranks, workspace);
     if (ws_bytes < w.bytes) return fail(MBRL_EWORKSPACE, "workspace %zu < %zu", ws_bytes, w.bytes);
+    if ((rc = pair_forced_check(g, p->N / nranks))) return rc;
     const int N = p->N, Nl = N / nranks, H = p->H, a = g.a, E = g.E, Ha = H * a;
     const int off = rank * Nl;   // this rank's global candidates [off, off + Nl)
     const bool fuse = update_kpt(N, p->K, a) != 0 && g_opt[MBRL_OPT_UNFUSED_UPDATE].load(std::memory_order_relaxed) == 0;
@@ -1886,7 +1936,7 @@ int mbrl_cem_plan_sharded(const mbrl_mlp_shape* shape, const void* packed, const
             (rc = hip_check(hipEventRecord(reinterpret_cast<hipEvent_t>(rollout_events[2 * it]), stream), "event")))
             return rc;
         rc = rollout_impl(g, packed, norm, cost, w.s0, 0, w.actions, nullptr, Nl, H, 0, w.local, nullptr, nullptr,
-                          stream);
+                          stream, pair_area_bytes(g, Nl) ? w.pair : nullptr);
         if (rc) return rc;
         if (rollout_events && rollout_events[2 * it + 1] &&
             (rc = hip_check(hipEventRecord(reinterpret_cast<hipEvent_t>(rollout_events[2 * it + 1]), stream), "event")))

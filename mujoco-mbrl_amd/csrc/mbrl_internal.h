@@ -157,7 +157,30 @@ struct RolloutArgs {
     // ensembles (E > 1): a 1-D grid of ntiles * E workgroups whose ids map member-major onto the 8
     // XCDs (xcd_unit), so each XCD's L2 holds the weights of one or two members instead of all E
     int xcd_map;
+    // column-split pairs (rollout_kernel PAIR): two workgroups share a 16-candidate tile, each owning
+    // half of every hidden layer's columns; halves cross through pair_data (sc1 stores / loads) under
+    // per-workgroup flags (pair_flags: one 128-byte line per workgroup, zeroed before every launch)
+    float* pair_data;
+    unsigned* pair_flags;
+    unsigned* pair_status;   // bit 0: a hand-off wait timed out (results of that launch are invalid)
 };
+
+// Column-split pair exchange area for ntiles * E tiles (rollout_kernel PAIR): the flags block first
+// (one 128-byte line per workgroup, then a status line; zeroed by one memset per launch), then per
+// workgroup two parities of its published layer columns (16 x Wpad / 2 floats) and two parities of its
+// output-layer half sum (16 x pw floats).
+struct PairLayout {
+    size_t flags_bytes, layer_floats, part_floats, bytes;
+};
+inline PairLayout pair_layout(int Wpad, int pw, int ntiles, int E) {
+    PairLayout p;
+    const size_t wgs = (size_t)2 * ntiles * E;
+    p.flags_bytes = (wgs + 1) * 128;
+    p.layer_floats = (size_t)2 * 16 * (Wpad / 2);
+    p.part_floats = (size_t)2 * 16 * pw;
+    p.bytes = p.flags_bytes + wgs * (p.layer_floats + p.part_floats) * sizeof(float);
+    return p;
+}
 
 // Workgroup -> (tile, member). Dispatch places workgroup w on XCD w % 8 (round robin), so XCD k runs
 // ids k, k + 8, k + 16, ... in that order; xcd_map hands XCD k the contiguous unit range
@@ -252,6 +275,11 @@ bool rollout_m8_supported(const RolloutArgs& A, int T);
 hipError_t launch_rollout_m8(const RolloutArgs& A, int T, hipStream_t stream);
 bool rollout_m4_supported(const RolloutArgs& A, int T, int NG);
 hipError_t launch_rollout_m4(const RolloutArgs& A, int T, int NG, hipStream_t stream);
+// Column-split pairs: 16-candidate tiles on two workgroups each (8 waves: 4 compute, 4 hand-off).
+// Supported for Wpad 512, fp32, goal-state cost, compile-time chunk counts, all 2 ntiles E workgroups
+// co-resident; A.pair_* point into a pair_layout() area.
+bool rollout_pair_supported(const RolloutArgs& A, int T);
+hipError_t launch_rollout_pair(const RolloutArgs& A, int T, hipStream_t stream);
 
 // F16X3 rollout (8 waves, 16 R candidates per workgroup, goal-state cost). Supported for
 // geometry.split_ok; the caller follows it with launch_rollout(redo = 1) at the same R.

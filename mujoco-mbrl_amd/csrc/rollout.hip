@@ -55,6 +55,11 @@
 #ifndef MBRL_LAYER_FLAGS
 #define MBRL_LAYER_FLAGS 0
 #endif
+// Timing ablation only (results are garbage): -DMBRL_PAIR_DIAG=1 keeps the column-split pairs' LDS
+// hand-off flow but drops every cross-workgroup store, poll and load.
+#ifndef MBRL_PAIR_DIAG
+#define MBRL_PAIR_DIAG 0
+#endif
 
 namespace mbrl {
 
@@ -313,6 +318,64 @@ __device__ __forceinline__ void stage_actions(const RolloutArgs& A, const EpiPar
     }
 }
 
+// ---- column-split pairs (rollout_kernel PAIR) --------------------------------------------------
+// Two workgroups share one 16-candidate tile. Half h computes the columns of virtual waves 4h..4h+3
+// of the 8-wave layout (its 4 compute waves), so every accumulator runs the 8-wave kernel's chains in
+// the canonical K order, and the output layer's four partials of half h are exactly halves 4h..4h+3
+// of the canonical sum: ((p0 + p1) + (p2 + p3)) + ((p4 + p5) + (p6 + p7)) = S_0 + S_1. The other 4
+// waves move the halves (MI355X_MICROARCH.md sc1 hand-off table, first row): after each layer barrier
+// every hand-off wave stores its compute wave's columns write-through (16-byte sc1 buffer stores),
+// drains them, and the last of the four (an LDS arrival counter) sets the workgroup's flag; one wave
+// polls the partner's flag (sc1 loads), the others wait on an LDS word it sets, and all four load the
+// partner's columns with sc1 loads into LDS, then count themselves into an LDS word the compute waves
+// wait on before their first read of partner columns. Half 0 owns the first K half of every layer,
+// so it starts on its own columns while the partner's arrive; half 1 trails it by one hand-off.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) unsigned gu32;
+constexpr int PAIR_SC1 = 16;   // buffer-op aux bit: sc1 (write-through stores, L1-bypassing loads)
+
+// Bounded poll of a partner's flag (relaxed agent-scope loads = sc1): false after ~200 ms, with bit 0
+// of the status word set, so a broken hand-off ends the launch instead of hanging the GPU.
+__device__ __forceinline__ bool pair_poll(gu32* flag, unsigned want, gu32* status) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {
+            __hip_atomic_fetch_or(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    return true;
+}
+
+typedef __attribute__((address_space(3))) uint32_t lu32;   // LDS words: ds_read / ds_write, not flat
+
+__device__ __forceinline__ void lds_wait_ge(const uint32_t* w, uint32_t need) {
+    while (*(const volatile lu32*)(w) < need) __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+}
+
+// This hand-off wave's stores are drained; count it in (LDS word arr) and let the last of the four
+// set the workgroup's flag to q + 1.
+__device__ __forceinline__ void pair_signal(uint32_t* arr, gu32* flag, unsigned q, int lane) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned old = 0;
+    if (lane == 0) old = atomicAdd(arr, 1u);
+    old = (unsigned)__shfl((int)old, 0, 64);
+    if (old == 4 * q + 3 && lane == 0) __hip_atomic_store(flag, q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Wait until the partner's flag reads q + 1: hand-off wave 0 polls it and publishes the match in LDS
+// (word go); the other three wait on that word.
+__device__ __forceinline__ void pair_await(gu32* pflag, uint32_t* go, unsigned q, int hw, int lane, gu32* status) {
+    if (hw == 0) {
+        pair_poll(pflag, q + 1, status);
+        if (lane == 0) *(volatile lu32*)(go) = q + 1;
+    } else {
+        lds_wait_ge(go, q + 1);
+    }
+}
+
 // K0C / NOT > 0: compile-time layer-0 / output chunk counts, enabling a 4-deep weight ring with
 // static register slots (three chunks = ~3000 MFMA cycles of load cover). K0C == 0: runtime counts,
 // 2-deep ring (any shape).
@@ -320,7 +383,7 @@ __device__ __forceinline__ void stage_actions(const RolloutArgs& A, const EpiPar
 // NW = 8 two waves share a SIMD: while one issues its weight loads the other keeps the matrix pipe
 // busy (a wave's own VMEM issue otherwise stalls its MFMA stream ~10 %: tools/ubench). The epilogue
 // (per-candidate VALU work) runs on waves 0-3.
-template <int T, int R, int K0C_T, int NOT_T, int NW>
+template <int T, int R, int K0C_T, int NOT_T, int NW, bool PAIR = false>
 __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A) {
     constexpr int M = 16 * R;
     constexpr int TW = 4 * T / NW;
@@ -334,6 +397,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
     // candidates x 8 waves, whose MFMA loop already takes the whole 256-VGPR budget
     constexpr bool EREG = SS <= MBRL_EPI_REG_SLOTS && !(R == 2 && NW == 8);
     static_assert(!RING || ((K0C_T + NOT_T) % NB == 0 && K0C_T % 2 == 0 && NOT_T % 2 == 0), "ring layout");
+    static_assert(!PAIR || (NW == 8 && R == 1 && RING && T % 2 == 0), "column-split pairs: 8 waves, 16 rows");
     // hidden-layer hand-offs by per-wave flags (hidden_store_flag / wait_layer): a wave starts layer
     // l + 1 as soon as the producers of its first K chunks have stored layer l, so the waves that win
     // the MFMA arbitration run ahead instead of idling at a barrier. Layer l + 1 consumes every wave's
@@ -348,7 +412,18 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int ntiles = (A.N + M - 1) / M;
     int tile, e;
-    xcd_unit(A.xcd_map, ntiles, tile, e);
+    int half = 0;          // PAIR: which column half of the tile this workgroup computes
+    if constexpr (PAIR) {
+        // pairs (u, u + 8) of each 16-id group: the same XCD under round-robin dispatch
+        const int u = blockIdx.x;
+        tile = (u >> 4) * 8 + (u & 7);
+        half = (u >> 3) & 1;
+        e = blockIdx.y;
+        if (tile >= ntiles) return;   // both halves of a padding pair leave together
+    } else {
+        xcd_unit(A.xcd_map, ntiles, tile, e);
+    }
+    const int cw = PAIR ? 4 * half + wave : wave;   // the 8-wave layout's wave whose columns this one computes
     if (A.redo) {
         // F16X3 redo pass (rollout_f16x3.hip): run only where the split kernel left MBRL_REDO_MARK
         bool any = false;
@@ -416,15 +491,115 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
     if (tid < NW) lflag[tid] = 0;
     __syncthreads();
 
+    // PAIR: lflag[0] counts the hand-off waves' finished partner copies (the compute waves wait on it),
+    // lflag[1] their drained publishes, lflag[2] the partner flag value seen by hand-off wave 0
+    [[maybe_unused]] const int pwait = PAIR ? (half ? 0 : 2 * T) : -1;   // first K chunk of the partner's columns
+    [[maybe_unused]] uint32_t xneed = 0;                                   // hand-offs consumed so far
+    if constexpr (PAIR) {
+        if (wave >= 4) {
+            // ---- hand-off waves: per step the same barriers as the compute waves, and after each one
+            // the hand-off of what the compute waves stored before it
+            const int hw = wave - 4;
+            const int sid = (e * ntiles + tile) * 2 + half;
+            const size_t per = (size_t)16 * A.Wpad + (size_t)32 * A.pw;          // floats per workgroup
+            gu32* const flags = (gu32*)(A.pair_flags);
+            gu32* const status = flags + (size_t)2 * ntiles * A.E * 32;
+            gu32* const myflag = flags + (size_t)sid * 32;
+            gu32* const pflag = flags + (size_t)(sid ^ 1) * 32;
+            const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+                A.pair_data, 0, (int)((size_t)2 * ntiles * A.E * per * sizeof(float)), 0x00020000);
+            const unsigned mine = (unsigned)((size_t)sid * per * sizeof(float));
+            const unsigned theirs = (unsigned)((size_t)(sid ^ 1) * per * sizeof(float));
+            const int ocw = 4 * (half ^ 1) + hw;   // the partner's compute wave paired with this one
+            unsigned q = 0;
+            // layer columns: publish this half's cw = 4 half + hw slice of buffer `buf`, copy the partner's in
+            auto layer = [&](float* buf) {
+                const unsigned slot = (unsigned)((((q & 1) * 4 + hw) * TW * 64 + lane) * 16);
+                const int row = (lane & 15) * A.lda + 4 * (lane >> 4);
+                f32x4 v[TW];
+#pragma unroll
+                for (int j = 0; j < TW; ++j) v[j] = *reinterpret_cast<const f32x4*>(buf + row + (4 * half + hw) * 16 * TW + 16 * j);
+                if constexpr (!MBRL_PAIR_DIAG) {
+#pragma unroll
+                    for (int j = 0; j < TW; ++j)
+                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[j]), xr, mine + slot + j * 1024, 0, PAIR_SC1);
+                    pair_signal(lflag + 1, myflag, q, lane);
+                    pair_await(pflag, lflag + 2, q, hw, lane, status);
+#pragma unroll
+                    for (int j = 0; j < TW; ++j)
+                        v[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, theirs + slot + j * 1024, 0, PAIR_SC1));
+                }
+#pragma unroll
+                for (int j = 0; j < TW; ++j) *reinterpret_cast<f32x4*>(buf + row + ocw * 16 * TW + 16 * j) = v[j];
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                if (lane == 0) atomicAdd(lflag, 1u);
+                ++q;
+            };
+            // output layer: this half's sum of its four partials, then S_0 + S_1 into partial slot 0
+            auto partials = [&]() {
+                const int ws = M * A.pw, nel = M * A.s;
+                const unsigned pslot = (unsigned)((16 * A.Wpad + (q & 1) * 16 * A.pw) * sizeof(float));
+                float so[NOT_T];
+#pragma unroll
+                for (int i = 0; i < NOT_T; ++i) {
+                    const int idx = 256 * i + 64 * hw + lane;
+                    so[i] = 0.f;
+                    if (idx < nel) {
+                        const int m = idx / A.s, ro = m * A.pw + (idx - m * A.s);
+                        so[i] = (L.part[ro] + L.part[ws + ro]) + (L.part[2 * ws + ro] + L.part[3 * ws + ro]);
+                        if constexpr (!MBRL_PAIR_DIAG)
+                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(so[i]), xr, mine + pslot + idx * 4, 0, PAIR_SC1);
+                    }
+                }
+                if constexpr (!MBRL_PAIR_DIAG) {
+                    pair_signal(lflag + 1, myflag, q, lane);
+                    pair_await(pflag, lflag + 2, q, hw, lane, status);
+                }
+#pragma unroll
+                for (int i = 0; i < NOT_T; ++i) {
+                    const int idx = 256 * i + 64 * hw + lane;
+                    if (idx < nel) {
+                        const float sp = MBRL_PAIR_DIAG ? 0.f : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, theirs + pslot + idx * 4, 0, PAIR_SC1));
+                        const int m = idx / A.s, ro = m * A.pw + (idx - m * A.s);
+                        L.part[ro] = so[i] + sp;    // S_0 + S_1 (exactly commutative)
+                    }
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                if (lane == 0) atomicAdd(lflag, 1u);
+                ++q;
+            };
+            for (int t = 0; t < A.H; ++t) {
+                if (t + 1 < A.H) fetch_actions<R>(A, tile, t + 1, awave, lane, av);
+                if (A.L > 1) {
+                    __syncthreads();     // layer 0 stored (actY)
+                    layer(actY);
+                }
+                for (int l = 1; l + 1 < A.L; ++l) {
+                    __syncthreads();     // hidden layer l stored (odd l: actX)
+                    layer((l & 1) ? actX : actY);
+                }
+                __syncthreads();         // output partials stored
+                partials();
+                if (t + 1 < A.H) {
+                    stage_actions<R, SS, EREG>(A, P, L, actX, awave, lane, av, acp);
+                    const float v = rowsum16(acp[0]);
+                    if ((lane & 15) == 0) acs[((t + 1) & 1) * M + epi_row(0, awave, lane)] = v;
+                }
+                __syncthreads();         // epilogue done
+            }
+            return;
+        }
+    }
+
     // ---- weight stream: this wave's slice of chunk g is at wb + g * cs (f32x4 units)
-    const f32x4* wb = reinterpret_cast<const f32x4*>(member) + wave * TW * 64 + lane;
+    const f32x4* wb = reinterpret_cast<const f32x4*>(member) + cw * TW * 64 + lane;
     const int cs = 4 * T * 64;
     const int C = A.chunks_per_step;
 #ifdef MBRL_BUFFER_LOAD
     (void)wb;
     const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(member), 0, (int)(A.stream_floats * sizeof(float)), 0x00020000);
-    const unsigned lane_off = (unsigned)((wave * TW * 64 + lane) * 16);
+    const unsigned lane_off = (unsigned)((cw * TW * 64 + lane) * 16);
 #define MBRL_LOAD_CHUNK(DST, G) \
     load_chunk_buf<TW>(DST, wrsrc, lane_off + (unsigned)(((G) < C ? (G) : (G) - C) * cs * 16))
 #else
@@ -453,6 +628,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
     do {                                                                             \
         MBRL_LOAD_CHUNK(ring[((SLOT) + NB - 1) % NB], g + NB - 1);                   \
         if (LFLAGS && (KC) + 1 < (NK) && ((KC) + 1) % TW == 0) wait_layer(lflag, ((KC) + 1) / TW, nstore); \
+        if (PAIR && (KC) + 1 == pwait) lds_wait_ge(lflag, 4 * ++xneed);             \
         if ((KC) + 1 < (NK)) read_a<R>(aAB[((KC) + 1) & 1], IN, A.lda, (KC) + 1, lane); \
         mma_hidden<TW, R>(acc, aAB[(KC) & 1], ring[SLOT]);                           \
         interleave_loads<TW, R>();                                                   \
@@ -468,7 +644,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
         if (actw && pass == 0 && t + 1 < A.H) fetch_actions<R>(A, tile, t + 1, awave, lane, av);
         // ---- layer 0: actX [s | a | 0-pad] -> actY (W)
         zero_acc<TW, R>(acc);
-        load_bias<TW>(bias, L.hbias, wave, lane);
+        load_bias<TW>(bias, L.hbias, cw, lane);
         read_a<R>(aAB[0], actX, A.lda, 0, lane);
         if constexpr (RING) {
             // a chunk whose 16 inputs are all zero padding (k >= s + a) is skipped: the accumulator starts
@@ -495,8 +671,8 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
         // so wave w only needs the columns it produced itself, in exactly the accumulator layout
         // (lane: 4 consecutive units of candidate lane & 15). No LDS store, barrier or re-read.
         if (A.L > 1) {
-            if constexpr (LFLAGS) hidden_store_flag<TW, R>(acc, bias, actY, A.lda, wave, lane, lflag, ++nstore);
-            else hidden_store<TW, R>(acc, bias, actY, A.lda, wave, lane);
+            if constexpr (LFLAGS) hidden_store_flag<TW, R>(acc, bias, actY, A.lda, cw, lane, lflag, ++nstore);
+            else hidden_store<TW, R>(acc, bias, actY, A.lda, cw, lane);
         }
         STAMP(1);
         // ---- hidden layers 1..L-1 (W -> W), alternating Y->X->Y...
@@ -504,8 +680,9 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
         float* out = actX;
         for (int l = 1; l < A.L; ++l) {
             zero_acc<TW, R>(acc);
-            load_bias<TW>(bias, L.hbias + l * A.Wpad, wave, lane);
+            load_bias<TW>(bias, L.hbias + l * A.Wpad, cw, lane);
             if constexpr (LFLAGS) wait_layer(lflag, 0, nstore);
+            if (PAIR && pwait == 0) lds_wait_ge(lflag, 4 * ++xneed);   // half 1: the partner's columns come first
             read_a<R>(aAB[0], in, A.lda, 0, lane);
             constexpr int KH = 4 * T;  // 4T % NB == 0: every hidden layer starts on the same slot
             constexpr int S0 = RING ? K0C_T % NB : 0;
@@ -513,8 +690,8 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
             for (int kc = 0; kc < KH; ++kc) MBRL_HIDDEN_CHUNK((S0 + kc) % NB, kc, KH, in);
             STAMP(2);
             if (l + 1 < A.L) {
-                if constexpr (LFLAGS) hidden_store_flag<TW, R>(acc, bias, out, A.lda, wave, lane, lflag, ++nstore);
-                else hidden_store<TW, R>(acc, bias, out, A.lda, wave, lane);
+                if constexpr (LFLAGS) hidden_store_flag<TW, R>(acc, bias, out, A.lda, cw, lane, lflag, ++nstore);
+                else hidden_store<TW, R>(acc, bias, out, A.lda, cw, lane);
             }
             STAMP(3);
             float* tmp = in; in = out; out = tmp;
@@ -599,22 +776,23 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
             const float* bout = L.hbias + A.L * A.Wpad;
             const int ws = M * A.pw;
             const int j = lane & 15;
+            if constexpr (PAIR) lds_wait_ge(lflag, 4 * ++xneed);   // S_0 + S_1 in partial slot 0
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const int m = epi_row(r, wave, lane);
                 const int n = tile * M + m;
                 float sc = 0.f;
-                auto slot = [&](int d, float om, float os, float goal, float cw, float bo) {
+                auto slot = [&](int d, float om, float os, float goal, float cwt, float bo) {
                     const int ro = m * A.pw + d;
-                    float o = sum_partials<NW>(L.part, ws, ro);
+                    float o = PAIR ? L.part[ro] : sum_partials<NW>(L.part, ws, ro);
                     o = o + bo;
                     const float sn = A.unnorm_s ? o * os + om : o;
                     if (A.has_sc) {
-                        const float x = (sn - goal) * cw;
+                        const float x = (sn - goal) * cwt;
                         sc += sqrtf(x * x + A.alpha_s2) - A.alpha_s;
                     }
                     actX[m * A.lda + d] = A.norm_s ? (sn - om) / os : sn;
-                    if (A.states_out != nullptr && n < A.N)
+                    if (A.states_out != nullptr && n < A.N && (!PAIR || half == 0))
                         A.states_out[(((size_t)e * A.H + t) * A.N + n) * A.s + d] = sn;
                 };
                 if constexpr (RING && EREG) {
@@ -660,7 +838,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
         for (int k = 0; k < NSEG; ++k) dst[k] = seg[k];
     }
 #endif
-    if (epi && (lane & 15) == 0) {
+    if (epi && (lane & 15) == 0 && (!PAIR || half == 0)) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int n = tile * M + epi_row(r, wave, lane);
@@ -713,6 +891,47 @@ hipError_t launch_rollout(const RolloutArgs& A, int T, int R, hipStream_t stream
     MBRL_CASE(1, 1) MBRL_CASE(2, 1) MBRL_CASE(4, 1) MBRL_CASE(8, 1) MBRL_CASE(16, 1)
     MBRL_CASE(1, 2) MBRL_CASE(2, 2) MBRL_CASE(4, 2) MBRL_CASE(8, 2)
 #undef MBRL_CASE
+    return hipErrorInvalidValue;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Column-split pairs: rollout_kernel<T, 1, K0C, NOT, 8, true>, 2 ceil(N / 16) E
+// workgroups, all co-resident (checked; a hand-off never waits on an undispatched workgroup).
+bool rollout_pair_supported(const RolloutArgs& A, int T) {
+    if (A.reward || A.redo || !A.pair_data || !A.pair_flags || T != 8) return false;
+    if (!((A.K0C == 2 || A.K0C == 6) && (A.NOT == 2 || A.NOT == 6))) return false;
+    RolloutArgs X = A;
+    X.nw = 8;
+    X.part_alias = 0;
+    return rollout_lds_bytes(X, 16) <= 160 * 1024;
+}
+
+template <int T, int K0C_T, int NOT_T>
+static hipError_t launch_pair_tr(const RolloutArgs& A_in, hipStream_t stream) {
+    RolloutArgs A = A_in;
+    A.nw = 8;
+    A.part_alias = 0;
+    const int ntiles = (A.N + 15) / 16;
+    const dim3 grid(16 * ((ntiles + 7) / 8), A.E);
+    const size_t lds = rollout_lds_bytes(A, 16);
+    const auto fn = &rollout_kernel<T, 1, K0C_T, NOT_T, 8, true>;
+    hipError_t e = ensure_dynamic_lds(reinterpret_cast<const void*>(fn), 160 * 1024);
+    if (e != hipSuccess) return e;
+    if (!grid_fits(reinterpret_cast<const void*>(fn), 512, lds, (int)(grid.x * grid.y)))
+        return hipErrorCooperativeLaunchTooLarge;
+    // every polled word (flags, status) zeroed before every launch: one memset node
+    e = hipMemsetAsync(A.pair_flags, 0, pair_layout(A.Wpad, A.pw, ntiles, A.E).flags_bytes, stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(fn, grid, dim3(512), lds, stream, A);
+    return hipGetLastError();
+}
+
+hipError_t launch_rollout_pair(const RolloutArgs& A, int T, hipStream_t stream) {
+    if (T != 8) return hipErrorInvalidValue;
+    if (A.K0C == 2 && A.NOT == 2) return launch_pair_tr<8, 2, 2>(A, stream);
+    if (A.K0C == 6 && A.NOT == 6) return launch_pair_tr<8, 6, 6>(A, stream);
+    if (A.K0C == 2 && A.NOT == 6) return launch_pair_tr<8, 2, 6>(A, stream);
+    if (A.K0C == 6 && A.NOT == 2) return launch_pair_tr<8, 6, 2>(A, stream);
     return hipErrorInvalidValue;
 }
 

@@ -23,7 +23,7 @@ MBRL_COMM_ID_BYTES = 128
 MBRL_EUNSUPPORTED = -2
 MBRL_COST_GOAL_STATE = 0
 MBRL_COST_MODEL_REWARD = 1
-ABI_VERSION = 7
+ABI_VERSION = 8
 MBRL_NAN_LAST = 0
 MBRL_NAN_FIRST = 1
 MBRL_PRECISION_F32 = 0
@@ -32,7 +32,8 @@ MBRL_PRECISION_F16X6 = 2
 PRECISIONS = {"f32": MBRL_PRECISION_F32, "f16x3": MBRL_PRECISION_F16X3, "f16x6": MBRL_PRECISION_F16X6}
 # mbrl_set_option switches (include/mbrl_cem.h MBRL_OPT_*): A/B runs and forced fallbacks in tests
 OPTIONS = {"rollout_tile": 0, "split_tile": 1, "debug_traj_abort": 2, "gd_single": 3, "debug_gd_abort": 4,
-           "unfused_update": 5, "adam_arith": 6, "xcd_map": 7, "train_tile": 8, "train_no_fold": 9}
+           "unfused_update": 5, "adam_arith": 6, "xcd_map": 7, "train_tile": 8, "train_no_fold": 9,
+           "rollout_pair": 10}
 
 
 def precision_code(name):
