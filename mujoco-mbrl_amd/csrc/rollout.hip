@@ -60,6 +60,12 @@
 #ifndef MBRL_PAIR_DIAG
 #define MBRL_PAIR_DIAG 0
 #endif
+// Issue priority of the two waves that share a SIMD (8-wave kernels; MI355X_MICROARCH.md "Two waves
+// per SIMD"): 0 none; 1 the younger half (waves 4-7) at s_setprio 1 for the whole launch; 2 the two
+// halves trade priority every K chunk, so neither finishes a layer alone.
+#ifndef MBRL_PRIO
+#define MBRL_PRIO 0
+#endif
 
 namespace mbrl {
 
@@ -629,6 +635,10 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
         MBRL_LOAD_CHUNK(ring[((SLOT) + NB - 1) % NB], g + NB - 1);                   \
         if (LFLAGS && (KC) + 1 < (NK) && ((KC) + 1) % TW == 0) wait_layer(lflag, ((KC) + 1) / TW, nstore); \
         if (PAIR && (KC) + 1 == pwait) lds_wait_ge(lflag, 4 * ++xneed);             \
+        if (MBRL_PRIO == 2 && NW == 8) {                                             \
+            if (young != (((KC) & 1) != 0)) __builtin_amdgcn_s_setprio(1);          \
+            else __builtin_amdgcn_s_setprio(0);                                      \
+        }                                                                            \
         if ((KC) + 1 < (NK)) read_a<R>(aAB[((KC) + 1) & 1], IN, A.lda, (KC) + 1, lane); \
         mma_hidden<TW, R>(acc, aAB[(KC) & 1], ring[SLOT]);                           \
         interleave_loads<TW, R>();                                                   \
@@ -636,6 +646,10 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
         ++g;                                                                         \
     } while (0)
 
+    [[maybe_unused]] const bool young = NW == 8 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256;
+    if constexpr (MBRL_PRIO == 1 && NW == 8) {
+        if (young) __builtin_amdgcn_s_setprio(1);
+    }
     for (int tp = 0; tp < A.H * npass; ++tp) {
         const int t = A.reward ? (tp >> 1) : tp;
         const int pass = A.reward ? (tp & 1) : 0;
@@ -1165,12 +1179,20 @@ __global__ void __launch_bounds__(64 * m8_waves(T, NOT_T), 1) rollout_m8_kernel(
     do {                                                                    \
         M8_LOAD(((SLOT) + NB - 1) % NB, g + NB - 1);                         \
         if (LFLAGS && (FL) && (KC) + 1 < (NK) && ((KC) + 1) % CPW == 0) wait_layer(lflag, ((KC) + 1) / CPW, nstore); \
+        if (MBRL_PRIO == 2 && NW == 8) {                                    \
+            if (young != (((KC) & 1) != 0)) __builtin_amdgcn_s_setprio(1); \
+            else __builtin_amdgcn_s_setprio(0);                             \
+        }                                                                   \
         if ((KC) + 1 < (NK)) read_b(bb[((KC) + 1) & 1], IN, 16 * ((KC) + 1)); \
         mma_pair(ring[SLOT], bb[(KC) & 1]);                                 \
         MBRL_PIN();                                                         \
         ++g;                                                                \
     } while (0)
 
+    [[maybe_unused]] const bool young = NW == 8 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256;
+    if constexpr (MBRL_PRIO == 1 && NW == 8) {
+        if (young) __builtin_amdgcn_s_setprio(1);
+    }
     for (int t = 0; t < A.H; ++t) {
         int g = 0;
         if (actw && t + 1 < A.H) fetch_a(t + 1);
