@@ -127,9 +127,16 @@ __device__ __forceinline__ void load_chunk(f32x4 (&b)[T], const f32x4* __restric
 // per-lane offsets: one VGPR of address per load instead of two).
 template <int T>
 __device__ __forceinline__ void load_chunk_buf(f32x4 (&b)[T], __amdgpu_buffer_rsrc_t rsrc, unsigned voff) {
+#ifdef MBRL_DIAG_NOLOAD  // timing ablation only: no weight stream (results are garbage)
+    (void)rsrc;
+    (void)voff;
+#pragma unroll
+    for (int j = 0; j < T; ++j) asm volatile("" : "+v"(b[j]));
+#else
 #pragma unroll
     for (int j = 0; j < T; ++j)
         b[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + (unsigned)(j * 64 * 16), 0, 0));
+#endif
 }
 
 template <int R>
