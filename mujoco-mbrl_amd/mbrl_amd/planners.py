@@ -22,6 +22,7 @@ user's callables run on device tensors (reference semantics, planners.py:199-210
 refit still run in the HIP extension.
 """
 import threading
+import warnings
 
 import numpy as np
 import torch
@@ -604,7 +605,18 @@ def _rccl_comm(dev, world, rank):
             obj[0] = buf.raw
         dist.broadcast_object_list(obj, src=0)
         comm = ctypes.c_void_p()
-        _lib.check(lib.mbrl_comm_init(ctypes.c_char_p(obj[0]), world, rank, ctypes.byref(comm)), "mbrl_comm_init")
+        rc = lib.mbrl_comm_init(ctypes.c_char_p(obj[0]), world, rank, ctypes.byref(comm))
+        # every rank learns whether every rank joined: if one could not, all of them take the
+        # per-iteration protocol over torch.distributed instead (the same plan, bit for bit)
+        ok = torch.tensor([1 if rc == 0 else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()) == 0:
+            if rc == 0:
+                lib.mbrl_comm_destroy(comm)
+            msg = lib.mbrl_last_error() if rc else b"another rank"
+            warnings.warn(f"mbrl_amd: RCCL communicator unavailable ({msg.decode(errors='replace')}); "
+                          "sharded plans use the torch.distributed protocol")
+            comm = False
         _COMMS[key] = comm
     return comm
 
@@ -646,7 +658,7 @@ def _cem_sharded_native(prob, s0, st, world, rank):
 
 def _cem_fused_sharded(prob, s0, st, world):
     import torch.distributed as dist
-    if SHARDED_NATIVE and dist.get_backend() == "nccl":
+    if SHARDED_NATIVE and dist.get_backend() == "nccl" and _rccl_comm(prob.device, world, dist.get_rank()):
         return _cem_sharded_native(prob, s0, st, world, dist.get_rank())
     st = dict(st, E=prob.mdesc["E"], a=prob.mdesc["a"])
     return cem_sharded_protocol(_FusedShardOps(prob, s0, st), st, world, dist.get_rank())

@@ -736,6 +736,44 @@ def _rccl_worker(rank, world, init_file, out_dir):
                          returns=torch.stack(list(res["returns"])).cpu().numpy(),
                          costs=torch.stack(list(res["costs"])).cpu().numpy(),
                          actions=res["actions"].cpu().numpy(), states=res["states"].cpu().numpy())
+        # a communicator that cannot be created (simulated: mbrl_comm_init fails) sends every rank to
+        # the protocol, with a warning, instead of failing the plan
+        real_load = planners._lib.load
+
+        class _NoComm:
+            def __init__(self, lib):
+                self._lib = lib
+
+            def __getattr__(self, name):
+                return getattr(self._lib, name)
+
+            def mbrl_comm_init(self, *args):
+                return -3
+
+            def mbrl_last_error(self):
+                return b"simulated"
+
+        planners._COMMS.clear()
+        planners.SHARDED_NATIVE = True
+        planners._lib.load = lambda: _NoComm(real_load())
+        try:
+            import warnings
+            cid, over = RCCL_CASES[0]
+            p = oc.synth_problem(cid, **over)
+            _, model_fn, cost_fn, sample_action = build(p)
+            md = fused.describe_model(model_fn)
+            prob = fused.device_problem(md, fused.describe_cost(cost_fn, md["s"], md), dev)
+            st = CEMPlanner._settings(sample_action, over["H"], dict(num_candidates=over["N"], num_iterations=3,
+                                                                     seed=p["rng_seed"], record=True))
+            with warnings.catch_warnings(record=True) as w:
+                warnings.simplefilter("always")
+                res = planners._cem_fused_sharded(prob, torch.from_numpy(p["s0"]).to(dev), st, world)
+            assert any("RCCL communicator unavailable" in str(x.message) for x in w)
+            np.savez(os.path.join(out_dir, f"c{cid}_nfail_r{rank}.npz"), mu=res["mu"].cpu().numpy(),
+                     elites=torch.stack(list(res["elites"])).cpu().numpy())
+        finally:
+            planners._lib.load = real_load
+            planners._COMMS.clear()
     finally:
         planners.SHARDED_NATIVE = True
         dist.destroy_process_group()
@@ -755,6 +793,9 @@ def test_sharded_plan_over_rccl():
         mp.start_processes(_rccl_worker, args=(1, os.path.join(d, "pg"), d), nprocs=1, join=True,
                            start_method="spawn")
         got = {(cid, n): dict(np.load(os.path.join(d, f"c{cid}_n{n}_r0.npz"))) for cid, _ in RCCL_CASES for n in (0, 1)}
+        fail = dict(np.load(os.path.join(d, f"c{RCCL_CASES[0][0]}_nfail_r0.npz")))
+    assert np.array_equal(fail["mu"], got[(RCCL_CASES[0][0], 0)]["mu"])
+    assert np.array_equal(fail["elites"], got[(RCCL_CASES[0][0], 0)]["elites"])
     for cid, over in RCCL_CASES:
         p = ocem.synth_problem(cid, **over)
         _, model_fn, cost_fn, sample_action = build(p)
