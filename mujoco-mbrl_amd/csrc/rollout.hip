@@ -211,6 +211,21 @@ __device__ __forceinline__ void hidden_store(const f32x4 (&acc)[R][T], const f32
     __syncthreads();
 }
 
+// hidden_store without the barrier (the column-split pairs' first of two layer-0 stores)
+template <int T, int R>
+__device__ __forceinline__ void hidden_store_nobar(const f32x4 (&acc)[R][T], const f32x4 (&bias)[T], float* out,
+                                                   int lda, int wave, int lane) {
+    const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int j = 0; j < T; ++j) {
+            f32x4 v = acc[r][j] + bias[j];
+            v = __builtin_elementwise_max(v, zero);
+            *reinterpret_cast<f32x4*>(out + (16 * r + (lane & 15)) * lda + wave * 16 * T + 16 * j + 4 * (lane >> 4)) = v;
+        }
+}
+
 // hidden_store without the barrier; then this wave's count of finished layer stores is published
 // in LDS (lflag[wave]) once its own ds_writes have completed (s_waitcnt lgkmcnt(0)).
 template <int T, int R>
@@ -335,7 +350,9 @@ __device__ __forceinline__ void stage_actions(const RolloutArgs& A, const EpiPar
 // Two workgroups share one 16-candidate tile. Half h computes the columns of virtual waves 4h..4h+3
 // of the 8-wave layout (its 4 compute waves), so every accumulator runs the 8-wave kernel's chains in
 // the canonical K order, and the output layer's four partials of half h are exactly halves 4h..4h+3
-// of the canonical sum: ((p0 + p1) + (p2 + p3)) + ((p4 + p5) + (p6 + p7)) = S_0 + S_1. The other 4
+// of the canonical sum: ((p0 + p1) + (p2 + p3)) + ((p4 + p5) + (p6 + p7)) = S_0 + S_1. With two
+// layer-0 chunks both halves compute all of layer 0 (the partner's columns with the partner's exact
+// MFMA sequence), so a step has L - 1 hand-offs. The other 4
 // waves move the halves (MI355X_MICROARCH.md sc1 hand-off table, first row): after each layer barrier
 // every hand-off wave stores its compute wave's columns write-through (16-byte sc1 buffer stores),
 // drains them, and the last of the four (an LDS arrival counter) sets the workgroup's flag; one wave
@@ -411,6 +428,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
     constexpr bool EREG = SS <= MBRL_EPI_REG_SLOTS && !(R == 2 && NW == 8);
     static_assert(!RING || ((K0C_T + NOT_T) % NB == 0 && K0C_T % 2 == 0 && NOT_T % 2 == 0), "ring layout");
     static_assert(!PAIR || (NW == 8 && R == 1 && RING && T % 2 == 0), "column-split pairs: 8 waves, 16 rows");
+    constexpr bool L0DUP = PAIR && K0C_T == 2;   // PAIR: layer 0 computed by both halves (below)
     // hidden-layer hand-offs by per-wave flags (hidden_store_flag / wait_layer): a wave starts layer
     // l + 1 as soon as the producers of its first K chunks have stored layer l, so the waves that win
     // the MFMA arbitration run ahead instead of idling at a barrier. Layer l + 1 consumes every wave's
@@ -585,7 +603,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
                 if (t + 1 < A.H) fetch_actions<R>(A, tile, t + 1, awave, lane, av);
                 if (A.L > 1) {
                     __syncthreads();     // layer 0 stored (actY)
-                    layer(actY);
+                    if constexpr (!L0DUP) layer(actY);   // L0DUP: both halves computed all of layer 0
                 }
                 for (int l = 1; l + 1 < A.L; ++l) {
                     __syncthreads();     // hidden layer l stored (odd l: actX)
@@ -626,6 +644,23 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
     f32x4 bias[TW];
 #pragma unroll
     for (int q = 0; q < NB - 1; ++q) MBRL_LOAD_CHUNK(ring[q], q);
+    // PAIR with two layer-0 chunks: this wave also computes the partner half's layer-0 columns (the
+    // partner wave's exact MFMA sequence, weights held in registers for the launch), so hidden
+    // layer 1 starts without a hand-off
+    [[maybe_unused]] const int ocw0 = PAIR ? 4 * (half ^ 1) + wave : 0;
+    [[maybe_unused]] f32x4 w0p[L0DUP ? K0C_T : 1][TW];
+    if constexpr (L0DUP) {
+#ifdef MBRL_BUFFER_LOAD
+        const unsigned poff = (unsigned)((ocw0 * TW * 64 + lane) * 16);
+#pragma unroll
+        for (int kc = 0; kc < K0C_T; ++kc) load_chunk_buf<TW>(w0p[kc], wrsrc, poff + (unsigned)(kc * cs * 16));
+#else
+#pragma unroll
+        for (int kc = 0; kc < K0C_T; ++kc)
+            load_chunk<TW>(w0p[kc], reinterpret_cast<const f32x4*>(member) + ocw0 * TW * 64 + lane + (size_t)kc * cs);
+#endif
+    }
+    int pwl = -1;   // PAIR: first partner K chunk of the current hidden layer (-1: no hand-off to wait for)
     float total[R];  // return of row epi_row(r, wave, lane), held by the 16 lanes of that row
 #pragma unroll
     for (int r = 0; r < R; ++r) total[r] = 0.f;
@@ -641,7 +676,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
     do {                                                                             \
         MBRL_LOAD_CHUNK(ring[((SLOT) + NB - 1) % NB], g + NB - 1);                   \
         if (LFLAGS && (KC) + 1 < (NK) && ((KC) + 1) % TW == 0) wait_layer(lflag, ((KC) + 1) / TW, nstore); \
-        if (PAIR && (KC) + 1 == pwait) lds_wait_ge(lflag, 4 * ++xneed);             \
+        if (PAIR && (KC) + 1 == pwl) lds_wait_ge(lflag, 4 * ++xneed);               \
         if (MBRL_PRIO == 2 && NW == 8) {                                             \
             if (young != (((KC) & 1) != 0)) __builtin_amdgcn_s_setprio(1);          \
             else __builtin_amdgcn_s_setprio(0);                                      \
@@ -692,8 +727,19 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
         // so wave w only needs the columns it produced itself, in exactly the accumulator layout
         // (lane: 4 consecutive units of candidate lane & 15). No LDS store, barrier or re-read.
         if (A.L > 1) {
-            if constexpr (LFLAGS) hidden_store_flag<TW, R>(acc, bias, actY, A.lda, cw, lane, lflag, ++nstore);
-            else hidden_store<TW, R>(acc, bias, actY, A.lda, cw, lane);
+            if constexpr (L0DUP) {
+                hidden_store_nobar<TW, R>(acc, bias, actY, A.lda, cw, lane);
+                zero_acc<TW, R>(acc);
+                load_bias<TW>(bias, L.hbias, ocw0, lane);
+#pragma unroll
+                for (int kc = 0; kc < K0C_T; ++kc)
+                    if (16 * kc < A.s + A.a) mma_hidden<TW, R>(acc, aAB[kc & 1], w0p[kc]);
+                hidden_store<TW, R>(acc, bias, actY, A.lda, ocw0, lane);
+            } else if constexpr (LFLAGS) {
+                hidden_store_flag<TW, R>(acc, bias, actY, A.lda, cw, lane, lflag, ++nstore);
+            } else {
+                hidden_store<TW, R>(acc, bias, actY, A.lda, cw, lane);
+            }
         }
         STAMP(1);
         // ---- hidden layers 1..L-1 (W -> W), alternating Y->X->Y...
@@ -703,7 +749,8 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
             zero_acc<TW, R>(acc);
             load_bias<TW>(bias, L.hbias + l * A.Wpad, cw, lane);
             if constexpr (LFLAGS) wait_layer(lflag, 0, nstore);
-            if (PAIR && pwait == 0) lds_wait_ge(lflag, 4 * ++xneed);   // half 1: the partner's columns come first
+            pwl = (L0DUP && l == 1) ? -1 : pwait;                   // layer 0's partner columns are local
+            if (PAIR && pwl == 0) lds_wait_ge(lflag, 4 * ++xneed);      // half 1: the partner's columns come first
             read_a<R>(aAB[0], in, A.lda, 0, lane);
             constexpr int KH = 4 * T;  // 4T % NB == 0: every hidden layer starts on the same slot
             constexpr int S0 = RING ? K0C_T % NB : 0;
