@@ -62,7 +62,9 @@
 #endif
 // Issue priority of the two waves that share a SIMD (8-wave kernels; MI355X_MICROARCH.md "Two waves
 // per SIMD"): 0 none; 1 the younger half (waves 4-7) at s_setprio 1 for the whole launch; 2 the two
-// halves trade priority every K chunk, so neither finishes a layer alone.
+// halves trade priority every K chunk, so neither finishes a layer alone; 3 every wave steps its
+// priority down 3 -> 2 -> 1 -> 0 at fixed chunks of each hidden layer (no branch), so the wave that
+// reaches a step first yields issue slots to the one behind it until that one reaches it too.
 #ifndef MBRL_PRIO
 #define MBRL_PRIO 0
 #endif
@@ -631,8 +633,12 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
     const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(member), 0, (int)(A.stream_floats * sizeof(float)), 0x00020000);
     const unsigned lane_off = (unsigned)((cw * TW * 64 + lane) * 16);
+#ifdef MBRL_DIAG_SAMECHUNK  // timing ablation only: every load re-reads chunk 0 (L1 hits; results garbage)
+#define MBRL_LOAD_CHUNK(DST, G) load_chunk_buf<TW>(DST, wrsrc, lane_off + 0u * (unsigned)(G))
+#else
 #define MBRL_LOAD_CHUNK(DST, G) \
     load_chunk_buf<TW>(DST, wrsrc, lane_off + (unsigned)(((G) < C ? (G) : (G) - C) * cs * 16))
+#endif
 #else
     auto chunk_ptr = [&](int g) { return wb + (size_t)(g < C ? g : g - C) * cs; };
 #define MBRL_LOAD_CHUNK(DST, G) load_chunk<TW>(DST, chunk_ptr(G))
@@ -680,6 +686,12 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
         if (MBRL_PRIO == 2 && NW == 8) {                                             \
             if (young != (((KC) & 1) != 0)) __builtin_amdgcn_s_setprio(1);          \
             else __builtin_amdgcn_s_setprio(0);                                      \
+        }                                                                            \
+        if (MBRL_PRIO == 3 && NW == 8 && (NK) >= 16) {                               \
+            if ((KC) == 0) __builtin_amdgcn_s_setprio(3);                            \
+            if ((KC) == (NK) / 2) __builtin_amdgcn_s_setprio(2);                     \
+            if ((KC) == 3 * (NK) / 4) __builtin_amdgcn_s_setprio(1);                 \
+            if ((KC) == 7 * (NK) / 8) __builtin_amdgcn_s_setprio(0);                 \
         }                                                                            \
         if ((KC) + 1 < (NK)) read_a<R>(aAB[((KC) + 1) & 1], IN, A.lda, (KC) + 1, lane); \
         mma_hidden<TW, R>(acc, aAB[(KC) & 1], ring[SLOT]);                           \
