@@ -216,13 +216,25 @@ def describe(model, cost, device):
     """(mdesc, cdesc) for closures the fused path may run, else (None, None): recognised by
     describe_model / describe_cost AND confirmed once by semantic_check (recognition goes by names
     and types; the check makes sure the arithmetic behind those names is the reference's)."""
+    mdesc, cdesc, _ = describe_problem(model, cost, device)
+    return mdesc, cdesc
+
+
+def describe_problem(model, cost, device, precision=_lib.MBRL_PRECISION_F32):
+    """describe() plus the recognised closures' DeviceProblem at `precision`: (mdesc, cdesc, prob),
+    or (None, None, None). The problem's cache key (every weight and statistic's version) is
+    computed once per call, for the semantic check and the plan alike."""
+    device = torch.device(device)
     mdesc = describe_model(model)
     cdesc = describe_cost(cost, mdesc["s"], mdesc) if mdesc is not None else None
     if mdesc is None or cdesc is None:
-        return None, None
-    if not semantic_check(model, cost, mdesc, cdesc, device):
-        return None, None
-    return mdesc, cdesc
+        return None, None, None
+    prob = device_problem(mdesc, cdesc, device)
+    if not semantic_check(model, cost, mdesc, cdesc, device, prob):
+        return None, None, None
+    if int(precision) != _lib.MBRL_PRECISION_F32:
+        prob = device_problem(mdesc, cdesc, device, precision)
+    return mdesc, cdesc, prob
 
 
 def _fn_sig(fn):
@@ -275,7 +287,7 @@ def _close(x, ref):
     return x.shape == ref.shape and bool(torch.all(torch.abs(x - ref) <= PROBE_RTOL * torch.clamp(ref.abs(), min=1.0)))
 
 
-def semantic_check(model, cost, mdesc, cdesc, device):
+def semantic_check(model, cost, mdesc, cdesc, device, prob=None):
     """One-time check (per closure identity and weights version) that the fused arithmetic equals
     the caller's callables: a one-step fused rollout of PROBE_ROWS random (state, action) rows
     against model(s, a) and cost(s', a) evaluated through the callables themselves (torch autograd
@@ -285,7 +297,8 @@ def semantic_check(model, cost, mdesc, cdesc, device):
     (the reference's semantics: planners.py:199-210 on the callables as given)."""
     import warnings
     device = torch.device(device)
-    prob = device_problem(mdesc, cdesc, device)
+    if prob is None:
+        prob = device_problem(mdesc, cdesc, device)
     sig = (_fn_sig(model), _fn_sig(cost))
     ok = prob.verified.get(sig)
     if ok is not None:

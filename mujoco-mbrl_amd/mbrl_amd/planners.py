@@ -173,9 +173,9 @@ class RandomShootingPlanner(ModelPlanner):
         with torch.cuda.device(dev):
             acts = action_list.to(device=dev, dtype=torch.float32).reshape(H, N, a).contiguous()
             s0 = initial_state.to(device=dev, dtype=torch.float32).contiguous()
-            mdesc, cdesc = fused.describe(model, cost, dev)
+            mdesc, cdesc, prob = fused.describe_problem(model, cost, dev,
+                                                        _lib.precision_code(kwargs.get("precision", "f32")))
             if mdesc is not None and cdesc is not None and mdesc["E"] == 1 and mdesc["a"] == a:
-                prob = fused.device_problem(mdesc, cdesc, dev, _lib.precision_code(kwargs.get("precision", "f32")))
                 states = torch.empty((1, H, N, mdesc["s"]), dtype=torch.float32, device=dev)
                 costs = fused.rollout(prob, s0, N, H, actions=acts, states_out=states)
                 states = states[0]
@@ -288,13 +288,12 @@ class CEMPlanner(ModelPlanner):
         dev = _device(kwargs)
         st = CEMPlanner._settings(sample_action, horizon, kwargs)
         with torch.cuda.device(dev):
-            mdesc, cdesc = fused.describe(model, cost, dev)
+            mdesc, cdesc, prob = fused.describe_problem(model, cost, dev, st["precision"])
             ws = None
             if st["distributed"] and torch.distributed.is_available() and torch.distributed.is_initialized() \
                     and torch.distributed.get_world_size() > 1:
                 ws = torch.distributed.get_world_size()
             if mdesc is not None and cdesc is not None:
-                prob = fused.device_problem(mdesc, cdesc, dev, st["precision"])
                 if ws is None:
                     res = _cem_fused_single(prob, initial_state, st)
                     if res.pop("_host", False):
@@ -332,14 +331,13 @@ def cem_plan_batch(initial_states, model, cost, sample_action, horizon, **kwargs
     st = CEMPlanner._settings(sample_action, horizon, kwargs)
     B = int(initial_states.shape[0])
     with torch.cuda.device(dev):
-        mdesc, cdesc = fused.describe(model, cost, dev)
+        mdesc, cdesc, prob = fused.describe_problem(model, cost, dev, st["precision"])
         if mdesc is None or cdesc is None:
             outs = [CEMPlanner.plan(initial_states[b], model, cost, sample_action, horizon,
                                     **dict(kwargs, seed=st["seed"], return_device=True)) for b in range(B)]
             states, actions = torch.stack([o[0] for o in outs]), torch.stack([o[1] for o in outs])
         else:
             lib = _lib.load()
-            prob = fused.device_problem(mdesc, cdesc, dev, st["precision"])
             N, K, H, I = st["N"], st["K"], st["H"], st["I"]
             a, s = mdesc["a"], mdesc["s"]
             params = _lib.CemParams(N, H, K, I, st["alpha"], st["lo"], st["hi"], 0.0, st["init_std"], 0,
