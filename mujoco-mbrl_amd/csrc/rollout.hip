@@ -423,7 +423,10 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
     constexpr int NT = 64 * NW;
     static_assert(TW >= 1 && TW * NW == 4 * T, "tiles per wave");
     constexpr bool RING = K0C_T > 0;
-    constexpr int NB = RING ? 4 : 2;
+#ifndef MBRL_RING_NB
+#define MBRL_RING_NB 4   // A/B of the prefetch depth only (2 also satisfies the ring layout)
+#endif
+    constexpr int NB = RING ? MBRL_RING_NB : 2;
     constexpr int SS = RING ? NOT_T : 1;    // register state slots per lane (ceil(s / 16) <= NOT); generic: LDS
     // per-lane epilogue parameter copies in registers (else the same values from LDS): not at 32
     // candidates x 8 waves, whose MFMA loop already takes the whole 256-VGPR budget
