@@ -57,3 +57,29 @@ def test_forced_pair_fails_loudly_where_it_cannot_run():
     with pytest.raises(RuntimeError, match="rollout_pair"):
         _plan(p, 256, 4, {"rollout_pair": 1})
     assert _lib is not None
+
+
+def _fuzz_shape(case):
+    rng = np.random.default_rng(9100 + case)
+    over = dict(s=int(rng.integers(1, 41)), a=int(rng.integers(1, 13)), W=int(rng.choice([300, 400, 512])),
+                L=int(rng.integers(2, 5)), E=int(rng.choice([1, 1, 2, 3])))
+    N = int(rng.choice([3, 16, 47, 200, 513]))
+    H = int(rng.integers(1, 9))
+    return over, N, H
+
+
+@pytest.mark.parametrize("case", range(8))
+def test_pair_plan_fuzz_equals_16_candidate_tiles(case):
+    """Random Wpad-512 shapes (state / action dims, widths below 512, 2-4 hidden layers, ensembles,
+    ragged N): column-split pairs and 16-candidate tiles give the same plan bit for bit, or the pair
+    kernel declines the shape loudly (no instance for its chunk counts)."""
+    over, N, H = _fuzz_shape(case)
+    p = ocem.synth_problem(3, N=N, H=H, **over)
+    try:
+        pair = _plan(p, N, H, {"rollout_pair": 1})
+    except RuntimeError as exc:
+        assert "rollout_pair" in str(exc)
+        return
+    m16 = _plan(p, N, H, {"rollout_tile": 16, "rollout_pair": 2})
+    for k in ("returns", "elites", "mu", "sigma", "actions", "states"):
+        assert torch.equal(pair[k], m16[k]), (case, over, N, H, k)
