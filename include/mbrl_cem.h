@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MBRL_ABI_VERSION 8
+#define MBRL_ABI_VERSION 9
 
 typedef struct ihipStream_t* mbrl_stream_t; /* == hipStream_t */
 typedef struct ihipEvent_t* mbrl_event_t;   /* == hipEvent_t  */
@@ -159,7 +159,11 @@ enum {
     MBRL_OPT_TRAIN_NO_FOLD = 9,     /* 1: the layer-0 weight gradient in its own launch (bit-identical) */
     MBRL_OPT_ROLLOUT_PAIR = 10,     /* column-split pairs in plans: 0 auto, 1 forced (MBRL_EUNSUPPORTED where
                                        they cannot run), 2 never; standalone rollouts never use them  */
-    MBRL_OPT_COUNT = 11
+    MBRL_OPT_SHARD_EMULATE = 11,    /* 1 (tests): mbrl_cem_plan_sharded with comm == NULL computes every
+                                       other rank's shard itself in place of the all-gather (G > 1 on one GPU) */
+    MBRL_OPT_DEBUG_PAIR_ABORT = 12, /* 1: the column-split pair kernel gives up at once (its redo runs);
+                                       2: no redo launch behind it (tests of the pair kernel's own results) */
+    MBRL_OPT_COUNT = 13
 };
 int mbrl_set_option(int32_t option, int32_t value);
 int mbrl_get_option(int32_t option);
@@ -167,7 +171,8 @@ int mbrl_get_option(int32_t option);
 /* ---- multi-GPU (the reference has no distributed code): an RCCL communicator the
  * library owns. mbrl_comm_unique_id on one rank, the MBRL_COMM_ID_BYTES broadcast to the others by the
  * caller (torch.distributed), then mbrl_comm_init on every rank at once (collective), with the rank's
- * GPU current. */
+ * GPU current. RCCL (librccl.so.1) is opened on the first of these calls, not at load time: without it
+ * they return MBRL_EUNSUPPORTED and everything else works. */
 #define MBRL_COMM_ID_BYTES 128
 typedef void* mbrl_comm_t;
 int mbrl_comm_unique_id(void* id_out);
@@ -259,7 +264,12 @@ int mbrl_cem_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_no
  * the [E][N / nranks] costs over `comm` as a step on `stream` (ncclAllGather), then every rank runs the
  * same selection over all N, the same refit and draws its own shard of the next proposals. Outputs are
  * bit-identical on every rank and to mbrl_cem_plan's for any nranks (records as mbrl_cem_plan's, over
- * all N). Replaces planners.cem_sharded_protocol's per-iteration Python loop. N % nranks == 0. */
+ * all N). Replaces planners.cem_sharded_protocol's per-iteration Python loop. N % nranks == 0.
+ * Every argument check runs before the first collective (the ranks pass the same shape, params and
+ * nranks, so they agree on it). A nonzero return with nranks > 1 has ABORTED `comm` (ncclCommAbort), so
+ * the other ranks' collectives fail instead of waiting for this one: drop it, do not destroy it.
+ * comm == NULL is allowed only under MBRL_OPT_SHARD_EMULATE (tests): each call then rolls out every
+ * rank's shard itself and fills the all-gather's rank-major buffer, so one GPU runs any nranks. */
 size_t mbrl_cem_plan_sharded_workspace_bytes(const mbrl_mlp_shape* shape, const mbrl_cem_params* params,
                                              int32_t nranks);
 int mbrl_cem_plan_sharded(const mbrl_mlp_shape* shape, const void* packed, const mbrl_norm* norm,

@@ -6,6 +6,7 @@
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
+#include <dlfcn.h>
 
 #include <atomic>
 #include <map>
@@ -1041,6 +1042,28 @@ static int pair_forced_check(const Geometry& g, int N) {
     return MBRL_OK;
 }
 
+// The argument checks of rollout_impl that depend on the problem only (not on N or the buffers): the
+// sharded plan runs them before its first collective.
+static int rollout_validate(const Geometry& g, const mbrl_norm* norm, const mbrl_cost* cost) {
+    if (norm) {
+        if (norm->unnormalize_reward && (!norm->rew_mean || !norm->rew_std))
+            return fail(MBRL_EINVAL, "reward unnormalisation requested without rew_mean/rew_std");
+        if ((norm->normalize_state || norm->unnormalize_state) && (!norm->obs_mean || !norm->obs_std))
+            return fail(MBRL_EINVAL, "state normalisation requested without obs_mean/obs_std");
+        if (norm->normalize_action && (!norm->act_mean || !norm->act_std))
+            return fail(MBRL_EINVAL, "action normalisation requested without act_mean/act_std");
+    }
+    if (cost && cost->kind == MBRL_COST_MODEL_REWARD) {
+        if (!g.reward) return fail(MBRL_EINVAL, "MODEL_REWARD cost needs a reward_head model");
+    } else if (cost) {
+        if (cost->kind != MBRL_COST_GOAL_STATE) return fail(MBRL_EUNSUPPORTED, "cost kind %d", cost->kind);
+        if (cost->has_state_cost && (!cost->weights || !cost->goal))
+            return fail(MBRL_EINVAL, "state cost without weights/goal");
+    }
+    if (16 * g.a > 768) return fail(MBRL_EUNSUPPORTED, "action_dim %d too large (max 48)", g.a);
+    return MBRL_OK;
+}
+
 // pair_area: a pair_area_bytes(g, N) block of the caller's workspace, or NULL (no column-split pairs).
 static int rollout_impl(const Geometry& g, const void* packed, const mbrl_norm* norm, const mbrl_cost* cost,
                         const float* s0, int s0_per_cand, const float* actions, const mbrl_sampler* sampler,
@@ -1050,6 +1073,7 @@ static int rollout_impl(const Geometry& g, const void* packed, const mbrl_norm* 
     if (N < 1 || H < 1) return fail(MBRL_EINVAL, "N=%d H=%d must be >= 1", N, H);
     if (!actions && !sampler) return fail(MBRL_EINVAL, "need either actions or a sampler");
     if (n_offset < 0) return fail(MBRL_EINVAL, "n_offset=%d < 0", n_offset);
+    if (int rc = rollout_validate(g, norm, cost)) return rc;
     RolloutArgs A{};
     A.packed = static_cast<const float*>(packed);
     A.member_stride = g.member_stride;
@@ -1062,23 +1086,14 @@ static int rollout_impl(const Geometry& g, const void* packed, const mbrl_norm* 
         A.act_mean = norm->act_mean; A.act_std = norm->act_std;
         A.norm_s = norm->normalize_state; A.unnorm_s = norm->unnormalize_state; A.norm_a = norm->normalize_action;
         A.unnorm_r = norm->unnormalize_reward; A.rew_mean = norm->rew_mean; A.rew_std = norm->rew_std;
-        if (A.unnorm_r && (!A.rew_mean || !A.rew_std))
-            return fail(MBRL_EINVAL, "reward unnormalisation requested without rew_mean/rew_std");
-        if ((A.norm_s || A.unnorm_s) && (!A.obs_mean || !A.obs_std))
-            return fail(MBRL_EINVAL, "state normalisation requested without obs_mean/obs_std");
-        if (A.norm_a && (!A.act_mean || !A.act_std))
-            return fail(MBRL_EINVAL, "action normalisation requested without act_mean/act_std");
     }
     if (cost && cost->kind == MBRL_COST_MODEL_REWARD) {
-        if (!g.reward) return fail(MBRL_EINVAL, "MODEL_REWARD cost needs a reward_head model");
         A.reward = 1;
     } else if (cost) {
-        if (cost->kind != MBRL_COST_GOAL_STATE) return fail(MBRL_EUNSUPPORTED, "cost kind %d", cost->kind);
         A.has_sc = cost->has_state_cost; A.has_ac = cost->has_action_cost;
         A.cw = cost->weights; A.goal = cost->goal;
         A.alpha_s = cost->alpha_state; A.alpha_s2 = cost->alpha_state * cost->alpha_state;
         A.alpha_a = cost->alpha_action; A.alpha_a2 = cost->alpha_action * cost->alpha_action;
-        if (A.has_sc && (!A.cw || !A.goal)) return fail(MBRL_EINVAL, "state cost without weights/goal");
     }
     A.s0 = s0; A.s0_per_cand = s0_per_cand;
     if (!actions) {
@@ -1097,7 +1112,6 @@ static int rollout_impl(const Geometry& g, const void* packed, const mbrl_norm* 
     const int G = (g.a + 3) / 4;
     (void)G;
     if (16 * R * g.a > 768) R = 1;
-    if (16 * g.a > 768) return fail(MBRL_EUNSUPPORTED, "action_dim %d too large (max 48)", g.a);
     // waves per workgroup as launch_rollout_t picks them: 8 for R = 1 (T >= 2), else 4
     A.nw = (R == 1 && g.T >= 2) ? 8 : 4;
     if ((g.precision == MBRL_PRECISION_F16X3 || g.precision == MBRL_PRECISION_F16X6) && g.split_ok && !A.reward) {
@@ -1148,8 +1162,20 @@ static int rollout_impl(const Geometry& g, const void* packed, const mbrl_norm* 
             P.pair_data = reinterpret_cast<float*>(static_cast<char*>(pair_area) +
                                                    pair_layout(g.Wpad, g.pw, ntiles, g.E).flags_bytes);
             if (rollout_pair_supported(P, g.T)) {
+                const int dpa = g_opt[MBRL_OPT_DEBUG_PAIR_ABORT].load(std::memory_order_relaxed);
+                P.debug_abort = dpa == 1;
                 const hipError_t err = launch_rollout_pair(P, g.T, stream);
-                if (err != hipErrorCooperativeLaunchTooLarge || po == 1) return hip_check(err, "rollout pair launch");
+                if (err == hipSuccess && dpa == 2) return MBRL_OK;   // tests: the pair launch's own results
+                if (err == hipSuccess) {
+                    // A pair's halves wait on each other, and a plain launch does not promise that both
+                    // are resident (another stream may hold CUs): a wait that timed out set bit 0 of the
+                    // status word after the flags and left its tile's costs invalid. The launch chosen
+                    // below then recomputes every candidate if that bit is set, else its workgroups exit
+                    // at once (bit-identical sums on every tile height).
+                    A.gate = P.pair_flags + (size_t)2 * ntiles * g.E * 32;
+                } else if (err != hipErrorCooperativeLaunchTooLarge || po == 1) {
+                    return hip_check(err, "rollout pair launch");
+                }
             } else if (po == 1) {
                 return fail(MBRL_EUNSUPPORTED, "rollout_pair forced: shape not supported by the pair kernel");
             }
@@ -1346,6 +1372,7 @@ int mbrl_set_option(int32_t option, int32_t value) {
         case MBRL_OPT_ADAM_ARITH: ok = value >= 0 && value <= 16; break;
         case MBRL_OPT_TRAIN_TILE: ok = value == 0 || value == 32 || value == 64; break;
         case MBRL_OPT_ROLLOUT_PAIR: ok = value >= 0 && value <= 2; break;
+        case MBRL_OPT_DEBUG_PAIR_ABORT: ok = value >= 0 && value <= 2; break;
         default: ok = value == 0 || value == 1; break;
     }
     if (!ok) return fail(MBRL_EINVAL, "option %d: value %d not allowed", option, value);
@@ -1825,16 +1852,62 @@ int mbrl_cem_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_no
 
 // ---- multi-GPU: an RCCL communicator owned by the library, and the sharded plan as
 // one call with the all-gather as a stream-ordered step.
-static int nccl_check(ncclResult_t r, const char* what) {
-    if (r == ncclSuccess) return MBRL_OK;
-    return fail(MBRL_EHIP, "%s: %s", what, ncclGetErrorString(r));
+//
+// RCCL is resolved at run time, on the first mbrl_comm_* / sharded call (dlopen of librccl.so.1, the
+// soname torch.distributed loads, so both share one RCCL in the process): the single-GPU library has
+// no link-time dependency on RCCL and loads on a host without it.
+struct Rccl {
+    const char* (*get_error_string)(ncclResult_t);
+    ncclResult_t (*get_unique_id)(ncclUniqueId*);
+    ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int);
+    ncclResult_t (*comm_destroy)(ncclComm_t);
+    ncclResult_t (*comm_abort)(ncclComm_t);
+    ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t);
+    std::string error;   // why the library could not be loaded ("" when it was)
+};
+
+static const Rccl& rccl() {
+    static Rccl r{};
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) {
+            const char* e = dlerror();
+            r.error = e ? e : "dlopen(librccl.so.1) failed";
+            return;
+        }
+        auto sym = [&](const char* name) {
+            void* p = dlsym(h, name);
+            if (!p && r.error.empty()) r.error = std::string("librccl: missing symbol ") + name;
+            return p;
+        };
+        r.get_error_string = reinterpret_cast<decltype(r.get_error_string)>(sym("ncclGetErrorString"));
+        r.get_unique_id = reinterpret_cast<decltype(r.get_unique_id)>(sym("ncclGetUniqueId"));
+        r.comm_init_rank = reinterpret_cast<decltype(r.comm_init_rank)>(sym("ncclCommInitRank"));
+        r.comm_destroy = reinterpret_cast<decltype(r.comm_destroy)>(sym("ncclCommDestroy"));
+        r.comm_abort = reinterpret_cast<decltype(r.comm_abort)>(sym("ncclCommAbort"));
+        r.all_gather = reinterpret_cast<decltype(r.all_gather)>(sym("ncclAllGather"));
+    });
+    return r;
+}
+
+static int rccl_ready() {
+    const Rccl& r = rccl();
+    return r.error.empty() ? MBRL_OK : fail(MBRL_EUNSUPPORTED, "RCCL unavailable: %s", r.error.c_str());
+}
+
+static int nccl_check(ncclResult_t res, const char* what) {
+    if (res == ncclSuccess) return MBRL_OK;
+    return fail(MBRL_EHIP, "%s: %s", what, rccl().get_error_string(res));
 }
 
 int mbrl_comm_unique_id(void* id_out) {
     static_assert(sizeof(ncclUniqueId) == MBRL_COMM_ID_BYTES, "ncclUniqueId size");
     if (!id_out) return fail(MBRL_EINVAL, "comm_unique_id: NULL");
+    if (int rc = rccl_ready()) return rc;
     ncclUniqueId id;
-    if (int rc = nccl_check(ncclGetUniqueId(&id), "ncclGetUniqueId")) return rc;
+    if (int rc = nccl_check(rccl().get_unique_id(&id), "ncclGetUniqueId")) return rc;
     memcpy(id_out, &id, sizeof(id));
     return MBRL_OK;
 }
@@ -1842,20 +1915,24 @@ int mbrl_comm_unique_id(void* id_out) {
 int mbrl_comm_init(const void* id, int32_t nranks, int32_t rank, mbrl_comm_t* comm_out) {
     if (!id || !comm_out || nranks < 1 || rank < 0 || rank >= nranks)
         return fail(MBRL_EINVAL, "comm_init: bad arguments (nranks %d, rank %d)", nranks, rank);
+    if (int rc = rccl_ready()) return rc;
     ncclUniqueId u;
     memcpy(&u, id, sizeof(u));
     ncclComm_t c = nullptr;
-    if (int rc = nccl_check(ncclCommInitRank(&c, nranks, u, rank), "ncclCommInitRank")) return rc;
+    if (int rc = nccl_check(rccl().comm_init_rank(&c, nranks, u, rank), "ncclCommInitRank")) return rc;
     *comm_out = reinterpret_cast<mbrl_comm_t>(c);
     return MBRL_OK;
 }
 
 int mbrl_comm_destroy(mbrl_comm_t comm) {
-    return comm ? nccl_check(ncclCommDestroy(reinterpret_cast<ncclComm_t>(comm)), "ncclCommDestroy") : MBRL_OK;
+    if (!comm) return MBRL_OK;
+    if (int rc = rccl_ready()) return rc;
+    return nccl_check(rccl().comm_destroy(reinterpret_cast<ncclComm_t>(comm)), "ncclCommDestroy");
 }
 
 struct ShardWs {
     float *local, *gathered, *costs, *actions, *mu[2], *sigma[2], *aelite, *states, *s0;
+    float* emu_actions;   // MBRL_OPT_SHARD_EMULATE: the other ranks' proposals, one shard at a time
     void* pair;
     unsigned long long* xchg;
     unsigned* status;
@@ -1864,6 +1941,8 @@ struct ShardWs {
     uint32_t* keys;
     size_t bytes;
 };
+
+static bool shard_emulated() { return g_opt[MBRL_OPT_SHARD_EMULATE].load(std::memory_order_relaxed) == 1; }
 
 static ShardWs shard_ws(const Geometry& g, const mbrl_cem_params* p, int G, void* base) {
     ShardWs w{};
@@ -1887,6 +1966,7 @@ static ShardWs shard_ws(const Geometry& g, const mbrl_cem_params* p, int G, void
     w.keys = (uint32_t*)take((size_t)p->N * 4);
     w.s0 = (float*)take((size_t)g.s * 4);
     w.pair = take(pair_area_bytes(g, Nl));
+    w.emu_actions = (float*)take(shard_emulated() && G > 1 ? (size_t)p->H * Nl * g.a * 4 : 0);
     w.bytes = o;
     return w;
 }
@@ -1898,25 +1978,33 @@ size_t mbrl_cem_plan_sharded_workspace_bytes(const mbrl_mlp_shape* shape, const 
     return shard_ws(g, params, nranks, nullptr).bytes;
 }
 
-int mbrl_cem_plan_sharded(const mbrl_mlp_shape* shape, const void* packed, const mbrl_norm* norm,
-                          const mbrl_cost* cost, const float* s0_in, const mbrl_cem_params* p, mbrl_comm_t comm,
-                          int32_t nranks, int32_t rank, float* mu, float* sigma, float* actions_out,
-                          float* states_out, float* cost_hist, float* returns_hist, int64_t* elite_hist,
-                          mbrl_event_t* rollout_events, void* workspace, size_t ws_bytes, mbrl_stream_t stream_) {
-    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
+// The body of mbrl_cem_plan_sharded. Every check that can reject the call runs before the first
+// collective, and each is a function of arguments every rank passes alike (shape, params, nranks,
+// the workspace size the same query gives), so the ranks agree on it; what can still fail later is a
+// HIP launch, after which the caller aborts the communicator.
+static int plan_sharded_body(const mbrl_mlp_shape* shape, const void* packed, const mbrl_norm* norm,
+                             const mbrl_cost* cost, const float* s0_in, const mbrl_cem_params* p, mbrl_comm_t comm,
+                             int32_t nranks, int32_t rank, float* mu, float* sigma, float* actions_out,
+                             float* states_out, float* cost_hist, float* returns_hist, int64_t* elite_hist,
+                             mbrl_event_t* rollout_events, void* workspace, size_t ws_bytes, hipStream_t stream) {
     Geometry g;
     int rc = shape_geometry(shape, &g);
     if (rc) return rc;
-    if (!p || !comm) return fail(MBRL_EINVAL, "plan_sharded: NULL params or comm");
+    // comm == NULL with MBRL_OPT_SHARD_EMULATE (tests): this call computes every other rank's shard
+    // itself and writes the rank-major buffer the all-gather would have delivered
+    const bool emulate = comm == nullptr && shard_emulated();
+    if (!p || (!comm && !emulate)) return fail(MBRL_EINVAL, "plan_sharded: NULL params or comm");
     if (p->N < 1 || p->H < 1 || p->K < 1 || p->K > p->N || p->iterations < 1)
         return fail(MBRL_EINVAL, "bad CEM params N=%d H=%d K=%d I=%d", p->N, p->H, p->K, p->iterations);
     if (nranks < 1 || rank < 0 || rank >= nranks || p->N % nranks)
         return fail(MBRL_EINVAL, "plan_sharded: N=%d over %d ranks (rank %d)", p->N, nranks, rank);
-    if (!actions_out || !states_out || !workspace || !s0_in)
-        return fail(MBRL_EINVAL, "plan_sharded: s0/actions_out/states_out/workspace NULL");
+    if (!actions_out || !states_out || !workspace || !s0_in || !packed)
+        return fail(MBRL_EINVAL, "plan_sharded: packed/s0/actions_out/states_out/workspace NULL");
     const ShardWs w = shard_ws(g, p, nranks, workspace);
     if (ws_bytes < w.bytes) return fail(MBRL_EWORKSPACE, "workspace %zu < %zu", ws_bytes, w.bytes);
     if ((rc = pair_forced_check(g, p->N / nranks))) return rc;
+    if ((rc = rollout_validate(g, norm, cost))) return rc;
+    if (!emulate && (rc = rccl_ready())) return rc;
     const int N = p->N, Nl = N / nranks, H = p->H, a = g.a, E = g.E, Ha = H * a;
     const int off = rank * Nl;   // this rank's global candidates [off, off + Nl)
     const bool fuse = update_kpt(N, p->K, a) != 0 && g_opt[MBRL_OPT_UNFUSED_UPDATE].load(std::memory_order_relaxed) == 0;
@@ -1942,9 +2030,26 @@ int mbrl_cem_plan_sharded(const mbrl_mlp_shape* shape, const void* packed, const
             (rc = hip_check(hipEventRecord(reinterpret_cast<hipEvent_t>(rollout_events[2 * it + 1]), stream), "event")))
             return rc;
         // the one collective of an iteration: every rank's [E][Nl] costs, rank-major
-        if ((rc = nccl_check(ncclAllGather(w.local, w.gathered, (size_t)E * Nl, ncclFloat,
-                                           reinterpret_cast<ncclComm_t>(comm), stream), "ncclAllGather")))
-            return rc;
+        if (!emulate) {
+            if ((rc = nccl_check(rccl().all_gather(w.local, w.gathered, (size_t)E * Nl, ncclFloat,
+                                                   reinterpret_cast<ncclComm_t>(comm), stream), "ncclAllGather")))
+                return rc;
+        } else {
+            // rank r's slot: its proposals of this iteration (drawn at its global offset from this
+            // iteration's mu / sigma, as its own previous update or initial draw made them) rolled out
+            for (int r = 0; r < nranks; ++r) {
+                float* slot = w.gathered + (size_t)r * E * Nl;
+                if (r == rank) {
+                    rc = hip_check(hipMemcpyAsync(slot, w.local, (size_t)E * Nl * 4, hipMemcpyDeviceToDevice, stream),
+                                   "emulated gather");
+                } else {
+                    if ((rc = sample_impl(&sp, H, a, Nl, r * Nl, w.emu_actions, stream))) return rc;
+                    rc = rollout_impl(g, packed, norm, cost, w.s0, 0, w.emu_actions, nullptr, Nl, H, 0, slot, nullptr,
+                                      nullptr, stream, pair_area_bytes(g, Nl) ? w.pair : nullptr);
+                }
+                if (rc) return rc;
+            }
+        }
         float* costs = w.gathered;
         if (E > 1) {   // (one rank: the identity)
             hipLaunchKernelGGL(shard_costs_kernel, dim3(256), dim3(256), 0, stream, w.gathered, nranks, E, Nl, w.costs);
@@ -1991,6 +2096,24 @@ int mbrl_cem_plan_sharded(const mbrl_mlp_shape* shape, const void* packed, const
                            states_out);
     }
     return hip_check(hipGetLastError(), "sharded plan launch");
+}
+
+int mbrl_cem_plan_sharded(const mbrl_mlp_shape* shape, const void* packed, const mbrl_norm* norm,
+                          const mbrl_cost* cost, const float* s0_in, const mbrl_cem_params* p, mbrl_comm_t comm,
+                          int32_t nranks, int32_t rank, float* mu, float* sigma, float* actions_out,
+                          float* states_out, float* cost_hist, float* returns_hist, int64_t* elite_hist,
+                          mbrl_event_t* rollout_events, void* workspace, size_t ws_bytes, mbrl_stream_t stream) {
+    const int rc = plan_sharded_body(shape, packed, norm, cost, s0_in, p, comm, nranks, rank, mu, sigma, actions_out,
+                                     states_out, cost_hist, returns_hist, elite_hist, rollout_events, workspace,
+                                     ws_bytes, reinterpret_cast<hipStream_t>(stream));
+    // A rank that stops early would leave the others waiting in an all-gather it never joins: abort the
+    // communicator, so their collectives fail instead (the caller must drop it; include/mbrl_cem.h).
+    if (rc != MBRL_OK && comm && nranks > 1 && rccl().error.empty()) {
+        const std::string msg = g_err;
+        (void)rccl().comm_abort(reinterpret_cast<ncclComm_t>(comm));
+        fail(rc, "%s (communicator aborted)", msg.c_str());
+    }
+    return rc;
 }
 
 #ifdef MBRL_STAMPS

@@ -162,7 +162,10 @@ struct RolloutArgs {
     // per-workgroup flags (pair_flags: one 128-byte line per workgroup, zeroed before every launch)
     float* pair_data;
     unsigned* pair_flags;
-    unsigned* pair_status;   // bit 0: a hand-off wait timed out (results of that launch are invalid)
+    int debug_abort;         // PAIR kernel: give up at once, as after a timed-out hand-off (MBRL_OPT_DEBUG_PAIR_ABORT)
+    // non-PAIR fp32 kernels: NULL, or the pair launch's status word (the line after its flags); the
+    // launch then recomputes its candidates only if bit 0 is set (a hand-off of the pair launch timed out)
+    const unsigned* gate;
 };
 
 // Column-split pair exchange area for ntiles * E tiles (rollout_kernel PAIR): the flags block first

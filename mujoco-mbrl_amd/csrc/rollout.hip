@@ -456,7 +456,15 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
         half = (u >> 3) & 1;
         e = blockIdx.y;
         if (tile >= ntiles) return;   // both halves of a padding pair leave together
+        if (A.debug_abort) {          // test hook: behave as a timed-out hand-off (the redo launch runs)
+            if (tid == 0)
+                __hip_atomic_fetch_or((gu32*)(A.pair_flags) + (size_t)2 * ntiles * A.E * 32, 1u, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
     } else {
+        // the redo behind a column-split pair launch: runs only if one of its hand-offs timed out
+        if (A.gate != nullptr && *A.gate == 0u) return;
         xcd_unit(A.xcd_map, ntiles, tile, e);
     }
     const int cw = PAIR ? 4 * half + wave : wave;   // the 8-wave layout's wave whose columns this one computes
@@ -1088,6 +1096,7 @@ __global__ void __launch_bounds__(64 * m8_waves(T, NOT_T), 1) rollout_m8_kernel(
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int ntiles = (A.N + M - 1) / M;
     int tile, e;
+    if (A.gate != nullptr && *A.gate == 0u) return;   // redo behind a pair launch (rollout_kernel)
     xcd_unit(A.xcd_map, ntiles, tile, e);
     const float* member = A.packed + (size_t)e * A.member_stride;
     float* const actX = L.act;

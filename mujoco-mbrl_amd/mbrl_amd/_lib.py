@@ -20,10 +20,13 @@ LIB_PATH = os.environ.get("MBRL_AMD_LIB") or os.path.join(os.path.dirname(os.pat
 
 MBRL_OK = 0
 MBRL_COMM_ID_BYTES = 128
+MBRL_EINVAL = -1
 MBRL_EUNSUPPORTED = -2
+MBRL_EHIP = -3
+MBRL_EWORKSPACE = -4
 MBRL_COST_GOAL_STATE = 0
 MBRL_COST_MODEL_REWARD = 1
-ABI_VERSION = 8
+ABI_VERSION = 9
 MBRL_NAN_LAST = 0
 MBRL_NAN_FIRST = 1
 MBRL_PRECISION_F32 = 0
@@ -33,7 +36,7 @@ PRECISIONS = {"f32": MBRL_PRECISION_F32, "f16x3": MBRL_PRECISION_F16X3, "f16x6":
 # mbrl_set_option switches (include/mbrl_cem.h MBRL_OPT_*): A/B runs and forced fallbacks in tests
 OPTIONS = {"rollout_tile": 0, "split_tile": 1, "debug_traj_abort": 2, "gd_single": 3, "debug_gd_abort": 4,
            "unfused_update": 5, "adam_arith": 6, "xcd_map": 7, "train_tile": 8, "train_no_fold": 9,
-           "rollout_pair": 10}
+           "rollout_pair": 10, "shard_emulate": 11, "debug_pair_abort": 12}
 
 
 def precision_code(name):

@@ -619,9 +619,14 @@ def _rccl_comm(dev, world, rank):
     return comm
 
 
-def _cem_sharded_native(prob, s0, st, world, rank):
+_OWN_COMM = object()
+
+
+def _cem_sharded_native(prob, s0, st, world, rank, comm=_OWN_COMM):
     """mbrl_cem_plan_sharded: this rank's shard of the plan, every iteration's all-gather included, in
-    one C-ABI call on the current stream (the result is the single-GPU plan's, on every rank)."""
+    one C-ABI call on the current stream (the result is the single-GPU plan's, on every rank).
+    comm: the library's RCCL communicator for the default group (default), or None under
+    _lib.option("shard_emulate", 1), where the call computes every rank's shard itself (tests)."""
     lib = _lib.load()
     dev = prob.device
     md = prob.mdesc
@@ -633,7 +638,8 @@ def _cem_sharded_native(prob, s0, st, world, rank):
     if need == 0:
         raise ValueError(f"num_candidates {N} must divide evenly over {world} ranks")
     ws = _workspace(("cem_sharded", str(dev)), need, dev)
-    comm = _rccl_comm(dev, world, rank)
+    if comm is _OWN_COMM:
+        comm = _rccl_comm(dev, world, rank)
     buf = torch.empty(H * (s + 3 * a), dtype=torch.float32, device=dev)
     both = buf[:H * (s + a)]
     states, actions = both[:H * s].view(H, s), both[H * s:].view(H, a)
@@ -642,12 +648,17 @@ def _cem_sharded_native(prob, s0, st, world, rank):
     cost_hist = torch.empty((I, E, N), dtype=torch.float32, device=dev) if rec else None
     ret_hist = torch.empty((I, N), dtype=torch.float32, device=dev) if rec else None
     elite_hist = torch.empty((I, K), dtype=torch.int64, device=dev) if rec else None
-    _lib.check(lib.mbrl_cem_plan_sharded(fused.ctypes_ref(prob.shape), _lib.ptr(prob.packed),
-                                         fused.ctypes_ref(prob.norm), fused.ctypes_ref(prob.cost), _lib.ptr(s0),
-                                         fused.ctypes_ref(params), comm, world, rank, _lib.ptr(mu), _lib.ptr(sigma),
-                                         _lib.ptr(actions), _lib.ptr(states), _lib.ptr(cost_hist), _lib.ptr(ret_hist),
-                                         _lib.ptr(elite_hist), _events(st, I), _lib.ptr(ws), ws.numel(),
-                                         _lib.stream_handle(dev)), "mbrl_cem_plan_sharded")
+    rc = lib.mbrl_cem_plan_sharded(fused.ctypes_ref(prob.shape), _lib.ptr(prob.packed), fused.ctypes_ref(prob.norm),
+                                   fused.ctypes_ref(prob.cost), _lib.ptr(s0), fused.ctypes_ref(params), comm, world, rank,
+                                   _lib.ptr(mu), _lib.ptr(sigma), _lib.ptr(actions), _lib.ptr(states),
+                                   _lib.ptr(cost_hist), _lib.ptr(ret_hist), _lib.ptr(elite_hist), _events(st, I),
+                                   _lib.ptr(ws), ws.numel(), _lib.stream_handle(dev))
+    if rc != _lib.MBRL_OK and comm and world > 1:
+        # the library aborted the communicator (so no other rank waits on this one): forget it, and
+        # the next plan builds a new one
+        for k in [k for k, v in _COMMS.items() if v is comm]:
+            del _COMMS[k]
+    _lib.check(rc, "mbrl_cem_plan_sharded")
     out = dict(states=states, actions=actions, mu=mu, sigma=sigma, _both=both)
     if rec:
         out.update(costs=cost_hist, returns=ret_hist, elites=elite_hist)

@@ -2,7 +2,9 @@
 computing half of every hidden layer's columns, halves crossing through L2) give the same plans as
 8- and 16-candidate tiles, bit for bit: every accumulator keeps the canonical K order and the output
 sum is the canonical ((p0 + p1) + (p2 + p3)) + ((p4 + p5) + (p6 + p7)). MBRL_OPT_ROLLOUT_PAIR = 1
-forces the pair kernel (a plan fails instead of falling back), so these tests prove it ran."""
+forces the pair kernel (a plan fails instead of falling back), and MBRL_OPT_DEBUG_PAIR_ABORT = 2 drops
+the gated redo launch behind it (which recomputes a launch whose hand-off timed out), so these tests
+compare the pair kernel's own results."""
 from contextlib import ExitStack
 
 import numpy as np
@@ -17,6 +19,7 @@ pytestmark = pytest.mark.gpu
 # (config, N, H): walker / cheetah at the 8- and 2-GPU shard sizes, ragged and tiny N, the ensemble
 # (humanoid E = 5: K0C = NOT = 6) and a 2x512 model (L = 2: one layer hand-off per step)
 CASES = [(4, 2048, 30), (3, 2048, 30), (3, 1024, 12), (4, 300, 7), (3, 17, 5), (3, 1, 3), (5, 200, 4)]
+PAIR_ONLY = {"rollout_pair": 1, "debug_pair_abort": 2}
 
 
 def _plan(p, N, H, opts):
@@ -32,7 +35,7 @@ def _plan(p, N, H, opts):
 @pytest.mark.parametrize("cid,N,H", CASES)
 def test_pair_plan_equals_every_tile_height(cid, N, H):
     p = ocem.synth_problem(cid, N=N, H=H)
-    pair = _plan(p, N, H, {"rollout_pair": 1})
+    pair = _plan(p, N, H, PAIR_ONLY)
     m16 = _plan(p, N, H, {"rollout_tile": 16, "rollout_pair": 2})
     m8 = _plan(p, N, H, {"rollout_tile": 8, "rollout_pair": 2})
     for k in ("returns", "elites", "mu", "sigma", "actions", "states"):
@@ -44,7 +47,7 @@ def test_pair_plan_equals_every_tile_height(cid, N, H):
 def test_pair_plan_two_hidden_layers():
     """L = 2 (one layer hand-off per step) at the shard size."""
     p = ocem.synth_problem(3, N=512, H=6, L=2)
-    pair = _plan(p, 512, 6, {"rollout_pair": 1})
+    pair = _plan(p, 512, 6, PAIR_ONLY)
     m16 = _plan(p, 512, 6, {"rollout_tile": 16, "rollout_pair": 2})
     for k in ("returns", "elites", "mu", "sigma", "actions", "states"):
         assert torch.equal(pair[k], m16[k]), k
@@ -76,10 +79,26 @@ def test_pair_plan_fuzz_equals_16_candidate_tiles(case):
     over, N, H = _fuzz_shape(case)
     p = ocem.synth_problem(3, N=N, H=H, **over)
     try:
-        pair = _plan(p, N, H, {"rollout_pair": 1})
+        pair = _plan(p, N, H, PAIR_ONLY)
     except RuntimeError as exc:
         assert "rollout_pair" in str(exc)
         return
     m16 = _plan(p, N, H, {"rollout_tile": 16, "rollout_pair": 2})
     for k in ("returns", "elites", "mu", "sigma", "actions", "states"):
         assert torch.equal(pair[k], m16[k]), (case, over, N, H, k)
+
+
+@pytest.mark.parametrize("cid,N,H", [(4, 2048, 8), (5, 200, 4)])
+def test_pair_hand_off_timeout_is_recomputed(cid, N, H):
+    """a plain launch does not promise that both halves of a pair are resident, so a
+    hand-off wait can time out. Every pair workgroup then sets bit 0 of the status word and the gated
+    launch behind it recomputes the candidates: MBRL_OPT_DEBUG_PAIR_ABORT = 1 makes every workgroup give
+    up at once, and the plan still equals the 16-candidate plan bit for bit (with the redo the default,
+    a normal pair plan is the same too)."""
+    p = ocem.synth_problem(cid, N=N, H=H)
+    aborted = _plan(p, N, H, {"rollout_pair": 1, "debug_pair_abort": 1})
+    gated = _plan(p, N, H, {"rollout_pair": 1})
+    m16 = _plan(p, N, H, {"rollout_tile": 16, "rollout_pair": 2})
+    for k in ("returns", "elites", "mu", "sigma", "actions", "states"):
+        assert torch.equal(aborted[k], m16[k]), (k, "aborted pair + redo vs 16")
+        assert torch.equal(gated[k], m16[k]), (k, "pair + idle redo vs 16")

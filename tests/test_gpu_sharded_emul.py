@@ -1,0 +1,120 @@
+"""The one-call sharded plan (mbrl_cem_plan_sharded, the default path of an RCCL process group) run
+at G = 2, 4 and 8 ranks on ONE GPU, through the C entry, rank by rank.
+
+RCCL will not put two ranks on one device, so under MBRL_OPT_SHARD_EMULATE a call with comm == NULL
+computes every other rank's shard itself (its proposals drawn at that rank's global offset, rolled out
+by the same kernels) and writes the rank-major buffer the all-gather would deliver. Everything else is
+the multi-rank code path: this rank's offset r * N / G, its own proposal draws (initial and fused into
+each update), the rank-major -> member-major cost permutation of ensembles, the selection over all N.
+Each rank's costs, returns, elites, mu, sigma, actions and states must equal mbrl_cem_plan's bit for
+bit (per-iteration semantics: /root/reference/src/mbrl/planners.py:189-216)."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import cem as ocem
+from test_gpu_parity import DEV, build
+
+pytestmark = pytest.mark.gpu
+
+KEYS = ("costs", "returns", "elites", "mu", "sigma", "actions", "states")
+
+
+def _problem(cid, N, H, **over):
+    from mbrl_amd import CEMPlanner, fused
+    p = ocem.synth_problem(cid, N=N, H=H, **over)
+    _, model_fn, cost_fn, sample_action = build(p)
+    dev = torch.device(DEV)
+    md = fused.describe_model(model_fn)
+    prob = fused.device_problem(md, fused.describe_cost(cost_fn, md["s"], md), dev)
+    st = CEMPlanner._settings(sample_action, H, dict(num_candidates=N, num_iterations=5, seed=p["rng_seed"],
+                                                     record=True))
+    s0 = torch.from_numpy(p["s0"]).to(dev)
+    return prob, st, s0
+
+
+def _single(prob, st, s0):
+    from mbrl_amd import planners
+    with torch.cuda.device(prob.device):
+        res = planners._cem_fused_single(prob, s0, st)
+    torch.cuda.synchronize()
+    return {k: res[k].cpu() for k in KEYS}
+
+
+def _emulated(prob, st, s0, world, rank):
+    from mbrl_amd import _lib, planners
+    with _lib.option("shard_emulate", 1), torch.cuda.device(prob.device):
+        res = planners._cem_sharded_native(prob, s0, st, world, rank, comm=None)
+        torch.cuda.synchronize()
+    return {k: res[k].cpu() for k in KEYS}
+
+
+def _assert_same(got, ref, tag):
+    for k in KEYS:
+        assert got[k].shape == ref[k].shape, (tag, k)
+        assert torch.equal(got[k], ref[k]), (tag, k, float((got[k].double() - ref[k].double()).abs().max()))
+
+
+# (cid, N, H, over, worlds): walker configs[3] at full size over 2/4/8 ranks (8-candidate tiles at
+# 2048 per rank); humanoid configs[4] (E = 5, N = 32768, H = 50) over 8 ranks: 4096 per rank, the
+# ensemble permutation and the unfused select / refit / draw path (K a exceeds the fused update);
+# cheetah configs[2] over 8 ranks (512 per rank); the reward head and cartpole at smaller sizes
+CASES = [
+    (4, 16384, 30, {}, (2, 4, 8)),
+    (5, 32768, 50, {}, (8,)),
+    (3, 4096, 30, {}, (8,)),
+    (6, 2048, 12, {}, (4,)),
+    (2, 1024, 20, {}, (8,)),
+]
+
+
+@pytest.mark.parametrize("cid,N,H,over,worlds", CASES, ids=[f"c{c[0]}_N{c[1]}_G{'-'.join(map(str, c[4]))}"
+                                                           for c in CASES])
+def test_sharded_plan_every_rank_equals_single_gpu_plan(cid, N, H, over, worlds):
+    prob, st, s0 = _problem(cid, N, H, **over)
+    ref = _single(prob, st, s0)
+    for world in worlds:
+        for rank in range(world):
+            _assert_same(_emulated(prob, st, s0, world, rank), ref, (cid, world, rank))
+    print(f"c{cid} N={N} H={H} E={prob.mdesc['E']}: ranks of G={worlds} bit-identical to mbrl_cem_plan "
+          f"(elites {tuple(ref['elites'].shape)}, mu[0,0] {float(ref['mu'][0, 0]):.6g})")
+
+
+def test_sharded_plan_through_the_c_entry_rejects_bad_calls():
+    """The C entry's refusals: N % nranks != 0 (workspace query 0, plan MBRL_EINVAL), comm == NULL
+    without the emulation switch, bad communicator arguments -- all before any collective."""
+    from mbrl_amd import _lib, fused
+    lib = _lib.load()
+    prob, st, s0 = _problem(3, 1000, 6)
+    params = _lib.CemParams(1000, 6, 100, 2, 0.1, -1.0, 1.0, 0.0, 0.5, 0, 1)
+    shape = fused.ctypes_ref(prob.shape)
+    assert lib.mbrl_cem_plan_sharded_workspace_bytes(shape, ctypes.byref(params), 3) == 0
+    assert lib.mbrl_cem_plan_sharded_workspace_bytes(shape, ctypes.byref(params), 8) > 0
+    need = lib.mbrl_cem_plan_sharded_workspace_bytes(shape, ctypes.byref(params), 8)
+    ws = torch.empty(need, dtype=torch.uint8, device=DEV)
+    out = torch.empty(6 * (17 + 3 * 6), dtype=torch.float32, device=DEV)
+
+    def call(nranks, rank, comm=None):
+        return lib.mbrl_cem_plan_sharded(shape, _lib.ptr(prob.packed), fused.ctypes_ref(prob.norm),
+                                         fused.ctypes_ref(prob.cost), _lib.ptr(s0), ctypes.byref(params), comm,
+                                         nranks, rank, _lib.ptr(out), _lib.ptr(out), _lib.ptr(out), _lib.ptr(out),
+                                         None, None, None, None, _lib.ptr(ws), ws.numel(), _lib.stream_handle(DEV))
+
+    assert call(8, 0) == _lib.MBRL_EINVAL                    # comm NULL, no emulation
+    assert b"comm" in lib.mbrl_last_error()
+    with _lib.option("shard_emulate", 1):
+        assert call(3, 0) == _lib.MBRL_EINVAL                 # 1000 % 3
+        assert b"1000 over 3 ranks" in lib.mbrl_last_error()
+        assert call(8, 8) == _lib.MBRL_EINVAL                 # rank out of range
+        emu_need = lib.mbrl_cem_plan_sharded_workspace_bytes(shape, ctypes.byref(params), 8)
+        assert emu_need > need                               # + one shard of emulated proposals
+        assert call(8, 0) == _lib.MBRL_EWORKSPACE             # the emulation's buffer is not in `ws`
+    torch.cuda.synchronize()
+    comm = ctypes.c_void_p()
+    ident = ctypes.create_string_buffer(_lib.MBRL_COMM_ID_BYTES)
+    assert lib.mbrl_comm_init(ident, 0, 0, ctypes.byref(comm)) == _lib.MBRL_EINVAL
+    assert lib.mbrl_comm_init(ident, 2, 2, ctypes.byref(comm)) == _lib.MBRL_EINVAL
+    assert lib.mbrl_comm_init(None, 2, 0, ctypes.byref(comm)) == _lib.MBRL_EINVAL
+    assert lib.mbrl_comm_destroy(None) == _lib.MBRL_OK
