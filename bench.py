@@ -27,9 +27,15 @@ Extra objects on the JSON line:
   cpu_baseline_torch -- the reference's own CPU arrangement beside it: torch on the host with
                   autograd on (planners.py:199-210), NumPy refit; same conditions.
   parity       -- iteration-0 returns of 256 sampled candidates re-computed by the CPU oracle.
+  plan_gpu_ms  -- mean device span of a timed plan: fence-free HIP events recorded on the plan's stream
+                  just before and just after the C call that enqueues it (so from the enqueue of its
+                  first launch to the end of its last kernel); host_ms_per_plan = ms_per_step minus it:
+                  the host's turn per plan (Python around the call, the result sync and copy-out).
   strong       -- BASELINE.json configs[3]: walker-walk N=16384 H=30 split over the ranks (strong
                   scaling, N/G candidates per GPU), same timing rules; at N=1 the single-GPU plan the
                   split is measured against.
+  strong_headline -- the headline cheetah N=4096 split over the ranks (N/G per GPU; north_star's
+                  ">= 6x at 8 GPUs" read as strong scaling), beside the weak-scaled line.
   variants     -- the same workload timed with the other rollout precisions (default headline: exact
                   fp32; variants: f16x6 and f16x3, fp32 emulated on the f16 matrix cores).
 """
@@ -372,15 +378,17 @@ def main():
         # leaves the GPU idle ~4 us, so bracketing all five would cost the plan ~40 us
         events = [[(make_event(), make_event()) if it == MEASURED_IT else None for it in range(ITERATIONS)]
                   for _ in range(args.steps)]
-        for ev in events:          # torch creates its events lazily: record once so the C ABI gets live handles
-            for pair in ev:
+        # one pair per plan around the C call that enqueues it: the plan's device span
+        spans = [(make_event(), make_event()) for _ in range(args.steps)]
+        for ev in events + [[sp] for sp in spans]:   # torch creates its events lazily: record once so
+            for pair in ev:                          # the C ABI gets live handles
                 if pair is not None:
                     pair[0].record()
                     pair[1].record()
         barrier()
         t0 = time.perf_counter()
         for k in range(args.steps):
-            plan(rollout_events=events[k])
+            plan(rollout_events=events[k], plan_events=spans[k])
         barrier()
         elapsed = time.perf_counter() - t0
         if dist is not None:
@@ -389,9 +397,17 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
         rollout_ms = [pair[0].elapsed_time(pair[1]) for ev in events for pair in ev if pair is not None]
+        span_ms = [sp[0].elapsed_time(sp[1]) for sp in spans]
+        if dist is not None:   # the slowest rank's device span, as elapsed is the slowest rank's wall time
+            t = torch.tensor([float(np.mean(span_ms))], dtype=torch.float64,
+                             device="cpu" if dist.get_backend() == "gloo" else dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            span_ms = [float(t.item())]
+        timed.plan_gpu_ms = float(np.mean(span_ms))
         return elapsed, float(np.mean(rollout_ms)) / 1e3, first
 
     elapsed, avg_rollout_s, first = timed(args.precision)
+    plan_gpu_ms = timed.plan_gpu_ms
     cand_steps = ITERATIONS * N * H * args.steps
     value = cand_steps / elapsed
     flop_launch = n_local * H * synthetic.flop_per_candidate_step(cfg)
@@ -412,6 +428,8 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
+        "plan_gpu_ms": plan_gpu_ms,
+        "host_ms_per_plan": elapsed / args.steps * 1e3 - plan_gpu_ms,
         "higher_is_better": True,
         "scaling": "strong" if args.strong else "weak",
         "vs_baseline": None,
@@ -448,7 +466,7 @@ def main():
         for other in others:
             v_elapsed, v_rollout_s, v_first = timed(other)
             var = dict(precision=other, value=cand_steps / v_elapsed, ms_per_step=v_elapsed / args.steps * 1e3,
-                       rollout_avg_launch_ms=v_rollout_s * 1e3,
+                       plan_gpu_ms=timed.plan_gpu_ms, rollout_avg_launch_ms=v_rollout_s * 1e3,
                        rollout_tflops_fp32_equivalent=flop_launch / v_rollout_s / 1e12, note=notes[other])
             if other != "f32":
                 # the split kernels are bound by the per-CU L2 weight stream: algorithmic bytes = every
@@ -479,8 +497,23 @@ def main():
                          f"{wcfg['L']}x{wcfg['W']} MLP I={ITERATIONS} K={Nw // 10} (BASELINE.json configs[3])",
                 scaling="strong", candidates_per_gpu=Nw // world, n_gpus=world,
                 value=ITERATIONS * Nw * wcfg["H"] * args.steps / w_elapsed, unit="candidate-timesteps/s",
-                ms_per_step=w_elapsed / args.steps * 1e3, rollout_avg_launch_ms=w_rollout_s * 1e3,
+                ms_per_step=w_elapsed / args.steps * 1e3, plan_gpu_ms=timed.plan_gpu_ms,
+                rollout_avg_launch_ms=w_rollout_s * 1e3,
                 rollout_frac=w_flop / w_rollout_s / 1e12 / PEAK_FP32_MFMA_TFLOPS)
+    if not args.no_strong and not args.strong and cfg["N"] % world == 0:
+        # the headline workload itself split over the ranks: N = 4096 in total, N/G per GPU
+        Nh = cfg["N"]
+        hkw = dict(kw, num_candidates=Nh, num_elites=Nh // 10)
+        h_elapsed, h_rollout_s, _ = timed(args.precision, prob, hkw) if world > 1 else (elapsed, avg_rollout_s, None)
+        h_flop = Nh // world * H * synthetic.flop_per_candidate_step(cfg)
+        out["strong_headline"] = dict(
+            workload=f"{cfg['name']} CEM N={Nh} H={H} (the headline workload split over the ranks)",
+            scaling="strong", candidates_per_gpu=Nh // world, n_gpus=world,
+            value=ITERATIONS * Nh * H * args.steps / h_elapsed, unit="candidate-timesteps/s",
+            ms_per_step=h_elapsed / args.steps * 1e3,
+            plan_gpu_ms=timed.plan_gpu_ms if world > 1 else plan_gpu_ms,
+            rollout_avg_launch_ms=h_rollout_s * 1e3,
+            rollout_frac=h_flop / h_rollout_s / 1e12 / PEAK_FP32_MFMA_TFLOPS)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.config, budget_s=args.cpu_budget)
         out["cpu_baseline_torch"] = cpu_torch_baseline(prob, budget_s=args.cpu_budget)

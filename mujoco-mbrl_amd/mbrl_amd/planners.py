@@ -241,7 +241,9 @@ class CEMPlanner(ModelPlanner):
     reference's sampler), init_std (None -> (hi - lo) / 4), action_bounds (None -> from
     sample_action's action_spec, else (-1, 1)), distributed (False), return_device (False),
     precision ("f32": exact fp32 MFMA; "f16x6" / "f16x3": fp32 emulated on the f16 matrix cores
-    with 33 / 22 significant operand bits, see include/mbrl_cem.h).
+    with 33 / 22 significant operand bits, see include/mbrl_cem.h). Timing hooks (bench.py):
+    rollout_events (per-iteration event pairs around the rollout launch), plan_events (one pair
+    recorded on the plan's stream just before and just after the C call that enqueues the plan).
     Returns the final Gaussian mean (clipped) and its predicted states (ensemble mean)."""
     defaults = dict(num_candidates=1000, num_elites=None, num_iterations=5, alpha=0.1, seed=None, init_std=None,
                     action_bounds=None, distributed=False, return_device=False, precision="f32")
@@ -279,7 +281,8 @@ class CEMPlanner(ModelPlanner):
         return dict(N=N, K=K, H=int(horizon), I=int(g("num_iterations")), alpha=float(g("alpha")), lo=lo, hi=hi,
                     init_std=init_std, seed=seed, distributed=bool(g("distributed")),
                     keep=bool(g("return_device")), record=bool(kwargs.get("record", False)),
-                    events=kwargs.get("rollout_events"), adim=sdesc[2] if sdesc else None,
+                    events=kwargs.get("rollout_events"), plan_events=kwargs.get("plan_events"),
+                    adim=sdesc[2] if sdesc else None,
                     precision=_lib.precision_code(g("precision")))
 
     @staticmethod
@@ -396,11 +399,16 @@ def _cem_plan_host(lib, prob, initial_state, st, params, ws):
     o_s0 = H * (s + 3 * a)
     arr[o_s0:o_s0 + s] = initial_state.detach().reshape(-1).to(torch.float32).numpy()
     o_act, o_mu, o_sg = H * s, H * (s + a), H * (s + 2 * a)
+    pev = st["plan_events"]
+    if pev is not None:
+        pev[0].record()
     _lib.check(lib.mbrl_cem_plan(fused.ctypes_ref(prob.shape), _lib.ptr(prob.packed), fused.ctypes_ref(prob.norm),
                                  fused.ctypes_ref(prob.cost), stage.at(o_s0), fused.ctypes_ref(params), stage.at(o_mu),
                                  stage.at(o_sg), stage.at(o_act), stage.at(0), None, None, None,
                                  _events(st, params.iterations), _lib.ptr(ws), ws.numel(), _lib.stream_handle(dev)),
                "mbrl_cem_plan")
+    if pev is not None:
+        pev[1].record()
     torch.cuda.current_stream(dev).synchronize()
     out = torch.from_numpy(arr[:o_s0].copy())
     return dict(states=out[:o_act].view(H, s), actions=out[o_act:o_mu].view(H, a), mu=out[o_mu:o_sg].view(H, a),
@@ -442,11 +450,16 @@ def _cem_fused_single(prob, initial_state, st):
     ret_hist = torch.empty((I, N), dtype=torch.float32, device=dev) if rec else None
     elite_hist = torch.empty((I, K), dtype=torch.int64, device=dev) if rec else None
     ev_arr = _events(st, I)
+    pev = st["plan_events"]
+    if pev is not None:
+        pev[0].record()
     _lib.check(lib.mbrl_cem_plan(fused.ctypes_ref(prob.shape), _lib.ptr(prob.packed), fused.ctypes_ref(prob.norm),
                                  fused.ctypes_ref(prob.cost), _lib.ptr(s0), fused.ctypes_ref(params), _lib.ptr(mu),
                                  _lib.ptr(sigma), _lib.ptr(actions), _lib.ptr(states), _lib.ptr(cost_hist),
                                  _lib.ptr(ret_hist), _lib.ptr(elite_hist), ev_arr, _lib.ptr(ws), ws.numel(),
                                  _lib.stream_handle(dev)), "mbrl_cem_plan")
+    if pev is not None:
+        pev[1].record()
     out = dict(states=states, actions=actions, mu=mu, sigma=sigma, _both=both)
     if rec:
         out.update(costs=cost_hist, returns=ret_hist, elites=elite_hist)
@@ -648,11 +661,16 @@ def _cem_sharded_native(prob, s0, st, world, rank, comm=_OWN_COMM):
     cost_hist = torch.empty((I, E, N), dtype=torch.float32, device=dev) if rec else None
     ret_hist = torch.empty((I, N), dtype=torch.float32, device=dev) if rec else None
     elite_hist = torch.empty((I, K), dtype=torch.int64, device=dev) if rec else None
+    pev = st.get("plan_events")
+    if pev is not None:
+        pev[0].record()
     rc = lib.mbrl_cem_plan_sharded(fused.ctypes_ref(prob.shape), _lib.ptr(prob.packed), fused.ctypes_ref(prob.norm),
                                    fused.ctypes_ref(prob.cost), _lib.ptr(s0), fused.ctypes_ref(params), comm, world, rank,
                                    _lib.ptr(mu), _lib.ptr(sigma), _lib.ptr(actions), _lib.ptr(states),
                                    _lib.ptr(cost_hist), _lib.ptr(ret_hist), _lib.ptr(elite_hist), _events(st, I),
                                    _lib.ptr(ws), ws.numel(), _lib.stream_handle(dev))
+    if pev is not None and rc == _lib.MBRL_OK:
+        pev[1].record()
     if rc != _lib.MBRL_OK and comm and world > 1:
         # the library aborted the communicator (so no other rank waits on this one): forget it, and
         # the next plan builds a new one
