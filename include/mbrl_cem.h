@@ -163,7 +163,11 @@ enum {
                                        other rank's shard itself in place of the all-gather (G > 1 on one GPU) */
     MBRL_OPT_DEBUG_PAIR_ABORT = 12, /* 1: the column-split pair kernel gives up at once (its redo runs);
                                        2: no redo launch behind it (tests of the pair kernel's own results) */
-    MBRL_OPT_COUNT = 13
+    MBRL_OPT_TRAJ_HOP = 13,         /* cooperative trajectory hand-offs: 0 auto, 1 (P, E) grid + sc1 granules,
+                                       2 per-member XCD grid + sc1, 3 XCD grid + L2-resident granules when
+                                       the roll call finds the member on one XCD (A/B; same results) */
+    MBRL_OPT_GD_HOP = 14,           /* the cooperative gd kernel's hand-offs, as MBRL_OPT_TRAJ_HOP             */
+    MBRL_OPT_COUNT = 15
 };
 int mbrl_set_option(int32_t option, int32_t value);
 int mbrl_get_option(int32_t option);

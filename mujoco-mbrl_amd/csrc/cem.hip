@@ -33,6 +33,8 @@ static std::atomic<int> g_opt[MBRL_OPT_COUNT];
 #define MBRL_PAIR_AUTO 0
 #endif
 static constexpr bool kPairAuto = MBRL_PAIR_AUTO;
+// traj_coop_kernel hand-off mode under MBRL_OPT_TRAJ_HOP = 0 (TrajArgs.hop_mode)
+static constexpr int kTrajHopDefault = 2;
 
 static int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 static int fail(int code, const char* fmt, ...) {
@@ -1239,6 +1241,8 @@ static int traj_impl(const Geometry& g, const void* packed, const mbrl_norm* nor
         return hip_check(launch_traj_reg(T, g.E, stream), "trajectory launch");
     if (xchg && status && traj_coop_supported(T, g.E) && xchg_bytes >= traj_coop_xchg_bytes(T, g.E)) {
         T.debug_abort = g_opt[MBRL_OPT_DEBUG_TRAJ_ABORT].load(std::memory_order_relaxed) != 0;
+        const int hop = g_opt[MBRL_OPT_TRAJ_HOP].load(std::memory_order_relaxed);
+        T.hop_mode = hop == 0 ? kTrajHopDefault : hop - 1;
         const hipError_t err = launch_traj_coop(T, g.E, xchg, status, stream);
         if (err != hipErrorCooperativeLaunchTooLarge) {   // too large: the grid cannot be co-resident
             int rc = hip_check(err, "trajectory launch");
@@ -1373,6 +1377,8 @@ int mbrl_set_option(int32_t option, int32_t value) {
         case MBRL_OPT_TRAIN_TILE: ok = value == 0 || value == 32 || value == 64; break;
         case MBRL_OPT_ROLLOUT_PAIR: ok = value >= 0 && value <= 2; break;
         case MBRL_OPT_DEBUG_PAIR_ABORT: ok = value >= 0 && value <= 2; break;
+        case MBRL_OPT_TRAJ_HOP: ok = value >= 0 && value <= 3; break;
+        case MBRL_OPT_GD_HOP: ok = value >= 0 && value <= 3; break;
         default: ok = value == 0 || value == 1; break;
     }
     if (!ok) return fail(MBRL_EINVAL, "option %d: value %d not allowed", option, value);
@@ -2344,6 +2350,8 @@ int mbrl_gd_plan_batch(const mbrl_mlp_shape* shape, const void* packed, const mb
         A.gate = nullptr;
         if (coop) {
             A.debug_abort = g_opt[MBRL_OPT_DEBUG_GD_ABORT].load(std::memory_order_relaxed) != 0;
+            const int hop = g_opt[MBRL_OPT_GD_HOP].load(std::memory_order_relaxed);
+            A.hop_mode = hop == 0 ? kTrajHopDefault : hop - 1;
             const hipError_t err = launch_gd_coop(A, xchg, status, st);
             if (err == hipErrorCooperativeLaunchTooLarge && n > 1) {   // fewer plans per group, same start
                 group = std::max(1, n / 2);

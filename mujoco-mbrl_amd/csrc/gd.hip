@@ -376,25 +376,25 @@ __host__ __device__ inline GcLds gc_lds(int s, int a, int W, int Wp, int L, int 
     return m;
 }
 
-__device__ __forceinline__ float gc_half_sum(float v) {
-#pragma unroll
-    for (int o = 16; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-
-// Publish this workgroup's 16 values (lane c == 0 of half-wave g holds value g) and gather all P
+// Publish this workgroup's 16 values (lane c == 16 of half-wave g holds value g) and gather all P
 // slices into `dst`; returns false on a timeout (status set). GR = Wp / 64 granules per lane: every
 // load of a sweep pass is in flight before the first compare (a runtime-bounded loop waited for
 // each load in turn: GR dependent fabric round trips per pass).
+// l2: every workgroup of the plan runs on this XCD (gd_roll_call), so the granules are stored with
+// L2-resident (sc0) stores instead of written through (sc1); the sc1 sweep reads the shared L2.
 template <int GR>
 __device__ __forceinline__ bool gc_exchange(gc_gu64* xchg, int Wp, int p, unsigned& phase, float val, float* dst,
-                                            int& abort_flag, unsigned* status) {
+                                            int& abort_flag, unsigned* status, bool l2) {
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = tid >> 5, c = tid & 31;
     const unsigned epoch = phase + 1u;
     gc_gu64* buf = xchg + (size_t)(phase & 1u) * Wp;
-    if (c == 0)
-        __hip_atomic_store(&buf[p * GC_ROWS + g], ((gc_u64)epoch << 32) | __float_as_uint(val), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+    if (c == 16) {   // the lane holding the half-wave's sum (halfwave_sum_hi)
+        const gc_u64 gr = ((gc_u64)epoch << 32) | __float_as_uint(val);
+        if (l2)
+            __hip_atomic_store(&buf[p * GC_ROWS + g], gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        else
+            __hip_atomic_store(&buf[p * GC_ROWS + g], gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     if (wave == 0) {
         const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
         for (;;) {
@@ -464,9 +464,14 @@ template <int K0R, int SM, int WI>
 __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_u64* __restrict__ xchg_all,
                                                              unsigned* __restrict__ status) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int p = blockIdx.x;
-    // plan blockIdx.y of a batch: its own start state, actions, states, hand-off block and workspace
-    const int pb = blockIdx.y;
+    // plan pb of a batch: its own start state, actions, states, hand-off block and workspace. hop_mode
+    // >= 1: plan (blockIdx.x & 7) + 8 blockIdx.y has the blocks with that blockIdx.x % 8 (one XCD under
+    // round-robin dispatch; speed only), else blockIdx.y
+    const bool xgrid = A.hop_mode >= 1;
+    const int p = xgrid ? (int)(blockIdx.x >> 3) : (int)blockIdx.x;
+    const int pb = xgrid ? (int)((blockIdx.x & 7) + 8 * blockIdx.y) : (int)blockIdx.y;
+    if (pb >= A.batch) return;
+    [[maybe_unused]] const int P = xgrid ? (int)(gridDim.x >> 3) : (int)gridDim.x;
     const float* s0 = A.s0 + (size_t)pb * A.s;
     float* actions = A.actions + (size_t)pb * A.H * A.a;
     float* states_out = A.states_out + (size_t)pb * (A.H + 1) * A.s;
@@ -525,12 +530,13 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
 #pragma unroll
     for (int k = 0; k < K0R; ++k) w0r[k] = (has_unit && k < K0) ? tw[A.tw_off[0] + (size_t)k * Wp + tid] : 0.0f;
     const float* wo = tw + A.tw_off[L];                       // Wout [s][W]
-    float wor[SM][WI];                                        // forward: Wout[g + 16 mm][c + 32 i]
+    using Dot = CoopDot<WI>;
+    float wor[SM][WI];                                        // forward: Wout[g + 16 mm][Dot::col(c, i)]
 #pragma unroll
     for (int mm = 0; mm < SM; ++mm)
 #pragma unroll
         for (int i = 0; i < WI; ++i) {
-            const int d = g + 16 * mm, k = c + 32 * i;
+            const int d = g + 16 * mm, k = Dot::col(c, i);
             wor[mm][i] = (d < s && k < W) ? wo[(size_t)d * W + k] : 0.0f;
         }
     float wob[16 * SM];                                       // backward: Wout[n][tid]
@@ -542,6 +548,44 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
     const float* hbias = bias;                                // [L][Wpad]
     const float* obias = bias + (size_t)L * Wp;
     __syncthreads();
+    // hop_mode 2: roll call (as traj_coop_kernel): XCC_IDs as granules in the parity-1 buffer, which
+    // phase 1 first overwrites only after every workgroup has read them (it gathers phase 0 first)
+    int& l2_flag = *(reinterpret_cast<int*>(smem + m.flag) + 1);
+    if (A.hop_mode == 2) {
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+        gc_gu64* roll = xchg + Wp;
+        constexpr unsigned RTAG = 0xFFFFFFFFu;
+        if (tid == 0)
+            __hip_atomic_store(&roll[p], ((gc_u64)RTAG << 32) | xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (wave == 0) {
+            const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+            bool same = true;
+            for (;;) {
+                const gc_u64 gv = lane < P ? __hip_atomic_load(&roll[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                           : (((gc_u64)RTAG << 32) | xcc);
+                if (__all((unsigned)(gv >> 32) == RTAG)) {
+                    same = __all((unsigned)gv == xcc);
+                    break;
+                }
+                if (__builtin_amdgcn_s_memrealtime() - t_start > 20000000ull) {   // 200 ms
+                    if (lane == 0) {
+                        abort_flag = 1;
+                        atomicOr(status, 1u);
+                    }
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (lane == 0) l2_flag = same ? 1 : 0;
+        }
+        __syncthreads();
+        if (abort_flag) return;
+    } else if (tid == 0) {
+        l2_flag = 0;
+    }
+    __syncthreads();
+    const bool l2 = l2_flag != 0;
 
     const float b1 = 0.9f, b2 = 0.999f, eps = 1e-8f;
     unsigned phase = 0;
@@ -556,7 +600,7 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
         if (has_unit) {
             float v = b0;
 #pragma unroll
-            for (int k = 0; k < K0R; ++k) v += w0r[k] * x0[k];
+            for (int k = 0; k < K0R; ++k) v = fmaf(w0r[k], x0[k], v);
             v = fmaxf(v, 0.0f);
             cur[tid] = v;
             ht[tid] = v;
@@ -564,12 +608,9 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
         __syncthreads();
         for (int l = 1; l < L; ++l) {
             const float* f = fw + (size_t)(l - 1) * GC_ROWS * m.rs + (size_t)g * m.rs;
-            float v = 0.f;
-#pragma unroll
-            for (int i = 0; i < WI; ++i) v += f[c + 32 * i] * cur[c + 32 * i];
-            v = gc_half_sum(v);
+            float v = halfwave_sum_hi(Dot::lds(f, cur, c));
             v = fmaxf(v + hbias[(size_t)l * Wp + p * GC_ROWS + g], 0.0f);
-            if (!gc_exchange<WI / 2>(xchg, Wp, p, phase, v, nxt, abort_flag, status)) return false;
+            if (!gc_exchange<WI / 2>(xchg, Wp, p, phase, v, nxt, abort_flag, status, l2)) return false;
             float* tmp = cur; cur = nxt; nxt = tmp;
             if (has_unit) ht[(size_t)l * Wp + tid] = cur[tid];
         }
@@ -581,13 +622,10 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
         for (int l = L - 1; l >= 1; --l) {
             // my 16 input gradients of layer l: k = 16p + g, lanes over n
             const float* b = bw + (size_t)(l - 1) * GC_ROWS * m.rs + (size_t)g * m.rs;
-            float v = 0.f;
-#pragma unroll
-            for (int i = 0; i < WI; ++i) v += b[c + 32 * i] * gcur[c + 32 * i];
-            v = gc_half_sum(v);
+            float v = halfwave_sum_hi(Dot::lds(b, gcur, c));
             const int k = p * GC_ROWS + g;
             v = ht[(size_t)(l - 1) * Wp + k] > 0.f ? v : 0.f;     // ReLU' of layer l - 1's output
-            if (!gc_exchange<WI / 2>(xchg, Wp, p, phase, v, gnxt, abort_flag, status)) return false;
+            if (!gc_exchange<WI / 2>(xchg, Wp, p, phase, v, gnxt, abort_flag, status, l2)) return false;
             float* tmp = gcur; gcur = gnxt; gnxt = tmp;
         }
         // layer 0 backward (redundant): g_x0[k] = sum_u W0[u][k] g_z0[u], a block reduction per k
@@ -625,12 +663,9 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
             // output layer (redundant): half-wave g owns rows g + 16 mm
 #pragma unroll
             for (int mm = 0; mm < SM; ++mm) {
-                float v = 0.f;
-#pragma unroll
-                for (int i = 0; i < WI; ++i) v += wor[mm][i] * cur[c + 32 * i];
-                v = gc_half_sum(v);
+                const float v = halfwave_sum_hi(Dot::reg(wor[mm], cur, c));
                 const int d = g + 16 * mm;
-                if (c == 0 && d < s) {
+                if (c == 16 && d < s) {
                     const float o = v + obias[d];
                     st[(t + 1) * s + d] = A.unnorm_s ? o * A.obs_std[d] + A.obs_mean[d] : o;
                 }
@@ -746,9 +781,13 @@ static hipError_t launch_gd_coop_w(const GdArgs& A, gc_u64* xchg, unsigned* stat
     hipError_t err = ensure_dynamic_lds(reinterpret_cast<const void*>(fn), 160 * 1024);
     if (err != hipSuccess) return err;
     const size_t lds = gc_lds(A.s, A.a, A.W, A.Wpad, A.L, A.H, 32).total;
-    if (!grid_fits(reinterpret_cast<const void*>(fn), GC_THREADS, lds, A.Wpad / GC_ROWS * A.batch))
+    const int P = A.Wpad / GC_ROWS;
+    if (!grid_fits(reinterpret_cast<const void*>(fn), GC_THREADS, lds, P * A.batch))
         return hipErrorCooperativeLaunchTooLarge;
-    hipLaunchKernelGGL(fn, dim3(A.Wpad / GC_ROWS, A.batch), dim3(GC_THREADS), lds, stream, A, xchg, status);
+    if (A.hop_mode >= 1)   // plan b on the blocks with blockIdx.x % 8 == b % 8 (grid.y: groups of 8 plans)
+        hipLaunchKernelGGL(fn, dim3(8 * P, (A.batch + 7) / 8), dim3(GC_THREADS), lds, stream, A, xchg, status);
+    else
+        hipLaunchKernelGGL(fn, dim3(P, A.batch), dim3(GC_THREADS), lds, stream, A, xchg, status);
     return hipGetLastError();
 }
 

@@ -306,6 +306,13 @@ struct TrajArgs {
     float* states_out;     // [E][H][s]
     const unsigned* gate;  // traj_kernel: when non-NULL, run only if *gate != 0 (the coop kernel gave up)
     int debug_abort;       // traj_coop_kernel: give up at once (tests of the fallback; MBRL_DEBUG_TRAJ_ABORT)
+    // traj_coop_kernel hand-off placement (MBRL_OPT_TRAJ_HOP): 0 = a (P, E) grid, agent-scope (sc1)
+    // granules; 1 = a 1-D grid of 8 P workgroups where member e's P share blockIdx % 8 == e (one XCD
+    // under round-robin dispatch), sc1 granules; 2 = that grid, and granules written with L2-resident
+    // (sc0) stores once a roll call at the start found every workgroup of the member on one XCD
+    // (s_getreg XCC_ID; else sc1 as in 1)
+    int hop_mode;
+    int E;                 // ensemble members (hop_mode >= 1: E <= 8)
 };
 hipError_t launch_traj(const TrajArgs& A, int E, hipStream_t stream);
 
@@ -335,6 +342,7 @@ struct GdArgs {
     int* iterations_out;                   // device int or NULL
     const unsigned* gate;                  // gd_plan_kernel: when non-NULL, run only if *gate != 0
     int debug_abort;                       // gd_coop_kernel: give up at once (MBRL_DEBUG_GD_ABORT)
+    int hop_mode;                          // gd_coop_kernel hand-offs, as TrajArgs.hop_mode (MBRL_OPT_GD_HOP)
     // batched plans (grid.y = batch): plan b reads s0 + b s, actions + b H a, writes states_out +
     // b (H+1) s and iterations_out + b; its m / v / hist lie plan_ws bytes after plan b-1's, its
     // hand-off block (2 Wpad granules, then the status word) xchg_stride granules after
@@ -395,5 +403,70 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
                               const mbrl_adam_hparams* hp = nullptr, int arith = 0,
                               const mbrl_adam_tensor* prior = nullptr, int prior_n = 0,
                               mbrl_adam_tensor* pending = nullptr, int* pending_n = nullptr);
+
+// ---- cooperative single-candidate kernels (traj.hip, gd.hip): the dot of one 16-row slice, one row
+// per half-wave (32 lanes), and its reduction
+typedef float coop_f32x4 __attribute__((ext_vector_type(4)));
+
+// The same sum, complete in lane 16 of each half-wave (c == 16) only: DPP row sums (row_ror 8, 4, 2,
+// 1: every lane of a 16-lane row holds its row's sum), then row_bcast:15 hands row 0's lane 15 to
+// row 1 (and row 2's to row 3). DPP moves cost a few cycles where each ds_swizzle step of
+// halfwave_sum waits on the LDS crossbar; a fixed order, so every workgroup gets the same bits.
+__device__ __forceinline__ float halfwave_sum_hi(float v) {
+    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false));
+    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x124, 0xF, 0xF, false));
+    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x122, 0xF, 0xF, false));
+    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x121, 0xF, 0xF, false));
+    return v + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x142, 0xA, 0xF,
+                                                                     false));
+}
+
+// Lane c's share of a 16-row dot over K = 32 WI columns: VW-wide LDS vectors at columns
+// VW c + 32 VW j + q (j < WI / VW), VW independent fmaf chains closed as a fixed tree.
+template <int WI>
+struct CoopDot {
+    static constexpr int VW = WI >= 4 ? 4 : 2;
+    static constexpr int NJ = WI / VW;
+    static __device__ __forceinline__ int col(int c, int i) { return VW * c + 32 * VW * (i / VW) + (i % VW); }
+    // w: LDS row (w[k] for column k), x: LDS vector
+    static __device__ __forceinline__ float lds(const float* w, const float* x, int c) {
+        float acc[VW] = {};
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int k = VW * c + 32 * VW * j;
+            if constexpr (VW == 4) {
+                const coop_f32x4 a = *reinterpret_cast<const coop_f32x4*>(w + k);
+                const coop_f32x4 b = *reinterpret_cast<const coop_f32x4*>(x + k);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) acc[q] = fmaf(a[q], b[q], acc[q]);
+            } else {
+#pragma unroll
+                for (int q = 0; q < VW; ++q) acc[q] = fmaf(w[k + q], x[k + q], acc[q]);
+            }
+        }
+        return close(acc);
+    }
+    // wr: this lane's weights in registers, wr[i] for column col(c, i)
+    static __device__ __forceinline__ float reg(const float (&wr)[WI], const float* x, int c) {
+        float acc[VW] = {};
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int k = VW * c + 32 * VW * j;
+            if constexpr (VW == 4) {
+                const coop_f32x4 b = *reinterpret_cast<const coop_f32x4*>(x + k);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) acc[q] = fmaf(wr[4 * j + q], b[q], acc[q]);
+            } else {
+#pragma unroll
+                for (int q = 0; q < VW; ++q) acc[q] = fmaf(wr[VW * j + q], x[k + q], acc[q]);
+            }
+        }
+        return close(acc);
+    }
+    static __device__ __forceinline__ float close(const float (&acc)[VW]) {
+        if constexpr (VW == 4) return (acc[0] + acc[1]) + (acc[2] + acc[3]);
+        else return acc[0] + acc[1];
+    }
+};
 
 }  // namespace mbrl

@@ -170,6 +170,8 @@ __device__ __forceinline__ float halfwave_sum(float v) {
     return v;
 }
 
+// halfwave_sum_hi and CoopDot: mbrl_internal.h (shared with gd.hip)
+
 struct CoopLds {
     int rs;                         // slice row stride (floats)
     size_t slices, x0, hA, hB, out, acts, hb, ob, om, os, flag, total;
@@ -202,14 +204,18 @@ template <int K0R, int SM, int WI>
 __global__ void __launch_bounds__(COOP_THREADS) traj_coop_kernel(const TrajArgs A, u64* __restrict__ xchg_all,
                                                                   unsigned* __restrict__ status) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int p = blockIdx.x, e = blockIdx.y;
-    [[maybe_unused]] const int P = gridDim.x;
+    // hop_mode >= 1: member e's workgroups are blocks e, e + 8, e + 16, ... (one XCD under round-robin
+    // dispatch: speed only, the granule protocol below holds on any placement)
+    const bool xgrid = A.hop_mode >= 1;
+    const int p = xgrid ? (int)(blockIdx.x >> 3) : (int)blockIdx.x;
+    const int e = xgrid ? (int)(blockIdx.x & 7) : (int)blockIdx.y;
+    if (e >= A.E) return;                      // the XCD slots past the ensemble
+    [[maybe_unused]] const int P = xgrid ? (int)(gridDim.x >> 3) : (int)gridDim.x;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int s = A.s, a = A.a, W = A.W, Wp = A.Wpad, K0 = s + a;
     const CoopLds m = coop_lds(s, a, W, Wp, A.L, A.H, K0R);
     float* slices = smem + m.slices;
     float* x0 = smem + m.x0;
-    float* out = smem + m.out;
     float* acts = smem + m.acts;
     float* hb = smem + m.hb;
     float* ob = smem + m.ob;
@@ -258,24 +264,67 @@ __global__ void __launch_bounds__(COOP_THREADS) traj_coop_kernel(const TrajArgs 
 #pragma unroll
     for (int k = 0; k < K0R; ++k)
         w0r[k] = (has_unit && k < K0) ? tw[A.tw_off[0] + (size_t)k * Wp + tid] : 0.0f;
-    // output rows d = g + 16 mm, columns c + 32 i (Wout row-major [s][W]), zero past s / W
+    // output rows d = g + 16 mm, columns CoopDot<WI>::col(c, i) (Wout row-major [s][W]), zero past s / W
     const int g = tid >> 5, c = tid & 31;
+    using Dot = CoopDot<WI>;
     float wor[SM][WI];
 #pragma unroll
     for (int mm = 0; mm < SM; ++mm)
 #pragma unroll
         for (int i = 0; i < WI; ++i) {
-            const int d = g + 16 * mm, k = c + 32 * i;
+            const int d = g + 16 * mm, k = Dot::col(c, i);
             wor[mm][i] = (d < s && k < W) ? tw[A.tw_off[A.L] + (size_t)d * W + k] : 0.0f;
         }
     __syncthreads();
 
+    // hop_mode 2: roll call. Each workgroup publishes its XCD (XCC_ID) as a granule in the parity-1
+    // buffer (first used by phase 1, which no workgroup can publish before every workgroup has read
+    // the roll call: phase 1 follows the gather of phase 0). If all P share one XCD they share its L2,
+    // and the granules travel as L2-resident stores (kept in the XCD's L2) read by sc1 loads; else as
+    // sc1 stores (written through) as on any placement.
+    int& l2_flag = *(reinterpret_cast<int*>(smem + m.flag) + 1);
+    if (A.hop_mode == 2) {
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+        gu64* roll = xchg + Wp;
+        constexpr unsigned RTAG = 0xFFFFFFFFu;
+        if (tid == 0)
+            __hip_atomic_store(&roll[p], ((u64)RTAG << 32) | xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (wave == 0) {
+            const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+            bool same = true;
+            for (;;) {
+                u64 gv = lane < P ? __hip_atomic_load(&roll[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                  : (((u64)RTAG << 32) | xcc);
+                if (__all((unsigned)(gv >> 32) == RTAG)) {
+                    same = __all((unsigned)gv == xcc);
+                    break;
+                }
+                if (__builtin_amdgcn_s_memrealtime() - t_start > 20000000ull) {  // 200 ms
+                    if (lane == 0) {
+                        abort_flag = 1;
+                        atomicOr(status, 1u);
+                    }
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (lane == 0) l2_flag = same ? 1 : 0;
+        }
+        __syncthreads();
+        if (abort_flag) return;
+    } else if (tid == 0) {
+        l2_flag = 0;
+    }
+    __syncthreads();
+    const bool l2 = l2_flag != 0;
 #ifdef MBRL_STAMPS
     unsigned long long tseg[TRAJ_NSEG] = {0, 0, 0, 0};
     unsigned long long tprev = __builtin_amdgcn_s_memrealtime();
 #endif
     int phase = 0;
     for (int t = 0; t < A.H; ++t) {
+        // x0 = (normalised s_t written by the last step's output lanes, normalised a_t)
         for (int d = tid; d < a; d += COOP_THREADS) x0[s + d] = acts[t * a + d];
         __syncthreads();
         float* cur = smem + m.hA;
@@ -283,24 +332,24 @@ __global__ void __launch_bounds__(COOP_THREADS) traj_coop_kernel(const TrajArgs 
         if (has_unit) {                                 // layer 0 (redundant in every workgroup)
             float v = b0;
 #pragma unroll
-            for (int k = 0; k < K0R; ++k) v += w0r[k] * x0[k];
+            for (int k = 0; k < K0R; ++k) v = fmaf(w0r[k], x0[k], v);
             cur[tid] = fmaxf(v, 0.0f);
         }
         __syncthreads();
         TSTAMP(0);
         for (int l = 1; l < A.L; ++l, ++phase) {
-            // my 16 units: row g (half-wave), lanes c split K
+            // my 16 units: row g (half-wave), lanes c split K; the sum lands in lane c == 16
             const float* ws = slices + (size_t)(l - 1) * COOP_ROWS * m.rs + (size_t)g * m.rs;
-            float v = 0.f;
-#pragma unroll
-            for (int i = 0; i < WI; ++i) v += ws[c + 32 * i] * cur[c + 32 * i];
-            v = halfwave_sum(v);
+            const float v = halfwave_sum_hi(Dot::lds(ws, cur, c));
             const unsigned epoch = (unsigned)phase + 1u;
             gu64* buf = xchg + (size_t)(phase & 1) * Wp;
-            if (c == 0) {
+            if (c == 16) {
                 const float y = fmaxf(v + hb[(l - 1) * COOP_ROWS + g], 0.0f);
-                __hip_atomic_store(&buf[p * COOP_ROWS + g], ((u64)epoch << 32) | __float_as_uint(y),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const u64 gr = ((u64)epoch << 32) | __float_as_uint(y);
+                if (l2)   // every reader shares this L2: a store that keeps the line there (sc0)
+                    __hip_atomic_store(&buf[p * COOP_ROWS + g], gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                else
+                    __hip_atomic_store(&buf[p * COOP_ROWS + g], gr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             TSTAMP(1);
             // gather all P slices: wave 0 sweeps the granules until every tag matches
@@ -334,23 +383,20 @@ __global__ void __launch_bounds__(COOP_THREADS) traj_coop_kernel(const TrajArgs 
             if (abort_flag) return;
             float* tmp = cur; cur = nxt; nxt = tmp;
         }
-        // output layer (redundant): half-wave g owns rows g + 16 mm
+        // output layer (redundant): half-wave g owns rows g + 16 mm; the lane holding a row's sum
+        // unnormalises it, stores the state and writes the next step's normalised input (x0 and cur
+        // are read / rewritten only after the barrier at the top of the next step)
 #pragma unroll
         for (int mm = 0; mm < SM; ++mm) {
-            float v = 0.f;
-#pragma unroll
-            for (int i = 0; i < WI; ++i) v += wor[mm][i] * cur[c + 32 * i];
-            v = halfwave_sum(v);
+            const float v = halfwave_sum_hi(Dot::reg(wor[mm], cur, c));
             const int d = g + 16 * mm;
-            if (c == 0 && d < s) out[d] = v + ob[d];
+            if (c == 16 && d < s) {
+                const float o = v + ob[d];
+                const float sn = A.unnorm_s ? o * os[d] + om[d] : o;
+                if (p == 0) A.states_out[((size_t)e * A.H + t) * s + d] = sn;
+                x0[d] = A.norm_s ? (sn - om[d]) / os[d] : sn;
+            }
         }
-        __syncthreads();
-        for (int d = tid; d < s; d += COOP_THREADS) {
-            const float sn = A.unnorm_s ? out[d] * os[d] + om[d] : out[d];
-            if (p == 0) A.states_out[((size_t)e * A.H + t) * s + d] = sn;
-            x0[d] = A.norm_s ? (sn - om[d]) / os[d] : sn;
-        }
-        // x0 is read again only after the barrier at the top of the next step
         TSTAMP(3);
     }
 #ifdef MBRL_STAMPS
@@ -379,15 +425,23 @@ bool traj_coop_supported(const TrajArgs& A, int E) {
 size_t traj_coop_xchg_bytes(const TrajArgs& A, int E) { return (size_t)E * 2 * A.Wpad * sizeof(u64); }
 
 template <int K0R, int SM, int WI>
-static hipError_t launch_coop_variant(const TrajArgs& A, int E, u64* xchg, unsigned* status, hipStream_t stream) {
+static hipError_t launch_coop_variant(const TrajArgs& A_in, int E, u64* xchg, unsigned* status, hipStream_t stream) {
     hipError_t err = ensure_dynamic_lds(reinterpret_cast<const void*>(&traj_coop_kernel<K0R, SM, WI>), 160 * 1024);
     if (err != hipSuccess) return err;
-    const size_t lds = coop_lds(A.s, A.a, A.W, A.Wpad, A.L, A.H, K0R).total;
-    if (!grid_fits(reinterpret_cast<const void*>(&traj_coop_kernel<K0R, SM, WI>), COOP_THREADS, lds,
-                   A.Wpad / COOP_ROWS * E))
+    const size_t lds = coop_lds(A_in.s, A_in.a, A_in.W, A_in.Wpad, A_in.L, A_in.H, K0R).total;
+    const int P = A_in.Wpad / COOP_ROWS;
+    if (!grid_fits(reinterpret_cast<const void*>(&traj_coop_kernel<K0R, SM, WI>), COOP_THREADS, lds, P * E))
         return hipErrorCooperativeLaunchTooLarge;
-    hipLaunchKernelGGL((traj_coop_kernel<K0R, SM, WI>), dim3(A.Wpad / COOP_ROWS, E), dim3(COOP_THREADS), lds,
-                       stream, A, xchg, status);
+    TrajArgs A = A_in;
+    A.E = E;
+    if (A.hop_mode >= 1 && E <= 8) {
+        hipLaunchKernelGGL((traj_coop_kernel<K0R, SM, WI>), dim3(8 * P), dim3(COOP_THREADS), lds, stream, A, xchg,
+                           status);
+    } else {
+        A.hop_mode = 0;
+        hipLaunchKernelGGL((traj_coop_kernel<K0R, SM, WI>), dim3(P, E), dim3(COOP_THREADS), lds, stream, A, xchg,
+                           status);
+    }
     return hipGetLastError();
 }
 
