@@ -30,7 +30,7 @@ static thread_local std::string g_err;
 static std::atomic<int> g_opt[MBRL_OPT_COUNT];
 // MBRL_OPT_ROLLOUT_PAIR = 0 (auto) takes column-split pairs for small plans when this is set
 #ifndef MBRL_PAIR_AUTO
-#define MBRL_PAIR_AUTO 0
+#define MBRL_PAIR_AUTO 1
 #endif
 static constexpr bool kPairAuto = MBRL_PAIR_AUTO;
 // traj_coop_kernel hand-off mode under MBRL_OPT_TRAJ_HOP = 0 (TrajArgs.hop_mode)
@@ -1157,7 +1157,12 @@ static int rollout_impl(const Geometry& g, const void* packed, const mbrl_norm* 
     if (pair_area && !A.reward && g_opt[MBRL_OPT_ROLLOUT_TILE].load(std::memory_order_relaxed) == 0) {
         const int po = g_opt[MBRL_OPT_ROLLOUT_PAIR].load(std::memory_order_relaxed);
         const int ntiles = (N + 15) / 16;
-        const bool want = po == 1 || (po == 0 && kPairAuto && (size_t)ntiles * g.E * 2 <= (size_t)device_cus());
+        // auto: where the pairs fill more than half the CUs and at most all of them (one workgroup per
+        // CU, all co-resident): the 2048-candidate shard of walker over 8 GPUs, 0.691 vs 0.715-0.722 ms
+        // per rollout on 8-candidate tiles with L2-resident hand-offs (profiles/r04/pair_l2_ab.json);
+        // at 1024 (half the chip) the 8-candidate tiles stay ahead, 0.54 vs 0.69 ms
+        const size_t pw = (size_t)ntiles * g.E * 2, cus = (size_t)device_cus();
+        const bool want = po == 1 || (po == 0 && kPairAuto && 2 * pw > cus && pw <= cus);
         if (want && pair_area_bytes(g, N) != 0) {
             RolloutArgs P = A;
             P.pair_flags = static_cast<unsigned*>(pair_area);
@@ -1166,6 +1171,7 @@ static int rollout_impl(const Geometry& g, const void* packed, const mbrl_norm* 
             if (rollout_pair_supported(P, g.T)) {
                 const int dpa = g_opt[MBRL_OPT_DEBUG_PAIR_ABORT].load(std::memory_order_relaxed);
                 P.debug_abort = dpa == 1;
+                P.pair_l2 = g_opt[MBRL_OPT_PAIR_L2].load(std::memory_order_relaxed) != 2;
                 const hipError_t err = launch_rollout_pair(P, g.T, stream);
                 if (err == hipSuccess && dpa == 2) return MBRL_OK;   // tests: the pair launch's own results
                 if (err == hipSuccess) {
@@ -1379,6 +1385,7 @@ int mbrl_set_option(int32_t option, int32_t value) {
         case MBRL_OPT_DEBUG_PAIR_ABORT: ok = value >= 0 && value <= 2; break;
         case MBRL_OPT_TRAJ_HOP: ok = value >= 0 && value <= 3; break;
         case MBRL_OPT_GD_HOP: ok = value >= 0 && value <= 3; break;
+        case MBRL_OPT_PAIR_L2: ok = value >= 0 && value <= 2; break;
         default: ok = value == 0 || value == 1; break;
     }
     if (!ok) return fail(MBRL_EINVAL, "option %d: value %d not allowed", option, value);

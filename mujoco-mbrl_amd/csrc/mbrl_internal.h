@@ -163,6 +163,7 @@ struct RolloutArgs {
     float* pair_data;
     unsigned* pair_flags;
     int debug_abort;         // PAIR kernel: give up at once, as after a timed-out hand-off (MBRL_OPT_DEBUG_PAIR_ABORT)
+    int pair_l2;             // PAIR kernel: L2-resident hand-offs when a roll call finds both halves on one XCD
     // non-PAIR fp32 kernels: NULL, or the pair launch's status word (the line after its flags); the
     // launch then recomputes its candidates only if bit 0 is set (a hand-off of the pair launch timed out)
     const unsigned* gate;

@@ -388,13 +388,29 @@ __device__ __forceinline__ void lds_wait_ge(const uint32_t* w, uint32_t need) {
 }
 
 // This hand-off wave's stores are drained; count it in (LDS word arr) and let the last of the four
-// set the workgroup's flag to q + 1.
-__device__ __forceinline__ void pair_signal(uint32_t* arr, gu32* flag, unsigned q, int lane) {
+// set the workgroup's flag to q + 1 (l2: both halves on one XCD, an L2-resident store; else sc1).
+__device__ __forceinline__ void pair_signal(uint32_t* arr, gu32* flag, unsigned q, int lane, bool l2) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     unsigned old = 0;
     if (lane == 0) old = atomicAdd(arr, 1u);
     old = (unsigned)__shfl((int)old, 0, 64);
-    if (old == 4 * q + 3 && lane == 0) __hip_atomic_store(flag, q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == 4 * q + 3 && lane == 0) {
+        if (l2)
+            __hip_atomic_store(flag, q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        else
+            __hip_atomic_store(flag, q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// Buffer stores of the hand-off payload: sc0 (the line stays in the XCD's L2) when both halves share
+// that L2, else sc1 (written through). The cache-policy operand must be an immediate.
+__device__ __forceinline__ void pair_store_b128(u32x4 v, __amdgpu_buffer_rsrc_t r, unsigned off, bool l2) {
+    if (l2) __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 1);
+    else __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16);
+}
+__device__ __forceinline__ void pair_store_b32(unsigned v, __amdgpu_buffer_rsrc_t r, unsigned off, bool l2) {
+    if (l2) __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, 1);
+    else __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, 16);
 }
 
 // Wait until the partner's flag reads q + 1: hand-off wave 0 polls it and publishes the match in LDS
@@ -556,6 +572,30 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
             const unsigned theirs = (unsigned)((size_t)(sid ^ 1) * per * sizeof(float));
             const int ocw = 4 * (half ^ 1) + hw;   // the partner's compute wave paired with this one
             unsigned q = 0;
+            // roll call (A.pair_l2): each half writes its XCD (XCC_ID + 1) to word 1 of its flag line and
+            // reads the partner's; on one XCD the halves share an L2, and every hand-off then travels as
+            // L2-resident (sc0) stores read by sc1 loads, else as written-through sc1 stores. Hand-off
+            // wave 0 decides for the workgroup (LDS word lflag[3]: 2 = one XCD, 1 = not).
+            bool l2 = false;
+            if (A.pair_l2 && !MBRL_PAIR_DIAG) {
+                if (hw == 0) {
+                    unsigned xcc;
+                    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+                    if (lane == 0) __hip_atomic_store(myflag + 1, xcc + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    unsigned px = 0;
+                    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+                    while ((px = __hip_atomic_load(pflag + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u) {
+                        if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {
+                            __hip_atomic_fetch_or(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(2);
+                    }
+                    if (lane == 0) *(volatile lu32*)(lflag + 3) = px == xcc + 1 ? 2u : 1u;
+                }
+                lds_wait_ge(lflag + 3, 1);
+                l2 = *(volatile lu32*)(lflag + 3) == 2u;
+            }
             // layer columns: publish this half's cw = 4 half + hw slice of buffer `buf`, copy the partner's in
             auto layer = [&](float* buf) {
                 const unsigned slot = (unsigned)((((q & 1) * 4 + hw) * TW * 64 + lane) * 16);
@@ -565,9 +605,8 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
                 for (int j = 0; j < TW; ++j) v[j] = *reinterpret_cast<const f32x4*>(buf + row + (4 * half + hw) * 16 * TW + 16 * j);
                 if constexpr (!MBRL_PAIR_DIAG) {
 #pragma unroll
-                    for (int j = 0; j < TW; ++j)
-                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v[j]), xr, mine + slot + j * 1024, 0, PAIR_SC1);
-                    pair_signal(lflag + 1, myflag, q, lane);
+                    for (int j = 0; j < TW; ++j) pair_store_b128(__builtin_bit_cast(u32x4, v[j]), xr, mine + slot + j * 1024, l2);
+                    pair_signal(lflag + 1, myflag, q, lane, l2);
                     pair_await(pflag, lflag + 2, q, hw, lane, status);
 #pragma unroll
                     for (int j = 0; j < TW; ++j)
@@ -591,12 +630,11 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
                     if (idx < nel) {
                         const int m = idx / A.s, ro = m * A.pw + (idx - m * A.s);
                         so[i] = (L.part[ro] + L.part[ws + ro]) + (L.part[2 * ws + ro] + L.part[3 * ws + ro]);
-                        if constexpr (!MBRL_PAIR_DIAG)
-                            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(so[i]), xr, mine + pslot + idx * 4, 0, PAIR_SC1);
+                        if constexpr (!MBRL_PAIR_DIAG) pair_store_b32(__float_as_uint(so[i]), xr, mine + pslot + idx * 4, l2);
                     }
                 }
                 if constexpr (!MBRL_PAIR_DIAG) {
-                    pair_signal(lflag + 1, myflag, q, lane);
+                    pair_signal(lflag + 1, myflag, q, lane, l2);
                     pair_await(pflag, lflag + 2, q, hw, lane, status);
                 }
 #pragma unroll

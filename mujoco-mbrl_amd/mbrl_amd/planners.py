@@ -152,8 +152,29 @@ class GradientDescentPlanner(ModelPlanner):
         return _to_host(states, keep), _to_host(actions, keep)
 
 
+def _rs_host(initial_state, model, cost, sample_action, H, N):
+    """RandomShootingPlanner on a host without a GPU (BASELINE configs[0]: the reference's own CPU
+    random-shooting path): the reference's a2 loop on the caller's callables, as written
+    (/root/reference/src/mbrl/planners.py:189-216: one sample_action(N * H) draw, time-major rows
+    t * N + n, H model calls, one cost call, view(H, N).sum(0)), then np.argmin (first index on ties,
+    :184). Returns (states [H, s], actions [H, a]) of the chosen candidate."""
+    s = initial_state.shape[0]
+    with torch.no_grad():
+        state_list = torch.zeros((N * H, s))
+        action_list = sample_action(batch_size=N * H)
+        for t in range(H):
+            states = (initial_state.unsqueeze(dim=0).repeat_interleave(N, dim=0) if t == 0
+                      else state_list[(t - 1) * N:t * N])
+            state_list[t * N:(t + 1) * N] = model(states, action_list[t * N:(t + 1) * N])
+        costs = cost(state_list, action_list).view(H, N).sum(0).detach().numpy()
+    i = int(np.argmin(costs))
+    return state_list.view(H, N, -1)[:, i], action_list.view(H, N, -1)[:, i]
+
+
 class RandomShootingPlanner(ModelPlanner):
-    """planners.py:140-216 on the GPU."""
+    """planners.py:140-216 on the GPU; on a host without one (torch.cuda.is_available() False), the
+    reference's own CPU loop on the given callables (_rs_host: BASELINE configs[0] is this planner on
+    CPU). With a GPU the HIP path always runs (and raises if the extension is missing)."""
     defaults = dict(num_trajectories=1000)
 
     @staticmethod
@@ -165,8 +186,10 @@ class RandomShootingPlanner(ModelPlanner):
 
     @staticmethod
     def _plan(initial_state, model, cost, sample_action, horizon, initial_trajectory, num_trajectories, **kwargs):
-        dev = _device(kwargs)
         N, H = int(num_trajectories), int(horizon)
+        if kwargs.get("device") is None and not torch.cuda.is_available():
+            return _rs_host(initial_state, model, cost, sample_action, H, N)
+        dev = _device(kwargs)
         # planners.py:200: one draw of N*H actions from the caller's sampler (host RNG), time-major
         action_list = sample_action(batch_size=N * H)
         a = action_list.shape[1]

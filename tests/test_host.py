@@ -2,6 +2,7 @@
 import functools
 
 import numpy as np
+import pytest
 import torch
 
 from oracle import cem as ocem
@@ -206,3 +207,70 @@ def test_policy_and_closures_pickle_like_the_reference_agent():
     s = torch.randn(5, 17)
     a = torch.rand(5, 6) * 2 - 1
     assert torch.equal(pol.model(s, a), back.model(s, a))
+
+
+def test_random_shooting_on_a_gpu_less_host_matches_reference_golden(golden):
+    """BASELINE configs[0] (the reference's random-shooting planner on CPU) through the public API on
+    a host without a GPU: the reference's a2 loop on the closures, np.argmin -- the chosen candidate,
+    its actions bit-exact and its states / every candidate's cost as the reference computed them
+    (tests/golden/config1_rs.npz, generated by the reference's own planners.py)."""
+    import numpy as np
+    import torch
+    from mbrl_amd import RandomShootingPlanner, planners
+    from oracle import cem as ocem
+    from test_gpu_parity import build
+    if torch.cuda.is_available():
+        pytest.skip("the GPU path runs when a GPU is present (tests/test_gpu_parity.py)")
+    g = golden("config1_rs")
+    p = ocem.synth_problem(1)
+    _, model_fn, cost_fn, sample_action = build(p)
+    np.random.seed(int(g["np_seed"]))
+    states, actions = RandomShootingPlanner.plan(torch.from_numpy(p["s0"]), model_fn, cost_fn, sample_action,
+                                                 p["cfg"]["H"], None, num_trajectories=p["cfg"]["N"])
+    assert np.array_equal(actions.numpy(), g["plan_actions"])
+    assert np.allclose(states.numpy(), g["plan_states"], rtol=1e-5, atol=1e-5)
+    # the costs of every candidate, through the same loop
+    N, H = p["cfg"]["N"], p["cfg"]["H"]
+    flat = torch.from_numpy(g["actions_flat"])
+    it = iter([flat])
+    st, ac = planners._rs_host(torch.from_numpy(p["s0"]), model_fn, cost_fn, lambda batch_size: next(it), H, N)
+    assert torch.equal(ac, flat.view(H, N, -1)[:, int(g["idx"])])
+
+
+def test_random_shooting_on_a_gpu_less_host_toy_known_answer():
+    """The reference's own known answer (src/mbrl/test_random_shooting.py:5-25: ring world, seed 0 ->
+    cost 18, states [1, 0, 9, 9, 8]) on the host path."""
+    import torch
+    from mbrl_amd import RandomShootingPlanner
+    if torch.cuda.is_available():
+        pytest.skip("the GPU path runs when a GPU is present (tests/test_gpu_parity.py)")
+    world_size, goal = 10, torch.tensor(9, dtype=torch.float)
+
+    def model(states, actions):
+        return torch.fmod((torch.fmod(states + actions, world_size) + world_size), world_size)
+
+    def sample_action(batch_size):
+        return torch.randint(low=-1, high=2, size=(batch_size, 1), dtype=torch.float)
+
+    def cost(states, actions):
+        return torch.abs(states - goal)
+
+    torch.manual_seed(0)
+    states, actions = RandomShootingPlanner.plan(torch.tensor([2], dtype=torch.float), model, cost, sample_action, 5,
+                                                 None, num_trajectories=1000)
+    assert states.numpy().ravel().tolist() == [1.0, 0.0, 9.0, 9.0, 8.0]
+    assert float(torch.abs(states - 9).sum()) == 18.0
+
+
+def test_cem_planner_on_a_gpu_less_host_raises():
+    """Only the random-shooting planner (configs[0]) has a host path: CEM needs the HIP extension."""
+    import torch
+    from mbrl_amd import CEMPlanner
+    from oracle import cem as ocem
+    from test_gpu_parity import build
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    p = ocem.synth_problem(2, N=64, H=4)
+    _, model_fn, cost_fn, sample_action = build(p)
+    with pytest.raises(RuntimeError, match="GPU"):
+        CEMPlanner.plan(torch.from_numpy(p["s0"]), model_fn, cost_fn, sample_action, 4, num_candidates=64)
