@@ -241,7 +241,6 @@ struct GemmLaunch {
     // fused Adam (mbrl_train_epoch): the step of a layer whose gradient the previous launch finished,
     // as extra workgroups after the products' tiles (ADAM_FUSED_CHUNK elements each)
     int adam_count, adam_blocks, adam_chunk;   // adam_chunk: elements per Adam workgroup
-    int adam_long;                             // 16 elements per thread instead of 4
     mbrl_adam_tensor adam_t[ADAM_FUSED_MAX];
     unsigned* zero_words;   // workgroup 0 zeroes zero_n words first (the fold's tickets; forward launch)
     int zero_n;
@@ -651,9 +650,8 @@ static hipError_t launch_gemm(GemmLaunch& L, bool loss_wg, hipStream_t stream) {
         blocks += L.d[i].tiles;
         kmax = max(kmax, L.d[i].K);
     }
-    // fused Adam blocks: chunks of 4 elements per thread of the launch's workgroup size (16 in a
-    // forward launch, which carries the previous step's deferred layer: fewer, longer workgroups)
-    const int chunk = 64 * (kmax >= 256 ? 16 : 4) * (L.adam_long ? 16 : 4);
+    // fused Adam blocks: chunks of 4 elements per thread of the launch's workgroup size
+    const int chunk = 64 * (kmax >= 256 ? 16 : 4) * 4;
     L.adam_chunk = chunk;
     L.adam_blocks = 0;
     for (int i = 0; i < L.adam_count; ++i) {
@@ -767,7 +765,6 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
         e = l == 0 ? launch_gemm<OP_GATHER, OP_DIRECT>(G, false, stream) : launch_gemm<OP_DIRECT, OP_DIRECT>(G, false, stream);
         G.zero_words = nullptr;
         G.adam_count = 0;
-        G.adam_long = 0;
         if (e != hipSuccess) return e;
     }
     // output layer (state head, reward head) + the loss gradient dY and its column sums

@@ -1,8 +1,8 @@
 """Counter-derived MFMA utilisation of the rollout kernel per config, from tools/mfma_pmc.sh output:
 per dispatch (averaged over the timed launches), FLOP issued = SQ_INSTS_VALU_MFMA_MOPS_F32 x 512, the
 clock = GRBM_GUI_ACTIVE / 8 XCDs / duration, util_issue = FLOP issued / (active cycles x 65536 FLOP per
-chip cycle: 256 CUs x 4 SIMDs x 64 fp32 MFMA FLOP/clk, 157.3 TF at 2.4 GHz), and
-SQ_VALU_MFMA_BUSY_CYCLES / (SQ_BUSY_CU_CYCLES x 4 SIMDs) as the busy-cycle form; beside the
+chip cycle: 256 CUs x 4 SIMDs x 64 fp32 MFMA FLOP/clk, 157.3 TF at 2.4 GHz), and the busy-cycle form
+SQ_VALU_MFMA_BUSY_CYCLES / (active cycles x 1024 SIMDs) (rocprofv3's MfmaUtil); beside the
 FLOP-derived frac = algorithmic FLOP / (duration x 157.3 TF) that bench.py reports.
 Usage: python tools/mfma_util.py <out dir> [label ...]"""
 import csv
@@ -30,9 +30,13 @@ def summarise(d, label):
             k = r["Dispatch_Id"]
             rows.setdefault(k, dict(kernel=r["Kernel_Name"], t=(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9))
             rows[k][r["Counter_Name"]] = float(r["Counter_Value"])
-    disp = sorted(rows.values(), key=lambda x: -x["t"])
-    # the plan's rollouts of the timed plans: the bench's last 3 plans x 5 iterations (drop warm-ups)
-    disp = list(rows.values())[-15:]
+    # the dominant kernel (most total time; a column-split pair launch is followed by its gated redo
+    # launch, whose workgroups exit at once), its last 15 dispatches: the bench's 3 timed plans x 5
+    by = {}
+    for x in rows.values():
+        by.setdefault(x["kernel"], []).append(x)
+    kern = max(by, key=lambda k: sum(x["t"] for x in by[k]))
+    disp = by[kern][-15:]
     avg = lambda k: sum(x[k] for x in disp) / len(disp)  # noqa: E731
     t = avg("t")
     grbm = avg("GRBM_GUI_ACTIVE") / 8
@@ -42,7 +46,16 @@ def summarise(d, label):
                padding=flop_issued / flop_alg - 1, frac_flop=flop_alg / t / 157.3e12,
                util_issue=flop_issued / (grbm * 65536), frac_issued_at_2p4=flop_issued / t / 157.3e12,
                sq_valu_mfma_busy_cycles=avg("SQ_VALU_MFMA_BUSY_CYCLES"), sq_busy_cu_cycles=avg("SQ_BUSY_CU_CYCLES"))
-    out["mfma_busy_over_cu_busy_x4"] = out["sq_valu_mfma_busy_cycles"] / max(out["sq_busy_cu_cycles"] * 4, 1)
+    # SQ_VALU_MFMA_BUSY_CYCLES summed over the SIMDs: its MfmaUtil form (rocprofv3's derived counter)
+    # is busy / (GRBM_GUI_ACTIVE max over XCDs x 1024 SIMDs); it reads 2139095040 (0x7F800000, the
+    # bits of +inf) on some dispatches -- a saturated value, reported as null
+    busy = out["sq_valu_mfma_busy_cycles"]
+    sat = any(x["SQ_VALU_MFMA_BUSY_CYCLES"] == 2139095040.0 for x in disp)
+    out["mfma_util_busy"] = None if sat else busy / (grbm * 1024)
+    out["mfma_busy_saturated"] = sat
+    out["other_kernels"] = {k: dict(dispatches=len(v), mean_ms=sum(x["t"] for x in v) / len(v) * 1e3)
+                            for k, v in by.items() if k != kern}
+    del out["sq_valu_mfma_busy_cycles"], out["sq_busy_cu_cycles"]
     return out
 
 
