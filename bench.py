@@ -40,6 +40,7 @@ Extra objects on the JSON line:
                   fp32; variants: f16x6 and f16x3, fp32 emulated on the f16 matrix cores).
 """
 import argparse
+import gc
 import json
 import os
 import sys
@@ -61,8 +62,8 @@ MEASURED_IT = 2     # the CEM iteration whose rollout launch bench.py brackets w
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=3, help="SURVEY.md §8d config id (default: cheetah-run CEM)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0,
@@ -386,11 +387,28 @@ def main():
                     pair[0].record()
                     pair[1].record()
         barrier()
+        gc_acc = [0.0, 0, None]          # the Python garbage collector's pauses inside the timed region
+
+        def gc_cb(phase, info):
+            if phase == "start":
+                gc_acc[2] = time.perf_counter()
+            elif gc_acc[2] is not None:
+                gc_acc[0] += time.perf_counter() - gc_acc[2]
+                gc_acc[1] += 1
+        gc.callbacks.append(gc_cb)
+        stamps = [0.0] * (args.steps + 1)
         t0 = time.perf_counter()
         for k in range(args.steps):
+            stamps[k] = time.perf_counter()
             plan(rollout_events=events[k], plan_events=spans[k])
+        stamps[args.steps] = time.perf_counter()
         barrier()
         elapsed = time.perf_counter() - t0
+        gc.callbacks.remove(gc_cb)
+        timed.gc = dict(ms=gc_acc[0] * 1e3, collections=gc_acc[1])
+        walls = np.diff(np.array(stamps)) * 1e3     # host wall time of each timed plan call
+        timed.walls = dict(median=float(np.median(walls)), p90=float(np.percentile(walls, 90)),
+                           max=float(walls.max()), min=float(walls.min()))
         if dist is not None:
             t = torch.tensor([elapsed], dtype=torch.float64,
                              device="cpu" if dist.get_backend() == "gloo" else dev)
@@ -408,6 +426,8 @@ def main():
 
     elapsed, avg_rollout_s, first = timed(args.precision)
     plan_gpu_ms = timed.plan_gpu_ms
+    gc_stats = timed.gc
+    wall_stats = timed.walls
     cand_steps = ITERATIONS * N * H * args.steps
     value = cand_steps / elapsed
     flop_launch = n_local * H * synthetic.flop_per_candidate_step(cfg)
@@ -430,6 +450,8 @@ def main():
         "ms_per_step": elapsed / args.steps * 1e3,
         "plan_gpu_ms": plan_gpu_ms,
         "host_ms_per_plan": elapsed / args.steps * 1e3 - plan_gpu_ms,
+        "host_gc_in_timed_region": gc_stats,
+        "plan_wall_ms": wall_stats,
         "higher_is_better": True,
         "scaling": "strong" if args.strong else "weak",
         "vs_baseline": None,

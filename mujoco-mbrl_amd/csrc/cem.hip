@@ -2263,10 +2263,11 @@ static GdWs gd_ws(const Geometry& g, int H, int B, void* base) {
     char* b = static_cast<char*>(base);
     const size_t ha = (size_t)H * g.a;
     const size_t row = ((size_t)((g.s + g.a + 3) & ~3) + (size_t)g.L * g.Wpad) * (g.reward ? 2 : 1);
-    const size_t coop = (size_t)(g.Wpad / 16) * H * g.L * g.Wpad * (g.reward ? 2 : 1);   // per-workgroup hidden-vector copies
+    // (the cooperative kernel keeps its ReLU masks in LDS; the saved layer inputs are the one-workgroup
+    // kernel's)
     w.xchg_stride = (size_t)2 * g.Wpad + 2;                                  // granules, then the status word
     const size_t xbytes = align256((size_t)B * w.xchg_stride * 8);
-    w.plan_ws = align256(ha * 4) * 2 + align256((H * row > coop ? H * row : coop) * 4);
+    w.plan_ws = align256(ha * 4) * 2 + align256(H * row * 4);
     w.xchg = b ? reinterpret_cast<unsigned long long*>(b) : nullptr;
     w.status = w.xchg ? reinterpret_cast<unsigned*>(w.xchg + 2 * g.Wpad) : nullptr;
     w.m = b ? reinterpret_cast<float*>(b + xbytes) : nullptr;

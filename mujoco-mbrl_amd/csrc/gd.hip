@@ -348,10 +348,16 @@ typedef __attribute__((address_space(1))) gc_u64 gc_gu64;
 
 struct GcLds {
     int rs;
-    size_t fw, bw, x0, hA, hB, gA, gB, out, gs, red, acts, m1, m2, grad, st, flag, total;
+    size_t fw, bw, x0, hA, hB, gA, gB, out, gs, red, acts, m1, m2, grad, st, flag, mk, total;
+    int mk_row;   // 32-bit words of ReLU masks per (pass, step): gc_mask_words
 };
 
-__host__ __device__ inline GcLds gc_lds(int s, int a, int W, int Wp, int L, int H, int K0R) {
+// ReLU masks the backward pass needs, per (pass, step), as bits in LDS: the last hidden layer's
+// whole output (the output layer's backward, one bit per unit: Wp / 32 words) and, for every other
+// layer, the 16 units this workgroup owns (the hidden layers' backward: one word each).
+__host__ __device__ inline int gc_mask_words(int Wp, int L) { return Wp / 32 + (L - 1); }
+
+__host__ __device__ inline GcLds gc_lds(int s, int a, int W, int Wp, int L, int H, int K0R, int passes = 1) {
     GcLds m;
     auto al4 = [](size_t n) { return (n + 3) & ~(size_t)3; };
     m.rs = W + 32;
@@ -372,6 +378,8 @@ __host__ __device__ inline GcLds gc_lds(int s, int a, int W, int Wp, int L, int 
     m.grad = o; o += al4((size_t)H * a);
     m.st = o;   o += al4((size_t)(H + 1) * s);
     m.flag = o; o += 4;
+    m.mk_row = gc_mask_words(Wp, L);
+    m.mk = o;   o += al4((size_t)passes * H * m.mk_row);
     m.total = o * sizeof(float);
     return m;
 }
@@ -480,7 +488,8 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
     status += (size_t)pb * A.xchg_stride * 2;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = tid >> 5, c = tid & 31;
     const int s = A.s, a = A.a, W = A.W, Wp = A.Wpad, K0 = s + a, L = A.L, H = A.H;
-    const GcLds m = gc_lds(s, a, W, Wp, L, H, K0R);
+    const GcLds m = gc_lds(s, a, W, Wp, L, H, K0R, A.reward ? 2 : 1);
+    unsigned* const mk = reinterpret_cast<unsigned*>(smem + m.mk);
     float* fw = smem + m.fw;
     float* bw = smem + m.bw;
     float* x0 = smem + m.x0;
@@ -496,10 +505,6 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
     const float* bias = A.packed + A.bias_off;
     const float* tw = A.packed + A.tw_base;
     gc_gu64* xchg = (gc_gu64*)xchg_all;
-    // this workgroup's copy of the hidden vectors: [H][L][Wp] per pass (state pass, then the reward
-    // pass of a reward-head model at rows H..2H-1)
-    float* hist = reinterpret_cast<float*>(reinterpret_cast<char*>(A.hist) + pb * A.plan_ws) +
-                  (size_t)p * (A.reward ? 2 : 1) * H * L * Wp;
 
     if (A.debug_abort) {                       // test hook: behave as a timed-out hand-off
         if (tid == 0) atomicOr(status, 1u);
@@ -594,17 +599,34 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
     float* nxt = smem + m.hB;
     float* gcur = smem + m.gA;
     float* gnxt = smem + m.gB;
-    // the trunk on x0 (layer 0 redundant, hidden layers through the hand-offs), activations into ht;
+    // ReLU masks of layer j's output (units > 0): j = L - 1 all Wp bits (words 0 .. Wp / 32 - 1,
+    // bit u % 32 of word u / 32), j < L - 1 this workgroup's units 16p .. 16p + 15 (word Wp / 32 + j,
+    // bit u - 16p). Written by the forward pass from each wave's ballot; the forward's activations are
+    // needed by the backward only through these signs.
+    const int own_w = (GC_ROWS * p) >> 6, own_b = (GC_ROWS * p) & 63;   // the wave holding my units, bit offset
+    auto put_mask = [&](unsigned* row, int j, float v) {
+        const unsigned long long bal = __ballot(has_unit && v > 0.f);
+        if (j == L - 1) {
+            if (lane == 0 && wave < Wp / 64) {
+                row[2 * wave] = (unsigned)bal;
+                row[2 * wave + 1] = (unsigned)(bal >> 32);
+            }
+        } else if (wave == own_w && lane == 0) {
+            row[Wp / 32 + j] = (unsigned)(bal >> own_b) & 0xFFFFu;
+        }
+    };
+    // the trunk on x0 (layer 0 redundant, hidden layers through the hand-offs), masks into row;
     // leaves the last hidden vector in cur. false: a hand-off gave up.
-    auto trunk = [&](float* ht) -> bool {
+    auto trunk = [&](unsigned* row) -> bool {
+        float v0 = 0.f;
         if (has_unit) {
             float v = b0;
 #pragma unroll
             for (int k = 0; k < K0R; ++k) v = fmaf(w0r[k], x0[k], v);
-            v = fmaxf(v, 0.0f);
-            cur[tid] = v;
-            ht[tid] = v;
+            v0 = fmaxf(v, 0.0f);
+            cur[tid] = v0;
         }
+        put_mask(row, 0, v0);
         __syncthreads();
         for (int l = 1; l < L; ++l) {
             const float* f = fw + (size_t)(l - 1) * GC_ROWS * m.rs + (size_t)g * m.rs;
@@ -612,19 +634,20 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
             v = fmaxf(v + hbias[(size_t)l * Wp + p * GC_ROWS + g], 0.0f);
             if (!gc_exchange<WI / 2>(xchg, Wp, p, phase, v, nxt, abort_flag, status, l2)) return false;
             float* tmp = cur; cur = nxt; nxt = tmp;
-            if (has_unit) ht[(size_t)l * Wp + tid] = cur[tid];
+            put_mask(row, l, has_unit ? cur[tid] : 0.f);
         }
         return true;
     };
     // reverse mode from gcur (d loss / d last hidden output, ReLU mask applied) through the hidden
     // layers (hand-offs) and layer 0 (redundant block reduction): use(k, d loss / d x0[k]), k < K0
-    auto trunk_back = [&](const float* ht, auto&& use) -> bool {
+    auto trunk_back = [&](const unsigned* row, auto&& use) -> bool {
         for (int l = L - 1; l >= 1; --l) {
             // my 16 input gradients of layer l: k = 16p + g, lanes over n
             const float* b = bw + (size_t)(l - 1) * GC_ROWS * m.rs + (size_t)g * m.rs;
             float v = halfwave_sum_hi(Dot::lds(b, gcur, c));
-            const int k = p * GC_ROWS + g;
-            v = ht[(size_t)(l - 1) * Wp + k] > 0.f ? v : 0.f;     // ReLU' of layer l - 1's output
+            // ReLU' of layer l - 1's output at my unit 16p + g (layer L - 1's full mask when l - 1 == L - 1
+            // cannot occur here: l - 1 < L - 1)
+            v = ((row[Wp / 32 + (l - 1)] >> g) & 1u) ? v : 0.f;
             if (!gc_exchange<WI / 2>(xchg, Wp, p, phase, v, gnxt, abort_flag, status, l2)) return false;
             float* tmp = gcur; gcur = gnxt; gnxt = tmp;
         }
@@ -658,8 +681,7 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
                 }
             }
             __syncthreads();
-            float* ht = hist + (size_t)t * L * Wp;
-            if (!trunk(ht)) return;
+            if (!trunk(mk + (size_t)t * m.mk_row)) return;
             // output layer (redundant): half-wave g owns rows g + 16 mm
 #pragma unroll
             for (int mm = 0; mm < SM; ++mm) {
@@ -679,7 +701,7 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
                     x0[d] = A.norm_s ? (sv - A.obs_mean[d]) / A.obs_std[d] : sv;
                 }
                 __syncthreads();
-                if (!trunk(hist + (size_t)(H + t) * L * Wp)) return;
+                if (!trunk(mk + (size_t)(H + t) * m.mk_row)) return;
                 __syncthreads();
             }
         }
@@ -687,12 +709,12 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
         for (int d = tid; d < 32; d += GC_THREADS) gs[d] = 0.f;
         __syncthreads();
         for (int t = H - 1; t >= 0; --t) {
-            const float* ht = hist + (size_t)t * L * Wp;
+            const unsigned* ht = mk + (size_t)t * m.mk_row;
             if (A.reward) {
                 // reward pass: d r_t / d head = grw through the reward row and the pass's ReLU masks;
                 // the state part joins d loss / d s_{t+1}, the action part waits in grad[t]
-                const float* hb = hist + (size_t)(H + t) * L * Wp;
-                if (has_unit) gcur[tid] = hb[(size_t)(L - 1) * Wp + tid] > 0.f ? wrb * grw : 0.f;
+                const unsigned* hb = mk + (size_t)(H + t) * m.mk_row;
+                if (has_unit) gcur[tid] = ((hb[tid >> 5] >> (tid & 31)) & 1u) ? wrb * grw : 0.f;
                 __syncthreads();
                 const bool ok = trunk_back(hb, [&](int k, float v) {
                     if (k < s) gs[k] += A.norm_s ? v / A.obs_std[k] : v;
@@ -715,7 +737,7 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
                 float v = 0.f;
 #pragma unroll
                 for (int n = 0; n < 16 * SM; ++n) v += wob[n] * gout[n];
-                gcur[tid] = ht[(size_t)(L - 1) * Wp + tid] > 0.f ? v : 0.f;
+                gcur[tid] = ((ht[tid >> 5] >> (tid & 31)) & 1u) ? v : 0.f;
             }
             __syncthreads();
             const bool ok = trunk_back(ht, [&](int k, float v) {
@@ -772,7 +794,7 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
 bool gd_coop_supported(const GdArgs& A) {
     const int K0 = A.s + A.a;
     if (A.L < 2 || A.W != A.Wpad || A.Wpad > GC_THREADS || A.Wpad < 64 || K0 > 32 || A.s > 32) return false;
-    return gc_lds(A.s, A.a, A.W, A.Wpad, A.L, A.H, 32).total <= 160 * 1024;
+    return gc_lds(A.s, A.a, A.W, A.Wpad, A.L, A.H, 32, A.reward ? 2 : 1).total <= 160 * 1024;
 }
 
 template <int WI>
@@ -780,7 +802,7 @@ static hipError_t launch_gd_coop_w(const GdArgs& A, gc_u64* xchg, unsigned* stat
     const auto fn = &gd_coop_kernel<32, 2, WI>;
     hipError_t err = ensure_dynamic_lds(reinterpret_cast<const void*>(fn), 160 * 1024);
     if (err != hipSuccess) return err;
-    const size_t lds = gc_lds(A.s, A.a, A.W, A.Wpad, A.L, A.H, 32).total;
+    const size_t lds = gc_lds(A.s, A.a, A.W, A.Wpad, A.L, A.H, 32, A.reward ? 2 : 1).total;
     const int P = A.Wpad / GC_ROWS;
     if (!grid_fits(reinterpret_cast<const void*>(fn), GC_THREADS, lds, P * A.batch))
         return hipErrorCooperativeLaunchTooLarge;
