@@ -346,6 +346,25 @@ constexpr int GC_ROWS = 16;
 typedef unsigned long long gc_u64;
 typedef __attribute__((address_space(1))) gc_u64 gc_gu64;
 
+// Diagnostic build only (-DMBRL_STAMPS): per-workgroup s_memrealtime sums (10 ns ticks) of the
+// cooperative kernel's segments, written to a buffer set by mbrl_diag_set_gd_stamps()
+// (tools/gd_stamps.py): forward layer 0, forward hidden (dots + hand-offs), forward output,
+// backward output layer, backward hidden, backward layer 0, Adam + stop test.
+#ifdef MBRL_STAMPS
+constexpr int GD_NSEG = 7;
+__device__ unsigned long long* g_mbrl_gd_stamps;
+#define GSTAMP(k)                                                      \
+    do {                                                               \
+        const unsigned long long _t = __builtin_amdgcn_s_memrealtime(); \
+        gseg[k] += _t - gprev;                                         \
+        gprev = _t;                                                    \
+    } while (0)
+#else
+#define GSTAMP(k) \
+    do {          \
+    } while (0)
+#endif
+
 struct GcLds {
     int rs;
     size_t fw, bw, x0, hA, hB, gA, gB, out, gs, red, acts, m1, m2, grad, st, flag, mk, total;
@@ -433,39 +452,57 @@ __device__ __forceinline__ bool gc_exchange(gc_gu64* xchg, int Wp, int p, unsign
 }
 
 // Wave-wide reduce-scatter of 32 values per lane by recursive halving: returns the sum over the
-// 64 lanes of v[lane >> 1] (both lanes of a pair hold it). 32 shuffles where a butterfly per value
-// takes 192.
+// 64 lanes of v[lane >> 1] (both lanes of a pair hold it). Each halving step adds the value a lane
+// keeps to the one its partner (lane ^ m) sends: m = 32 and 16 by v_permlane32_swap /
+// v_permlane16_swap (the swap hands each half-wave / row the other's value, and the two outputs
+// summed are keep + partner's), m = 8, 4, 2, 1 by DPP moves (row_ror:8; row_half_mirror then the quad
+// mirror for lane ^ 4; quad_perm for ^ 2, ^ 1). No LDS crossbar traffic (ds_bpermute) where the
+// r03 form had 32 per lane.
+// v_permlane32_swap / v_permlane16_swap as inline asm: both registers are read and written. (The
+// ROCm 7.2 clang builtins return the swapped pair wrongly here: __builtin_amdgcn_permlane32_swap's two
+// results were read from ONE register, v_add_f32 vX, vY, vY after the swap -- tools/ubench/rs_check.hip.)
+// The s_nops cover the VALU-write -> permlane-read and permlane-write -> VALU-read hazards, which the
+// compiler's hazard recognizer does not see through inline asm.
+__device__ __forceinline__ void permlane32_swap(float& x, float& y) {
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(x), "+v"(y));
+}
+__device__ __forceinline__ void permlane16_swap(float& x, float& y) {
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 1" : "+v"(x), "+v"(y));
+}
+#define GC_DPP(v, ctrl) \
+    __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, (v)), (ctrl), 0xF, 0xF, false))
 __device__ __forceinline__ float wave_reduce_scatter32(const float (&v)[32], int lane) {
     float a16[16], a8[8], a4[4], a2[2];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        const bool hi = lane & 32;
-        const float keep = hi ? v[j + 16] : v[j], send = hi ? v[j] : v[j + 16];
-        a16[j] = keep + __shfl_xor(send, 32, 64);
+    for (int j = 0; j < 16; ++j) {   // lane ^ 32: lanes < 32 keep v[j], lanes >= 32 keep v[j + 16]
+        float x = v[j], y = v[j + 16];
+        permlane32_swap(x, y);
+        a16[j] = x + y;
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const bool hi = lane & 16;
-        const float keep = hi ? a16[j + 8] : a16[j], send = hi ? a16[j] : a16[j + 8];
-        a8[j] = keep + __shfl_xor(send, 16, 64);
+    for (int j = 0; j < 8; ++j) {    // lane ^ 16: even rows keep a16[j], odd rows a16[j + 8]
+        float x = a16[j], y = a16[j + 8];
+        permlane16_swap(x, y);
+        a8[j] = x + y;
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < 4; ++j) {    // lane ^ 8 (row_ror:8)
         const bool hi = lane & 8;
         const float keep = hi ? a8[j + 4] : a8[j], send = hi ? a8[j] : a8[j + 4];
-        a4[j] = keep + __shfl_xor(send, 8, 64);
+        a4[j] = keep + GC_DPP(send, 0x128);
     }
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < 2; ++j) {    // lane ^ 4: half-row mirror (7 - i), then quad mirror (i ^ 3)
         const bool hi = lane & 4;
         const float keep = hi ? a4[j + 2] : a4[j], send = hi ? a4[j] : a4[j + 2];
-        a2[j] = keep + __shfl_xor(send, 4, 64);
+        a2[j] = keep + GC_DPP(GC_DPP(send, 0x141), 0x1B);
     }
-    const bool hi = lane & 2;
+    const bool hi = lane & 2;        // lane ^ 2: quad_perm [2, 3, 0, 1]
     const float keep = hi ? a2[1] : a2[0], send = hi ? a2[0] : a2[1];
-    const float a1 = keep + __shfl_xor(send, 2, 64);
-    return a1 + __shfl_xor(a1, 1, 64);
+    const float a1 = keep + GC_DPP(send, 0x4E);
+    return a1 + GC_DPP(a1, 0xB1);    // lane ^ 1: quad_perm [1, 0, 3, 2]
 }
+#undef GC_DPP
 
 // K0R >= s + a: layer-0 inputs per thread; SM: output rows per half-wave (16 SM >= s); WI = W / 32.
 template <int K0R, int SM, int WI>
@@ -595,6 +632,10 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
     const float b1 = 0.9f, b2 = 0.999f, eps = 1e-8f;
     unsigned phase = 0;
     int done = 0;
+#ifdef MBRL_STAMPS
+    unsigned long long gseg[GD_NSEG] = {0, 0, 0, 0, 0, 0, 0};
+    unsigned long long gprev = __builtin_amdgcn_s_memrealtime();
+#endif
     float* cur = smem + m.hA;
     float* nxt = smem + m.hB;
     float* gcur = smem + m.gA;
@@ -628,6 +669,7 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
         }
         put_mask(row, 0, v0);
         __syncthreads();
+        GSTAMP(0);
         for (int l = 1; l < L; ++l) {
             const float* f = fw + (size_t)(l - 1) * GC_ROWS * m.rs + (size_t)g * m.rs;
             float v = halfwave_sum_hi(Dot::lds(f, cur, c));
@@ -636,6 +678,7 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
             float* tmp = cur; cur = nxt; nxt = tmp;
             put_mask(row, l, has_unit ? cur[tid] : 0.f);
         }
+        GSTAMP(1);
         return true;
     };
     // reverse mode from gcur (d loss / d last hidden output, ReLU mask applied) through the hidden
@@ -651,6 +694,7 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
             if (!gc_exchange<WI / 2>(xchg, Wp, p, phase, v, gnxt, abort_flag, status, l2)) return false;
             float* tmp = gcur; gcur = gnxt; gnxt = tmp;
         }
+        GSTAMP(4);
         // layer 0 backward (redundant): g_x0[k] = sum_u W0[u][k] g_z0[u], a block reduction per k
         static_assert(K0R == 32, "wave_reduce_scatter32");
         const float gu = has_unit ? gcur[tid] : 0.f;
@@ -666,47 +710,65 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
             use(k, v);
         }
         __syncthreads();
+        GSTAMP(5);
         return true;
     };
     for (int it = 0; it < A.iterations; ++it) {
-        // ================= forward
-        for (int t = 0; t < H; ++t) {
-            for (int d = tid; d < K0; d += GC_THREADS) {
-                if (d < s) {
-                    const float sv = st[t * s + d];
-                    x0[d] = A.norm_s ? (sv - A.obs_mean[d]) / A.obs_std[d] : sv;
-                } else {
-                    const float av = acts[t * a + d - s];
-                    x0[d] = A.norm_a ? (av - A.act_mean[d - s]) / A.act_std[d - s] : av;
-                }
+        // ================= forward. x0 = (norm(s_t), norm(a_t)): the output lanes of step t - 1 write
+        // its state part, threads d < a its action part, one barrier before layer 0
+        for (int d = tid; d < K0; d += GC_THREADS) {
+            if (d < s) {
+                const float sv = st[d];
+                x0[d] = A.norm_s ? (sv - A.obs_mean[d]) / A.obs_std[d] : sv;
+            } else {
+                const float av = acts[d - s];
+                x0[d] = A.norm_a ? (av - A.act_mean[d - s]) / A.act_std[d - s] : av;
             }
-            __syncthreads();
+        }
+        __syncthreads();
+        for (int t = 0; t < H; ++t) {
             if (!trunk(mk + (size_t)t * m.mk_row)) return;
-            // output layer (redundant): half-wave g owns rows g + 16 mm
+            // output layer (redundant): half-wave g owns rows g + 16 mm; the lane holding row d's sum
+            // stores s_{t+1} and its normalised copy (layer 0 read x0 before the trunk's barriers)
 #pragma unroll
             for (int mm = 0; mm < SM; ++mm) {
                 const float v = halfwave_sum_hi(Dot::reg(wor[mm], cur, c));
                 const int d = g + 16 * mm;
                 if (c == 16 && d < s) {
                     const float o = v + obias[d];
-                    st[(t + 1) * s + d] = A.unnorm_s ? o * A.obs_std[d] + A.obs_mean[d] : o;
+                    const float sn = A.unnorm_s ? o * A.obs_std[d] + A.obs_mean[d] : o;
+                    st[(t + 1) * s + d] = sn;
+                    x0[d] = A.norm_s ? (sn - A.obs_mean[d]) / A.obs_std[d] : sn;
                 }
             }
-            __syncthreads();
             if (A.reward) {
                 // the cost call's trunk pass on (norm(s_{t+1}), norm(a_t)): x0's action part still
-                // holds norm(a_t); only its activations are needed for the backward pass
-                for (int d = tid; d < s; d += GC_THREADS) {
-                    const float sv = st[(t + 1) * s + d];
-                    x0[d] = A.norm_s ? (sv - A.obs_mean[d]) / A.obs_std[d] : sv;
-                }
+                // holds norm(a_t); only its ReLU masks are needed for the backward pass
                 __syncthreads();
                 if (!trunk(mk + (size_t)(H + t) * m.mk_row)) return;
-                __syncthreads();
             }
+            if (t + 1 < H)   // x0's action part for step t + 1 (its layer 0 reads after the barrier)
+                for (int j = tid; j < a; j += GC_THREADS) {
+                    const float av = acts[(t + 1) * a + j];
+                    x0[s + j] = A.norm_a ? (av - A.act_mean[j]) / A.act_std[j] : av;
+                }
+            __syncthreads();
+            GSTAMP(2);
         }
         // ================= backward, t = H-1 .. 0
+        // gout[d] = d loss / d (output row d) of step t from gs[d] = d (later steps) / d s_{t+1}[d]:
+        // + SmoothAbs' of the state cost at s_{t+1}, through unnormalise_state
+        auto gout_of = [&](int d, float gg, int t1) {
+            if (A.has_sc) {
+                const float x = st[t1 * s + d] - A.goal[d];
+                const float wx = x * A.cw[d];
+                gg += wx * A.cw[d] / sqrtf(wx * wx + A.alpha_s * A.alpha_s);
+            }
+            return A.unnorm_s ? gg * A.obs_std[d] : gg;
+        };
         for (int d = tid; d < 32; d += GC_THREADS) gs[d] = 0.f;
+        if (!A.reward)   // step H - 1's gout (no later step); later ones come from the use() below
+            for (int d = tid; d < s; d += GC_THREADS) gout[d] = gout_of(d, 0.f, H);
         __syncthreads();
         for (int t = H - 1; t >= 0; --t) {
             const unsigned* ht = mk + (size_t)t * m.mk_row;
@@ -721,17 +783,9 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
                     else grad[t * a + k - s] = A.norm_a ? v / A.act_std[k - s] : v;
                 });
                 if (!ok) return;
+                for (int d = tid; d < s; d += GC_THREADS) gout[d] = gout_of(d, gs[d], t + 1);
+                __syncthreads();
             }
-            for (int d = tid; d < s; d += GC_THREADS) {
-                float gg = gs[d];
-                if (A.has_sc) {
-                    const float x = st[(t + 1) * s + d] - A.goal[d];
-                    const float wx = x * A.cw[d];
-                    gg += wx * A.cw[d] / sqrtf(wx * wx + A.alpha_s * A.alpha_s);
-                }
-                gout[d] = A.unnorm_s ? gg * A.obs_std[d] : gg;
-            }
-            __syncthreads();
             // output layer backward (redundant): thread k = tid; ReLU mask of the last hidden layer
             if (has_unit) {
                 float v = 0.f;
@@ -740,9 +794,14 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
                 gcur[tid] = ((ht[tid >> 5] >> (tid & 31)) & 1u) ? v : 0.f;
             }
             __syncthreads();
+            GSTAMP(3);
             const bool ok = trunk_back(ht, [&](int k, float v) {
                 if (k < s) {
-                    gs[k] = A.norm_s ? v / A.obs_std[k] : v;
+                    const float gk = A.norm_s ? v / A.obs_std[k] : v;
+                    gs[k] = gk;
+                    // without a reward pass, step t - 1's gout follows from gk alone (read after the
+                    // barrier that closes trunk_back)
+                    if (!A.reward && t > 0) gout[k] = gout_of(k, gk, t);
                 } else {
                     const int j = k - s;
                     float ga = A.norm_a ? v / A.act_std[j] : v;
@@ -780,8 +839,13 @@ __global__ void __launch_bounds__(GC_THREADS) gd_coop_kernel(const GdArgs A, gc_
             __syncthreads();
         }
         done = it + 1;
+        GSTAMP(6);
         if (change / (float)(H * a) < A.stop) break;
     }
+#ifdef MBRL_STAMPS
+    if (tid == 0 && g_mbrl_gd_stamps != nullptr)
+        for (int k = 0; k < GD_NSEG; ++k) g_mbrl_gd_stamps[((size_t)pb * P + p) * GD_NSEG + k] = gseg[k];
+#endif
     if (p == 0) {
         for (int i = tid; i < H * a; i += GC_THREADS) actions[i] = acts[i];
         for (int i = tid; i < (H + 1) * s; i += GC_THREADS) states_out[i] = st[i];
@@ -838,3 +902,9 @@ hipError_t launch_gd_plan(const GdArgs& A, hipStream_t stream) {
 }
 
 }  // namespace mbrl
+
+#ifdef MBRL_STAMPS
+extern "C" int mbrl_diag_set_gd_stamps(void* buf) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(mbrl::g_mbrl_gd_stamps), &buf, sizeof(buf));
+}
+#endif
