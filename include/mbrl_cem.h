@@ -169,7 +169,8 @@ enum {
     MBRL_OPT_GD_HOP = 14,           /* the cooperative gd kernel's hand-offs, as MBRL_OPT_TRAJ_HOP             */
     MBRL_OPT_PAIR_L2 = 15,          /* column-split pair hand-offs: 0 / 1 L2-resident when both halves share an
                                        XCD (roll call), 2 always written through (A/B; same results)     */
-    MBRL_OPT_COUNT = 16
+    MBRL_OPT_TRAIN_XCD = 16,        /* training launches: 1 row bands in XCD order (A/B; same bits)           */
+    MBRL_OPT_COUNT = 17
 };
 int mbrl_set_option(int32_t option, int32_t value);
 int mbrl_get_option(int32_t option);

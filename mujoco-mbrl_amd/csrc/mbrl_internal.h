@@ -385,6 +385,7 @@ struct TrainShape {
     int s, a, W, L, reward, H;   // state / action dims, hidden width, hidden layers, reward head, horizon
     int tile;                    // backward C tile height: 0 auto, 32, 64 (MBRL_OPT_TRAIN_TILE; same bits)
     int fold;                    // 1: the layer-0 weight gradient folds into the dH_0 launch (same bits)
+    int xcd;                     // 1: row-band tiles in XCD order in every launch (MBRL_OPT_TRAIN_XCD; same bits)
 };
 struct TrainTensors {
     const float* const* weight;  // L + 1 (+ 1 reward head) nn.Linear weights [out][in]

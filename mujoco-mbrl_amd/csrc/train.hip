@@ -247,6 +247,9 @@ struct GemmLaunch {
     int adam_first[ADAM_FUSED_MAX + 1];
     mbrl_adam_hparams hp;
     int arith;
+    // product 0's tiles in XCD order (MBRL_OPT_TRAIN_XCD): every 64-row band of the batch on XCD
+    // (band % 8) in every launch, so a launch reads the rows the previous launch wrote on its own XCD
+    int xcd;
 };
 
 __device__ __forceinline__ int64_t batch_row(const GemmLaunch& L, int r) {
@@ -586,7 +589,14 @@ __global__ __launch_bounds__(64 * NW) void train_gemm_kernel(const GemmLaunch L)
     if (b == 0 && L.zero_words)
         for (int i = threadIdx.x; i < L.zero_n; i += 64 * NW) L.zero_words[i] = 0u;
     if (b < L.d[0].tiles) {
-        gemm_tile<NW, A0, B0, TMX>(L, L.d[0], b, red);
+        int tile = b;
+        if (L.xcd) {   // block b on XCD b % 8 (round-robin dispatch) takes a tile of a 64-row band of that XCD
+            constexpr int G = 2 / TMX;                    // tile rows per 64-row band
+            const int tn_all = L.d[0].tiles_n, per = G * tn_all, x = b & 7, j = b >> 3;
+            const int u = j / per, r = j - u * per;
+            tile = ((x + 8 * u) * G + r / tn_all) * tn_all + r % tn_all;
+        }
+        gemm_tile<NW, A0, B0, TMX>(L, L.d[0], tile, red);
         return;
     }
     int r = b - L.d[0].tiles;
@@ -662,6 +672,9 @@ static hipError_t launch_gemm(GemmLaunch& L, bool loss_wg, hipStream_t stream) {
     blocks += L.adam_blocks;
     if (!loss_wg) L.loss_out = nullptr;
     ++L.slot;
+    // XCD order needs whole groups of 8 64-row bands (a bijection of the tiles)
+    const int tiles_m0 = L.d[0].tiles / L.d[0].tiles_n;
+    L.xcd = L.xcd && (tiles_m0 % (8 * (2 / TMX)) == 0);
     if constexpr (TMX == 2) {   // chosen only for long K (launch_train_grads): 16 waves
         if (kmax < 256) return hipErrorInvalidValue;
         hipLaunchKernelGGL((train_gemm_kernel<16, A0, B0, A1, B1, TMX>), dim3(blocks), dim3(64 * 16), 0, stream, L);
@@ -731,6 +744,7 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
 
     GemmLaunch G{};
     G.idx = idx; G.gs = w.states; G.ga = w.actions; G.gns = w.next_states; G.grw = w.rewards;
+    const int xcd_opt = t.xcd;
     G.H = t.H; G.s = t.s; G.a = t.a;
     G.xstore = B.xbuf;
     G.slot = -1;
@@ -762,6 +776,7 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
             G.adam_count = 0;
             for (int i = 0; i < prior_n; ++i) G.adam_t[G.adam_count++] = prior[i];
         }
+        G.xcd = xcd_opt;
         e = l == 0 ? launch_gemm<OP_GATHER, OP_DIRECT>(G, false, stream) : launch_gemm<OP_DIRECT, OP_DIRECT>(G, false, stream);
         G.zero_words = nullptr;
         G.adam_count = 0;
@@ -781,6 +796,7 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
         O.s = t.s; O.loss_part = B.loss_part; O.colsum_out = B.cs_dy;
         finish(D, R, J, W);
         G.nd = 1;
+        G.xcd = xcd_opt;
         if ((e = launch_gemm<OP_DIRECT, OP_DIRECT>(G, false, stream)) != hipSuccess) return e;
     }
     const int loss_parts = G.d[0].tiles;
@@ -848,6 +864,7 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
         }
         G.loss_part = B.loss_part; G.loss_parts = loss_parts; G.loss_out = loss_out;
         const bool loss_wg = l == l_end && loss_out != nullptr;
+        G.xcd = xcd_opt;
         e = l == 0    ? launch_gemm<OP_TRANS, OP_TRANS>(G, loss_wg, stream)
             : tmx == 2 ? launch_gemm<OP_DIRECT, OP_TRANS, OP_TRANS, OP_TRANS, 2>(G, loss_wg, stream)
                        : launch_gemm<OP_DIRECT, OP_TRANS, OP_TRANS, OP_TRANS>(G, loss_wg, stream);

@@ -37,7 +37,8 @@ PRECISIONS = {"f32": MBRL_PRECISION_F32, "f16x3": MBRL_PRECISION_F16X3, "f16x6":
 OPTIONS = {"rollout_tile": 0, "split_tile": 1, "debug_traj_abort": 2, "gd_single": 3, "debug_gd_abort": 4,
            "unfused_update": 5, "adam_arith": 6, "xcd_map": 7, "train_tile": 8, "train_no_fold": 9,
            "rollout_pair": 10, "shard_emulate": 11, "debug_pair_abort": 12,
-           "traj_hop": 13, "gd_hop": 14, "pair_l2": 15}
+           "traj_hop": 13, "gd_hop": 14, "pair_l2": 15,
+           "train_xcd": 16}
 
 
 def precision_code(name):
