@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MBRL_ABI_VERSION 9
+#define MBRL_ABI_VERSION 10
 
 typedef struct ihipStream_t* mbrl_stream_t; /* == hipStream_t */
 typedef struct ihipEvent_t* mbrl_event_t;   /* == hipEvent_t  */
@@ -170,7 +170,9 @@ enum {
     MBRL_OPT_PAIR_L2 = 15,          /* column-split pair hand-offs: 0 / 1 L2-resident when both halves share an
                                        XCD (roll call), 2 always written through (A/B; same results)     */
     MBRL_OPT_TRAIN_XCD = 16,        /* training launches: 1 row bands in XCD order (A/B; same bits)           */
-    MBRL_OPT_COUNT = 17
+    MBRL_OPT_TRAIN_SPLIT = 17,      /* 1: two-hidden-layer training in the five-launch layout instead of the
+                                       fused three-launch step (A/B, tests; same bits)                    */
+    MBRL_OPT_COUNT = 18
 };
 int mbrl_set_option(int32_t option, int32_t value);
 int mbrl_get_option(int32_t option);
@@ -399,6 +401,12 @@ typedef struct {
 } mbrl_train_data;
 
 size_t mbrl_train_workspace_bytes(const mbrl_train_model* model, int32_t batch);
+/* Byte offset in the workspace of a 32-bit status word the fused training step (two hidden layers)
+ * sets bit 0 of if one of its bounded in-launch waits timed out -- a workgroup-dispatch order the
+ * kernels rely on was not kept and an Adam step may have raced a read of its weights. Never expected;
+ * the word is sticky (the caller zeroes the workspace once and reads the word after training).
+ * (size_t)-1 for a bad shape. */
+size_t mbrl_train_status_offset(const mbrl_train_model* model, int32_t batch);
 int mbrl_train_grads(const mbrl_train_model* model, const mbrl_train_data* data, const int64_t* batch_idx,
                      int32_t batch, float* loss_out, void* workspace, size_t ws_bytes, mbrl_stream_t stream);
 

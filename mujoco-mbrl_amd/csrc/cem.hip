@@ -1598,6 +1598,7 @@ static int train_shape(const mbrl_train_model* m, TrainShape* t) {
     t->tile = g_opt[MBRL_OPT_TRAIN_TILE].load(std::memory_order_relaxed);
     t->fold = g_opt[MBRL_OPT_TRAIN_NO_FOLD].load(std::memory_order_relaxed) == 0 ? 1 : 0;
     t->xcd = g_opt[MBRL_OPT_TRAIN_XCD].load(std::memory_order_relaxed) == 1 ? 1 : 0;
+    t->split = g_opt[MBRL_OPT_TRAIN_SPLIT].load(std::memory_order_relaxed) == 1 ? 1 : 0;
     return MBRL_OK;
 }
 
@@ -1605,6 +1606,12 @@ size_t mbrl_train_workspace_bytes(const mbrl_train_model* model, int32_t batch) 
     TrainShape t;
     if (batch < 1 || train_shape(model, &t) != MBRL_OK) return 0;
     return train_ws_floats(t, batch) * sizeof(float);
+}
+
+size_t mbrl_train_status_offset(const mbrl_train_model* model, int32_t batch) {
+    TrainShape t;
+    if (batch < 1 || train_shape(model, &t) != MBRL_OK) return (size_t)-1;
+    return train_status_offset(t, batch);
 }
 
 int mbrl_train_grads(const mbrl_train_model* model, const mbrl_train_data* data, const int64_t* batch_idx,

@@ -386,6 +386,7 @@ struct TrainShape {
     int tile;                    // backward C tile height: 0 auto, 32, 64 (MBRL_OPT_TRAIN_TILE; same bits)
     int fold;                    // 1: the layer-0 weight gradient folds into the dH_0 launch (same bits)
     int xcd;                     // 1: row-band tiles in XCD order in every launch (MBRL_OPT_TRAIN_XCD; same bits)
+    int split;                   // 1: the five-launch layout where the fused step applies (MBRL_OPT_TRAIN_SPLIT; same bits)
 };
 struct TrainTensors {
     const float* const* weight;  // L + 1 (+ 1 reward head) nn.Linear weights [out][in]
@@ -395,6 +396,7 @@ struct TrainTensors {
     const float *states, *actions, *next_states, *rewards;   // stacked transitions [T][H][.]
 };
 size_t train_ws_floats(const TrainShape& t, int batch);
+size_t train_status_offset(const TrainShape& t, int batch);   // bytes: the fused step's status word
 // adam (optional): the step of every layer's weight and bias (linear1.weight, linear1.bias, ...)
 // folded into the backward launches, bit-identical to a separate mbrl_adam_step after the gradient.
 // With the layer-0 fold one layer's step cannot ride in this step's launches: it comes back in

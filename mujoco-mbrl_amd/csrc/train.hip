@@ -198,6 +198,13 @@ struct Output {
     int adam;                 // EPI_GRAD: also take this layer's Adam step in place (nothing reads it
                               // in this launch): weight at aw (= c0 layout), bias at ab
     mbrl_adam_tensor aw, ab;
+    // EPI_GRAD with adam, fused step: this launch's dH tiles read the weight block being stepped; the
+    // tile waits until wait_ticket[n0 / 32] (their arrivals per column block) reaches wait_count.
+    // Those tiles have lower workgroup ids, so they were dispatched first and always finish; the
+    // bounded spin only guards against a hang (bit 0 of wait_status on timeout).
+    const unsigned* wait_ticket;
+    unsigned wait_count;
+    unsigned* wait_status;
     // EPI_MASK of dH_0 with fold (launch_train_grads): the tile also yields the layer-0 weight
     // gradient's partial over each of its 32-row blocks -- exactly what wave tr of the separate dW_0
     // launch summed -- into fold_part[tr][W][K0]; the last of a column block's tiles to finish (a
@@ -302,6 +309,24 @@ __device__ __forceinline__ void stash_input(const GemmLaunch& L, const GemmDesc&
 template <int NW, int TMX>
 __device__ void fold_dw0(const GemmLaunch& L, const GemmDesc& D, int tm, int n0, float (*red)[TT * TMX][TT + 1]);
 
+// One lane polls an arrival counter (sc1 loads) until it reaches `need`, then the workgroup goes on.
+// Used only where the awaited workgroups have lower ids than the waiter (dispatched before it), so the
+// wait always ends; the 1 s bound (s_memrealtime, 100 MHz) turns a broken assumption into bit 0 of
+// *status instead of a hang.
+__device__ __forceinline__ void wait_arrivals(const unsigned* counter, unsigned need, unsigned* status) {
+    if (threadIdx.x == 0) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {
+                if (status) atomicOr(status, 1u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    __syncthreads();
+}
+
 // TMX = 1: 32 x 32 C tiles; TMX = 2: 64 x 32 (the W x W backward products, so that a launch's tiles
 // fit one round of the CUs). Each element's K order is the same for both (the K split over the waves
 // depends on K and NW only), so the tile height never changes a bit of the result.
@@ -378,6 +403,9 @@ __device__ void gemm_tile(const GemmLaunch& L, const GemmDesc& D, int tile, floa
 #pragma unroll
             for (int v = 0; v < 4; ++v) red[wave][16 * x + 4 * q + v][16 * y + c] = acc[x][y][v];
     __syncthreads();
+
+    if (O.mode == EPI_GRAD && O.adam && O.wait_ticket)
+        wait_arrivals(O.wait_ticket + n0 / TT, O.wait_count, O.wait_status);
 
     // the fused epilogue, EPT C elements per thread; each element sums the waves' partials in wave
     // order. Elements of this tile that feed the next layer's bias gradient (EPI_MASK, EPI_LOSS)
@@ -630,6 +658,397 @@ __global__ __launch_bounds__(64 * NW) void train_gemm_kernel(const GemmLaunch L)
     }
 }
 
+// ================================================================================================
+// The fused step for two hidden layers (the reference's Model / ModelWithReward, models.py:97-132):
+// three launches per batch instead of five. Every product is the same MFMA chains over the same K
+// ranges as in the five-launch layout, and every sum of partials runs in the same order, so the
+// gradients, losses and Adam steps are the same floats (tests/test_gpu_train_native.py pins it):
+//   F  train_fused_fwd_kernel: per 32 x 32 tile of H_1, the tile's 32 rows of H_0 are recomputed into
+//      LDS (K0 = s + a is small: the layer-0 launch's 4-wave K split, summed in its wave order), then
+//      the H_1 tile is the layer-1 launch's tile with its A operand from LDS. Removes a launch and
+//      the H_0 round trip through memory before the layer-1 products.
+//   O  train_fused_out_kernel: per 32 x 32 tile of dH_1, the tile's 32 rows of dY (the output-layer
+//      launch's tile: loss partials and dY column sums from the first column tile), dH_1 =
+//      (dY W_out) * (H_1 > 0), and the output layer's weight-gradient partial over the tile's 32 rows
+//      -- exactly wave tm of the separate dW_out product -- summed in wave order by the column block's
+//      last arriver (the dW_0 fold's hand-off). Removes a launch and the dY round trip.
+//   B  launch_gemm: dH_0 with the folded dW_0 and its Adam step, dW_1 -- whose tiles step W_1 in place
+//      once the dH_0 tiles of their column block have read it -- and the output layer's Adam step as
+//      extra workgroups. No Adam step is deferred to the next batch.
+constexpr int FUSED_WMAX = 512;    // H_0 rows of the tile in LDS: 32 x (W + 4) floats
+constexpr int FUSED_K0MAX = 64;    // s + a: one 16-deep chunk per wave of the layer-0 launch's split
+
+struct FusedArgs {
+    const int64_t* idx;
+    const float *gs, *ga, *gns, *grw;   // stacked transitions (GemmLaunch's meaning)
+    int H, s, a;
+    int R, W, K0, J, tiles_n, tiles_r;
+    int nw0;                            // waves of the separate layer-0 launch (its K split)
+    int nwb;                            // waves of the separate backward launches (K = R): the dH_1 split
+    const float *w0, *b0, *w1, *b1;
+    const float *wo, *wo_r, *bo, *bo_r; // output layer: state rows from wo / bo, the reward row from *_r
+    float *act0, *act1, *xstore;
+    float *dh1, *cs_dh1, *cs_dy, *loss_part, *out_part;
+    float *dwo, *dwo_r, *dbo, *dbo_r;
+    unsigned* out_ticket;               // [tiles_n] arrivals per column block of dH_1 tiles (O)
+    unsigned* zero_words;               // F's workgroup 0 zeroes zero_n words (both folds' tickets)
+    int zero_n;
+    float scale_s, scale_r, inv_s, inv_r;
+};
+
+// A wave's K range in a launch of nw waves (gemm_tile's split: contiguous 16-deep chunks).
+__device__ __forceinline__ void wave_k_range(int K, int nw, int w, int& kb0, int& kb1) {
+    const int chunks = (K + 15) >> 4, per = (chunks + nw - 1) / nw;
+    kb0 = w * per * 16;
+    kb1 = min(K, (w + 1) * per * 16);
+}
+
+// Four consecutive k of one row of a row-major matrix (row stride ld), zero past K or for an absent
+// row: load_operand<OP_DIRECT>'s values (float4 when aligned, else element by element).
+__device__ __forceinline__ f32x4 row4(const float* row, bool valid, int k0, int K, bool vec) {
+    f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (!valid) return v;
+    if (vec && k0 + 3 < K) return *reinterpret_cast<const f32x4*>(row + k0);
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+        if (k0 + e < K) v[e] = row[k0 + e];
+    return v;
+}
+
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void train_fused_fwd_kernel(const FusedArgs F) {
+    constexpr int NT = 64 * NW, EPT = TT * TT / NT, MAXPER = NW == 16 ? 2 : 4;
+    constexpr int HLD = FUSED_WMAX + 4, XLD = FUSED_K0MAX + 4;
+    __shared__ float red[NW][TT][TT + 1];
+    __shared__ __attribute__((aligned(16))) float h0[TT][HLD];
+    __shared__ __attribute__((aligned(16))) float xr[TT][XLD];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, q = lane >> 4, c = lane & 15;
+    const int tm = blockIdx.x / F.tiles_n, tn = blockIdx.x - tm * F.tiles_n, m0 = tm * TT, n0 = tn * TT;
+    const int W = F.W, K0 = F.K0, R = F.R;
+    if (blockIdx.x == 0 && F.zero_words)
+        for (int i = tid; i < F.zero_n; i += NT) F.zero_words[i] = 0u;
+    // the layer-1 operands first (this wave's K range of W_1's rows n0..n0+31, and the bias): their
+    // latency overlaps the gather and the H_0 recompute
+    int kb0, kb1;
+    wave_k_range(W, NW, wave, kb0, kb1);
+    const bool vec1 = (W % 4 == 0) && (reinterpret_cast<uintptr_t>(F.w1) & 15) == 0;
+    f32x4 bw[MAXPER][2];
+#pragma unroll
+    for (int u = 0; u < MAXPER; ++u)
+#pragma unroll
+        for (int y = 0; y < 2; ++y) {
+            const int n = n0 + 16 * y + c, kb = kb0 + 16 * u;
+            bw[u][y] = row4(F.w1 + (int64_t)min(n, W - 1) * W, n < W && kb < kb1, kb + 4 * q, W, vec1);
+        }
+    float pre[EPT];
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+        const int e = tid + j * NT, n = n0 + (e & 31);
+        pre[j] = n < W ? F.b1[n] : 0.0f;
+    }
+    // the batch's 32 input rows, gathered through the row indices (zero past K0 to the chunk end);
+    // the first column tile keeps them for the layer-0 weight gradient, as the layer-0 launch did
+    const int k0pad = (K0 + 15) & ~15;
+    for (int e = tid; e < TT * k0pad; e += NT) {
+        const int r = e / k0pad, k = e - r * k0pad, m = m0 + r;
+        float v = 0.0f;
+        if (m < R && k < K0) {
+            const int64_t src = F.idx[m / F.H] * F.H + m % F.H;
+            v = k < F.s ? F.gs[src * F.s + k] : F.ga[src * F.a + (k - F.s)];
+            if (tn == 0) F.xstore[(int64_t)m * K0 + k] = v;
+        }
+        xr[r][k] = v;
+    }
+    __syncthreads();
+    // H_0 rows m0..m0+31, all W columns: wave w takes the 16-column blocks y = w, w + NW, ...; each
+    // 16 x 16 block is the sum, in wave order, of the layer-0 launch's per-wave chains (nw0 waves,
+    // empty ones adding +0), then bias and ReLU -- that launch's epilogue
+    const int ny = (W + 15) >> 4;
+    const bool vec0 = (K0 % 4 == 0) && (reinterpret_cast<uintptr_t>(F.w0) & 15) == 0;
+    for (int y = wave; y < ny; y += NW) {
+        const int n = 16 * y + c;
+        f32x4 tot[2];
+        for (int vw = 0; vw < F.nw0; ++vw) {
+            int a0, a1;
+            wave_k_range(K0, F.nw0, vw, a0, a1);
+            f32x4 p[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
+            for (int kb = a0; kb < a1; kb += 16) {
+                const f32x4 b = row4(F.w0 + (int64_t)min(n, W - 1) * K0, n < W, kb + 4 * q, K0, vec0);
+                f32x4 a[2];
+#pragma unroll
+                for (int x = 0; x < 2; ++x) a[x] = *reinterpret_cast<const f32x4*>(&xr[16 * x + c][kb + 4 * q]);
+#pragma unroll
+                for (int s = 0; s < 4; ++s)
+#pragma unroll
+                    for (int x = 0; x < 2; ++x) p[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[x][s], b[s], p[x], 0, 0, 0);
+            }
+#pragma unroll
+            for (int x = 0; x < 2; ++x) tot[x] = vw == 0 ? p[x] : tot[x] + p[x];
+        }
+        const float bias = n < W ? F.b0[n] : 0.0f;
+#pragma unroll
+        for (int x = 0; x < 2; ++x)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const int row = 16 * x + 4 * q + v;
+                float h = tot[x][v] + bias;
+                h = h > 0.0f ? h : 0.0f;
+                h0[row][n] = (n < W && m0 + row < R) ? h : 0.0f;
+            }
+    }
+    __syncthreads();
+    // this tile's columns of H_0 (every element stored by exactly one workgroup)
+    for (int e = tid; e < TT * TT; e += NT) {
+        const int r = e >> 5, col = e & 31, m = m0 + r, n = n0 + col;
+        if (m < R && n < W) F.act0[(int64_t)m * W + n] = h0[r][n];
+    }
+    // the H_1 tile: the layer-1 launch's chains with the A operand from LDS
+    f32x4 acc[2][2];
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y) acc[x][y] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int u = 0; u < MAXPER; ++u) {
+        const int kb = kb0 + 16 * u;
+        if (kb >= kb1) break;
+        f32x4 a[2];
+#pragma unroll
+        for (int x = 0; x < 2; ++x) a[x] = *reinterpret_cast<const f32x4*>(&h0[16 * x + c][kb + 4 * q]);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int x = 0; x < 2; ++x)
+#pragma unroll
+                for (int y = 0; y < 2; ++y)
+                    acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[x][s], bw[u][y][s], acc[x][y], 0, 0, 0);
+    }
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) red[wave][16 * x + 4 * q + v][16 * y + c] = acc[x][y][v];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+        const int e = tid + j * NT, row = e >> 5, col = e & 31, m = m0 + row, n = n0 + col;
+        if (m >= R || n >= W) continue;
+        float v = red[0][row][col];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) v = v + red[w][row][col];
+        v = v + pre[j];
+        F.act1[(int64_t)m * W + n] = v > 0.0f ? v : 0.0f;
+    }
+}
+
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void train_fused_out_kernel(const FusedArgs F) {
+    constexpr int NT = 64 * NW, EPT = TT * TT / NT, MAXPER = NW == 16 ? 2 : 4;
+    __shared__ float red[NW][TT][TT + 1];
+    __shared__ float dy[TT][TT + 1];    // the tile's 32 rows of dY (columns past J zero)
+    __shared__ float hm[TT][TT + 1];    // H_1 of the tile: the ReLU mask and the dW_out operand
+    __shared__ unsigned last;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, q = lane >> 4, c = lane & 15;
+    const int tm = blockIdx.x / F.tiles_n, tn = blockIdx.x - tm * F.tiles_n, m0 = tm * TT, n0 = tn * TT;
+    const int W = F.W, J = F.J, R = F.R, S = F.s;
+    // ---- the output-layer tile (tm, 0): Y = H_1 W_out^T + b_out over this wave's K range
+    int kb0, kb1;
+    wave_k_range(W, NW, wave, kb0, kb1);
+    const bool veca = (W % 4 == 0) && (reinterpret_cast<uintptr_t>(F.act1) & 15) == 0;
+    const bool vecb = (W % 4 == 0) && ((reinterpret_cast<uintptr_t>(F.wo) | reinterpret_cast<uintptr_t>(F.wo_r)) & 15) == 0;
+    f32x4 av[MAXPER][2], bv[MAXPER][2];
+#pragma unroll
+    for (int u = 0; u < MAXPER; ++u) {
+        const int kb = kb0 + 16 * u;
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+            const int m = m0 + 16 * x + c;
+            av[u][x] = row4(F.act1 + (int64_t)min(m, R - 1) * W, m < R && kb < kb1, kb + 4 * q, W, veca);
+        }
+#pragma unroll
+        for (int y = 0; y < 2; ++y) {
+            const int o = 16 * y + c;
+            const float* row = o < S ? F.wo + (int64_t)o * W : F.wo_r;
+            bv[u][y] = row4(row, o < J && kb < kb1, kb + 4 * q, W, vecb);
+        }
+    }
+    // the loss epilogue's y - t = acc - (t - bias), and the tile's H_1 block (mask, dW_out operand)
+    float pre[EPT];
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+        const int e = tid + j * NT, m = m0 + (e >> 5), o = e & 31;
+        pre[j] = 0.0f;
+        if (m >= R || o >= J) continue;
+        const int64_t src = F.idx[m / F.H] * F.H + m % F.H;
+        const float t = o < S ? F.gns[src * S + o] : F.grw[src];
+        pre[j] = t - (o < S ? F.bo[o] : F.bo_r[o - S]);
+    }
+    for (int e = tid; e < TT * TT; e += NT) {
+        const int r = e >> 5, col = e & 31, m = m0 + r, n = n0 + col;
+        hm[r][col] = (m < R && n < W) ? F.act1[(int64_t)m * W + n] : 0.0f;
+    }
+    f32x4 acc[2][2];
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y) acc[x][y] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int u = 0; u < MAXPER; ++u) {
+        if (kb0 + 16 * u >= kb1) break;
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int x = 0; x < 2; ++x)
+#pragma unroll
+                for (int y = 0; y < 2; ++y)
+                    acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u][x][s], bv[u][y][s], acc[x][y], 0, 0, 0);
+    }
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) red[wave][16 * x + 4 * q + v][16 * y + c] = acc[x][y][v];
+    __syncthreads();
+    // the output-layer launch's EPI_LOSS epilogue: dY = (Y - T) * 2 / numel, the loss terms
+    float loss_s = 0.0f, loss_r = 0.0f;
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+        const int e = tid + j * NT, row = e >> 5, col = e & 31, m = m0 + row;
+        float v = 0.0f;
+        if (m < R && col < J) {
+            v = red[0][row][col];
+#pragma unroll
+            for (int w = 1; w < NW; ++w) v = v + red[w][row][col];
+            const float d = v - pre[j];
+            if (col < S) loss_s = loss_s + d * d * F.inv_s;
+            else loss_r = loss_r + d * d * F.inv_r;
+            v = d * (col < S ? F.scale_s : F.scale_r);
+        }
+        dy[row][col] = v;
+    }
+    __syncthreads();
+    if (tn == 0) {
+        // dY's column sums over the tile's rows (db_out), read back by this launch's last arriver
+        if (tid < TT && tid < J) {
+            float t = dy[0][tid];
+            for (int r = 1; r < TT; ++r) t = t + dy[r][tid];
+            __hip_atomic_store(F.cs_dy + (int64_t)tm * J + tid, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            loss_s += __shfl_xor(loss_s, o);
+            loss_r += __shfl_xor(loss_r, o);
+        }
+        float* sl = &red[1][0][0];      // red[1] is free: every wave's partials were summed above
+        if (lane == 0) {
+            sl[2 * wave] = loss_s;
+            sl[2 * wave + 1] = loss_r;
+        }
+        __syncthreads();
+        if (tid < 2) {
+            float t = sl[tid];
+            for (int w = 1; w < NW; ++w) t = t + sl[2 * w + tid];
+            F.loss_part[tm * 2 + tid] = t;
+        }
+    }
+    // ---- tasks 0-3: the dH_1 tile, K = J (the [dH_1 + dW_out] launch's split over nwb waves: one
+    // 16-deep chunk per wave, the rest adding +0), masked by H_1 > 0. Tasks 4-7: the dW_out partial
+    // over rows m0..m0+31 (that launch's wave tm: its two 16-row chunks, M = J, N = this column block)
+    for (int task = wave; task < 8; task += NW) {   // (4 waves: each takes one block of both)
+      if (task < 4) {
+        const int x = task >> 1, y = task & 1, n = n0 + 16 * y + c;
+        f32x4 tot = {0.0f, 0.0f, 0.0f, 0.0f};
+        const int nch = (J + 15) >> 4;
+        for (int ch = 0; ch < nch; ++ch) {
+            f32x4 a, b, p = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int k = 16 * ch + 4 * q + s;     // an output unit o
+                a[s] = dy[16 * x + c][k];
+                b[s] = (k < J && n < W) ? (k < S ? F.wo[(int64_t)k * W + n] : F.wo_r[(int64_t)(k - S) * W + n]) : 0.0f;
+            }
+#pragma unroll
+            for (int s = 0; s < 4; ++s) p = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], p, 0, 0, 0);
+            tot = ch == 0 ? p : tot + p;
+        }
+        for (int w = nch; w < F.nwb; ++w) tot = tot + f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const int row = 16 * x + 4 * q + v, m = m0 + row;
+            const float g = hm[row][16 * y + c] > 0.0f ? tot[v] : 0.0f;
+            const float keep = (m < R && n < W) ? g : 0.0f;
+            if (m < R && n < W) F.dh1[(int64_t)m * W + n] = g;
+            red[0][row][16 * y + c] = keep;
+        }
+      } else {
+        const int x = (task - 4) >> 1, y = (task - 4) & 1;
+        f32x4 p = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            f32x4 a, b;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int r = 16 * u + 4 * q + s;      // a row of the batch tile (K of this product)
+                a[s] = dy[r][16 * x + c];
+                b[s] = hm[r][16 * y + c];
+            }
+#pragma unroll
+            for (int s = 0; s < 4; ++s) p = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], p, 0, 0, 0);
+        }
+        const int i = n0 + 16 * y + c;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const int o = 16 * x + 4 * q + v;
+            if (o < J && i < W)    // sc1 (write-through) stores, read back by the last arriver
+                __hip_atomic_store(F.out_part + ((int64_t)tm * J + o) * W + i, p[v], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // dH_1's column sums over the tile's 32 rows (the next launch's db_1), in row order
+    if (tid < TT && n0 + tid < W) {
+        float t = red[0][0][tid];
+        for (int r = 1; r < TT; ++r) t = t + red[0][r][tid];
+        F.cs_dh1[(int64_t)tm * W + n0 + tid] = t;
+    }
+    // the column block's last arriver sums the dW_out partials in wave order (row tiles past the
+    // batch: the empty waves' +0), and the first column block's also db_out from dY's column sums
+    if (tid == 0) {
+        const unsigned t = __hip_atomic_fetch_add(&F.out_ticket[tn], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = (t + 1 == (unsigned)F.tiles_r) ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!last) return;
+    for (int e = tid; e < J * TT; e += NT) {
+        const int o = e / TT, i = n0 + (e - o * TT);
+        if (i >= W) continue;
+        float p[16];
+#pragma unroll
+        for (int w = 0; w < 16; ++w)
+            p[w] = (w < F.tiles_r && w < F.nwb)
+                       ? __hip_atomic_load(F.out_part + ((int64_t)w * J + o) * W + i, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT)
+                       : 0.0f;
+        float v = p[0];
+#pragma unroll
+        for (int w = 1; w < 16; ++w)
+            if (w < F.nwb) v = v + p[w];
+        if (o < S) F.dwo[(int64_t)o * W + i] = v;
+        else F.dwo_r[(int64_t)(o - S) * W + i] = v;
+    }
+    if (tn == 0 && tid < J) {
+        float g = __hip_atomic_load(F.cs_dy + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int i = 1; i < F.tiles_r; ++i)
+            g = g + __hip_atomic_load(F.cs_dy + (int64_t)i * J + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid < S) F.dbo[tid] = g;
+        else F.dbo_r[tid - S] = g;
+    }
+}
+
 static Operand direct(const float* p0, const float* p1, int split, int ld, int rows) {
     Operand o{};
     o.p0 = p0; o.p1 = p1 ? p1 : p0; o.split = p1 ? split : rows; o.ld = ld; o.kind = OP_DIRECT; o.rows = rows;
@@ -692,7 +1111,9 @@ static hipError_t launch_gemm(GemmLaunch& L, bool loss_wg, hipStream_t stream) {
 struct TrainWs {
     float* act[MBRL_TRAIN_MAX_LAYERS];
     float *dh[2], *dy, *loss_part, *xbuf, *cs_dy, *cs_dh[2], *fold_part;
-    unsigned* tickets;
+    float* out_part;      // fused step: the output layer's weight-gradient partials [row tile][J][W]
+    unsigned* tickets;    // [ceil(W / 32)] the dW_0 fold's, then [ceil(W / 32)] the fused dW_out fold's
+    unsigned* status;     // fused step: bit 0 = a bounded wait timed out (never expected)
     size_t floats;
 };
 
@@ -713,12 +1134,19 @@ static TrainWs train_ws(const TrainShape& t, int batch, float* base) {
     w.cs_dh[0] = take(tiles_r * W);
     w.cs_dh[1] = take(tiles_r * W);
     w.fold_part = take(tiles_r * W * (size_t)(t.s + t.a));   // the folded dW_0's per-32-row partials
-    w.tickets = reinterpret_cast<unsigned*>(take((W + TT - 1) / TT));
+    w.out_part = take(tiles_r * J * W);
+    w.tickets = reinterpret_cast<unsigned*>(take(2 * ((W + TT - 1) / TT)));
+    w.status = reinterpret_cast<unsigned*>(take(1));
     w.floats = off;
     return w;
 }
 
 size_t train_ws_floats(const TrainShape& t, int batch) { return train_ws(t, batch, nullptr).floats; }
+
+size_t train_status_offset(const TrainShape& t, int batch) {
+    float* base = reinterpret_cast<float*>(static_cast<uintptr_t>(64));   // any aligned base: offsets only
+    return (size_t)(reinterpret_cast<char*>(train_ws(t, batch, base).status) - reinterpret_cast<char*>(base));
+}
 
 // Whether the layer-0 weight gradient folds into the dH_0 launch bit-identically: its separate launch
 // (M = W, K = R) gives each of its waves one 32-row block of the batch (16 waves at R >= 256, else 4).
@@ -726,6 +1154,14 @@ static int fold_waves(const TrainShape& t, int R) {
     if (t.fold == 0 || t.L < 1) return 0;
     const int nw = R >= 256 ? 16 : 4, chunks = (R + 15) / 16, per = (chunks + nw - 1) / nw;
     return per == 2 ? nw : 0;
+}
+
+// Whether the fused three-launch step applies (train_fused_*_kernel): two hidden layers, the dW_0
+// fold (its 32-row waves are also the dW_out partials' row tiles), dY within one 32-column tile, the
+// layer-0 input within one chunk per wave of its launch, H_0's tile rows within LDS.
+static bool fused_step(const TrainShape& t, int fold_nw) {
+    const int J = t.s + (t.reward ? 1 : 0), K0 = t.s + t.a;
+    return t.split == 0 && t.L == 2 && fold_nw > 0 && J <= TT && K0 <= FUSED_K0MAX && t.W <= FUSED_WMAX;
 }
 
 hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const int64_t* idx, int batch,
@@ -753,8 +1189,40 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
         G.arith = arith;
     }
     hipError_t e;
+    const bool fused = fused_step(t, fold_nw);
+    const int tiles_n = (W + TT - 1) / TT;
+    if (fused) {   // F and O (train_fused_*_kernel); the backward launch below is B
+        // a step the five-launch layout deferred (a smaller batch before this one): F reads W_1
+        if (prior_n > 0 && (e = launch_adam_step(prior, prior_n, *hp, arith, stream)) != hipSuccess) return e;
+        FusedArgs F{};
+        F.idx = idx; F.gs = w.states; F.ga = w.actions; F.gns = w.next_states; F.grw = w.rewards;
+        F.H = t.H; F.s = t.s; F.a = t.a;
+        F.R = R; F.W = W; F.K0 = K0; F.J = J; F.tiles_n = tiles_n; F.tiles_r = tiles_r;
+        F.nw0 = K0 >= 256 ? 16 : 4;
+        F.nwb = fold_nw;
+        F.w0 = w.weight[0]; F.b0 = w.bias[0]; F.w1 = w.weight[1]; F.b1 = w.bias[1];
+        F.wo = w.weight[L]; F.wo_r = wo_r; F.bo = w.bias[L]; F.bo_r = bo_r;
+        F.act0 = B.act[0]; F.act1 = B.act[1]; F.xstore = B.xbuf;
+        F.dh1 = B.dh[1]; F.cs_dh1 = B.cs_dh[1]; F.cs_dy = B.cs_dy; F.loss_part = B.loss_part;
+        F.out_part = B.out_part;
+        F.dwo = w.weight_grad[L]; F.dwo_r = t.reward ? w.weight_grad[L + 1] : w.weight_grad[L];
+        F.dbo = w.bias_grad[L]; F.dbo_r = t.reward ? w.bias_grad[L + 1] : w.bias_grad[L];
+        F.out_ticket = B.tickets + tiles_n;
+        F.zero_words = B.tickets; F.zero_n = 2 * tiles_n;
+        F.scale_s = 2.0f / (float)((int64_t)batch * t.s); F.scale_r = 2.0f / (float)batch;
+        F.inv_s = 1.0f / (float)((int64_t)batch * t.s); F.inv_r = 1.0f / (float)batch;
+        const dim3 grid(tiles_r * tiles_n);
+        if (W >= 256) {   // the wave count of the separate launches whose K is W
+            hipLaunchKernelGGL(train_fused_fwd_kernel<16>, grid, dim3(64 * 16), 0, stream, F);
+            hipLaunchKernelGGL(train_fused_out_kernel<16>, grid, dim3(64 * 16), 0, stream, F);
+        } else {
+            hipLaunchKernelGGL(train_fused_fwd_kernel<4>, grid, dim3(64 * 4), 0, stream, F);
+            hipLaunchKernelGGL(train_fused_out_kernel<4>, grid, dim3(64 * 4), 0, stream, F);
+        }
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     // forward through the hidden layers
-    for (int l = 0; l < L; ++l) {
+    for (int l = 0; l < (fused ? 0 : L); ++l) {
         GemmDesc& D = G.d[0];
         D = GemmDesc{};
         if (l == 0) {
@@ -783,7 +1251,7 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
         if (e != hipSuccess) return e;
     }
     // output layer (state head, reward head) + the loss gradient dY and its column sums
-    {
+    if (!fused) {
         GemmDesc& D = G.d[0];
         D = GemmDesc{};
         D.A = direct(B.act[L - 1], nullptr, 0, W, R);
@@ -799,11 +1267,11 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
         G.xcd = xcd_opt;
         if ((e = launch_gemm<OP_DIRECT, OP_DIRECT>(G, false, stream)) != hipSuccess) return e;
     }
-    const int loss_parts = G.d[0].tiles;
+    const int loss_parts = fused ? tiles_r : G.d[0].tiles;
     // backward: layer l = L (output) .. 0; launch l: dH_{l-1} (l >= 1) and dW_l, db_l. With the fold
     // (fold_waves) launch 1 also finishes dW_0 / db_0 and launch 0 does not exist.
     const int l_end = fold_nw ? 1 : 0;
-    for (int l = L; l >= l_end; --l) {
+    for (int l = fused ? L - 1 : L; l >= l_end; --l) {
         const bool out_layer = l == L;
         const float* g_in = out_layer ? B.dy : B.dh[l % 2];   // dL/d(pre-activation of layer l), [R][n_out]
         const float* cs_in = out_layer ? B.cs_dy : B.cs_dh[l % 2];
@@ -855,6 +1323,15 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
             G.d[G.nd - 1].out.aw = adam[0];
             G.d[G.nd - 1].out.ab = adam[1];
         }
+        if (adam && fused && l == 1) {
+            // the dH_0 tiles of a column block read that block of W_1: the dW_1 tiles step it in place
+            // after those tiles' fold tickets (dH_0 tiles have the lower ids)
+            Output& O = G.d[G.nd - 1].out;
+            O.adam = 1; O.aw = adam[2]; O.ab = adam[3];
+            O.wait_ticket = B.tickets;
+            O.wait_count = (unsigned)((R + TT * tmx - 1) / (TT * tmx));
+            O.wait_status = B.status;
+        }
         // layer l + 1's gradient is complete (previous launch) and this launch does not read its
         // parameters: its Adam step rides along (with the reward head when l + 1 is the output layer)
         G.adam_count = 0;
@@ -870,7 +1347,7 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
                        : launch_gemm<OP_DIRECT, OP_TRANS, OP_TRANS, OP_TRANS>(G, loss_wg, stream);
         if (e != hipSuccess) return e;
     }
-    if (adam && fold_nw) {   // layer 1's step (launch 0's passenger before the fold): the next forward launch's
+    if (adam && fold_nw && !fused) {   // layer 1's step (launch 0's passenger before the fold): the next forward launch's
         const int n = (L == 1 && t.reward) ? 4 : 2;
         for (int i = 0; i < n; ++i) pending[i] = adam[2 + i];
         *pending_n = n;

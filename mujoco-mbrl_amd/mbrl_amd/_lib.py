@@ -26,7 +26,7 @@ MBRL_EHIP = -3
 MBRL_EWORKSPACE = -4
 MBRL_COST_GOAL_STATE = 0
 MBRL_COST_MODEL_REWARD = 1
-ABI_VERSION = 9
+ABI_VERSION = 10
 MBRL_NAN_LAST = 0
 MBRL_NAN_FIRST = 1
 MBRL_PRECISION_F32 = 0
@@ -38,7 +38,7 @@ OPTIONS = {"rollout_tile": 0, "split_tile": 1, "debug_traj_abort": 2, "gd_single
            "unfused_update": 5, "adam_arith": 6, "xcd_map": 7, "train_tile": 8, "train_no_fold": 9,
            "rollout_pair": 10, "shard_emulate": 11, "debug_pair_abort": 12,
            "traj_hop": 13, "gd_hop": 14, "pair_l2": 15,
-           "train_xcd": 16}
+           "train_xcd": 16, "train_split": 17}
 
 
 def precision_code(name):
@@ -57,7 +57,8 @@ EXPORTED = (
     "mbrl_refit_workspace_bytes", "mbrl_cem_refit", "mbrl_sample_actions",
     "mbrl_trajectory_workspace_bytes", "mbrl_trajectory", "mbrl_cem_workspace_bytes", "mbrl_cem_plan",
     "mbrl_cem_plan_batch_workspace_bytes", "mbrl_cem_plan_batch", "mbrl_gd_workspace_bytes", "mbrl_gd_plan",
-    "mbrl_cem_update", "mbrl_adam_step", "mbrl_train_workspace_bytes", "mbrl_train_grads",
+    "mbrl_cem_update", "mbrl_adam_step", "mbrl_train_workspace_bytes", "mbrl_train_status_offset",
+    "mbrl_train_grads",
     "mbrl_train_epoch", "mbrl_gd_batch_workspace_bytes", "mbrl_gd_plan_batch", "mbrl_host_alloc",
     "mbrl_host_free", "mbrl_comm_unique_id", "mbrl_comm_init", "mbrl_comm_destroy",
     "mbrl_cem_plan_sharded_workspace_bytes", "mbrl_cem_plan_sharded",
@@ -165,6 +166,7 @@ def load():
                                    c_float, c_float, P, P, P, c_size_t, P]),
         "mbrl_adam_step": (c_int32, [POINTER(AdamTensor), c_int32, POINTER(AdamHparams), P]),
         "mbrl_train_workspace_bytes": (c_size_t, [POINTER(TrainModel), c_int32]),
+        "mbrl_train_status_offset": (c_size_t, [POINTER(TrainModel), c_int32]),
         "mbrl_train_grads": (c_int32, [POINTER(TrainModel), POINTER(TrainData), P, c_int32, P, P, c_size_t, P]),
         "mbrl_train_epoch": (c_int32, [POINTER(TrainModel), POINTER(TrainData), P, c_int64, c_int32, POINTER(AdamTensor),
                                        c_int32, POINTER(AdamHparams), P, P, P, P, c_size_t, P]),

@@ -124,7 +124,9 @@ class _NativeGrads:
         need = self.lib.mbrl_train_workspace_bytes(ctypes.byref(m), int(batch_size))
         if need == 0:
             _lib.check(-1, "mbrl_train_workspace_bytes")
-        self.ws = torch.empty(need, dtype=torch.uint8, device=dev)
+        # zeroed once: the fused step's sticky status word lives in it (mbrl_train_status_offset)
+        self.ws = torch.zeros(need, dtype=torch.uint8, device=dev)
+        self.status_at = int(self.lib.mbrl_train_status_offset(ctypes.byref(m), int(batch_size)))
         self.loss = torch.zeros(3, dtype=torch.float32, device=dev)
         self.ptrs = [t.data_ptr() for t in self.params]
         self.dev = dev
@@ -187,6 +189,14 @@ class _NativeGrads:
                                                   self._lib.stream_handle(self.dev)), "mbrl_train_epoch")
         adam.epoch_done(self.params)
         return losses
+
+    def check_status(self):
+        """Raise if an in-launch wait of the fused step timed out (the workgroup dispatch order its
+        Adam placement relies on was not kept): the parameters may then be off. Never expected."""
+        word = int(self.ws[self.status_at:self.status_at + 4].view(torch.int32).item())
+        if word & 1:
+            raise RuntimeError("mbrl_amd: a fused training step's bounded wait timed out (status word "
+                               f"{word:#x}); the parameters of that step may be wrong")
 
     def run(self, idx):
         """The batch gradient for the rows `idx` (int64, on the device) into p.grad."""
@@ -282,6 +292,8 @@ def _train_loop_on(dev, model, dataset, optimizer, batch_size, num_epochs, step_
         for p in model.parameters():      # release the graph-pool grads; the eager path re-allocates
             p.grad = None
     # (the native path leaves the last batch's gradients in .grad, as the reference's loop does)
+    if native is not None:
+        native.check_status()
     model.train_iterations += 1
 
 

@@ -262,3 +262,47 @@ def test_layer0_gradient_fold_is_bitwise_neutral(kind, W, L, H, B):
     for (ka, ma, va), (kb, mb, vb) in zip(sa, sb):
         assert ka == kb and torch.equal(ma, mb) and torch.equal(va, vb)
     assert ra == rb and len(ra) > 0
+
+
+@pytest.mark.parametrize("kind,s,a,W,H,B", [("model", 17, 6, 512, 1, 512), ("reward", 17, 6, 512, 1, 512),
+                                           ("reward", 17, 6, 200, 1, 400), ("model", 17, 6, 50, 1, 512),
+                                           ("model", 24, 8, 333, 2, 150), ("model", 5, 1, 96, 1, 100),
+                                           ("reward", 31, 33, 256, 1, 300), ("model", 11, 2, 512, 3, 171)])
+def test_fused_step_is_bitwise_neutral(kind, s, a, W, H, B):
+    """Two hidden layers train in three launches (H_0 recomputed per H_1 tile, dY per dH_1 tile, the
+    output layer's weight gradient folded; W_1's Adam step in the dH_0 launch after the tiles that
+    read it) instead of five (MBRL_OPT_TRAIN_SPLIT = 1). The same chains in the same order: equal
+    gradients and losses from mbrl_train_grads, and equal parameters, optimizer state and losses
+    after three epochs of mbrl_train_epoch whose last batch is short (and takes the five-launch
+    path); the status word of the bounded in-launch waits stays clear."""
+    from mbrl_amd import _lib, models
+    ds = _dataset(s, a, H, 3 * B + 37, seed=W + s)
+    _, ins, outs = ds.stacked(DEV)
+    reward = kind == "reward"
+    idx = torch.randperm(ds.num_transitions(), generator=torch.Generator().manual_seed(B))[:B].to(DEV)
+    grads, trained = {}, {}
+    for split in (1, 0):
+        with _lib.option("train_split", split):
+            m = _model(kind, s, a, W, 2, seed=W)
+            nat = models._NativeGrads(m, ins, outs, ds.horizon, B, reward)
+            loss, parts = nat.run(idx)
+            torch.cuda.synchronize()
+            grads[split] = [loss.clone(), parts[0].clone(), parts[1].clone()] + [p.grad.clone() for p in m.parameters()]
+            nat.check_status()
+            m = _model(kind, s, a, W, 2, seed=W)
+            opt = torch.optim.Adam(m.parameters(), lr=1e-3, weight_decay=1e-4 if reward else 0.0)
+            w = _Writer()
+            np.random.seed(3)
+            m.train_model(ds, opt, batch_size=B, num_epochs=3, writer=w)
+            torch.cuda.synchronize()
+            trained[split] = ([p.detach().clone() for p in m.parameters()],
+                              [(float(st["step"]), st["exp_avg"].clone(), st["exp_avg_sq"].clone())
+                               for st in opt.state.values()], w.rows)
+    for i, (x, y) in enumerate(zip(grads[0], grads[1])):
+        assert torch.equal(x, y), (i, float((x - y).abs().max()))
+    (pa, sa, ra), (pb, sb, rb) = trained[0], trained[1]
+    for i, (x, y) in enumerate(zip(pa, pb)):
+        assert torch.equal(x, y), (i, float((x - y).abs().max()))
+    for (ka, ma, va), (kb, mb, vb) in zip(sa, sb):
+        assert ka == kb and torch.equal(ma, mb) and torch.equal(va, vb)
+    assert ra == rb and len(ra) > 0
