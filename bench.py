@@ -80,6 +80,8 @@ def parse():
                     help="HBM bytes per rollout launch from a rocprofv3 PMC pass (profiles/)")
     ap.add_argument("--no-strong", action="store_true",
                     help="skip the strong-scaling walker object (BASELINE.json configs[3])")
+    ap.add_argument("--no-train", action="store_true",
+                    help="skip the model-training object (SURVEY.md §8f rank 2)")
     return ap.parse_args()
 
 
@@ -294,6 +296,47 @@ def cpu_torch_baseline(prob, budget_s=20.0):
                 sample=f"{plans} CEM plan(s) (I={ITERATIONS}, N={n_sample}, H={H}): torch on the host, autograd on, "
                        f"the reference's _generate_trajectories loop + NumPy refit, {elapsed:.1f} s; "
                        f"value_no_grad: {plans_ng} plan(s) at N={n_ng} under torch.no_grad(), {el_ng:.1f} s")
+
+
+def train_line(dev, W=512, epochs=10):
+    """the reference's train_model (models.py:53-93; Adam, experiment.py:55-62)
+    for a 2 x W Model on 10k synthetic cheetah-shaped transitions (s = 17, a = 6), batch 512 -- on this
+    GPU through mbrl_train_epoch (csrc/train.hip: the fused three-launch step, Adam in its launches).
+    One warm-up epoch, then `epochs` timed between two events on the training stream (GPU-bound: one
+    host call per epoch). FLOP per step: forward 2R(K0 W + W^2 + W s), the same for the weight
+    gradients, 2R(W s + W^2) for the input gradients (R = 512 rows)."""
+    from mbrl_amd import data, models
+    rng = np.random.Generator(np.random.PCG64(5))
+    rolls = []
+    for _ in range(20):
+        st = rng.standard_normal((501, 17)).astype(np.float32)
+        rolls.append(data.Rollout(states=list(torch.from_numpy(st)), observations=list(torch.from_numpy(st)),
+                                  actions=list(torch.from_numpy(rng.uniform(-1, 1, (500, 6)).astype(np.float32))),
+                                  rewards=list(torch.from_numpy(rng.standard_normal(500).astype(np.float32)))))
+    ds = data.TransitionsDataset(rollouts=rolls)
+    ds.set_data_mode("state_only")
+    torch.manual_seed(0)
+    m = models.Model(17, 6, hidden_units=W).to(dev)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    np.random.seed(1)
+    m.train_model(ds, opt, batch_size=512, num_epochs=1)
+    torch.cuda.synchronize(dev)
+    np.random.seed(2)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record()
+    m.train_model(ds, opt, batch_size=512, num_epochs=epochs)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    steps = epochs * ((ds.num_transitions() + 511) // 512)
+    R, K0, s = 512, 23, 17
+    flop = 2 * (2 * R * (K0 * W + W * W + W * s)) + 2 * R * (W * s + W * W)
+    gpu_us = e0.elapsed_time(e1) * 1e3 / steps
+    return dict(workload=f"train_model Model(17, 6) 2x{W}, batch 512, Adam, 10k synthetic transitions "
+                         f"(SURVEY.md §8f rank 2)", steps_per_s=steps / wall, us_per_step=wall / steps * 1e6,
+                gpu_us_per_step=gpu_us, launches_per_step=3, flop_per_step=flop,
+                frac=flop / (gpu_us * 1e-6) / 1e12 / PEAK_FP32_MFMA_TFLOPS, epochs=epochs, steps=steps)
 
 
 def parity_sample(prob, res, n=256):
@@ -536,6 +579,8 @@ def main():
             plan_gpu_ms=timed.plan_gpu_ms if world > 1 else plan_gpu_ms,
             rollout_avg_launch_ms=h_rollout_s * 1e3,
             rollout_frac=h_flop / h_rollout_s / 1e12 / PEAK_FP32_MFMA_TFLOPS)
+    if rank == 0 and not args.no_train:
+        out["train"] = train_line(dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.config, budget_s=args.cpu_budget)
         out["cpu_baseline_torch"] = cpu_torch_baseline(prob, budget_s=args.cpu_budget)

@@ -152,12 +152,22 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 __device__ unsigned long long* g_train_stamps;
 #define TSTAMP(k)                                                                                    \
     do {                                                                                             \
-        if (g_train_stamps && threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1)) \
+        const unsigned probe_ = L.nd > 1 ? (unsigned)L.d[0].tiles : gridDim.x - 1;                 \
+        if (g_train_stamps && threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == probe_))        \
             g_train_stamps[L.slot * 8 + (blockIdx.x == 0 ? 0 : 4) + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+// the fused kernels: slot `slot_`, first workgroup and the last
+#define FSTAMP(slot_, k)                                                                             \
+    do {                                                                                             \
+        if (g_train_stamps && threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1)) \
+            g_train_stamps[(slot_) * 8 + (blockIdx.x == 0 ? 0 : 4) + (k)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 #else
 #define TSTAMP(k) \
     do {          \
+    } while (0)
+#define FSTAMP(slot_, k) \
+    do {                 \
     } while (0)
 #endif
 
@@ -165,6 +175,7 @@ enum { OP_DIRECT = 0, OP_TRANS = 1, OP_GATHER = 2 };
 enum { EPI_ACT = 0, EPI_LOSS = 1, EPI_MASK = 2, EPI_GRAD = 3 };
 constexpr int TT = 32;              // C tile edge
 constexpr int ADAM_FUSED_MAX = 4;   // tensors per fused Adam role (a layer's weight and bias, or both heads')
+constexpr int FOLD_K0MAX = 64;      // the dW_0 fold stages its tile's input rows in LDS up to this K0
 
 // Logical operand X(i, k), i < rows, k < K, over a row-major storage matrix S whose rows below
 // `split` live at p0 and the rest at p1 (the state and reward heads as one matrix).
@@ -193,6 +204,7 @@ struct Output {
     float* g0;                // EPI_GRAD: the bias gradient, g0[m] / g1[m - split], from colsum_in
     float* g1;
     const float* colsum_in;   // EPI_GRAD: [colsum_tiles][M] column sums of this layer's output gradient
+                              // (NULL: the bias gradient is finished elsewhere -- the fused step's O)
     int colsum_tiles;
     float* colsum_out;        // EPI_MASK / EPI_LOSS: [row tile][N] column sums of the stored C
     int adam;                 // EPI_GRAD: also take this layer's Adam step in place (nothing reads it
@@ -205,6 +217,8 @@ struct Output {
     const unsigned* wait_ticket;
     unsigned wait_count;
     unsigned* wait_status;
+    unsigned* arrive_ticket;  // EPI_MASK, fused step: one add per tile to [n0 / 32] once its K loop (every
+                              // read of the weight block) is done -- what wait_ticket counts
     // EPI_MASK of dH_0 with fold (launch_train_grads): the tile also yields the layer-0 weight
     // gradient's partial over each of its 32-row blocks -- exactly what wave tr of the separate dW_0
     // launch summed -- into fold_part[tr][W][K0]; the last of a column block's tiles to finish (a
@@ -306,8 +320,31 @@ __device__ __forceinline__ void stash_input(const GemmLaunch& L, const GemmDesc&
         if (m < D.M && k0 + e < D.K) L.xstore[(int64_t)m * D.K + k0 + e] = v[e];
 }
 
-template <int NW, int TMX>
-__device__ void fold_dw0(const GemmLaunch& L, const GemmDesc& D, int tm, int n0, float (*red)[TT * TMX][TT + 1]);
+template <int NW, int TMX, int DI>
+__device__ __forceinline__ void fold_dw0(const GemmLaunch& L, int tm, int n0, float (*red)[TT * TMX][TT + 1],
+                                         const float (*xs)[FOLD_K0MAX]);
+
+// p[0] + p[stride] + ... + p[(n - 1) stride], summed in index order like a plain loop, with the loads
+// of each 16 terms in flight together (a loop that loads one term per iteration pays the memory
+// latency n times: ~10 us for the 16 row tiles of a bias gradient). SC1: agent-scope (sc1) loads.
+template <bool SC1>
+__device__ __forceinline__ float ordered_sum(const float* p, int64_t stride, int n) {
+    float g = 0.0f;
+    for (int i0 = 0; i0 < n; i0 += 16) {
+        float t[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const float* a = p + (int64_t)(i0 + u) * stride;
+            t[u] = i0 + u >= n ? 0.0f
+                   : SC1       ? __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                               : *a;
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+            if (i0 + u < n) g = i0 + u == 0 ? t[u] : g + t[u];
+    }
+    return g;
+}
 
 // One lane polls an arrival counter (sc1 loads) until it reaches `need`, then the workgroup goes on.
 // Used only where the awaited workgroups have lower ids than the waiter (dispatched before it), so the
@@ -330,8 +367,13 @@ __device__ __forceinline__ void wait_arrivals(const unsigned* counter, unsigned 
 // TMX = 1: 32 x 32 C tiles; TMX = 2: 64 x 32 (the W x W backward products, so that a launch's tiles
 // fit one round of the CUs). Each element's K order is the same for both (the K split over the waves
 // depends on K and NW only), so the tile height never changes a bit of the result.
-template <int NW, int AK, int BK, int TMX>
-__device__ void gemm_tile(const GemmLaunch& L, const GemmDesc& D, int tile, float (*red)[TT * TMX][TT + 1]) {
+// DI: which of the launch's products, a constant index into the kernel arguments. Always inlined: a
+// call that is not would take the argument block's address, and the compiler copies the whole block
+// (1.5 KB) to scratch per lane for that (the 4-wave backward launch did until r04).
+template <int NW, int AK, int BK, int TMX, int DI>
+__device__ __forceinline__ void gemm_tile(const GemmLaunch& L, int tile, float (*red)[TT * TMX][TT + 1],
+                                          float (*xs)[FOLD_K0MAX]) {
+    const GemmDesc& D = L.d[DI];
     constexpr int NT = 64 * NW;
     constexpr int TM = TT * TMX;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, q = lane >> 4, c = lane & 15;
@@ -350,18 +392,36 @@ __device__ void gemm_tile(const GemmLaunch& L, const GemmDesc& D, int tile, floa
     // their latency overlaps the products'
     const Output& O = D.out;
     constexpr int EPT = TM * TT / NT;       // C elements per thread in the epilogue
-    float pre[EPT];
+    float pre[EPT], ap[EPT], am[EPT], av[EPT];
 #pragma unroll
     for (int j = 0; j < EPT; ++j) {
         const int e = tid + j * NT, m = m0 + (e >> 5), n = n0 + (e & 31);
-        pre[j] = 0.0f;
+        pre[j] = ap[j] = am[j] = av[j] = 0.0f;
         if (m >= D.M || n >= D.N) continue;
         if (O.mode == EPI_ACT) pre[j] = n < O.bsplit ? O.b0[n] : O.b1[n - O.bsplit];
         else if (O.mode == EPI_MASK) pre[j] = O.mask[(int64_t)m * O.ldm + n];
+        else if (O.mode == EPI_GRAD && O.adam) {   // the in-place Adam step's operands (only this tile
+            const int64_t i = (int64_t)m * O.ldc + n;   // writes them; the weight is only read by others)
+            ap[j] = O.aw.param[i];
+            am[j] = O.aw.exp_avg[i];
+            av[j] = O.aw.exp_avg_sq[i];
+        }
         else if (O.mode == EPI_LOSS) {
             const int64_t src = batch_row(L, m);
             const float t = n < O.s ? L.gns[src * O.s + n] : L.grw[src];
             pre[j] = t - (n < O.bsplit ? O.b0[n] : O.b1[n - O.bsplit]);   // y - t = acc - (t - bias)
+        }
+    }
+    // the dW_0 fold's operand, the tile's rows of the gathered input: loaded now, into LDS after the
+    // K loop (its latency then hides behind the products')
+    constexpr int XPT = TM * FOLD_K0MAX / NT;
+    float xv[XPT];
+    const bool xstage = O.mode == EPI_MASK && O.fold && O.fold_k0 <= FOLD_K0MAX;
+    if (xstage) {
+#pragma unroll
+        for (int j = 0; j < XPT; ++j) {
+            const int e = tid + j * NT, r = e / FOLD_K0MAX, k = e % FOLD_K0MAX;
+            xv[j] = (k < O.fold_k0 && m0 + r < D.M) ? O.fold_x[(int64_t)(m0 + r) * O.fold_k0 + k] : 0.0f;
         }
     }
     TSTAMP(1);
@@ -402,7 +462,17 @@ __device__ void gemm_tile(const GemmLaunch& L, const GemmDesc& D, int tile, floa
         for (int y = 0; y < 2; ++y)
 #pragma unroll
             for (int v = 0; v < 4; ++v) red[wave][16 * x + 4 * q + v][16 * y + c] = acc[x][y][v];
+    if (xstage) {
+#pragma unroll
+        for (int j = 0; j < XPT; ++j) {
+            const int e = tid + j * NT;
+            xs[e / FOLD_K0MAX][e % FOLD_K0MAX] = xv[j];
+        }
+    }
     __syncthreads();
+    // every wave's K loop is done: this tile no longer reads the weight block (its loads were consumed)
+    if (O.mode == EPI_MASK && O.arrive_ticket && tid == 0)
+        __hip_atomic_fetch_add(O.arrive_ticket + n0 / TT, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
     if (O.mode == EPI_GRAD && O.adam && O.wait_ticket)
         wait_arrivals(O.wait_ticket + n0 / TT, O.wait_count, O.wait_status);
@@ -434,19 +504,21 @@ __device__ void gemm_tile(const GemmLaunch& L, const GemmDesc& D, int tile, floa
         dst[n] = v;
         if (O.mode == EPI_GRAD && O.adam) {
             const int64_t i = (int64_t)m * O.ldc + n;
-            adam_element(O.aw.param[i], v, O.aw.exp_avg[i], O.aw.exp_avg_sq[i], O.aw.step_size, O.aw.bc2_sqrt, L.hp,
+            adam_element(ap[j], v, am[j], av[j], O.aw.step_size, O.aw.bc2_sqrt, L.hp, L.arith);
+            O.aw.param[i] = ap[j];
+            O.aw.exp_avg[i] = am[j];
+            O.aw.exp_avg_sq[i] = av[j];
+        }
+    }
+    // EPI_GRAD: the first column tile also finishes the bias gradient of each row m from the column
+    // sums the launch that produced this layer's output gradient left per row tile
+    if (O.mode == EPI_GRAD && O.colsum_in && n0 == 0 && tid < TM && m0 + tid < D.M) {
+        const int m = m0 + tid;
+        const float g = ordered_sum<false>(O.colsum_in + m, D.M, O.colsum_tiles);
+        (m < O.split ? O.g0[m] : O.g1[m - O.split]) = g;
+        if (O.adam)
+            adam_element(O.ab.param[m], g, O.ab.exp_avg[m], O.ab.exp_avg_sq[m], O.ab.step_size, O.ab.bc2_sqrt, L.hp,
                          L.arith);
-        }
-        // EPI_GRAD: the first column tile also finishes the bias gradient of row m from the column
-        // sums the launch that produced this layer's output gradient left per row tile
-        if (O.mode == EPI_GRAD && n0 == 0 && col == 0) {
-            float g = O.colsum_in[m];
-            for (int i = 1; i < O.colsum_tiles; ++i) g = g + O.colsum_in[(int64_t)i * D.M + m];
-            (m < O.split ? O.g0[m] : O.g1[m - O.split]) = g;
-            if (O.adam)
-                adam_element(O.ab.param[m], g, O.ab.exp_avg[m], O.ab.exp_avg_sq[m], O.ab.step_size, O.ab.bc2_sqrt,
-                             L.hp, L.arith);
-        }
     }
     if (O.mode == EPI_MASK || O.mode == EPI_LOSS) {   // per-32-row-tile column sums (the next bias gradient)
         __syncthreads();
@@ -466,7 +538,7 @@ __device__ void gemm_tile(const GemmLaunch& L, const GemmDesc& D, int tile, floa
             else
                 *dst = t;
         }
-        if (O.mode == EPI_MASK && O.fold) fold_dw0<NW, TMX>(L, D, tm, n0, red);
+        if (O.mode == EPI_MASK && O.fold) fold_dw0<NW, TMX, DI>(L, tm, n0, red, xs);
     }
     if (O.mode == EPI_LOSS) {   // the tile's loss: a butterfly per wave, then the waves in order
 #pragma unroll
@@ -497,8 +569,10 @@ __device__ void gemm_tile(const GemmLaunch& L, const GemmDesc& D, int tile, floa
 // same loads and MFMAs in the same order run here per 32-row half of the tile, so every partial is
 // the same float, and the last arriver sums them in wave order with the empty waves' +0 -- the
 // separate launch's result bit for bit.
-template <int NW, int TMX>
-__device__ void fold_dw0(const GemmLaunch& L, const GemmDesc& D, int tm, int n0, float (*red)[TT * TMX][TT + 1]) {
+template <int NW, int TMX, int DI>
+__device__ __forceinline__ void fold_dw0(const GemmLaunch& L, int tm, int n0, float (*red)[TT * TMX][TT + 1],
+                                         const float (*xs)[FOLD_K0MAX]) {
+    const GemmDesc& D = L.d[DI];
     constexpr int TM = TT * TMX;
     const Output& O = D.out;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, q = lane >> 4, c = lane & 15;
@@ -534,7 +608,8 @@ __device__ void fold_dw0(const GemmLaunch& L, const GemmDesc& D, int tm, int n0,
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const int r = k0 + 4 * q + e;
-                    b[y][e] = (kk < K0 && r < R) ? O.fold_x[(int64_t)r * K0 + kk] : 0.0f;
+                    b[y][e] = (kk < K0 && r < R) ? (K0 <= FOLD_K0MAX ? xs[r - m0][kk] : O.fold_x[(int64_t)r * K0 + kk])
+                                                 : 0.0f;
                 }
             }
 #pragma unroll
@@ -596,9 +671,7 @@ __device__ void fold_dw0(const GemmLaunch& L, const GemmDesc& D, int tm, int n0,
     }
     if (tid < TT && n0 + tid < W) {          // db_0: the column sums of dH_0 over the 32-row tiles
         const int j = n0 + tid;
-        float g = __hip_atomic_load(O.colsum_out + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (int i = 1; i < O.fold_cs_tiles; ++i)
-            g = g + __hip_atomic_load(O.colsum_out + (int64_t)i * W + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const float g = ordered_sum<true>(O.colsum_out + j, W, O.fold_cs_tiles);
         O.fold_db[j] = g;
         if (O.fold_adam)
             adam_element(O.fold_ab.param[j], g, O.fold_ab.exp_avg[j], O.fold_ab.exp_avg_sq[j], O.fold_ab.step_size,
@@ -611,6 +684,7 @@ __device__ void fold_dw0(const GemmLaunch& L, const GemmDesc& D, int tm, int n0,
 template <int NW, int A0, int B0, int A1, int B1, int TMX>
 __global__ __launch_bounds__(64 * NW) void train_gemm_kernel(const GemmLaunch L) {
     __shared__ float red[NW][TT * TMX][TT + 1];
+    __shared__ float xs[TT * TMX][FOLD_K0MAX];   // the dW_0 fold's input rows (dH_0 launches only)
     TSTAMP(0);
     // (constant indices only: a dynamic index into the kernel arguments would copy them to scratch)
     const int b = blockIdx.x;
@@ -624,13 +698,13 @@ __global__ __launch_bounds__(64 * NW) void train_gemm_kernel(const GemmLaunch L)
             const int u = j / per, r = j - u * per;
             tile = ((x + 8 * u) * G + r / tn_all) * tn_all + r % tn_all;
         }
-        gemm_tile<NW, A0, B0, TMX>(L, L.d[0], tile, red);
+        gemm_tile<NW, A0, B0, TMX, 0>(L, tile, red, xs);
         return;
     }
     int r = b - L.d[0].tiles;
     if constexpr (A1 >= 0) {
         if (L.nd > 1 && r < L.d[1].tiles) {
-            gemm_tile<NW, A1, B1, TMX>(L, L.d[1], r, red);
+            gemm_tile<NW, A1, B1, TMX, 1>(L, r, red, xs);
             return;
         }
         if (L.nd > 1) r -= L.d[1].tiles;
@@ -646,15 +720,25 @@ __global__ __launch_bounds__(64 * NW) void train_gemm_kernel(const GemmLaunch L)
         return;
     }
     // the loss workgroup: partials of the output-layer launch, summed in tile order
-    if (threadIdx.x < 2 && L.loss_out) {
-        float t = 0.0f;
-        for (int i = 0; i < L.loss_parts; ++i) t = t + L.loss_part[i * 2 + threadIdx.x];
-        L.loss_out[1 + threadIdx.x] = t;
-        if (threadIdx.x == 0) {
-            float u = 0.0f;
-            for (int i = 0; i < L.loss_parts; ++i) u = u + L.loss_part[i * 2] + L.loss_part[i * 2 + 1];
-            L.loss_out[0] = u;
+    if (threadIdx.x < 2 && L.loss_out) {   // (loads 16 at a time in flight, sums in the same order)
+        float t = 0.0f, u = 0.0f;
+        for (int i0 = 0; i0 < L.loss_parts; i0 += 16) {
+            float ps[16], pr[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const bool in = i0 + k < L.loss_parts;
+                ps[k] = in ? L.loss_part[(i0 + k) * 2] : 0.0f;
+                pr[k] = in ? L.loss_part[(i0 + k) * 2 + 1] : 0.0f;
+            }
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                if (i0 + k < L.loss_parts) {
+                    t = t + (threadIdx.x == 0 ? ps[k] : pr[k]);
+                    u = u + ps[k] + pr[k];
+                }
         }
+        L.loss_out[1 + threadIdx.x] = t;
+        if (threadIdx.x == 0) L.loss_out[0] = u;
     }
 }
 
@@ -683,7 +767,6 @@ struct FusedArgs {
     const float *gs, *ga, *gns, *grw;   // stacked transitions (GemmLaunch's meaning)
     int H, s, a;
     int R, W, K0, J, tiles_n, tiles_r;
-    int nw0;                            // waves of the separate layer-0 launch (its K split)
     int nwb;                            // waves of the separate backward launches (K = R): the dH_1 split
     const float *w0, *b0, *w1, *b1;
     const float *wo, *wo_r, *bo, *bo_r; // output layer: state rows from wo / bo, the reward row from *_r
@@ -691,6 +774,11 @@ struct FusedArgs {
     float *dh1, *cs_dh1, *cs_dy, *loss_part, *out_part;
     float *dwo, *dwo_r, *dbo, *dbo_r;
     unsigned* out_ticket;               // [tiles_n] arrivals per column block of dH_1 tiles (O)
+    float* db1;                         // O's last arrivers: db_1 from dH_1's column sums (+ b_1's Adam step)
+    int adam;
+    mbrl_adam_tensor ab1;
+    mbrl_adam_hparams hp;
+    int arith;
     unsigned* zero_words;               // F's workgroup 0 zeroes zero_n words (both folds' tickets)
     int zero_n;
     float scale_s, scale_r, inv_s, inv_r;
@@ -715,9 +803,11 @@ __device__ __forceinline__ f32x4 row4(const float* row, bool valid, int k0, int 
     return v;
 }
 
-template <int NW>
+// KCH: 16-deep chunks of K0 (2: K0 <= 32, 4: K0 <= 64), one per wave of the layer-0 launch (4 waves)
+template <int NW, int KCH>
 __global__ __launch_bounds__(64 * NW) void train_fused_fwd_kernel(const FusedArgs F) {
-    constexpr int NT = 64 * NW, EPT = TT * TT / NT, MAXPER = NW == 16 ? 2 : 4;
+    constexpr int NT = 64 * NW, EPT = TT * TT / NT, MAXPER = NW == 16 ? 2 : 4, MAXY = NW == 16 ? 2 : 4;
+    constexpr int NW0 = 4;   // the layer-0 launch's waves (K0 < 256)
     constexpr int HLD = FUSED_WMAX + 4, XLD = FUSED_K0MAX + 4;
     __shared__ float red[NW][TT][TT + 1];
     __shared__ __attribute__((aligned(16))) float h0[TT][HLD];
@@ -725,8 +815,20 @@ __global__ __launch_bounds__(64 * NW) void train_fused_fwd_kernel(const FusedArg
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, q = lane >> 4, c = lane & 15;
     const int tm = blockIdx.x / F.tiles_n, tn = blockIdx.x - tm * F.tiles_n, m0 = tm * TT, n0 = tn * TT;
     const int W = F.W, K0 = F.K0, R = F.R;
+    FSTAMP(0, 0);
     if (blockIdx.x == 0 && F.zero_words)
         for (int i = tid; i < F.zero_n; i += NT) F.zero_words[i] = 0u;
+    // the batch's 32 input rows are gathered through the row indices: the indices first, then every
+    // operand load of the launch while they travel, then the rows (a straight-line sequence, so the
+    // waits for the indices and the rows do not wait for the weight loads issued between them)
+    constexpr int GPT = TT * 16 * KCH / NT;      // gathered elements per thread (k0pad <= 16 KCH)
+    const int k0pad = (K0 + 15) & ~15;
+    int64_t gi[GPT];
+#pragma unroll
+    for (int j = 0; j < GPT; ++j) {
+        const int e = tid + j * NT, r = e / k0pad, k = e - r * k0pad, m = m0 + r;
+        gi[j] = (r < TT && m < R && k < K0) ? F.idx[m / F.H] : -1;
+    }
     // the layer-1 operands first (this wave's K range of W_1's rows n0..n0+31, and the bias): their
     // latency overlaps the gather and the H_0 recompute
     int kb0, kb1;
@@ -746,46 +848,64 @@ __global__ __launch_bounds__(64 * NW) void train_fused_fwd_kernel(const FusedArg
         const int e = tid + j * NT, n = n0 + (e & 31);
         pre[j] = n < W ? F.b1[n] : 0.0f;
     }
-    // the batch's 32 input rows, gathered through the row indices (zero past K0 to the chunk end);
-    // the first column tile keeps them for the layer-0 weight gradient, as the layer-0 launch did
-    const int k0pad = (K0 + 15) & ~15;
-    for (int e = tid; e < TT * k0pad; e += NT) {
-        const int r = e / k0pad, k = e - r * k0pad, m = m0 + r;
-        float v = 0.0f;
-        if (m < R && k < K0) {
-            const int64_t src = F.idx[m / F.H] * F.H + m % F.H;
-            v = k < F.s ? F.gs[src * F.s + k] : F.ga[src * F.a + (k - F.s)];
-            if (tn == 0) F.xstore[(int64_t)m * K0 + k] = v;
+    // W_0's rows for this wave's 16-column blocks of H_0 (y = wave, wave + NW, ...), every chunk
+    const int ny = (W + 15) >> 4, nch0 = (K0 + 15) >> 4;
+    const bool vec0 = (K0 % 4 == 0) && (reinterpret_cast<uintptr_t>(F.w0) & 15) == 0;
+    f32x4 w0r[MAXY][KCH];
+    float b0r[MAXY];
+#pragma unroll
+    for (int yy = 0; yy < MAXY; ++yy) {
+        const int n = 16 * (wave + yy * NW) + c;
+        b0r[yy] = n < W ? F.b0[n] : 0.0f;
+#pragma unroll
+        for (int ch = 0; ch < KCH; ++ch)
+            w0r[yy][ch] = row4(F.w0 + (int64_t)min(n, W - 1) * K0, n < W && ch < nch0, 16 * ch + 4 * q, K0, vec0);
+    }
+    // the rows (zero past K0 to the chunk end); the first column tile keeps them for the layer-0 weight
+    // gradient, as the layer-0 launch did
+    float gv[GPT];
+#pragma unroll
+    for (int j = 0; j < GPT; ++j) {
+        const int e = tid + j * NT, r = e / k0pad, k = e - r * k0pad, m = m0 + r;
+        gv[j] = 0.0f;
+        if (gi[j] >= 0) {
+            const int64_t src = gi[j] * F.H + m % F.H;
+            gv[j] = k < F.s ? F.gs[src * F.s + k] : F.ga[src * F.a + (k - F.s)];
         }
-        xr[r][k] = v;
+    }
+#pragma unroll
+    for (int j = 0; j < GPT; ++j) {
+        const int e = tid + j * NT, r = e / k0pad, k = e - r * k0pad, m = m0 + r;
+        if (r < TT) xr[r][k] = gv[j];
+        if (gi[j] >= 0 && tn == 0) F.xstore[(int64_t)m * K0 + k] = gv[j];
     }
     __syncthreads();
+    FSTAMP(0, 1);
     // H_0 rows m0..m0+31, all W columns: wave w takes the 16-column blocks y = w, w + NW, ...; each
-    // 16 x 16 block is the sum, in wave order, of the layer-0 launch's per-wave chains (nw0 waves,
+    // 16 x 16 block is the sum, in wave order, of the layer-0 launch's per-wave chains (NW0 waves,
     // empty ones adding +0), then bias and ReLU -- that launch's epilogue
-    const int ny = (W + 15) >> 4;
-    const bool vec0 = (K0 % 4 == 0) && (reinterpret_cast<uintptr_t>(F.w0) & 15) == 0;
-    for (int y = wave; y < ny; y += NW) {
-        const int n = 16 * y + c;
+#pragma unroll
+    for (int yy = 0; yy < MAXY; ++yy) {
+        const int y = wave + yy * NW, n = 16 * y + c;
+        if (y >= ny) break;
         f32x4 tot[2];
-        for (int vw = 0; vw < F.nw0; ++vw) {
-            int a0, a1;
-            wave_k_range(K0, F.nw0, vw, a0, a1);
+#pragma unroll
+        for (int vw = 0; vw < NW0; ++vw) {      // wave vw of the layer-0 launch: chunk vw (or nothing)
             f32x4 p[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
-            for (int kb = a0; kb < a1; kb += 16) {
-                const f32x4 b = row4(F.w0 + (int64_t)min(n, W - 1) * K0, n < W, kb + 4 * q, K0, vec0);
+            if (vw < KCH && vw < nch0) {
                 f32x4 a[2];
 #pragma unroll
-                for (int x = 0; x < 2; ++x) a[x] = *reinterpret_cast<const f32x4*>(&xr[16 * x + c][kb + 4 * q]);
+                for (int x = 0; x < 2; ++x) a[x] = *reinterpret_cast<const f32x4*>(&xr[16 * x + c][16 * vw + 4 * q]);
 #pragma unroll
                 for (int s = 0; s < 4; ++s)
 #pragma unroll
-                    for (int x = 0; x < 2; ++x) p[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[x][s], b[s], p[x], 0, 0, 0);
+                    for (int x = 0; x < 2; ++x)
+                        p[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[x][s], w0r[yy][vw < KCH ? vw : 0][s], p[x], 0, 0, 0);
             }
 #pragma unroll
             for (int x = 0; x < 2; ++x) tot[x] = vw == 0 ? p[x] : tot[x] + p[x];
         }
-        const float bias = n < W ? F.b0[n] : 0.0f;
+        const float bias = b0r[yy];
 #pragma unroll
         for (int x = 0; x < 2; ++x)
 #pragma unroll
@@ -797,6 +917,7 @@ __global__ __launch_bounds__(64 * NW) void train_fused_fwd_kernel(const FusedArg
             }
     }
     __syncthreads();
+    FSTAMP(0, 2);
     // this tile's columns of H_0 (every element stored by exactly one workgroup)
     for (int e = tid; e < TT * TT; e += NT) {
         const int r = e >> 5, col = e & 31, m = m0 + r, n = n0 + col;
@@ -840,6 +961,7 @@ __global__ __launch_bounds__(64 * NW) void train_fused_fwd_kernel(const FusedArg
         v = v + pre[j];
         F.act1[(int64_t)m * W + n] = v > 0.0f ? v : 0.0f;
     }
+    FSTAMP(0, 3);
 }
 
 template <int NW>
@@ -852,6 +974,7 @@ __global__ __launch_bounds__(64 * NW) void train_fused_out_kernel(const FusedArg
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, q = lane >> 4, c = lane & 15;
     const int tm = blockIdx.x / F.tiles_n, tn = blockIdx.x - tm * F.tiles_n, m0 = tm * TT, n0 = tn * TT;
     const int W = F.W, J = F.J, R = F.R, S = F.s;
+    FSTAMP(1, 0);
     // ---- the output-layer tile (tm, 0): Y = H_1 W_out^T + b_out over this wave's K range
     int kb0, kb1;
     wave_k_range(W, NW, wave, kb0, kb1);
@@ -929,6 +1052,7 @@ __global__ __launch_bounds__(64 * NW) void train_fused_out_kernel(const FusedArg
         dy[row][col] = v;
     }
     __syncthreads();
+    FSTAMP(1, 1);
     if (tn == 0) {
         // dY's column sums over the tile's rows (db_out), read back by this launch's last arriver
         if (tid < TT && tid < J) {
@@ -1007,14 +1131,16 @@ __global__ __launch_bounds__(64 * NW) void train_fused_out_kernel(const FusedArg
         }
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    // dH_1's column sums over the tile's 32 rows (the next launch's db_1), in row order
+    // dH_1's column sums over the tile's 32 rows, in row order (db_1: this column block's last arriver)
     if (tid < TT && n0 + tid < W) {
         float t = red[0][0][tid];
         for (int r = 1; r < TT; ++r) t = t + red[0][r][tid];
-        F.cs_dh1[(int64_t)tm * W + n0 + tid] = t;
+        __hip_atomic_store(F.cs_dh1 + (int64_t)tm * W + n0 + tid, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    FSTAMP(1, 2);
     // the column block's last arriver sums the dW_out partials in wave order (row tiles past the
     // batch: the empty waves' +0), and the first column block's also db_out from dY's column sums
     if (tid == 0) {
@@ -1022,6 +1148,7 @@ __global__ __launch_bounds__(64 * NW) void train_fused_out_kernel(const FusedArg
         last = (t + 1 == (unsigned)F.tiles_r) ? 1u : 0u;
     }
     __syncthreads();
+    FSTAMP(1, 3);
     if (!last) return;
     for (int e = tid; e < J * TT; e += NT) {
         const int o = e / TT, i = n0 + (e - o * TT);
@@ -1041,11 +1168,19 @@ __global__ __launch_bounds__(64 * NW) void train_fused_out_kernel(const FusedArg
         else F.dwo_r[(int64_t)(o - S) * W + i] = v;
     }
     if (tn == 0 && tid < J) {
-        float g = __hip_atomic_load(F.cs_dy + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (int i = 1; i < F.tiles_r; ++i)
-            g = g + __hip_atomic_load(F.cs_dy + (int64_t)i * J + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const float g = ordered_sum<true>(F.cs_dy + tid, J, F.tiles_r);
         if (tid < S) F.dbo[tid] = g;
         else F.dbo_r[tid - S] = g;
+    }
+    // db_1 of this column block (the five-launch layout's dW_1 launch summed the same column sums in the
+    // same order), and b_1's Adam step: nothing reads b_1 before the next batch's F
+    if (tid >= 64 && tid < 64 + TT && n0 + tid - 64 < W) {
+        const int n = n0 + tid - 64;
+        const float g = ordered_sum<true>(F.cs_dh1 + n, W, F.tiles_r);
+        F.db1[n] = g;
+        if (F.adam)
+            adam_element(F.ab1.param[n], g, F.ab1.exp_avg[n], F.ab1.exp_avg_sq[n], F.ab1.step_size, F.ab1.bc2_sqrt,
+                         F.hp, F.arith);
     }
 }
 
@@ -1112,7 +1247,8 @@ struct TrainWs {
     float* act[MBRL_TRAIN_MAX_LAYERS];
     float *dh[2], *dy, *loss_part, *xbuf, *cs_dy, *cs_dh[2], *fold_part;
     float* out_part;      // fused step: the output layer's weight-gradient partials [row tile][J][W]
-    unsigned* tickets;    // [ceil(W / 32)] the dW_0 fold's, then [ceil(W / 32)] the fused dW_out fold's
+    unsigned* tickets;    // [ceil(W / 32)] each: the dW_0 fold's, the fused dW_out fold's, the fused dH_0
+                          // tiles' W_1-read arrivals
     unsigned* status;     // fused step: bit 0 = a bounded wait timed out (never expected)
     size_t floats;
 };
@@ -1135,7 +1271,7 @@ static TrainWs train_ws(const TrainShape& t, int batch, float* base) {
     w.cs_dh[1] = take(tiles_r * W);
     w.fold_part = take(tiles_r * W * (size_t)(t.s + t.a));   // the folded dW_0's per-32-row partials
     w.out_part = take(tiles_r * J * W);
-    w.tickets = reinterpret_cast<unsigned*>(take(2 * ((W + TT - 1) / TT)));
+    w.tickets = reinterpret_cast<unsigned*>(take(3 * ((W + TT - 1) / TT)));
     w.status = reinterpret_cast<unsigned*>(take(1));
     w.floats = off;
     return w;
@@ -1171,6 +1307,7 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
     const int R = batch * t.H, W = t.W, K0 = t.s + t.a, J = t.s + (t.reward ? 1 : 0), L = t.L;
     const int tiles_r = (R + TT - 1) / TT;
     const int fold_nw = fold_waves(t, R);
+    const bool fused = fused_step(t, fold_nw);
     if (pending_n) *pending_n = 0;
     if ((prior_n > 0 && !prior) || prior_n > ADAM_FUSED_MAX || (adam && fold_nw && (!pending || !pending_n)))
         return hipErrorInvalidValue;
@@ -1183,13 +1320,12 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
     const int xcd_opt = t.xcd;
     G.H = t.H; G.s = t.s; G.a = t.a;
     G.xstore = B.xbuf;
-    G.slot = -1;
+    G.slot = fused ? 1 : -1;   // diagnostic stamps: the fused step's F and O are slots 0 and 1
     if (adam) {
         G.hp = *hp;
         G.arith = arith;
     }
     hipError_t e;
-    const bool fused = fused_step(t, fold_nw);
     const int tiles_n = (W + TT - 1) / TT;
     if (fused) {   // F and O (train_fused_*_kernel); the backward launch below is B
         // a step the five-launch layout deferred (a smaller batch before this one): F reads W_1
@@ -1198,7 +1334,6 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
         F.idx = idx; F.gs = w.states; F.ga = w.actions; F.gns = w.next_states; F.grw = w.rewards;
         F.H = t.H; F.s = t.s; F.a = t.a;
         F.R = R; F.W = W; F.K0 = K0; F.J = J; F.tiles_n = tiles_n; F.tiles_r = tiles_r;
-        F.nw0 = K0 >= 256 ? 16 : 4;
         F.nwb = fold_nw;
         F.w0 = w.weight[0]; F.b0 = w.bias[0]; F.w1 = w.weight[1]; F.b1 = w.bias[1];
         F.wo = w.weight[L]; F.wo_r = wo_r; F.bo = w.bias[L]; F.bo_r = bo_r;
@@ -1208,15 +1343,22 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
         F.dwo = w.weight_grad[L]; F.dwo_r = t.reward ? w.weight_grad[L + 1] : w.weight_grad[L];
         F.dbo = w.bias_grad[L]; F.dbo_r = t.reward ? w.bias_grad[L + 1] : w.bias_grad[L];
         F.out_ticket = B.tickets + tiles_n;
-        F.zero_words = B.tickets; F.zero_n = 2 * tiles_n;
+        F.db1 = w.bias_grad[1];
+        if (adam) {
+            F.adam = 1; F.ab1 = adam[3]; F.hp = *hp; F.arith = arith;
+        }
+        F.zero_words = B.tickets; F.zero_n = 3 * tiles_n;
         F.scale_s = 2.0f / (float)((int64_t)batch * t.s); F.scale_r = 2.0f / (float)batch;
         F.inv_s = 1.0f / (float)((int64_t)batch * t.s); F.inv_r = 1.0f / (float)batch;
         const dim3 grid(tiles_r * tiles_n);
-        if (W >= 256) {   // the wave count of the separate launches whose K is W
-            hipLaunchKernelGGL(train_fused_fwd_kernel<16>, grid, dim3(64 * 16), 0, stream, F);
+        // the wave count of the separate launches whose K is W; K0's chunks
+        if (W >= 256) {
+            if (K0 <= 32) hipLaunchKernelGGL((train_fused_fwd_kernel<16, 2>), grid, dim3(64 * 16), 0, stream, F);
+            else hipLaunchKernelGGL((train_fused_fwd_kernel<16, 4>), grid, dim3(64 * 16), 0, stream, F);
             hipLaunchKernelGGL(train_fused_out_kernel<16>, grid, dim3(64 * 16), 0, stream, F);
         } else {
-            hipLaunchKernelGGL(train_fused_fwd_kernel<4>, grid, dim3(64 * 4), 0, stream, F);
+            if (K0 <= 32) hipLaunchKernelGGL((train_fused_fwd_kernel<4, 2>), grid, dim3(64 * 4), 0, stream, F);
+            else hipLaunchKernelGGL((train_fused_fwd_kernel<4, 4>), grid, dim3(64 * 4), 0, stream, F);
             hipLaunchKernelGGL(train_fused_out_kernel<4>, grid, dim3(64 * 4), 0, stream, F);
         }
         if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -1308,6 +1450,7 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
             D.B = l == 0 ? transposed(B.xbuf, nullptr, 0, K0, n_in, -1) : transposed(B.act[l - 1], nullptr, 0, W, n_in, -1);
             Output& O = D.out;
             O.mode = EPI_GRAD; O.ldc = n_in; O.colsum_in = cs_in; O.colsum_tiles = tiles_r;
+            if (fused) O.colsum_in = nullptr;   // db_1 (and b_1's Adam step) came from O's last arrivers
             if (out_layer) {
                 O.c0 = w.weight_grad[L]; O.c1 = t.reward ? w.weight_grad[L + 1] : w.weight_grad[L];
                 O.split = t.reward ? t.s : J;
@@ -1325,12 +1468,13 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
         }
         if (adam && fused && l == 1) {
             // the dH_0 tiles of a column block read that block of W_1: the dW_1 tiles step it in place
-            // after those tiles' fold tickets (dH_0 tiles have the lower ids)
+            // once those tiles' K loops are done (dH_0 tiles have the lower ids)
             Output& O = G.d[G.nd - 1].out;
-            O.adam = 1; O.aw = adam[2]; O.ab = adam[3];
-            O.wait_ticket = B.tickets;
+            O.adam = 1; O.aw = adam[2];
+            O.wait_ticket = B.tickets + 2 * tiles_n;
             O.wait_count = (unsigned)((R + TT * tmx - 1) / (TT * tmx));
             O.wait_status = B.status;
+            G.d[0].out.arrive_ticket = B.tickets + 2 * tiles_n;
         }
         // layer l + 1's gradient is complete (previous launch) and this launch does not read its
         // parameters: its Adam step rides along (with the reward head when l + 1 is the output layer)

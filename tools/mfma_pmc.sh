@@ -15,7 +15,7 @@ for l in ${*:-c2 c3 c4 c4s2048 c5 c6}; do
   timeout -k 10 240 rocprofv3 --kernel-include-regex "rollout_(m8_)?kernel" \
       --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 GRBM_GUI_ACTIVE \
       --output-format csv -d "$OUT/$l" -o run -- \
-      python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-variants --no-strong ${ARGS[$l]} > "$OUT/$l.log" 2>&1
+      python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-variants --no-train --no-strong ${ARGS[$l]} > "$OUT/$l.log" 2>&1
   rc=$?; echo "$l pmc rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 "$OUT/$l.log"; exit $rc; fi
 done

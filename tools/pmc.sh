@@ -4,7 +4,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
-CMD="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-variants ${BENCH_ARGS:-}"
+CMD="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-variants --no-train ${BENCH_ARGS:-}"
 rm -rf gpurun_out/pmc && mkdir -p gpurun_out/pmc
 i=0
 for set in "${@}"; do

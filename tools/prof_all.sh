@@ -14,7 +14,7 @@ STEPS=${STEPS:-20}
 for l in $LABELS; do
   rm -rf $OUT/$l
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$l -o run -- \
-      python3 bench.py --steps $STEPS --warmup 3 --no-cpu-baseline --no-variants --no-strong ${ARGS[$l]} \
+      python3 bench.py --steps $STEPS --warmup 3 --no-cpu-baseline --no-variants --no-train --no-strong ${ARGS[$l]} \
       > $OUT/$l.log 2>&1
   rc=$?; echo "$l rocprof rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 $OUT/$l.log; exit $rc; fi

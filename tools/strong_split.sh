@@ -10,7 +10,7 @@ OUT=gpurun_out/strong_split.jsonl
 for spec in "3 4096" "3 2048" "3 1024" "3 512" "4 16384" "4 8192" "4 4096" "4 2048"; do
   set -- $spec
   timeout -k 10 300 python bench.py --config $1 --candidates $2 --steps ${STEPS:-30} --warmup 5 --no-cpu-baseline \
-      --no-variants --no-strong > gpurun_out/ss.log 2>&1
+      --no-variants --no-strong --no-train > gpurun_out/ss.log 2>&1
   rc=$?
   if [ $rc -ne 0 ]; then tail -5 gpurun_out/ss.log; exit $rc; fi
   tail -1 gpurun_out/ss.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps(dict(config=$1, candidates=$2, ms_per_plan=d['ms_per_step'], rollout_ms=d['roofline']['avg_launch_ms'], frac=d['roofline']['frac'])))" >> $OUT
