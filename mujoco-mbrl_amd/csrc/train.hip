@@ -576,8 +576,27 @@ __device__ __forceinline__ void fold_dw0(const GemmLaunch& L, int tm, int n0, fl
     constexpr int TM = TT * TMX;
     const Output& O = D.out;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, q = lane >> 4, c = lane & 15;
-    const int R = D.M, W = D.N, K0 = O.fold_k0, m0 = tm * TM;
+    const int R = D.M, W = D.N, K0 = O.fold_k0, m0 = tm * TT * TMX;
     const int kt = (K0 + TT - 1) / TT;
+    // the last arriver's Adam operands for this column block of W_0 / b_0, loaded by every tile now
+    // (one element per thread at K0 <= 32) so that its tail has one memory round trip, not three
+    constexpr int NT = 64 * NW, FPT = (TT * FOLD_K0MAX + NT - 1) / NT;
+    float fp[FPT], fm[FPT], fv[FPT], bp = 0.0f, bm = 0.0f, bv = 0.0f;
+    const bool fpre = O.fold_adam && K0 <= FOLD_K0MAX;
+#pragma unroll
+    for (int u = 0; u < FPT; ++u) {
+        const int e = tid + u * NT, j = n0 + e / max(K0, 1), kk = e - (e / max(K0, 1)) * K0;
+        const bool in = fpre && e < TT * K0 && j < W;
+        const int64_t i = (int64_t)j * K0 + kk;
+        fp[u] = in ? O.fold_aw.param[i] : 0.0f;
+        fm[u] = in ? O.fold_aw.exp_avg[i] : 0.0f;
+        fv[u] = in ? O.fold_aw.exp_avg_sq[i] : 0.0f;
+    }
+    if (fpre && tid < TT && n0 + tid < W) {
+        bp = O.fold_ab.param[n0 + tid];
+        bm = O.fold_ab.exp_avg[n0 + tid];
+        bv = O.fold_ab.exp_avg_sq[n0 + tid];
+    }
     for (int task = wave; task < TMX * kt; task += NW) {
         const int h = task / kt, kb = task - (task / kt) * kt;
         const int r0 = m0 + TT * h;
@@ -649,9 +668,16 @@ __device__ __forceinline__ void fold_dw0(const GemmLaunch& L, int tm, int n0, fl
     __syncthreads();
     if (!last) return;
     const int ntr = (R + TT - 1) / TT;      // non-empty waves of the separate launch
-    for (int e = tid; e < TT * K0; e += 64 * NW) {
-        const int j = n0 + e / K0, kk = e - (e / K0) * K0;
-        if (j >= W) continue;
+    // every load of the tail first (db_0's column sums, then the partials): one round trip
+    float cs[16];
+    const bool csfast = O.fold_cs_tiles <= 16, dbt = tid < TT && n0 + tid < W;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        cs[i] = (dbt && csfast && i < O.fold_cs_tiles)
+                    ? __hip_atomic_load(O.colsum_out + (int64_t)i * W + n0 + tid, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT)
+                    : 0.0f;
+    auto sum_partials = [&](int j, int kk) {
         float p[16];                         // fold_nw <= 16: every load in flight before the sum
 #pragma unroll
         for (int w = 0; w < 16; ++w)
@@ -663,19 +689,50 @@ __device__ __forceinline__ void fold_dw0(const GemmLaunch& L, int tm, int n0, fl
 #pragma unroll
         for (int w = 1; w < 16; ++w)
             if (w < O.fold_nw) v = v + p[w];
-        const int64_t i = (int64_t)j * K0 + kk;
-        O.fold_dw[i] = v;
-        if (O.fold_adam)
-            adam_element(O.fold_aw.param[i], v, O.fold_aw.exp_avg[i], O.fold_aw.exp_avg_sq[i], O.fold_aw.step_size,
-                         O.fold_aw.bc2_sqrt, L.hp, L.arith);
+        return v;
+    };
+    if (fpre) {                              // the Adam operands are in registers (fp / fm / fv)
+#pragma unroll
+        for (int u = 0; u < FPT; ++u) {
+            const int e = tid + u * NT, j = n0 + e / K0, kk = e - (e / K0) * K0;
+            if (e >= TT * K0 || j >= W) continue;
+            const float v = sum_partials(j, kk);
+            const int64_t i = (int64_t)j * K0 + kk;
+            O.fold_dw[i] = v;
+            adam_element(fp[u], v, fm[u], fv[u], O.fold_aw.step_size, O.fold_aw.bc2_sqrt, L.hp, L.arith);
+            O.fold_aw.param[i] = fp[u];
+            O.fold_aw.exp_avg[i] = fm[u];
+            O.fold_aw.exp_avg_sq[i] = fv[u];
+        }
+    } else {
+        for (int e = tid; e < TT * K0; e += NT) {
+            const int j = n0 + e / K0, kk = e - (e / K0) * K0;
+            if (j >= W) continue;
+            const float v = sum_partials(j, kk);
+            const int64_t i = (int64_t)j * K0 + kk;
+            O.fold_dw[i] = v;
+            if (O.fold_adam)
+                adam_element(O.fold_aw.param[i], v, O.fold_aw.exp_avg[i], O.fold_aw.exp_avg_sq[i],
+                             O.fold_aw.step_size, O.fold_aw.bc2_sqrt, L.hp, L.arith);
+        }
     }
-    if (tid < TT && n0 + tid < W) {          // db_0: the column sums of dH_0 over the 32-row tiles
+    if (dbt) {                               // db_0: the column sums of dH_0 over the 32-row tiles
         const int j = n0 + tid;
-        const float g = ordered_sum<true>(O.colsum_out + j, W, O.fold_cs_tiles);
+        float g = cs[0];
+#pragma unroll
+        for (int i = 1; i < 16; ++i)
+            if (i < O.fold_cs_tiles) g = g + cs[i];
+        if (!csfast) g = ordered_sum<true>(O.colsum_out + j, W, O.fold_cs_tiles);
         O.fold_db[j] = g;
-        if (O.fold_adam)
+        if (fpre) {
+            adam_element(bp, g, bm, bv, O.fold_ab.step_size, O.fold_ab.bc2_sqrt, L.hp, L.arith);
+            O.fold_ab.param[j] = bp;
+            O.fold_ab.exp_avg[j] = bm;
+            O.fold_ab.exp_avg_sq[j] = bv;
+        } else if (O.fold_adam) {
             adam_element(O.fold_ab.param[j], g, O.fold_ab.exp_avg[j], O.fold_ab.exp_avg_sq[j], O.fold_ab.step_size,
                          O.fold_ab.bc2_sqrt, L.hp, L.arith);
+        }
     }
 }
 
@@ -771,6 +828,7 @@ struct FusedArgs {
     const float *w0, *b0, *w1, *b1;
     const float *wo, *wo_r, *bo, *bo_r; // output layer: state rows from wo / bo, the reward row from *_r
     float *act0, *act1, *xstore;
+    float* tgt;                         // [R][J] the batch's targets, gathered by F's first column tiles for O
     float *dh1, *cs_dh1, *cs_dy, *loss_part, *out_part;
     float *dwo, *dwo_r, *dbo, *dbo_r;
     unsigned* out_ticket;               // [tiles_n] arrivals per column block of dH_1 tiles (O)
@@ -818,9 +876,9 @@ __global__ __launch_bounds__(64 * NW) void train_fused_fwd_kernel(const FusedArg
     FSTAMP(0, 0);
     if (blockIdx.x == 0 && F.zero_words)
         for (int i = tid; i < F.zero_n; i += NT) F.zero_words[i] = 0u;
-    // the batch's 32 input rows are gathered through the row indices: the indices first, then every
-    // operand load of the launch while they travel, then the rows (a straight-line sequence, so the
-    // waits for the indices and the rows do not wait for the weight loads issued between them)
+    // the batch's 32 input rows are gathered through the row indices: the indices, the rows, then every
+    // weight operand of the launch (in-order vmcnt: a wait for the rows then waits for nothing issued
+    // after them, and the weights travel while the rows do)
     constexpr int GPT = TT * 16 * KCH / NT;      // gathered elements per thread (k0pad <= 16 KCH)
     const int k0pad = (K0 + 15) & ~15;
     int64_t gi[GPT];
@@ -829,8 +887,34 @@ __global__ __launch_bounds__(64 * NW) void train_fused_fwd_kernel(const FusedArg
         const int e = tid + j * NT, r = e / k0pad, k = e - r * k0pad, m = m0 + r;
         gi[j] = (r < TT && m < R && k < K0) ? F.idx[m / F.H] : -1;
     }
-    // the layer-1 operands first (this wave's K range of W_1's rows n0..n0+31, and the bias): their
-    // latency overlaps the gather and the H_0 recompute
+    // the first column tiles also gather the targets O's loss epilogue needs (J <= 32: 32 x 32 slots)
+    constexpr int TPT = TT * TT / NT;
+    float tv[TPT];
+    int64_t tsrc[TPT];
+#pragma unroll
+    for (int j = 0; j < TPT; ++j) {
+        const int e = tid + j * NT, r = e >> 5, o = e & 31;
+        tsrc[j] = (tn == 0 && o < F.J && m0 + r < R) ? F.idx[(m0 + r) / F.H] * F.H + (m0 + r) % F.H : -1;
+    }
+    // the rows (zero past K0 to the chunk end); the first column tile keeps them for the layer-0 weight
+    // gradient, as the layer-0 launch did
+    float gv[GPT];
+#pragma unroll
+    for (int j = 0; j < GPT; ++j) {
+        const int e = tid + j * NT, r = e / k0pad, k = e - r * k0pad, m = m0 + r;
+        gv[j] = 0.0f;
+        if (gi[j] >= 0) {
+            const int64_t src = gi[j] * F.H + m % F.H;
+            gv[j] = k < F.s ? F.gs[src * F.s + k] : F.ga[src * F.a + (k - F.s)];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < TPT; ++j) {
+        const int o = (tid + j * NT) & 31;
+        tv[j] = tsrc[j] < 0 ? 0.0f : o < F.s ? F.gns[tsrc[j] * F.s + o] : F.grw[tsrc[j]];
+    }
+    // the layer-1 operands (this wave's K range of W_1's rows n0..n0+31, and the bias), issued behind
+    // the rows: their latency overlaps the rows' and the H_0 recompute
     int kb0, kb1;
     wave_k_range(W, NW, wave, kb0, kb1);
     const bool vec1 = (W % 4 == 0) && (reinterpret_cast<uintptr_t>(F.w1) & 15) == 0;
@@ -861,23 +945,16 @@ __global__ __launch_bounds__(64 * NW) void train_fused_fwd_kernel(const FusedArg
         for (int ch = 0; ch < KCH; ++ch)
             w0r[yy][ch] = row4(F.w0 + (int64_t)min(n, W - 1) * K0, n < W && ch < nch0, 16 * ch + 4 * q, K0, vec0);
     }
-    // the rows (zero past K0 to the chunk end); the first column tile keeps them for the layer-0 weight
-    // gradient, as the layer-0 launch did
-    float gv[GPT];
-#pragma unroll
-    for (int j = 0; j < GPT; ++j) {
-        const int e = tid + j * NT, r = e / k0pad, k = e - r * k0pad, m = m0 + r;
-        gv[j] = 0.0f;
-        if (gi[j] >= 0) {
-            const int64_t src = gi[j] * F.H + m % F.H;
-            gv[j] = k < F.s ? F.gs[src * F.s + k] : F.ga[src * F.a + (k - F.s)];
-        }
-    }
 #pragma unroll
     for (int j = 0; j < GPT; ++j) {
         const int e = tid + j * NT, r = e / k0pad, k = e - r * k0pad, m = m0 + r;
         if (r < TT) xr[r][k] = gv[j];
         if (gi[j] >= 0 && tn == 0) F.xstore[(int64_t)m * K0 + k] = gv[j];
+    }
+#pragma unroll
+    for (int j = 0; j < TPT; ++j) {
+        const int e = tid + j * NT, r = e >> 5, o = e & 31;
+        if (tsrc[j] >= 0) F.tgt[(int64_t)(m0 + r) * F.J + o] = tv[j];
     }
     __syncthreads();
     FSTAMP(0, 1);
@@ -975,6 +1052,14 @@ __global__ __launch_bounds__(64 * NW) void train_fused_out_kernel(const FusedArg
     const int tm = blockIdx.x / F.tiles_n, tn = blockIdx.x - tm * F.tiles_n, m0 = tm * TT, n0 = tn * TT;
     const int W = F.W, J = F.J, R = F.R, S = F.s;
     FSTAMP(1, 0);
+    // b_1's Adam operands for this column block (threads 64-95), for the last arriver's tail
+    const bool b1t = tid >= 64 && tid < 64 + TT && n0 + tid - 64 < W;
+    float b1p = 0.0f, b1m = 0.0f, b1v = 0.0f;
+    if (F.adam && b1t) {
+        b1p = F.ab1.param[n0 + tid - 64];
+        b1m = F.ab1.exp_avg[n0 + tid - 64];
+        b1v = F.ab1.exp_avg_sq[n0 + tid - 64];
+    }
     // ---- the output-layer tile (tm, 0): Y = H_1 W_out^T + b_out over this wave's K range
     int kb0, kb1;
     wave_k_range(W, NW, wave, kb0, kb1);
@@ -1003,9 +1088,7 @@ __global__ __launch_bounds__(64 * NW) void train_fused_out_kernel(const FusedArg
         const int e = tid + j * NT, m = m0 + (e >> 5), o = e & 31;
         pre[j] = 0.0f;
         if (m >= R || o >= J) continue;
-        const int64_t src = F.idx[m / F.H] * F.H + m % F.H;
-        const float t = o < S ? F.gns[src * S + o] : F.grw[src];
-        pre[j] = t - (o < S ? F.bo[o] : F.bo_r[o - S]);
+        pre[j] = F.tgt[(int64_t)m * J + o] - (o < S ? F.bo[o] : F.bo_r[o - S]);
     }
     for (int e = tid; e < TT * TT; e += NT) {
         const int r = e >> 5, col = e & 31, m = m0 + r, n = n0 + col;
@@ -1150,6 +1233,15 @@ __global__ __launch_bounds__(64 * NW) void train_fused_out_kernel(const FusedArg
     __syncthreads();
     FSTAMP(1, 3);
     if (!last) return;
+    // every load of the tail first (db_out's and db_1's column sums, then the partials): one round trip
+    const bool dyt = tn == 0 && tid < J, tfast = F.tiles_r <= 16;
+    float cs[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const float* src = dyt ? F.cs_dy + (int64_t)i * J + tid : F.cs_dh1 + (int64_t)i * W + n0 + tid - 64;
+        cs[i] = ((dyt || b1t) && tfast && i < F.tiles_r)
+                    ? __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0f;
+    }
     for (int e = tid; e < J * TT; e += NT) {
         const int o = e / TT, i = n0 + (e - o * TT);
         if (i >= W) continue;
@@ -1167,20 +1259,26 @@ __global__ __launch_bounds__(64 * NW) void train_fused_out_kernel(const FusedArg
         if (o < S) F.dwo[(int64_t)o * W + i] = v;
         else F.dwo_r[(int64_t)(o - S) * W + i] = v;
     }
-    if (tn == 0 && tid < J) {
-        const float g = ordered_sum<true>(F.cs_dy + tid, J, F.tiles_r);
-        if (tid < S) F.dbo[tid] = g;
-        else F.dbo_r[tid - S] = g;
-    }
-    // db_1 of this column block (the five-launch layout's dW_1 launch summed the same column sums in the
-    // same order), and b_1's Adam step: nothing reads b_1 before the next batch's F
-    if (tid >= 64 && tid < 64 + TT && n0 + tid - 64 < W) {
-        const int n = n0 + tid - 64;
-        const float g = ordered_sum<true>(F.cs_dh1 + n, W, F.tiles_r);
-        F.db1[n] = g;
-        if (F.adam)
-            adam_element(F.ab1.param[n], g, F.ab1.exp_avg[n], F.ab1.exp_avg_sq[n], F.ab1.step_size, F.ab1.bc2_sqrt,
-                         F.hp, F.arith);
+    if (dyt || b1t) {
+        float g = cs[0];
+#pragma unroll
+        for (int i = 1; i < 16; ++i)
+            if (i < F.tiles_r) g = g + cs[i];
+        if (dyt) {              // db_out
+            if (!tfast) g = ordered_sum<true>(F.cs_dy + tid, J, F.tiles_r);
+            if (tid < S) F.dbo[tid] = g;
+            else F.dbo_r[tid - S] = g;
+        } else {                // db_1 (the five-launch layout's dW_1 launch summed the same column sums in
+            const int n = n0 + tid - 64;   // the same order) and b_1's Adam step: nothing reads b_1 before
+            if (!tfast) g = ordered_sum<true>(F.cs_dh1 + n, W, F.tiles_r);   // the next batch's F
+            F.db1[n] = g;
+            if (F.adam) {
+                adam_element(b1p, g, b1m, b1v, F.ab1.step_size, F.ab1.bc2_sqrt, F.hp, F.arith);
+                F.ab1.param[n] = b1p;
+                F.ab1.exp_avg[n] = b1m;
+                F.ab1.exp_avg_sq[n] = b1v;
+            }
+        }
     }
 }
 
@@ -1247,6 +1345,7 @@ struct TrainWs {
     float* act[MBRL_TRAIN_MAX_LAYERS];
     float *dh[2], *dy, *loss_part, *xbuf, *cs_dy, *cs_dh[2], *fold_part;
     float* out_part;      // fused step: the output layer's weight-gradient partials [row tile][J][W]
+    float* tgt;           // fused step: the batch's targets [R][J] (F gathers, O reads)
     unsigned* tickets;    // [ceil(W / 32)] each: the dW_0 fold's, the fused dW_out fold's, the fused dH_0
                           // tiles' W_1-read arrivals
     unsigned* status;     // fused step: bit 0 = a bounded wait timed out (never expected)
@@ -1271,6 +1370,7 @@ static TrainWs train_ws(const TrainShape& t, int batch, float* base) {
     w.cs_dh[1] = take(tiles_r * W);
     w.fold_part = take(tiles_r * W * (size_t)(t.s + t.a));   // the folded dW_0's per-32-row partials
     w.out_part = take(tiles_r * J * W);
+    w.tgt = take(R * J);
     w.tickets = reinterpret_cast<unsigned*>(take(3 * ((W + TT - 1) / TT)));
     w.status = reinterpret_cast<unsigned*>(take(1));
     w.floats = off;
@@ -1337,7 +1437,7 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
         F.nwb = fold_nw;
         F.w0 = w.weight[0]; F.b0 = w.bias[0]; F.w1 = w.weight[1]; F.b1 = w.bias[1];
         F.wo = w.weight[L]; F.wo_r = wo_r; F.bo = w.bias[L]; F.bo_r = bo_r;
-        F.act0 = B.act[0]; F.act1 = B.act[1]; F.xstore = B.xbuf;
+        F.act0 = B.act[0]; F.act1 = B.act[1]; F.xstore = B.xbuf; F.tgt = B.tgt;
         F.dh1 = B.dh[1]; F.cs_dh1 = B.cs_dh[1]; F.cs_dy = B.cs_dy; F.loss_part = B.loss_part;
         F.out_part = B.out_part;
         F.dwo = w.weight_grad[L]; F.dwo_r = t.reward ? w.weight_grad[L + 1] : w.weight_grad[L];
