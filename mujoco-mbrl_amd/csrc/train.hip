@@ -500,8 +500,11 @@ __device__ __forceinline__ void gemm_tile(const GemmLaunch& L, int tile, float (
             v = d * (n < O.s ? O.scale_s : O.scale_r);
         }
         keep[j] = v;
-        float* dst = m < O.split ? O.c0 + (int64_t)m * O.ldc : O.c1 + (int64_t)(m - O.split) * O.ldc;
-        dst[n] = v;
+        // (with the dW_0 fold nothing reads dH_0 after this launch: its tiles keep it in LDS only)
+        if (!(O.mode == EPI_MASK && O.fold)) {
+            float* dst = m < O.split ? O.c0 + (int64_t)m * O.ldc : O.c1 + (int64_t)(m - O.split) * O.ldc;
+            dst[n] = v;
+        }
         if (O.mode == EPI_GRAD && O.adam) {
             const int64_t i = (int64_t)m * O.ldc + n;
             adam_element(ap[j], v, am[j], av[j], O.aw.step_size, O.aw.bc2_sqrt, L.hp, L.arith);
