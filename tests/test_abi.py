@@ -177,3 +177,20 @@ def test_options_are_set_through_the_abi_not_the_environment():
     csrc = os.path.join(REPO, "mujoco-mbrl_amd", "csrc")
     for f in os.listdir(csrc):
         assert "getenv" not in open(os.path.join(csrc, f)).read(), f
+
+
+def test_training_workspace_and_status_word_sizing():
+    """mbrl_train_workspace_bytes / mbrl_train_status_offset need no GPU: the fused step's status word
+    lies inside the workspace, 4-byte aligned, for every shape; bad shapes give 0 / (size_t)-1."""
+    from mbrl_amd import _lib
+    lib = _lib.load()
+    for s, a, W, L, reward, H, B in [(17, 6, 512, 2, 0, 1, 512), (17, 6, 200, 2, 1, 1, 400), (5, 1, 50, 3, 0, 2, 37)]:
+        m = _lib.TrainModel()
+        m.state_dim, m.action_dim, m.hidden, m.n_hidden, m.reward_head, m.horizon = s, a, W, L, reward, H
+        need = lib.mbrl_train_workspace_bytes(ctypes.byref(m), B)
+        at = lib.mbrl_train_status_offset(ctypes.byref(m), B)
+        assert need > 0 and at % 4 == 0 and at + 4 <= need, (s, W, L, need, at)
+    bad = _lib.TrainModel()
+    bad.state_dim, bad.action_dim, bad.hidden, bad.n_hidden, bad.reward_head, bad.horizon = 17, 6, 512, 0, 0, 1
+    assert lib.mbrl_train_workspace_bytes(ctypes.byref(bad), 512) == 0
+    assert lib.mbrl_train_status_offset(ctypes.byref(bad), 512) == ctypes.c_size_t(-1).value
