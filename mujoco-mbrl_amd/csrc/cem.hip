@@ -1675,8 +1675,15 @@ int mbrl_train_epoch(const mbrl_train_model* model, const mbrl_train_data* data,
     // after the last batch
     mbrl_adam_tensor carry[2][4];
     int carry_n = 0;
+    // the fused step's F gathers the next batch's rows while it runs when both batches are full-size
+    // fused ones (alternating gather slots; the first batch gathers its own)
+    TrainGather gather{};
     for (int64_t b = 0; b < batches; ++b) {
         const int n = (int)std::min<int64_t>(batch_size, rows - b * batch_size);
+        const int n_next = b + 1 < batches ? (int)std::min<int64_t>(batch_size, rows - (b + 1) * batch_size) : 0;
+        const bool hand = n_next == n && t.W > 32 && train_fused_applies(t, n);   // (F's second column tiles)
+        gather.idx_next = hand ? order + (b + 1) * batch_size : nullptr;
+        gather.batch_next = hand ? n_next : 0;
         for (int i = 0; i < count; ++i) {
             table[i].step_size = step_sizes[b * count + i];
             table[i].bc2_sqrt = bc2_sqrt[b * count + i];
@@ -1685,9 +1692,11 @@ int mbrl_train_epoch(const mbrl_train_model* model, const mbrl_train_data* data,
         int next_n = 0;
         if (int rc = hip_check(launch_train_grads(t, w, order + b * batch_size, n, losses ? losses + 3 * b : nullptr,
                                                   static_cast<float*>(workspace), st, fold ? table.data() : nullptr,
-                                                  hparams, ar, carry[b & 1], carry_n, next, &next_n),
+                                                  hparams, ar, carry[b & 1], carry_n, next, &next_n, &gather),
                                "train_epoch grads"))
             return rc;
+        gather.pre_rows = hand ? 1 : 0;
+        if (hand) gather.slot ^= 1;
         carry_n = next_n;
         if (!fold)
             if (int rc = hip_check(launch_adam_step(table.data(), count, *hparams, ar, st), "train_epoch adam")) return rc;

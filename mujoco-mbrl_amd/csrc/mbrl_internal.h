@@ -402,11 +402,23 @@ size_t train_status_offset(const TrainShape& t, int batch);   // bytes: the fuse
 // With the layer-0 fold one layer's step cannot ride in this step's launches: it comes back in
 // pending[0 .. *pending_n) (then required with adam) for the caller to pass as the next step's
 // `prior` (taken by its first launch) or to run with launch_adam_step.
+// The fused step (two hidden layers) can gather the NEXT batch's rows while it runs: `next`
+// (rows idx_next[0 .. batch_next)) goes to the gather buffers of slot `slot ^ 1`, and the next call
+// then passes pre_rows = 1 with that slot (mbrl_train_epoch). train_fused_applies: whether a batch of
+// `batch` transitions takes the fused step.
+struct TrainGather {
+    const int64_t* idx_next;
+    int batch_next;
+    int pre_rows;
+    int slot;
+};
+bool train_fused_applies(const TrainShape& t, int batch);
 hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const int64_t* idx, int batch,
                               float* loss_out, float* ws, hipStream_t stream, const mbrl_adam_tensor* adam = nullptr,
                               const mbrl_adam_hparams* hp = nullptr, int arith = 0,
                               const mbrl_adam_tensor* prior = nullptr, int prior_n = 0,
-                              mbrl_adam_tensor* pending = nullptr, int* pending_n = nullptr);
+                              mbrl_adam_tensor* pending = nullptr, int* pending_n = nullptr,
+                              const TrainGather* gather = nullptr);
 
 // ---- cooperative single-candidate kernels (traj.hip, gd.hip): the dot of one 16-row slice, one row
 // per half-wave (32 lanes), and its reduction

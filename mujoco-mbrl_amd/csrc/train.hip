@@ -16,6 +16,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <utility>
+
 #include "../../include/mbrl_cem.h"
 #include "mbrl_internal.h"
 
@@ -832,6 +834,10 @@ struct FusedArgs {
     const float *wo, *wo_r, *bo, *bo_r; // output layer: state rows from wo / bo, the reward row from *_r
     float *act0, *act1, *xstore;
     float* tgt;                         // [R][J] the batch's targets, gathered by F's first column tiles for O
+    int pre_rows;                       // 1: xstore / tgt already hold this batch (the previous F gathered it)
+    const int64_t* idx_next;            // non-NULL: F's second column tiles gather the next batch's rows
+    int R_next;                         //   (R_next of them) into xnext / tnext
+    float *xnext, *tnext;
     float *dh1, *cs_dh1, *cs_dy, *loss_part, *out_part;
     float *dwo, *dwo_r, *dbo, *dbo_r;
     unsigned* out_ticket;               // [tiles_n] arrivals per column block of dH_1 tiles (O)
@@ -884,11 +890,13 @@ __global__ __launch_bounds__(64 * NW) void train_fused_fwd_kernel(const FusedArg
     // after them, and the weights travel while the rows do)
     constexpr int GPT = TT * 16 * KCH / NT;      // gathered elements per thread (k0pad <= 16 KCH)
     const int k0pad = (K0 + 15) & ~15;
-    int64_t gi[GPT];
+    const bool nx = F.idx_next != nullptr && tn == 1;   // the second column tiles gather the next batch
+    int64_t gi[GPT], gn[GPT];
 #pragma unroll
     for (int j = 0; j < GPT; ++j) {
         const int e = tid + j * NT, r = e / k0pad, k = e - r * k0pad, m = m0 + r;
-        gi[j] = (r < TT && m < R && k < K0) ? F.idx[m / F.H] : -1;
+        gi[j] = (r < TT && m < R && k < K0) ? (F.pre_rows ? 0 : F.idx[m / F.H]) : -1;
+        gn[j] = (nx && r < TT && m < F.R_next && k < K0) ? F.idx_next[m / F.H] : -1;
     }
     // the first column tiles also gather the targets O's loss epilogue needs (J <= 32: 32 x 32 slots)
     constexpr int TPT = TT * TT / NT;
@@ -896,8 +904,10 @@ __global__ __launch_bounds__(64 * NW) void train_fused_fwd_kernel(const FusedArg
     int64_t tsrc[TPT];
 #pragma unroll
     for (int j = 0; j < TPT; ++j) {
-        const int e = tid + j * NT, r = e >> 5, o = e & 31;
-        tsrc[j] = (tn == 0 && o < F.J && m0 + r < R) ? F.idx[(m0 + r) / F.H] * F.H + (m0 + r) % F.H : -1;
+        const int e = tid + j * NT, r = e >> 5, o = e & 31, m = m0 + r;
+        tsrc[j] = -1;
+        if (!F.pre_rows && tn == 0 && o < F.J && m < R) tsrc[j] = F.idx[m / F.H] * F.H + m % F.H;
+        if (nx && o < F.J && m < F.R_next) tsrc[j] = F.idx_next[m / F.H] * F.H + m % F.H;
     }
     // the rows (zero past K0 to the chunk end); the first column tile keeps them for the layer-0 weight
     // gradient, as the layer-0 launch did
@@ -907,9 +917,20 @@ __global__ __launch_bounds__(64 * NW) void train_fused_fwd_kernel(const FusedArg
         const int e = tid + j * NT, r = e / k0pad, k = e - r * k0pad, m = m0 + r;
         gv[j] = 0.0f;
         if (gi[j] >= 0) {
-            const int64_t src = gi[j] * F.H + m % F.H;
-            gv[j] = k < F.s ? F.gs[src * F.s + k] : F.ga[src * F.a + (k - F.s)];
+            if (F.pre_rows) {
+                gv[j] = F.xstore[(int64_t)m * K0 + k];
+            } else {
+                const int64_t src = gi[j] * F.H + m % F.H;
+                gv[j] = k < F.s ? F.gs[src * F.s + k] : F.ga[src * F.a + (k - F.s)];
+            }
         }
+    }
+    float gx[GPT];
+#pragma unroll
+    for (int j = 0; j < GPT; ++j) {
+        const int e = tid + j * NT, r = e / k0pad, k = e - r * k0pad, m = m0 + r;
+        const int64_t src = gn[j] * F.H + m % F.H;
+        gx[j] = gn[j] < 0 ? 0.0f : k < F.s ? F.gs[src * F.s + k] : F.ga[src * F.a + (k - F.s)];
     }
 #pragma unroll
     for (int j = 0; j < TPT; ++j) {
@@ -952,12 +973,13 @@ __global__ __launch_bounds__(64 * NW) void train_fused_fwd_kernel(const FusedArg
     for (int j = 0; j < GPT; ++j) {
         const int e = tid + j * NT, r = e / k0pad, k = e - r * k0pad, m = m0 + r;
         if (r < TT) xr[r][k] = gv[j];
-        if (gi[j] >= 0 && tn == 0) F.xstore[(int64_t)m * K0 + k] = gv[j];
+        if (gi[j] >= 0 && tn == 0 && !F.pre_rows) F.xstore[(int64_t)m * K0 + k] = gv[j];
+        if (gn[j] >= 0) F.xnext[(int64_t)m * K0 + k] = gx[j];
     }
 #pragma unroll
     for (int j = 0; j < TPT; ++j) {
         const int e = tid + j * NT, r = e >> 5, o = e & 31;
-        if (tsrc[j] >= 0) F.tgt[(int64_t)(m0 + r) * F.J + o] = tv[j];
+        if (tsrc[j] >= 0) (nx ? F.tnext : F.tgt)[(int64_t)(m0 + r) * F.J + o] = tv[j];
     }
     __syncthreads();
     FSTAMP(0, 1);
@@ -1347,6 +1369,7 @@ static hipError_t launch_gemm(GemmLaunch& L, bool loss_wg, hipStream_t stream) {
 struct TrainWs {
     float* act[MBRL_TRAIN_MAX_LAYERS];
     float *dh[2], *dy, *loss_part, *xbuf, *cs_dy, *cs_dh[2], *fold_part;
+    float *xbuf2, *tgt2;  // the fused step's second gather slot (the next batch's rows and targets)
     float* out_part;      // fused step: the output layer's weight-gradient partials [row tile][J][W]
     float* tgt;           // fused step: the batch's targets [R][J] (F gathers, O reads)
     unsigned* tickets;    // [ceil(W / 32)] each: the dW_0 fold's, the fused dW_out fold's, the fused dH_0
@@ -1374,6 +1397,8 @@ static TrainWs train_ws(const TrainShape& t, int batch, float* base) {
     w.fold_part = take(tiles_r * W * (size_t)(t.s + t.a));   // the folded dW_0's per-32-row partials
     w.out_part = take(tiles_r * J * W);
     w.tgt = take(R * J);
+    w.xbuf2 = take(R * (t.s + t.a));
+    w.tgt2 = take(R * J);
     w.tickets = reinterpret_cast<unsigned*>(take(3 * ((W + TT - 1) / TT)));
     w.status = reinterpret_cast<unsigned*>(take(1));
     w.floats = off;
@@ -1403,10 +1428,12 @@ static bool fused_step(const TrainShape& t, int fold_nw) {
     return t.split == 0 && t.L == 2 && fold_nw > 0 && J <= TT && K0 <= FUSED_K0MAX && t.W <= FUSED_WMAX;
 }
 
+bool train_fused_applies(const TrainShape& t, int batch) { return fused_step(t, fold_waves(t, batch * t.H)); }
+
 hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const int64_t* idx, int batch,
                               float* loss_out, float* ws, hipStream_t stream, const mbrl_adam_tensor* adam,
                               const mbrl_adam_hparams* hp, int arith, const mbrl_adam_tensor* prior, int prior_n,
-                              mbrl_adam_tensor* pending, int* pending_n) {
+                              mbrl_adam_tensor* pending, int* pending_n, const TrainGather* gather) {
     const int R = batch * t.H, W = t.W, K0 = t.s + t.a, J = t.s + (t.reward ? 1 : 0), L = t.L;
     const int tiles_r = (R + TT - 1) / TT;
     const int fold_nw = fold_waves(t, R);
@@ -1414,7 +1441,15 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
     if (pending_n) *pending_n = 0;
     if ((prior_n > 0 && !prior) || prior_n > ADAM_FUSED_MAX || (adam && fold_nw && (!pending || !pending_n)))
         return hipErrorInvalidValue;
-    const TrainWs B = train_ws(t, batch, ws);
+    TrainWs B = train_ws(t, batch, ws);
+    // the fused step's gather slot: the caller alternates them when F gathers the next batch
+    float *xnext = B.xbuf2, *tnext = B.tgt2;
+    if (fused && gather && gather->slot) {
+        std::swap(B.xbuf, B.xbuf2);
+        std::swap(B.tgt, B.tgt2);
+        xnext = B.xbuf2;
+        tnext = B.tgt2;
+    }
     const float* wo_r = t.reward ? w.weight[L + 1] : nullptr;
     const float* bo_r = t.reward ? w.bias[L + 1] : w.bias[L];
 
@@ -1441,6 +1476,15 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
         F.w0 = w.weight[0]; F.b0 = w.bias[0]; F.w1 = w.weight[1]; F.b1 = w.bias[1];
         F.wo = w.weight[L]; F.wo_r = wo_r; F.bo = w.bias[L]; F.bo_r = bo_r;
         F.act0 = B.act[0]; F.act1 = B.act[1]; F.xstore = B.xbuf; F.tgt = B.tgt;
+        if (gather) {   // (the workspace layout depends on the batch size: only equal batches hand over)
+            F.pre_rows = gather->pre_rows;
+            if (gather->idx_next && gather->batch_next == batch && tiles_n > 1) {
+                F.idx_next = gather->idx_next;
+                F.R_next = gather->batch_next * t.H;
+                F.xnext = xnext;
+                F.tnext = tnext;
+            }
+        }
         F.dh1 = B.dh[1]; F.cs_dh1 = B.cs_dh[1]; F.cs_dy = B.cs_dy; F.loss_part = B.loss_part;
         F.out_part = B.out_part;
         F.dwo = w.weight_grad[L]; F.dwo_r = t.reward ? w.weight_grad[L + 1] : w.weight_grad[L];
