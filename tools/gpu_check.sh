@@ -25,7 +25,7 @@ fi
 if [ "$STEP" = all ] || [ "$STEP" = prof ]; then
   rm -rf gpurun_out/prof
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
-      python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-variants --no-train ${PROF_ARGS:-} > gpurun_out/prof.log 2>&1
+      python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-variants --no-train --no-strong ${PROF_ARGS:-} > gpurun_out/prof.log 2>&1
   rc=$?; echo "rocprof rc=$rc"; tail -3 gpurun_out/prof.log
   find gpurun_out/prof -name "*stats*" | head
   python3 tools/prof_summary.py gpurun_out/prof gpurun_out/prof.log 20 gpurun_out/prof/rollout_summary.json
