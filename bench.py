@@ -579,7 +579,7 @@ def main():
             plan_gpu_ms=timed.plan_gpu_ms if world > 1 else plan_gpu_ms,
             rollout_avg_launch_ms=h_rollout_s * 1e3,
             rollout_frac=h_flop / h_rollout_s / 1e12 / PEAK_FP32_MFMA_TFLOPS)
-    if rank == 0 and not args.no_train:
+    if rank == 0 and world == 1 and not args.no_train:   # (single-GPU runs only: no rank waits on it)
         out["train"] = train_line(dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.config, budget_s=args.cpu_budget)
