@@ -306,3 +306,37 @@ def test_fused_step_is_bitwise_neutral(kind, s, a, W, H, B):
     for (ka, ma, va), (kb, mb, vb) in zip(sa, sb):
         assert ka == kb and torch.equal(ma, mb) and torch.equal(va, vb)
     assert ra == rb and len(ra) > 0
+
+
+@pytest.mark.parametrize("case", range(12))
+def test_fused_step_random_shapes_bitwise(case):
+    """The fused three-launch step against the five-launch layout at random shapes it accepts (two
+    hidden layers, s + a <= 64, J <= 32, W <= 512, batch rows in the dW_0 fold's ranges): gradients and
+    losses bit for bit, and the status word clear."""
+    from mbrl_amd import _lib, models
+    rng = np.random.default_rng(7000 + case)
+    kind = "reward" if case % 3 == 2 else "model"
+    s = int(rng.integers(1, 31 if kind == "reward" else 32))
+    a = int(rng.integers(1, 64 - s + 1))
+    W = int(rng.choice([33, 50, 64, 97, 128, 200, 255, 256, 333, 400, 512]))
+    H = int(rng.integers(1, 3))
+    lo, hi = [(64, 128), (256, 512)][int(rng.integers(0, 2))]
+    B = int(rng.integers(lo // H + 1, hi // H + 1))
+    R = B * H
+    nw = 16 if R >= 256 else 4   # train.hip fold_waves: the fused step needs the dW_0 fold (per == 2)
+    assert lo < R <= hi and (((R + 15) // 16 + nw - 1) // nw) == 2
+    ds = _dataset(s, a, H, 3 * B + 5, seed=case)
+    _, ins, outs = ds.stacked(DEV)
+    reward = kind == "reward"
+    idx = torch.randperm(ds.num_transitions(), generator=torch.Generator().manual_seed(case))[:B].to(DEV)
+    got = {}
+    for split in (1, 0):
+        with _lib.option("train_split", split):
+            m = _model(kind, s, a, W, 2, seed=case)
+            nat = models._NativeGrads(m, ins, outs, ds.horizon, B, reward)
+            loss, parts = nat.run(idx)
+            torch.cuda.synchronize()
+            nat.check_status()
+            got[split] = [loss.clone(), parts[0].clone(), parts[1].clone()] + [p.grad.clone() for p in m.parameters()]
+    for i, (x, y) in enumerate(zip(got[0], got[1])):
+        assert torch.equal(x, y), (case, kind, s, a, W, H, B, i, float((x - y).abs().max()))
