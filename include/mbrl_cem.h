@@ -417,7 +417,9 @@ int mbrl_train_grads(const mbrl_train_model* model, const mbrl_train_data* data,
  * step's scalars step_sizes[b * count + i], bc2_sqrt[b * count + i] (host arrays, computed as for
  * mbrl_adam_step). The host issues every launch of the epoch in one call. losses: [batches][3]
  * device floats (total, state, reward per batch) or NULL. workspace as for mbrl_train_grads with
- * batch = batch_size. */
+ * batch = batch_size. Two hidden layers (the reference's models): three launches per batch with the
+ * Adam step inside them, each batch's launches also gathering the next batch's rows; the result is
+ * the per-batch calls' bit for bit (tests/test_gpu_train_native.py). */
 int mbrl_train_epoch(const mbrl_train_model* model, const mbrl_train_data* data, const int64_t* order, int64_t rows,
                      int32_t batch_size, const mbrl_adam_tensor* tensors, int32_t count,
                      const mbrl_adam_hparams* hparams, const float* step_sizes, const float* bc2_sqrt, float* losses,
