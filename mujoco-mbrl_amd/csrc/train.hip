@@ -426,7 +426,7 @@ __device__ __forceinline__ void gemm_tile(const GemmLaunch& L, int tile, float (
             xv[j] = (k < O.fold_k0 && m0 + r < D.M) ? O.fold_x[(int64_t)(m0 + r) * O.fold_k0 + k] : 0.0f;
         }
     }
-    TSTAMP(1);
+    // (stamp slots: 0 entry, 1 K loop done, 2 after the reduction barrier / arrival wait, 3 exit)
     // up to GROUP chunks' operands in flight at once, then their MFMAs: with the usual 1-4 chunks
     // per wave the loads' latency is paid once
     constexpr int GROUP = NW == 16 ? (TMX == 2 ? 1 : 2) : 4;   // TMX 2 at 16 waves: the 128-VGPR budget
@@ -456,7 +456,7 @@ __device__ __forceinline__ void gemm_tile(const GemmLaunch& L, int tile, float (
                         acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][x][s], b[u][y][s], acc[x][y], 0, 0, 0);
         }
     }
-    TSTAMP(2);
+    TSTAMP(1);
     // lane l holds C rows 16x + 4q + v, column 16y + c
 #pragma unroll
     for (int x = 0; x < 2 * TMX; ++x)
@@ -478,6 +478,7 @@ __device__ __forceinline__ void gemm_tile(const GemmLaunch& L, int tile, float (
 
     if (O.mode == EPI_GRAD && O.adam && O.wait_ticket)
         wait_arrivals(O.wait_ticket + n0 / TT, O.wait_count, O.wait_status);
+    TSTAMP(2);
 
     // the fused epilogue, EPT C elements per thread; each element sums the waves' partials in wave
     // order. Elements of this tile that feed the next layer's bias gradient (EPI_MASK, EPI_LOSS)

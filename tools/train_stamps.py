@@ -4,7 +4,8 @@ the first tile of a launch's second product, else the last workgroup). Two runs:
 (gradient only) and the last step of an mbrl_train_epoch over whole batches (Adam in the launches).
 Usage: make -C mujoco-mbrl_amd diag && python tools/train_stamps.py [W] [split]
 
-Stamp points: gemm launches (train_gemm_kernel): entry, epilogue operands issued, K loop done, exit.
+Stamp points: gemm launches (train_gemm_kernel): entry, K loop done, after the partial-sum barrier
+(and a dW tile's arrival wait), exit.
 Fused F: entry, input gathered, H_0 rows in LDS, exit. Fused O: entry, dY in LDS, dH_1 / dW_out
 partials stored, ticket taken (last arriver's sum after)."""
 import ctypes
