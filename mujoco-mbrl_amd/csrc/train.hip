@@ -813,12 +813,15 @@ __global__ __launch_bounds__(64 * NW) void train_gemm_kernel(const GemmLaunch L)
 //   F  train_fused_fwd_kernel: per 32 x 32 tile of H_1, the tile's 32 rows of H_0 are recomputed into
 //      LDS (K0 = s + a is small: the layer-0 launch's 4-wave K split, summed in its wave order), then
 //      the H_1 tile is the layer-1 launch's tile with its A operand from LDS. Removes a launch and
-//      the H_0 round trip through memory before the layer-1 products.
+//      the H_0 round trip through memory before the layer-1 products. The first column tiles also
+//      gather the batch's targets for O; in mbrl_train_epoch the second column tiles gather the next
+//      batch's rows and targets into the other gather slot.
 //   O  train_fused_out_kernel: per 32 x 32 tile of dH_1, the tile's 32 rows of dY (the output-layer
 //      launch's tile: loss partials and dY column sums from the first column tile), dH_1 =
 //      (dY W_out) * (H_1 > 0), and the output layer's weight-gradient partial over the tile's 32 rows
 //      -- exactly wave tm of the separate dW_out product -- summed in wave order by the column block's
-//      last arriver (the dW_0 fold's hand-off). Removes a launch and the dY round trip.
+//      last arriver (the dW_0 fold's hand-off), which also finishes db_out, db_1 and b_1's Adam step.
+//      Removes a launch and the dY round trip.
 //   B  launch_gemm: dH_0 with the folded dW_0 and its Adam step, dW_1 -- whose tiles step W_1 in place
 //      once the dH_0 tiles of their column block have read it -- and the output layer's Adam step as
 //      extra workgroups. No Adam step is deferred to the next batch.
