@@ -104,9 +104,19 @@ bool grid_fits(const void* fn, int threads, size_t lds, int blocks) {
 // ------------------------------------------------------------------------------------------------
 // Weight packing: nn.Linear [out][in] -> fragment stream (see rollout.hip header)
 // ------------------------------------------------------------------------------------------------
-// Hidden-type layer (layer 0 or W->W): chunk kc holds K rows 16kc..16kc+15 for this wave's T tiles.
+// Canonical K order of a W->W layer (r05, DESIGN.md §3 "half-rotated K order"): an output column in
+// the second half (n >= Wpad / 2) consumes its K chunks rotated by half, [nkc/2, nkc) then
+// [0, nkc/2), so the column half a workgroup owns always starts on the inputs it produced itself
+// (the column-split pairs' hand-off then lands behind half a layer of compute). Every fp32 tile
+// height packs and reads the same order, so their sums stay bit-identical.
+__device__ __forceinline__ int rot_chunk(int kc, int nkc, int n, int Wpad, int rot) {
+    return (rot && 2 * n >= Wpad) ? (kc + nkc / 2) % nkc : kc;
+}
+
+// Hidden-type layer (layer 0 or W->W): chunk kc holds K rows 16kc..16kc+15 for this wave's T tiles
+// (rot: a W->W layer, second-half columns in the rotated order above).
 __global__ void pack_hidden_kernel(const float* __restrict__ w, int in_real, int out_real, int nkc, int T,
-                                   float* __restrict__ dst /* chunk base */) {
+                                   int rot, float* __restrict__ dst /* chunk base */) {
     const size_t total = (size_t)nkc * 4 * T * 64 * 4;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
         const int s = (int)(i & 3);
@@ -116,7 +126,7 @@ __global__ void pack_hidden_kernel(const float* __restrict__ w, int in_real, int
         const int wave = (int)((frag / T) & 3);
         const int kc = (int)(frag / T / 4);
         const int n = wave * 16 * T + 16 * j + (lane & 15);
-        const int k = 16 * kc + 4 * (lane >> 4) + s;
+        const int k = 16 * rot_chunk(kc, nkc, n, 64 * T, rot) + 4 * (lane >> 4) + s;
         dst[i] = (n < out_real && k < in_real) ? w[(size_t)n * in_real + k] : 0.0f;
     }
 }
@@ -164,7 +174,7 @@ __device__ __forceinline__ void m8kp_index(size_t i, int& lane, int& wave, size_
 }
 
 __global__ void pack_m8_hidden_kernel(const float* __restrict__ w, int in_real, int out_real, int nkc, int T,
-                                      int kp, float* __restrict__ dst) {
+                                      int kp, int rot, float* __restrict__ dst) {
     const size_t total = (size_t)nkc * T * 1024;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
         int n, k;
@@ -173,7 +183,7 @@ __global__ void pack_m8_hidden_kernel(const float* __restrict__ w, int in_real, 
             size_t kc;
             m8kp_index(i, lane, wave, kc, s, q);
             n = 32 * wave + 4 * (lane >> 3) + (lane & 3);
-            k = 16 * (int)kc + 4 * q + s;
+            k = 16 * rot_chunk((int)kc, nkc, n, 64 * T, rot) + 4 * q + s;
         } else {
             const int q = (int)(i & 3);
             const int lane = (int)((i >> 2) & 63);
@@ -182,7 +192,7 @@ __global__ void pack_m8_hidden_kernel(const float* __restrict__ w, int in_real, 
             const int wave = (int)(cw % T);
             const int kc = (int)(cw / T);
             n = 64 * wave + 32 * ((lane >> 2) & 1) + 4 * (lane >> 3) + (lane & 3);
-            k = 16 * kc + 4 * q + s;
+            k = 16 * rot_chunk(kc, nkc, n, 64 * T, rot) + 4 * q + s;
         }
         dst[i] = (n < out_real && k < in_real) ? w[(size_t)n * in_real + k] : 0.0f;
     }
@@ -1460,7 +1470,8 @@ int mbrl_mlp_pack(const mbrl_mlp_shape* shape, const float* const* weights, cons
             if (l < g.L) {
                 const int in_real = l == 0 ? g.s + g.a : g.W;
                 const int nkc = l == 0 ? g.K0C : 4 * g.T;
-                hipLaunchKernelGGL(pack_hidden_kernel, dim3(256), dim3(256), 0, stream, w, in_real, g.W, nkc, g.T, dst);
+                const int rot = l > 0;   // W->W layers: the half-rotated K order of the second column half
+                hipLaunchKernelGGL(pack_hidden_kernel, dim3(256), dim3(256), 0, stream, w, in_real, g.W, nkc, g.T, rot, dst);
                 hipLaunchKernelGGL(pack_bias_kernel, dim3(4), dim3(256), 0, stream, b, g.W, g.Wpad, bias_base + (size_t)l * g.Wpad);
                 hipLaunchKernelGGL(pack_transposed_kernel, dim3(256), dim3(256), 0, stream, w, in_real, g.W, g.Wpad, plain);
                 if (g.split_ok) {
@@ -1473,10 +1484,10 @@ int mbrl_mlp_pack(const mbrl_mlp_shape* shape, const float* const* weights, cons
                 }
                 if (g.m8_ok) {
                     hipLaunchKernelGGL(pack_m8_hidden_kernel, dim3(256), dim3(256), 0, stream, w, in_real, g.W, nkc,
-                                       g.T, (int)(g.T == 4 && g.NOT == 2), m8_base + m8_chunk * 1024 * (size_t)g.T);
+                                       g.T, (int)(g.T == 4 && g.NOT == 2), rot, m8_base + m8_chunk * 1024 * (size_t)g.T);
                     if (g.m4_ok)   // the same chunks without KP pairing (the m8 chunk index = the m4 one here)
                         hipLaunchKernelGGL(pack_m8_hidden_kernel, dim3(256), dim3(256), 0, stream, w, in_real, g.W, nkc,
-                                           g.T, 0, m4_base + m8_chunk * 1024 * (size_t)g.T);
+                                           g.T, 0, rot, m4_base + m8_chunk * 1024 * (size_t)g.T);
                     m8_chunk += nkc;
                 }
                 chunk += nkc;

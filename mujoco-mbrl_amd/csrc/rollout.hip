@@ -484,6 +484,9 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
         xcd_unit(A.xcd_map, ntiles, tile, e);
     }
     const int cw = PAIR ? 4 * half + wave : wave;   // the 8-wave layout's wave whose columns this one computes
+    // half-rotated K order of the W->W layers (cem.hip rot_chunk): a wave whose columns lie in the
+    // second half reads K chunk (kc + 2T) mod 4T at position kc; rof = that offset in floats
+    const int rof = 2 * cw >= NW ? 16 * 2 * T : 0;
     if (A.redo) {
         // F16X3 redo pass (rollout_f16x3.hip): run only where the split kernel left MBRL_REDO_MARK
         bool any = false;
@@ -552,8 +555,10 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
     __syncthreads();
 
     // PAIR: lflag[0] counts the hand-off waves' finished partner copies (the compute waves wait on it),
-    // lflag[1] their drained publishes, lflag[2] the partner flag value seen by hand-off wave 0
-    [[maybe_unused]] const int pwait = PAIR ? (half ? 0 : 2 * T) : -1;   // first K chunk of the partner's columns
+    // lflag[1] their drained publishes, lflag[2] the partner flag value seen by hand-off wave 0.
+    // Both halves run their own K half first (the half-rotated K order, cem.hip rot_chunk): the
+    // partner's columns are K positions [2T, 4T) of every hidden layer for either half.
+    [[maybe_unused]] const int pwait = PAIR ? 2 * T : -1;   // first K position of the partner's columns
     [[maybe_unused]] uint32_t xneed = 0;                                   // hand-offs consumed so far
     if constexpr (PAIR) {
         if (wave >= 4) {
@@ -730,7 +735,8 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
 #define MBRL_HIDDEN_CHUNK(SLOT, KC, NK, IN)                                          \
     do {                                                                             \
         MBRL_LOAD_CHUNK(ring[((SLOT) + NB - 1) % NB], g + NB - 1);                   \
-        if (LFLAGS && (KC) + 1 < (NK) && ((KC) + 1) % TW == 0) wait_layer(lflag, ((KC) + 1) / TW, nstore); \
+        if (LFLAGS && (KC) + 1 < (NK) && ((KC) + 1) % TW == 0)                        \
+            wait_layer(lflag, (((KC) + 1 + rof / 16) % (NK)) / TW, nstore);            \
         if (PAIR && (KC) + 1 == pwl) lds_wait_ge(lflag, 4 * ++xneed);               \
         if (MBRL_PRIO == 2 && NW == 8) {                                             \
             if (young != (((KC) & 1) != 0)) __builtin_amdgcn_s_setprio(1);          \
@@ -809,14 +815,16 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
         for (int l = 1; l < A.L; ++l) {
             zero_acc<TW, R>(acc);
             load_bias<TW>(bias, L.hbias + l * A.Wpad, cw, lane);
-            if constexpr (LFLAGS) wait_layer(lflag, 0, nstore);
-            pwl = (L0DUP && l == 1) ? -1 : pwait;                   // layer 0's partner columns are local
-            if (PAIR && pwl == 0) lds_wait_ge(lflag, 4 * ++xneed);      // half 1: the partner's columns come first
-            read_a<R>(aAB[0], in, A.lda, 0, lane);
             constexpr int KH = 4 * T;  // 4T % NB == 0: every hidden layer starts on the same slot
             constexpr int S0 = RING ? K0C_T % NB : 0;
+            if constexpr (LFLAGS) wait_layer(lflag, (rof / 16) / TW, nstore);
+            pwl = (L0DUP && l == 1) ? -1 : pwait;                   // layer 0's partner columns are local
+            // K position kc reads chunk kc + rof/16 (kc < 2T) or kc - rof/16 (kc >= 2T): two bases
+            const float* const inLo = in + rof;
+            const float* const inHi = in - rof;
+            read_a<R>(aAB[0], inLo, A.lda, 0, lane);
 #pragma unroll
-            for (int kc = 0; kc < KH; ++kc) MBRL_HIDDEN_CHUNK((S0 + kc) % NB, kc, KH, in);
+            for (int kc = 0; kc < KH; ++kc) MBRL_HIDDEN_CHUNK((S0 + kc) % NB, kc, KH, (kc + 1 < KH / 2 ? inLo : inHi));
             STAMP(2);
             if (l + 1 < A.L) {
                 if constexpr (LFLAGS) hidden_store_flag<TW, R>(acc, bias, out, A.lda, cw, lane, lflag, ++nstore);
@@ -1146,6 +1154,9 @@ __global__ void __launch_bounds__(64 * m8_waves(T, NOT_T), 1) rollout_m8_kernel(
     const int awave = wave - 2;
     float* acs = L.aterm;
     const int cand = lane & 7;
+    // the half-rotated K order of the W->W layers (rollout_kernel): waves whose features lie in the
+    // second half start at chunk KH / 2
+    const int rofc = 2 * FPW * wave >= 64 * T ? KH / 2 : 0;
     float av[1][MAX_A_PER_LANE];
     float acp[1];
     auto fetch_a = [&](int t) {
@@ -1294,7 +1305,8 @@ __global__ void __launch_bounds__(64 * m8_waves(T, NOT_T), 1) rollout_m8_kernel(
 #define M8_CHUNK(SLOT, KC, NK, IN, FL)                                      \
     do {                                                                    \
         M8_LOAD(((SLOT) + NB - 1) % NB, g + NB - 1);                         \
-        if (LFLAGS && (FL) && (KC) + 1 < (NK) && ((KC) + 1) % CPW == 0) wait_layer(lflag, ((KC) + 1) / CPW, nstore); \
+        if (LFLAGS && (FL) && (KC) + 1 < (NK) && ((KC) + 1) % CPW == 0)      \
+            wait_layer(lflag, (((KC) + 1 + rofc) % (NK)) / CPW, nstore);     \
         if (MBRL_PRIO == 2 && NW == 8) {                                    \
             if (young != (((KC) & 1) != 0)) __builtin_amdgcn_s_setprio(1); \
             else __builtin_amdgcn_s_setprio(0);                             \
@@ -1340,10 +1352,13 @@ __global__ void __launch_bounds__(64 * m8_waves(T, NOT_T), 1) rollout_m8_kernel(
         for (int l = 1; l < A.L; ++l) {
             zero_acc8();
             load_bias8(L.hbias + l * A.Wpad);
-            if constexpr (LFLAGS) wait_layer(lflag, 0, nstore);
-            read_b(bb[0], in, 0);
+            if constexpr (LFLAGS) wait_layer(lflag, rofc / CPW, nstore);
+            // the half-rotated K order (rollout_kernel): position kc reads chunk (kc + rofc) mod KH
+            const float* const inLo = in + 16 * rofc;
+            const float* const inHi = in - 16 * rofc;
+            read_b(bb[0], inLo, 0);
 #pragma unroll
-            for (int kc = 0; kc < KH; ++kc) M8_CHUNK((K0C_T + kc) % NB, kc, KH, in, true);
+            for (int kc = 0; kc < KH; ++kc) M8_CHUNK((K0C_T + kc) % NB, kc, KH, (kc + 1 < KH / 2 ? inLo : inHi), true);
             STAMP(2);
             store_layer(out);
             if (l + 1 < A.L) publish_layer();   // the last hidden layer is read back by its own wave only
@@ -1714,9 +1729,13 @@ __global__ void __launch_bounds__(64 * T, 1) rollout_m4_kernel(const RolloutArgs
         for (int l = 1; l < A.L; ++l) {
             acc = f32x4{0.f, 0.f, 0.f, 0.f};
             bias = *reinterpret_cast<const f32x4*>(L.hbias + l * A.Wpad + row0);
-            read_b(bb[0], in, 0);
+            // the half-rotated K order (rollout_kernel): second-half rows start at chunk KH / 2
+            const int rof = 2 * wave >= T ? 16 * (KH / 2) : 0;
+            const float* const inLo = in + rof;
+            const float* const inHi = in - rof;
+            read_b(bb[0], inLo, 0);
 #pragma unroll
-            for (int kc = 0; kc < KH; ++kc) M4_CHUNK((K0C_T + kc) % NB, kc, KH, in);
+            for (int kc = 0; kc < KH; ++kc) M4_CHUNK((K0C_T + kc) % NB, kc, KH, (kc + 1 < KH / 2 ? inLo : inHi));
             store_layer(out);
             if (l + 1 < A.L) __syncthreads();   // the last hidden layer is read back by its own wave only
             float* tmp = in; in = out; out = tmp;
