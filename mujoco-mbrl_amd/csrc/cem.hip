@@ -916,15 +916,30 @@ __global__ void __launch_bounds__(1024) cem_update_kernel(const UpdateArgs U) {
 // (init_mu, init_sigma) and, with `actions`, draws row t of iteration 0's proposals for candidate
 // slice j (fill2_kernel + sample_kernel, bit-identical: the same floats go into cem_action).
 // s0_src (optional): the plan's start state, device or mapped host memory, copied once into the
-// workspace (s0_dst) so that every later launch reads device memory.
+// workspace (s0_dst) so that every later launch reads device memory. draw_off: the global candidate
+// index of local candidate 0 (a sharded plan's rank offset; 0 otherwise). zero[2] / zero_words[2]:
+// the plan's hand-off words (the column-split pairs' flags, the trajectory kernel's granules and
+// status), zeroed here once per plan instead of by a memset before each launch that polls them.
+struct InitZero {
+    unsigned* ptr[2];
+    size_t words[2];
+};
+
 __global__ void __launch_bounds__(1024) cem_init_kernel(uint64_t seed, float init_mu, float init_sigma, float lo,
                                                         float hi, int H, int a, int N, float* __restrict__ mu,
                                                         float* __restrict__ sigma, float* __restrict__ actions,
                                                         const float* __restrict__ s0_src, int s,
-                                                        float* __restrict__ s0_dst) {
+                                                        float* __restrict__ s0_dst, int draw_off, InitZero zero) {
     const int S = gridDim.x / H;
     const int t = blockIdx.x / S, j = blockIdx.x - (blockIdx.x / S) * S, b = blockIdx.y;
     const size_t ro = ((size_t)b * H + t) * a;
+    {
+        const size_t gid = ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x;
+        const size_t gsz = (size_t)gridDim.x * gridDim.y * blockDim.x;
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+            for (size_t i = gid; zero.ptr[r] && i < zero.words[r]; i += gsz) zero.ptr[r][i] = 0u;
+    }
     if (s0_src && blockIdx.x == 0 && b == 0)
         for (int d = threadIdx.x; d < s; d += blockDim.x) s0_dst[d] = s0_src[d];
     if (j == 0)
@@ -937,7 +952,7 @@ __global__ void __launch_bounds__(1024) cem_init_kernel(uint64_t seed, float ini
     for (int idx = threadIdx.x; idx < (n1 - n0) * G; idx += blockDim.x) {
         const int n = n0 + idx / G, g = idx - (idx / G) * G;
         float z[4];
-        cem_normal4(seed, nbase + (uint32_t)n, (uint32_t)t, 0u, (uint32_t)g, z);
+        cem_normal4(seed, nbase + (uint32_t)draw_off + (uint32_t)n, (uint32_t)t, 0u, (uint32_t)g, z);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int d = 4 * g + j;
@@ -1054,6 +1069,23 @@ static int pair_forced_check(const Geometry& g, int N) {
     return MBRL_OK;
 }
 
+// The hand-off words a plan's first launch zeroes (cem_init_kernel): the pair flags of a shard of Nl
+// candidates (when the workspace offers pairs) and the trajectory kernel's granules with the status
+// word right behind them (the workspaces lay them out so; else the trajectory launch keeps its memset).
+static InitZero plan_zero(const Geometry& g, int Nl, void* pair, unsigned long long* xchg, size_t xchg_bytes,
+                          unsigned* status) {
+    InitZero z{};
+    if (pair && pair_area_bytes(g, Nl)) {
+        z.ptr[0] = static_cast<unsigned*>(pair);
+        z.words[0] = pair_layout(g.Wpad, g.pw, (Nl + 15) / 16, g.E).zero_bytes / 4;
+    }
+    if (xchg && status && reinterpret_cast<char*>(status) == reinterpret_cast<char*>(xchg) + xchg_bytes) {
+        z.ptr[1] = reinterpret_cast<unsigned*>(xchg);
+        z.words[1] = (xchg_bytes + 16) / 4;
+    }
+    return z;
+}
+
 // The argument checks of rollout_impl that depend on the problem only (not on N or the buffers): the
 // sharded plan runs them before its first collective.
 static int rollout_validate(const Geometry& g, const mbrl_norm* norm, const mbrl_cost* cost) {
@@ -1077,10 +1109,13 @@ static int rollout_validate(const Geometry& g, const mbrl_norm* norm, const mbrl
 }
 
 // pair_area: a pair_area_bytes(g, N) block of the caller's workspace, or NULL (no column-split pairs).
+// pair_epoch: NULL (the pair flags are zeroed by a memset before a pair launch), or the plan's counter
+// of pair launches, whose flags its first launch zeroed (cem_init_kernel): each pair launch takes the
+// next epoch (RolloutArgs), and a memset only when the epochs would outgrow the 32-bit flags.
 static int rollout_impl(const Geometry& g, const void* packed, const mbrl_norm* norm, const mbrl_cost* cost,
                         const float* s0, int s0_per_cand, const float* actions, const mbrl_sampler* sampler,
                         int N, int H, int n_offset, float* costs, float* actions_out, float* states_out,
-                        hipStream_t stream, void* pair_area = nullptr) {
+                        hipStream_t stream, void* pair_area = nullptr, unsigned* pair_epoch = nullptr) {
     if (!packed || !s0 || !costs) return fail(MBRL_EINVAL, "packed, s0 and costs must be non-NULL");
     if (N < 1 || H < 1) return fail(MBRL_EINVAL, "N=%d H=%d must be >= 1", N, H);
     if (!actions && !sampler) return fail(MBRL_EINVAL, "need either actions or a sampler");
@@ -1182,15 +1217,26 @@ static int rollout_impl(const Geometry& g, const void* packed, const mbrl_norm* 
                 const int dpa = g_opt[MBRL_OPT_DEBUG_PAIR_ABORT].load(std::memory_order_relaxed);
                 P.debug_abort = dpa == 1;
                 P.pair_l2 = g_opt[MBRL_OPT_PAIR_L2].load(std::memory_order_relaxed) != 2;
+                const unsigned qs = pair_handoffs(H, g.L);
+                if (pair_epoch && (uint64_t)(*pair_epoch + 1) * qs + 16 < (1ull << 31)) {
+                    P.pair_epoch = ++*pair_epoch;   // flags zeroed by the plan's first launch
+                    P.pair_prezeroed = 1;
+                } else {
+                    P.pair_epoch = 1;               // a memset before the launch; the plan restarts its epochs
+                    P.pair_prezeroed = 0;
+                    if (pair_epoch) *pair_epoch = 1;
+                }
+                P.pair_base = (P.pair_epoch - 1) * qs;
                 const hipError_t err = launch_rollout_pair(P, g.T, stream);
                 if (err == hipSuccess && dpa == 2) return MBRL_OK;   // tests: the pair launch's own results
                 if (err == hipSuccess) {
                     // A pair's halves wait on each other, and a plain launch does not promise that both
-                    // are resident (another stream may hold CUs): a wait that timed out set bit 0 of the
-                    // status word after the flags and left its tile's costs invalid. The launch chosen
-                    // below then recomputes every candidate if that bit is set, else its workgroups exit
-                    // at once (bit-identical sums on every tile height).
+                    // are resident (another stream may hold CUs): a wait that timed out raised the status
+                    // word after the flags to the launch's epoch and left its tile's costs invalid. The
+                    // launch chosen below then recomputes every candidate if it did, else its workgroups
+                    // exit at once (bit-identical sums on every tile height).
                     A.gate = P.pair_flags + (size_t)2 * ntiles * g.E * 32;
+                    A.gate_epoch = P.pair_epoch;
                 } else if (err != hipErrorCooperativeLaunchTooLarge || po == 1) {
                     return hip_check(err, "rollout pair launch");
                 }
@@ -1237,10 +1283,12 @@ static int rollout_impl(const Geometry& g, const void* packed, const mbrl_norm* 
     return hip_check(launch_rollout(A, g.T, R, stream), "rollout launch");
 }
 
+// prezeroed: the plan's first launch zeroed xchg and status (cem_init_kernel), so no memset here.
 static int traj_impl(const Geometry& g, const void* packed, const mbrl_norm* norm, const float* s0,
                      const float* actions, int H, float* states_out, unsigned long long* xchg, size_t xchg_bytes,
-                     unsigned* status, hipStream_t stream) {
+                     unsigned* status, hipStream_t stream, int prezeroed = 0) {
     TrajArgs T{};
+    T.prezeroed = prezeroed;
     T.packed = static_cast<const float*>(packed);
     T.member_stride = g.member_stride;
     T.bias_off = g.stream_floats;
@@ -1825,20 +1873,18 @@ int mbrl_cem_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_no
     PlanWs w = plan_ws(g, p, workspace);
     if (ws_bytes < w.bytes) return fail(MBRL_EWORKSPACE, "workspace %zu < %zu", ws_bytes, w.bytes);
     if ((rc = pair_forced_check(g, p->N))) return rc;
-    const int Ha = p->H * g.a;
     // Launches per iteration: rollout + one fused update (select, refit, next proposals) where it fits;
     // else the proposal draw, rollout, select and refit as separate launches.
     const bool fuse = update_kpt(p->N, p->K, g.a) != 0 && g_opt[MBRL_OPT_UNFUSED_UPDATE].load(std::memory_order_relaxed) == 0;
     const bool fuse_draw = fuse && update_samples(p->N, g.a);
-    if (fuse_draw)
-        hipLaunchKernelGGL(cem_init_kernel, dim3(p->H * draw_slices(p->H, 1, p->N, g.a), 1), dim3(1024), 0, stream,
-                           p->seed, p->init_mu, p->init_sigma, p->lo, p->hi, p->H, g.a, p->N, w.mu[0], w.sigma[0],
-                           w.actions, s0_in, g.s, w.s0);
-    else {
-        hipLaunchKernelGGL(fill2_kernel, dim3((Ha + 255) / 256), dim3(256), 0, stream, w.mu[0], p->init_mu, w.sigma[0],
-                           p->init_sigma, Ha);
-        hipLaunchKernelGGL(copy_kernel, dim3(1), dim3(64), 0, stream, s0_in, (size_t)g.s, w.s0);
-    }
+    // one first launch: distribution rows, the s0 copy, iteration 0's proposals (where the update
+    // fuses the draw), and the plan's hand-off words zeroed (no memset before the pair / trajectory
+    // launches)
+    const InitZero z = plan_zero(g, p->N, w.pair, w.xchg, w.xchg_bytes, w.status);
+    hipLaunchKernelGGL(cem_init_kernel, dim3(p->H * (fuse_draw ? draw_slices(p->H, 1, p->N, g.a) : 1), 1), dim3(1024), 0,
+                       stream, p->seed, p->init_mu, p->init_sigma, p->lo, p->hi, p->H, g.a, p->N, w.mu[0], w.sigma[0],
+                       fuse_draw ? w.actions : nullptr, s0_in, g.s, w.s0, 0, z);
+    unsigned pair_epoch = 0;
     const float* s0 = w.s0;   // the workspace copy (s0_in may be mapped host memory)
     int cur = 0;
     for (int it = 0; it < p->iterations; ++it) {
@@ -1852,7 +1898,8 @@ int mbrl_cem_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_no
             if (rc) return rc;
         }
         rc = rollout_impl(g, packed, norm, cost, s0, 0, fuse_draw ? w.actions : nullptr, fuse_draw ? nullptr : &sp, p->N,
-                          p->H, 0, costs, w.actions, nullptr, stream, pair_area_bytes(g, p->N) ? w.pair : nullptr);
+                          p->H, 0, costs, w.actions, nullptr, stream, pair_area_bytes(g, p->N) ? w.pair : nullptr,
+                          z.ptr[0] ? &pair_epoch : nullptr);
         if (rc) return rc;
         if (rollout_events && rollout_events[2 * it + 1]) {
             rc = hip_check(hipEventRecord(reinterpret_cast<hipEvent_t>(rollout_events[2 * it + 1]), stream), "event");
@@ -1881,7 +1928,8 @@ int mbrl_cem_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_no
     }
     // final mean's rollout -> predicted states [E][H][s] (E == 1: straight into states_out), member mean
     float* per_member = g.E == 1 ? states_out : w.states;
-    rc = traj_impl(g, packed, norm, s0, actions_out, p->H, per_member, w.xchg, w.xchg_bytes, w.status, stream);
+    rc = traj_impl(g, packed, norm, s0, actions_out, p->H, per_member, w.xchg, w.xchg_bytes, w.status, stream,
+                   z.ptr[1] != nullptr);
     if (rc) return rc;
     if (g.E > 1) {
         const int Hs = p->H * g.s;
@@ -2046,17 +2094,22 @@ static int plan_sharded_body(const mbrl_mlp_shape* shape, const void* packed, co
     if ((rc = pair_forced_check(g, p->N / nranks))) return rc;
     if ((rc = rollout_validate(g, norm, cost))) return rc;
     if (!emulate && (rc = rccl_ready())) return rc;
-    const int N = p->N, Nl = N / nranks, H = p->H, a = g.a, E = g.E, Ha = H * a;
+    const int N = p->N, Nl = N / nranks, H = p->H, a = g.a, E = g.E;
     const int off = rank * Nl;   // this rank's global candidates [off, off + Nl)
     const bool fuse = update_kpt(N, p->K, a) != 0 && g_opt[MBRL_OPT_UNFUSED_UPDATE].load(std::memory_order_relaxed) == 0;
     const bool fuse_draw = fuse && update_samples(Nl, a);
-    // distribution rows, the workspace copy of s0, iteration 0's proposals of this shard
-    hipLaunchKernelGGL(fill2_kernel, dim3((Ha + 255) / 256), dim3(256), 0, stream, w.mu[0], p->init_mu, w.sigma[0],
-                       p->init_sigma, Ha);
-    hipLaunchKernelGGL(copy_kernel, dim3(1), dim3(64), 0, stream, s0_in, (size_t)g.s, w.s0);
-    mbrl_sampler sp0{};
-    sp0.seed = p->seed; sp0.iteration = 0; sp0.mu = w.mu[0]; sp0.sigma = w.sigma[0]; sp0.lo = p->lo; sp0.hi = p->hi;
-    if ((rc = sample_impl(&sp0, H, a, Nl, off, w.actions, stream))) return rc;
+    // one first launch: distribution rows, the workspace copy of s0, iteration 0's proposals of this
+    // shard (global candidates [off, off + Nl)), the hand-off words zeroed (mbrl_cem_plan)
+    const InitZero z = plan_zero(g, Nl, w.pair, w.xchg, w.xchg_bytes, w.status);
+    hipLaunchKernelGGL(cem_init_kernel, dim3(H * (fuse_draw ? draw_slices(H, 1, Nl, a) : 1), 1), dim3(1024), 0, stream,
+                       p->seed, p->init_mu, p->init_sigma, p->lo, p->hi, H, a, Nl, w.mu[0], w.sigma[0],
+                       fuse_draw ? w.actions : nullptr, s0_in, g.s, w.s0, off, z);
+    if (!fuse_draw) {
+        mbrl_sampler sp0{};
+        sp0.seed = p->seed; sp0.iteration = 0; sp0.mu = w.mu[0]; sp0.sigma = w.sigma[0]; sp0.lo = p->lo; sp0.hi = p->hi;
+        if ((rc = sample_impl(&sp0, H, a, Nl, off, w.actions, stream))) return rc;
+    }
+    unsigned pair_epoch = 0;
     int cur = 0;
     for (int it = 0; it < p->iterations; ++it) {
         mbrl_sampler sp{};
@@ -2065,7 +2118,7 @@ static int plan_sharded_body(const mbrl_mlp_shape* shape, const void* packed, co
             (rc = hip_check(hipEventRecord(reinterpret_cast<hipEvent_t>(rollout_events[2 * it]), stream), "event")))
             return rc;
         rc = rollout_impl(g, packed, norm, cost, w.s0, 0, w.actions, nullptr, Nl, H, 0, w.local, nullptr, nullptr,
-                          stream, pair_area_bytes(g, Nl) ? w.pair : nullptr);
+                          stream, pair_area_bytes(g, Nl) ? w.pair : nullptr, z.ptr[0] ? &pair_epoch : nullptr);
         if (rc) return rc;
         if (rollout_events && rollout_events[2 * it + 1] &&
             (rc = hip_check(hipEventRecord(reinterpret_cast<hipEvent_t>(rollout_events[2 * it + 1]), stream), "event")))
@@ -2086,7 +2139,8 @@ static int plan_sharded_body(const mbrl_mlp_shape* shape, const void* packed, co
                 } else {
                     if ((rc = sample_impl(&sp, H, a, Nl, r * Nl, w.emu_actions, stream))) return rc;
                     rc = rollout_impl(g, packed, norm, cost, w.s0, 0, w.emu_actions, nullptr, Nl, H, 0, slot, nullptr,
-                                      nullptr, stream, pair_area_bytes(g, Nl) ? w.pair : nullptr);
+                                      nullptr, stream, pair_area_bytes(g, Nl) ? w.pair : nullptr,
+                                      z.ptr[0] ? &pair_epoch : nullptr);
                 }
                 if (rc) return rc;
             }
@@ -2129,7 +2183,8 @@ static int plan_sharded_body(const mbrl_mlp_shape* shape, const void* packed, co
     }
     // the final mean's states, on every rank (the same on each)
     float* per_member = E == 1 ? states_out : w.states;
-    rc = traj_impl(g, packed, norm, w.s0, actions_out, H, per_member, w.xchg, w.xchg_bytes, w.status, stream);
+    rc = traj_impl(g, packed, norm, w.s0, actions_out, H, per_member, w.xchg, w.xchg_bytes, w.status, stream,
+                   z.ptr[1] != nullptr);
     if (rc) return rc;
     if (E > 1) {
         const int Hs = H * g.s;
@@ -2223,7 +2278,7 @@ int mbrl_cem_plan_batch(const mbrl_mlp_shape* shape, const void* packed, const m
     if (fuse_draw)
         hipLaunchKernelGGL(cem_init_kernel, dim3(p->H * draw_slices(p->H, B, p->N, g.a), B), dim3(1024), 0, stream,
                            p->seed, p->init_mu, p->init_sigma, p->lo, p->hi, p->H, g.a, p->N, w.mu[0], w.sigma[0],
-                           w.actions, nullptr, 0, nullptr);
+                           w.actions, nullptr, 0, nullptr, 0, InitZero{});
     else
         hipLaunchKernelGGL(fill2_kernel, dim3((BHa + 255) / 256), dim3(256), 0, stream, w.mu[0], p->init_mu,
                            w.sigma[0], p->init_sigma, BHa);

@@ -159,30 +159,46 @@ struct RolloutArgs {
     int xcd_map;
     // column-split pairs (rollout_kernel PAIR): two workgroups share a 16-candidate tile, each owning
     // half of every hidden layer's columns; halves cross through pair_data (sc1 stores / loads) under
-    // per-workgroup flags (pair_flags: one 128-byte line per workgroup, zeroed before every launch)
+    // per-workgroup flags (pair_flags: one 128-byte line per workgroup). The flags are zeroed once per
+    // plan (cem_init_kernel) or, for a lone rollout, by a memset before the launch (pair_prezeroed 0);
+    // within a plan every pair launch has its own epoch (1, 2, ...), so a flag that still holds an
+    // earlier launch's value never reads as this launch's:
+    //   hand-off q's flag value   pair_base + q + 1     (pair_base = (epoch - 1) * hand-offs per launch)
+    //   roll call (word 1)        16 epoch + XCC_ID + 1
+    //   status word               max(..., epoch) when one of this launch's hand-offs timed out
     float* pair_data;
     unsigned* pair_flags;
+    unsigned pair_epoch, pair_base;
+    int pair_prezeroed;
     int debug_abort;         // PAIR kernel: give up at once, as after a timed-out hand-off (MBRL_OPT_DEBUG_PAIR_ABORT)
     int pair_l2;             // PAIR kernel: L2-resident hand-offs when a roll call finds both halves on one XCD
     // non-PAIR fp32 kernels: NULL, or the pair launch's status word (the line after its flags); the
-    // launch then recomputes its candidates only if bit 0 is set (a hand-off of the pair launch timed out)
+    // launch then recomputes its candidates only if the word reached gate_epoch (the pair launch's
+    // epoch: one of its hand-offs timed out)
     const unsigned* gate;
+    unsigned gate_epoch;
 };
 
+// Hand-offs one pair launch makes at most (rollout.hip: a layer hand-off per hidden layer after layer
+// 0 plus the output half sums, per step): the epoch stride of the pair flags.
+inline unsigned pair_handoffs(int H, int L) { return (unsigned)H * (unsigned)(L + 1) + 1u; }
+
 // Column-split pair exchange area for ntiles * E tiles (rollout_kernel PAIR): the flags block first
-// (one 128-byte line per workgroup, then a status line; zeroed by one memset per launch), then per
-// workgroup two parities of its published layer columns (16 x Wpad / 2 floats) and two parities of its
-// output-layer half sum (16 x pw floats).
+// (one 128-byte line per workgroup, then a status line), then per workgroup two parities of its
+// output-layer half sums as tagged 8-byte granules {value, tag} (16 x pw each), then per workgroup two
+// parities of its published layer columns (16 x Wpad / 2 floats). The flags and the granules -- the
+// words a reader polls -- are zeroed once per plan (zero_bytes from the start; see RolloutArgs).
 struct PairLayout {
-    size_t flags_bytes, layer_floats, part_floats, bytes;
+    size_t flags_bytes, gran_bytes, layer_floats, zero_bytes, bytes;
 };
 inline PairLayout pair_layout(int Wpad, int pw, int ntiles, int E) {
     PairLayout p;
     const size_t wgs = (size_t)2 * ntiles * E;
     p.flags_bytes = (wgs + 1) * 128;
+    p.gran_bytes = wgs * 2 * 16 * (size_t)pw * 8;
     p.layer_floats = (size_t)2 * 16 * (Wpad / 2);
-    p.part_floats = (size_t)2 * 16 * pw;
-    p.bytes = p.flags_bytes + wgs * (p.layer_floats + p.part_floats) * sizeof(float);
+    p.zero_bytes = p.flags_bytes + p.gran_bytes;
+    p.bytes = p.zero_bytes + wgs * p.layer_floats * sizeof(float);
     return p;
 }
 
@@ -307,6 +323,7 @@ struct TrajArgs {
     float* states_out;     // [E][H][s]
     const unsigned* gate;  // traj_kernel: when non-NULL, run only if *gate != 0 (the coop kernel gave up)
     int debug_abort;       // traj_coop_kernel: give up at once (tests of the fallback; MBRL_DEBUG_TRAJ_ABORT)
+    int prezeroed;         // traj_coop_kernel: the granules and status word were zeroed by the plan's first launch
     // traj_coop_kernel hand-off placement (MBRL_OPT_TRAJ_HOP): 0 = a (P, E) grid, agent-scope (sc1)
     // granules; 1 = a 1-D grid of 8 P workgroups where member e's P share blockIdx % 8 == e (one XCD
     // under round-robin dispatch), sc1 granules; 2 = that grid, and granules written with L2-resident
@@ -443,6 +460,7 @@ template <int WI>
 struct CoopDot {
     static constexpr int VW = WI >= 4 ? 4 : 2;
     static constexpr int NJ = WI / VW;
+    static_assert(WI % VW == 0, "CoopDot: WI must be a multiple of the vector width (else columns are skipped)");
     static __device__ __forceinline__ int col(int c, int i) { return VW * c + 32 * VW * (i / VW) + (i % VW); }
     // w: LDS row (w[k] for column k), x: LDS vector
     static __device__ __forceinline__ float lds(const float* w, const float* x, int c) {

@@ -366,13 +366,18 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) unsigned gu32;
 constexpr int PAIR_SC1 = 16;   // buffer-op aux bit: sc1 (write-through stores, L1-bypassing loads)
 
-// Bounded poll of a partner's flag (relaxed agent-scope loads = sc1): false after ~200 ms, with bit 0
-// of the status word set, so a broken hand-off ends the launch instead of hanging the GPU.
-__device__ __forceinline__ bool pair_poll(gu32* flag, unsigned want, gu32* status) {
+// Bounded poll of a partner's flag (relaxed agent-scope loads = sc1): false after ~200 ms, with the
+// status word raised to this launch's epoch, so a broken hand-off ends the launch instead of hanging
+// the GPU (and the gated redo launch behind it recomputes the candidates).
+__device__ __forceinline__ void pair_fail(gu32* status, unsigned epoch) {
+    __hip_atomic_fetch_max(status, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ bool pair_poll(gu32* flag, unsigned want, gu32* status, unsigned epoch) {
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
         if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {
-            __hip_atomic_fetch_or(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            pair_fail(status, epoch);
             return false;
         }
         __builtin_amdgcn_s_sleep(2);
@@ -387,18 +392,19 @@ __device__ __forceinline__ void lds_wait_ge(const uint32_t* w, uint32_t need) {
     asm volatile("" ::: "memory");
 }
 
-// This hand-off wave's stores are drained; count it in (LDS word arr) and let the last of the four
-// set the workgroup's flag to q + 1 (l2: both halves on one XCD, an L2-resident store; else sc1).
-__device__ __forceinline__ void pair_signal(uint32_t* arr, gu32* flag, unsigned q, int lane, bool l2) {
+// This hand-off wave's stores are drained; count it in (LDS word arr, the ns-th signal of the launch)
+// and let the last of the four set the workgroup's flag to `value` (l2: both halves on one XCD, an
+// L2-resident store; else sc1).
+__device__ __forceinline__ void pair_signal(uint32_t* arr, gu32* flag, unsigned value, unsigned ns, int lane, bool l2) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     unsigned old = 0;
     if (lane == 0) old = atomicAdd(arr, 1u);
     old = (unsigned)__shfl((int)old, 0, 64);
-    if (old == 4 * q + 3 && lane == 0) {
+    if (old == 4 * ns + 3 && lane == 0) {
         if (l2)
-            __hip_atomic_store(flag, q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         else
-            __hip_atomic_store(flag, q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -408,16 +414,20 @@ __device__ __forceinline__ void pair_store_b128(u32x4 v, __amdgpu_buffer_rsrc_t 
     if (l2) __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 1);
     else __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16);
 }
-__device__ __forceinline__ void pair_store_b32(unsigned v, __amdgpu_buffer_rsrc_t r, unsigned off, bool l2) {
-    if (l2) __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, 1);
-    else __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, 16);
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+// A tagged 8-byte granule {value, tag}: one store, read untorn (MI355X_MICROARCH.md, granules), so a
+// reader that sees the tag holds the value and needs no flag.
+__device__ __forceinline__ void pair_store_b64(u32x2 v, __amdgpu_buffer_rsrc_t r, unsigned off, bool l2) {
+    if (l2) __builtin_amdgcn_raw_buffer_store_b64(v, r, off, 0, 1);
+    else __builtin_amdgcn_raw_buffer_store_b64(v, r, off, 0, 16);
 }
 
-// Wait until the partner's flag reads q + 1: hand-off wave 0 polls it and publishes the match in LDS
-// (word go); the other three wait on that word.
-__device__ __forceinline__ void pair_await(gu32* pflag, uint32_t* go, unsigned q, int hw, int lane, gu32* status) {
+// Wait until the partner's flag reads base + q + 1: hand-off wave 0 polls it and publishes the match
+// in LDS (word go: q + 1); the other three wait on that word.
+__device__ __forceinline__ void pair_await(gu32* pflag, uint32_t* go, unsigned base, unsigned q, int hw, int lane,
+                                           gu32* status, unsigned epoch) {
     if (hw == 0) {
-        pair_poll(pflag, q + 1, status);
+        pair_poll(pflag, base + q + 1, status, epoch);
         if (lane == 0) *(volatile lu32*)(go) = q + 1;
     } else {
         lds_wait_ge(go, q + 1);
@@ -473,14 +483,12 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
         e = blockIdx.y;
         if (tile >= ntiles) return;   // both halves of a padding pair leave together
         if (A.debug_abort) {          // test hook: behave as a timed-out hand-off (the redo launch runs)
-            if (tid == 0)
-                __hip_atomic_fetch_or((gu32*)(A.pair_flags) + (size_t)2 * ntiles * A.E * 32, 1u, __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT);
+            if (tid == 0) pair_fail((gu32*)(A.pair_flags) + (size_t)2 * ntiles * A.E * 32, A.pair_epoch);
             return;
         }
     } else {
         // the redo behind a column-split pair launch: runs only if one of its hand-offs timed out
-        if (A.gate != nullptr && *A.gate == 0u) return;
+        if (A.gate != nullptr && *A.gate < A.gate_epoch) return;
         xcd_unit(A.xcd_map, ntiles, tile, e);
     }
     const int cw = PAIR ? 4 * half + wave : wave;   // the 8-wave layout's wave whose columns this one computes
@@ -566,37 +574,47 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
             // the hand-off of what the compute waves stored before it
             const int hw = wave - 4;
             const int sid = (e * ntiles + tile) * 2 + half;
-            const size_t per = (size_t)16 * A.Wpad + (size_t)32 * A.pw;          // floats per workgroup
+            // pair_data (pair_layout): every workgroup's granules (2 parities x 16 pw), then every
+            // workgroup's layer columns (2 parities x 16 x Wpad / 2 floats)
+            const size_t nwg = (size_t)2 * ntiles * A.E;
+            const size_t gper = (size_t)2 * 16 * A.pw;             // granules per workgroup
+            const size_t lper = (size_t)16 * A.Wpad;               // layer floats per workgroup
+            const size_t gbytes = nwg * gper * 8;
             gu32* const flags = (gu32*)(A.pair_flags);
-            gu32* const status = flags + (size_t)2 * ntiles * A.E * 32;
+            gu32* const status = flags + nwg * 32;
             gu32* const myflag = flags + (size_t)sid * 32;
             gu32* const pflag = flags + (size_t)(sid ^ 1) * 32;
             const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-                A.pair_data, 0, (int)((size_t)2 * ntiles * A.E * per * sizeof(float)), 0x00020000);
-            const unsigned mine = (unsigned)((size_t)sid * per * sizeof(float));
-            const unsigned theirs = (unsigned)((size_t)(sid ^ 1) * per * sizeof(float));
+                A.pair_data, 0, (int)(gbytes + nwg * lper * sizeof(float)), 0x00020000);
+            const unsigned mine = (unsigned)(gbytes + (size_t)sid * lper * sizeof(float));
+            const unsigned theirs = (unsigned)(gbytes + (size_t)(sid ^ 1) * lper * sizeof(float));
+            const unsigned gmine = (unsigned)((size_t)sid * gper * 8);
+            const unsigned gtheirs = (unsigned)((size_t)(sid ^ 1) * gper * 8);
             const int ocw = 4 * (half ^ 1) + hw;   // the partner's compute wave paired with this one
-            unsigned q = 0;
-            // roll call (A.pair_l2): each half writes its XCD (XCC_ID + 1) to word 1 of its flag line and
-            // reads the partner's; on one XCD the halves share an L2, and every hand-off then travels as
-            // L2-resident (sc0) stores read by sc1 loads, else as written-through sc1 stores. Hand-off
-            // wave 0 decides for the workgroup (LDS word lflag[3]: 2 = one XCD, 1 = not).
+            unsigned q = 0;    // hand-offs so far (layer columns and output half sums)
+            unsigned ns = 0;   // flag signals so far (layer columns only)
+            // roll call (A.pair_l2): each half writes its XCD (16 epoch + XCC_ID + 1) to word 1 of its flag
+            // line and reads the partner's; on one XCD the halves share an L2, and every hand-off then
+            // travels as L2-resident (sc0) stores read by sc1 loads, else as written-through sc1 stores.
+            // Hand-off wave 0 decides for the workgroup (LDS word lflag[3]: 2 = one XCD, 1 = not).
+            const unsigned epoch = A.pair_epoch, fbase = A.pair_base;
             bool l2 = false;
             if (A.pair_l2 && !MBRL_PAIR_DIAG) {
                 if (hw == 0) {
                     unsigned xcc;
                     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
-                    if (lane == 0) __hip_atomic_store(myflag + 1, xcc + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const unsigned me = 16u * epoch + xcc + 1;
+                    if (lane == 0) __hip_atomic_store(myflag + 1, me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     unsigned px = 0;
                     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-                    while ((px = __hip_atomic_load(pflag + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u) {
+                    while ((px = __hip_atomic_load(pflag + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < 16u * epoch) {
                         if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {
-                            __hip_atomic_fetch_or(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            pair_fail(status, epoch);
                             break;
                         }
                         __builtin_amdgcn_s_sleep(2);
                     }
-                    if (lane == 0) *(volatile lu32*)(lflag + 3) = px == xcc + 1 ? 2u : 1u;
+                    if (lane == 0) *(volatile lu32*)(lflag + 3) = px == me ? 2u : 1u;
                 }
                 lds_wait_ge(lflag + 3, 1);
                 l2 = *(volatile lu32*)(lflag + 3) == 2u;
@@ -611,8 +629,8 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
                 if constexpr (!MBRL_PAIR_DIAG) {
 #pragma unroll
                     for (int j = 0; j < TW; ++j) pair_store_b128(__builtin_bit_cast(u32x4, v[j]), xr, mine + slot + j * 1024, l2);
-                    pair_signal(lflag + 1, myflag, q, lane, l2);
-                    pair_await(pflag, lflag + 2, q, hw, lane, status);
+                    pair_signal(lflag + 1, myflag, fbase + q + 1, ns++, lane, l2);
+                    pair_await(pflag, lflag + 2, fbase, q, hw, lane, status, epoch);
 #pragma unroll
                     for (int j = 0; j < TW; ++j)
                         v[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, theirs + slot + j * 1024, 0, PAIR_SC1));
@@ -623,32 +641,61 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
                 if (lane == 0) atomicAdd(lflag, 1u);
                 ++q;
             };
-            // output layer: this half's sum of its four partials, then S_0 + S_1 into partial slot 0
+            // output layer: this half's sum of its four partials, then S_0 + S_1 into partial slot 0. The
+            // half sums cross as tagged granules (tag = the flag value this hand-off would carry, unique
+            // within the plan; the granules are zeroed with the flags): each lane stores its own and
+            // polls the partner's at the same index -- one fabric round trip where a flag costs a drain,
+            // the flag store, its poll and then the payload load (MI355X_MICROARCH.md handoff-1to1 vs
+            // handoff-flag).
             auto partials = [&]() {
                 const int ws = M * A.pw, nel = M * A.s;
-                const unsigned pslot = (unsigned)((16 * A.Wpad + (q & 1) * 16 * A.pw) * sizeof(float));
-                float so[NOT_T];
+                const unsigned gslot = (unsigned)((q & 1) * 16 * A.pw * 8);
+                const unsigned tag = fbase + q + 1;
+                float so[NOT_T], sp[NOT_T];
+                unsigned need = 0;
 #pragma unroll
                 for (int i = 0; i < NOT_T; ++i) {
                     const int idx = 256 * i + 64 * hw + lane;
                     so[i] = 0.f;
+                    sp[i] = 0.f;
                     if (idx < nel) {
                         const int m = idx / A.s, ro = m * A.pw + (idx - m * A.s);
                         so[i] = (L.part[ro] + L.part[ws + ro]) + (L.part[2 * ws + ro] + L.part[3 * ws + ro]);
-                        if constexpr (!MBRL_PAIR_DIAG) pair_store_b32(__float_as_uint(so[i]), xr, mine + pslot + idx * 4, l2);
+                        if constexpr (!MBRL_PAIR_DIAG)
+                            pair_store_b64(u32x2{__float_as_uint(so[i]), tag}, xr, gmine + gslot + idx * 8, l2);
+                        need |= 1u << i;
                     }
                 }
                 if constexpr (!MBRL_PAIR_DIAG) {
-                    pair_signal(lflag + 1, myflag, q, lane, l2);
-                    pair_await(pflag, lflag + 2, q, hw, lane, status);
+                    unsigned got = 0;
+                    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+                    while (true) {
+                        u32x2 v[NOT_T];
+#pragma unroll
+                        for (int i = 0; i < NOT_T; ++i) {   // every load in flight before the first compare
+                            const int idx = min(256 * i + 64 * hw + lane, nel - 1);
+                            v[i] = __builtin_amdgcn_raw_buffer_load_b64(xr, gtheirs + gslot + idx * 8, 0, PAIR_SC1);
+                        }
+#pragma unroll
+                        for (int i = 0; i < NOT_T; ++i)
+                            if ((need >> i) & 1u && !((got >> i) & 1u) && v[i].y == tag) {
+                                sp[i] = __uint_as_float(v[i].x);
+                                got |= 1u << i;
+                            }
+                        if (got == need) break;
+                        if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {
+                            pair_fail(status, epoch);
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
                 }
 #pragma unroll
                 for (int i = 0; i < NOT_T; ++i) {
                     const int idx = 256 * i + 64 * hw + lane;
                     if (idx < nel) {
-                        const float sp = MBRL_PAIR_DIAG ? 0.f : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, theirs + pslot + idx * 4, 0, PAIR_SC1));
                         const int m = idx / A.s, ro = m * A.pw + (idx - m * A.s);
-                        L.part[ro] = so[i] + sp;    // S_0 + S_1 (exactly commutative)
+                        L.part[ro] = so[i] + sp[i];    // S_0 + S_1 (exactly commutative)
                     }
                 }
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1056,9 +1103,12 @@ static hipError_t launch_pair_tr(const RolloutArgs& A_in, hipStream_t stream) {
     if (e != hipSuccess) return e;
     if (!grid_fits(reinterpret_cast<const void*>(fn), 512, lds, (int)(grid.x * grid.y)))
         return hipErrorCooperativeLaunchTooLarge;
-    // every polled word (flags, status) zeroed before every launch: one memset node
-    e = hipMemsetAsync(A.pair_flags, 0, pair_layout(A.Wpad, A.pw, ntiles, A.E).flags_bytes, stream);
-    if (e != hipSuccess) return e;
+    // every polled word (flags, status) zero before the first launch of its epochs: the plan's first
+    // launch cleared them (cem_init_kernel), else one memset node here (a lone rollout, epoch 1)
+    if (!A.pair_prezeroed) {
+        e = hipMemsetAsync(A.pair_flags, 0, pair_layout(A.Wpad, A.pw, ntiles, A.E).zero_bytes, stream);
+        if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(fn, grid, dim3(512), lds, stream, A);
     return hipGetLastError();
 }
@@ -1142,7 +1192,7 @@ __global__ void __launch_bounds__(64 * m8_waves(T, NOT_T), 1) rollout_m8_kernel(
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int ntiles = (A.N + M - 1) / M;
     int tile, e;
-    if (A.gate != nullptr && *A.gate == 0u) return;   // redo behind a pair launch (rollout_kernel)
+    if (A.gate != nullptr && *A.gate < A.gate_epoch) return;   // redo behind a pair launch (rollout_kernel)
     xcd_unit(A.xcd_map, ntiles, tile, e);
     const float* member = A.packed + (size_t)e * A.member_stride;
     float* const actX = L.act;

@@ -458,14 +458,17 @@ static hipError_t launch_coop_width(const TrajArgs& A, int E, u64* xchg, unsigne
 
 hipError_t launch_traj_coop(const TrajArgs& A, int E, unsigned long long* xchg, unsigned* status,
                             hipStream_t stream) {
-    // one memset when the status word directly follows the granules (the workspaces lay them out so)
-    const size_t xb = traj_coop_xchg_bytes(A, E);
-    const bool adjacent = reinterpret_cast<char*>(status) == reinterpret_cast<char*>(xchg) + xb;
-    hipError_t err = hipMemsetAsync(xchg, 0, adjacent ? xb + 16 : xb, stream);
-    if (err != hipSuccess) return err;
-    if (!adjacent) {
-        err = hipMemsetAsync(status, 0, sizeof(unsigned), stream);
+    // one memset when the status word directly follows the granules (the workspaces lay them out so);
+    // none when the plan's first launch zeroed both (cem_init_kernel)
+    if (!A.prezeroed) {
+        const size_t xb = traj_coop_xchg_bytes(A, E);
+        const bool adjacent = reinterpret_cast<char*>(status) == reinterpret_cast<char*>(xchg) + xb;
+        hipError_t err = hipMemsetAsync(xchg, 0, adjacent ? xb + 16 : xb, stream);
         if (err != hipSuccess) return err;
+        if (!adjacent) {
+            err = hipMemsetAsync(status, 0, sizeof(unsigned), stream);
+            if (err != hipSuccess) return err;
+        }
     }
     return coop_k0r(A) == 32 ? launch_coop_width<32, 2>(A, E, xchg, status, stream)
                              : launch_coop_width<96, 5>(A, E, xchg, status, stream);

@@ -71,3 +71,24 @@ def test_bench_gpus_2_launches_two_ranks():
     assert d["n_gpus"] == 2 and d["config"]["world_size"] == 2 and d["config"]["backend"] == "gloo"
     assert d["config"]["candidates_per_gpu"] == 4096 and d["scaling"] == "weak"
     assert d["strong"]["candidates_per_gpu"] == 8192 and d["strong"]["n_gpus"] == 2
+
+
+@pytest.mark.gpu
+def test_bench_gpus_8_launches_eight_ranks():
+    """The driver's SCALE node runs `bench.py --gpus 8`: the 8-rank line is produced here first, eight
+    rank processes over gloo sharing this box's one GPU (the N = 8 sharded protocol, the weak line at
+    4096 candidates per rank, the walker split at 2048 and the headline split at 512 per rank)."""
+    env = dict(os.environ, MBRL_DIST_BACKEND="gloo")
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "8", "--steps", "2",
+                          "--warmup", "1", "--no-variants", "--no-cpu-baseline"], capture_output=True, text=True,
+                         timeout=280, cwd=REPO, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["config"]["world_size"] == 8 and d["config"]["backend"] == "gloo"
+    assert d["config"]["candidates_per_gpu"] == 4096 and d["scaling"] == "weak"
+    assert d["strong"]["candidates_per_gpu"] == 2048 and d["strong"]["n_gpus"] == 8
+    assert d["strong_headline"]["candidates_per_gpu"] == 512 and d["strong_headline"]["n_gpus"] == 8
+    assert d["plan_gpu_ms"] > 0 and d["value"] > 0 and d["roofline"]["frac"] > 0
