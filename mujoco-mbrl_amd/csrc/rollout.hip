@@ -325,7 +325,7 @@ __device__ __forceinline__ void load_epi_params(const RolloutArgs& A, const LdsM
 template <int R, int SS, bool REG = (SS <= MBRL_EPI_REG_SLOTS)>
 __device__ __forceinline__ void stage_actions(const RolloutArgs& A, const EpiParams<SS>& P, const LdsMap& L, float* act,
                                               int wave, int lane, const float (&av)[R][MAX_A_PER_LANE],
-                                              float (&acp)[R]) {
+                                              float (&acp)[R], int lda) {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int m = epi_row(r, wave, lane);
@@ -339,7 +339,7 @@ __device__ __forceinline__ void stage_actions(const RolloutArgs& A, const EpiPar
                 const float am = REG ? P.am[k] : L.act_mean[d];
                 const float as = REG ? P.as[k] : L.act_std[d];
                 const float xn = A.norm_a ? (x - am) / as : x;
-                act[m * A.lda + A.s + d] = xn;
+                act[m * lda + A.s + d] = xn;
                 if (A.reward) L.aterm[m * A.a + d] = xn;   // the state pass re-reads a_t
                 if (A.has_ac) c += coshf(x / A.alpha_a) - 1.0f;
             }
@@ -467,6 +467,15 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
     // input, so no buffer is overwritten while another wave still reads it (the ping-pong invariant
     // the barriers kept).
     constexpr bool LFLAGS = RING && MBRL_LAYER_FLAGS;
+    // LDS row strides: compile-time for the ring instances (make_geometry: lda = max(Wpad, 16 K0C) + 4,
+    // pw = 16 NOT + 4; the launcher checks them), so every LDS address of a row block, partial or
+    // slot is one base register plus an immediate offset. With runtime strides hipcc hoisted one
+    // address register per (row, slot, partial) out of the step loop and spilled them on the
+    // 32-candidate kernel (76 B/lane of scratch, ~18 MB of scratch write-back per walker launch).
+    constexpr int LDAC = (64 * T > 16 * K0C_T ? 64 * T : 16 * K0C_T) + 4;
+    constexpr int PWC = 16 * NOT_T + 4;
+    const int lda = RING ? LDAC : A.lda;
+    const int pw = RING ? PWC : A.pw;
     uint32_t nstore = 0;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const LdsMap L = lds_map(A, smem, M);
@@ -537,16 +546,16 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
         const int m = i / A.s, d = i - (i / A.s) * A.s;
         const int n = min(tile * M + m, A.N - 1);
         const float sv = A.s0_per_cand ? A.s0[(size_t)n * A.s + d] : A.s0[d];
-        actX[m * A.lda + d] = A.norm_s ? (sv - L.obs_mean[d]) / L.obs_std[d] : sv;
+        actX[m * lda + d] = A.norm_s ? (sv - L.obs_mean[d]) / L.obs_std[d] : sv;
     }
     for (int i = tid; i < M * A.k0pad_extra; i += NT) {
         const int m = i / A.k0pad_extra, j = i - (i / A.k0pad_extra) * A.k0pad_extra;
-        actX[m * A.lda + A.s + A.a + j] = 0.f;
+        actX[m * lda + A.s + A.a + j] = 0.f;
     }
     EpiParams<SS> P;
     load_epi_params<SS>(A, L, lane, P);
     if (actw) {
-        stage_actions<R, SS, EREG>(A, P, L, actX, awave, lane, av, acp);
+        stage_actions<R, SS, EREG>(A, P, L, actX, awave, lane, av, acp, lda);
         if (split)
 #pragma unroll
             for (int r = 0; r < R; ++r) {
@@ -577,7 +586,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
             // pair_data (pair_layout): every workgroup's granules (2 parities x 16 pw), then every
             // workgroup's layer columns (2 parities x 16 x Wpad / 2 floats)
             const size_t nwg = (size_t)2 * ntiles * A.E;
-            const size_t gper = (size_t)2 * 16 * A.pw;             // granules per workgroup
+            const size_t gper = (size_t)2 * 16 * pw;             // granules per workgroup
             const size_t lper = (size_t)16 * A.Wpad;               // layer floats per workgroup
             const size_t gbytes = nwg * gper * 8;
             gu32* const flags = (gu32*)(A.pair_flags);
@@ -622,7 +631,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
             // layer columns: publish this half's cw = 4 half + hw slice of buffer `buf`, copy the partner's in
             auto layer = [&](float* buf) {
                 const unsigned slot = (unsigned)((((q & 1) * 4 + hw) * TW * 64 + lane) * 16);
-                const int row = (lane & 15) * A.lda + 4 * (lane >> 4);
+                const int row = (lane & 15) * lda + 4 * (lane >> 4);
                 f32x4 v[TW];
 #pragma unroll
                 for (int j = 0; j < TW; ++j) v[j] = *reinterpret_cast<const f32x4*>(buf + row + (4 * half + hw) * 16 * TW + 16 * j);
@@ -648,8 +657,8 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
             // the flag store, its poll and then the payload load (MI355X_MICROARCH.md handoff-1to1 vs
             // handoff-flag).
             auto partials = [&]() {
-                const int ws = M * A.pw, nel = M * A.s;
-                const unsigned gslot = (unsigned)((q & 1) * 16 * A.pw * 8);
+                const int ws = M * pw, nel = M * A.s;
+                const unsigned gslot = (unsigned)((q & 1) * 16 * pw * 8);
                 const unsigned tag = fbase + q + 1;
                 float so[NOT_T], sp[NOT_T];
                 unsigned need = 0;
@@ -659,7 +668,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
                     so[i] = 0.f;
                     sp[i] = 0.f;
                     if (idx < nel) {
-                        const int m = idx / A.s, ro = m * A.pw + (idx - m * A.s);
+                        const int m = idx / A.s, ro = m * pw + (idx - m * A.s);
                         so[i] = (L.part[ro] + L.part[ws + ro]) + (L.part[2 * ws + ro] + L.part[3 * ws + ro]);
                         if constexpr (!MBRL_PAIR_DIAG)
                             pair_store_b64(u32x2{__float_as_uint(so[i]), tag}, xr, gmine + gslot + idx * 8, l2);
@@ -694,7 +703,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
                 for (int i = 0; i < NOT_T; ++i) {
                     const int idx = 256 * i + 64 * hw + lane;
                     if (idx < nel) {
-                        const int m = idx / A.s, ro = m * A.pw + (idx - m * A.s);
+                        const int m = idx / A.s, ro = m * pw + (idx - m * A.s);
                         L.part[ro] = so[i] + sp[i];    // S_0 + S_1 (exactly commutative)
                     }
                 }
@@ -715,7 +724,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
                 __syncthreads();         // output partials stored
                 partials();
                 if (t + 1 < A.H) {
-                    stage_actions<R, SS, EREG>(A, P, L, actX, awave, lane, av, acp);
+                    stage_actions<R, SS, EREG>(A, P, L, actX, awave, lane, av, acp, lda);
                     const float v = rowsum16(acp[0]);
                     if ((lane & 15) == 0) acs[((t + 1) & 1) * M + epi_row(0, awave, lane)] = v;
                 }
@@ -795,7 +804,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
             if ((KC) == 3 * (NK) / 4) __builtin_amdgcn_s_setprio(1);                 \
             if ((KC) == 7 * (NK) / 8) __builtin_amdgcn_s_setprio(0);                 \
         }                                                                            \
-        if ((KC) + 1 < (NK)) read_a<R>(aAB[((KC) + 1) & 1], IN, A.lda, (KC) + 1, lane); \
+        if ((KC) + 1 < (NK)) read_a<R>(aAB[((KC) + 1) & 1], IN, lda, (KC) + 1, lane); \
         mma_hidden<TW, R>(acc, aAB[(KC) & 1], ring[SLOT]);                           \
         interleave_loads<TW, R>();                                                   \
         MBRL_PIN();                                                                  \
@@ -815,7 +824,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
         // ---- layer 0: actX [s | a | 0-pad] -> actY (W)
         zero_acc<TW, R>(acc);
         load_bias<TW>(bias, L.hbias, cw, lane);
-        read_a<R>(aAB[0], actX, A.lda, 0, lane);
+        read_a<R>(aAB[0], actX, lda, 0, lane);
         if constexpr (RING) {
             // a chunk whose 16 inputs are all zero padding (k >= s + a) is skipped: the accumulator starts
             // at +0 and a round-to-nearest sum never turns +0 into -0, so adding exact zero products
@@ -823,7 +832,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
 #pragma unroll
             for (int kc = 0; kc < K0C_T; ++kc) {
                 MBRL_LOAD_CHUNK(ring[((kc % NB) + NB - 1) % NB], g + NB - 1);
-                if (kc + 1 < K0C_T) read_a<R>(aAB[(kc + 1) & 1], actX, A.lda, kc + 1, lane);
+                if (kc + 1 < K0C_T) read_a<R>(aAB[(kc + 1) & 1], actX, lda, kc + 1, lane);
                 if (16 * kc < A.s + A.a) mma_hidden<TW, R>(acc, aAB[kc & 1], ring[kc % NB]);
                 interleave_loads<TW, R>();
                 MBRL_PIN();
@@ -833,7 +842,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
             for (int kc = 0; kc < A.K0C; kc += 2) {
                 MBRL_HIDDEN_CHUNK(0, 0, 2, actX + 16 * kc);
                 MBRL_HIDDEN_CHUNK(1, 1, 2, actX + 16 * kc);
-                if (kc + 2 < A.K0C) read_a<R>(aAB[0], actX, A.lda, kc + 2, lane);
+                if (kc + 2 < A.K0C) read_a<R>(aAB[0], actX, lda, kc + 2, lane);
             }
         }
         STAMP(0);
@@ -842,17 +851,17 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
         // (lane: 4 consecutive units of candidate lane & 15). No LDS store, barrier or re-read.
         if (A.L > 1) {
             if constexpr (L0DUP) {
-                hidden_store_nobar<TW, R>(acc, bias, actY, A.lda, cw, lane);
+                hidden_store_nobar<TW, R>(acc, bias, actY, lda, cw, lane);
                 zero_acc<TW, R>(acc);
                 load_bias<TW>(bias, L.hbias, ocw0, lane);
 #pragma unroll
                 for (int kc = 0; kc < K0C_T; ++kc)
                     if (16 * kc < A.s + A.a) mma_hidden<TW, R>(acc, aAB[kc & 1], w0p[kc]);
-                hidden_store<TW, R>(acc, bias, actY, A.lda, ocw0, lane);
+                hidden_store<TW, R>(acc, bias, actY, lda, ocw0, lane);
             } else if constexpr (LFLAGS) {
-                hidden_store_flag<TW, R>(acc, bias, actY, A.lda, cw, lane, lflag, ++nstore);
+                hidden_store_flag<TW, R>(acc, bias, actY, lda, cw, lane, lflag, ++nstore);
             } else {
-                hidden_store<TW, R>(acc, bias, actY, A.lda, cw, lane);
+                hidden_store<TW, R>(acc, bias, actY, lda, cw, lane);
             }
         }
         STAMP(1);
@@ -869,13 +878,13 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
             // K position kc reads chunk kc + rof/16 (kc < 2T) or kc - rof/16 (kc >= 2T): two bases
             const float* const inLo = in + rof;
             const float* const inHi = in - rof;
-            read_a<R>(aAB[0], inLo, A.lda, 0, lane);
+            read_a<R>(aAB[0], inLo, lda, 0, lane);
 #pragma unroll
             for (int kc = 0; kc < KH; ++kc) MBRL_HIDDEN_CHUNK((S0 + kc) % NB, kc, KH, (kc + 1 < KH / 2 ? inLo : inHi));
             STAMP(2);
             if (l + 1 < A.L) {
-                if constexpr (LFLAGS) hidden_store_flag<TW, R>(acc, bias, out, A.lda, cw, lane, lflag, ++nstore);
-                else hidden_store<TW, R>(acc, bias, out, A.lda, cw, lane);
+                if constexpr (LFLAGS) hidden_store_flag<TW, R>(acc, bias, out, lda, cw, lane, lflag, ++nstore);
+                else hidden_store<TW, R>(acc, bias, out, lda, cw, lane);
             }
             STAMP(3);
             float* tmp = in; in = out; out = tmp;
@@ -888,12 +897,12 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
             for (int r = 0; r < R; ++r)
 #pragma unroll
                 for (int kc = 0; kc < TW; ++kc) aout[r][kc] = __builtin_elementwise_max(acc[r][kc] + bias[kc], zero4);
-            float* part = L.part + wave * M * A.pw;
+            float* part = L.part + wave * M * pw;
 #define MBRL_OUT_CHUNK(SLOT, J)                                                   \
     do {                                                                          \
         MBRL_LOAD_CHUNK(ring[((SLOT) + NB - 1) % NB], g + NB - 1);                \
         MBRL_PIN();                                                               \
-        mma_out<TW, R, NHO>(aout, ring[SLOT], part, A.pw, J, lane);               \
+        mma_out<TW, R, NHO>(aout, ring[SLOT], part, pw, J, lane);               \
         MBRL_PIN();                                                               \
         ++g;                                                                      \
     } while (0)
@@ -919,7 +928,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
             // reward-head model. State pass: s_{t+1} -> states_out, next input [norm(s_{t+1}) | norm(a_t)].
             // Reward pass: cost_t = unnormalize_reward(reward head), next input [norm(s_{t+1}) | norm(a_{t+1})].
             const float* bout = L.hbias + A.L * A.Wpad;
-            const int ws = M * A.pw;
+            const int ws = M * pw;
             const int j = lane & 15;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
@@ -927,7 +936,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
                 const int n = tile * M + m;
                 float rc = 0.f;
                 for (int d = j; d <= A.s; d += 16) {
-                    const int ro = m * A.pw + d;
+                    const int ro = m * pw + d;
                     float o = 0.f;
                     if (pass == 0 || d == A.s) {
                         o = sum_partials<NW>(L.part, ws, ro) + bout[d];
@@ -943,22 +952,22 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
                         } else {
                             xn = L.sterm[m * A.s + d];
                         }
-                        actX[m * A.lda + d] = xn;
+                        actX[m * lda + d] = xn;
                     } else if (pass == 1) {
                         rc = A.unnorm_r ? o * rstd + rmean : o;
                     }
                 }
-                for (int d = A.s + A.a + j; d < A.s + A.a + A.k0pad_extra; d += 16) actX[m * A.lda + d] = 0.f;
+                for (int d = A.s + A.a + j; d < A.s + A.a + A.k0pad_extra; d += 16) actX[m * lda + d] = 0.f;
                 if (pass == 0) {
-                    for (int d = j; d < A.a; d += 16) actX[m * A.lda + A.s + d] = L.aterm[m * A.a + d];
+                    for (int d = j; d < A.a; d += 16) actX[m * lda + A.s + d] = L.aterm[m * A.a + d];
                 } else {
                     total[r] += rowsum16(rc);
                 }
             }
-            if (pass == 1 && t + 1 < A.H) stage_actions<R, SS, EREG>(A, P, L, actX, wave, lane, av, acp);
+            if (pass == 1 && t + 1 < A.H) stage_actions<R, SS, EREG>(A, P, L, actX, wave, lane, av, acp, lda);
         } else if (epi) {
             const float* bout = L.hbias + A.L * A.Wpad;
-            const int ws = M * A.pw;
+            const int ws = M * pw;
             const int j = lane & 15;
             if constexpr (PAIR) lds_wait_ge(lflag, 4 * ++xneed);   // S_0 + S_1 in partial slot 0
 #pragma unroll
@@ -967,7 +976,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
                 const int n = tile * M + m;
                 float sc = 0.f;
                 auto slot = [&](int d, float om, float os, float goal, float cwt, float bo) {
-                    const int ro = m * A.pw + d;
+                    const int ro = m * pw + d;
                     float o = PAIR ? L.part[ro] : sum_partials<NW>(L.part, ws, ro);
                     o = o + bo;
                     const float sn = A.unnorm_s ? o * os + om : o;
@@ -975,7 +984,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
                         const float x = (sn - goal) * cwt;
                         sc += sqrtf(x * x + A.alpha_s2) - A.alpha_s;
                     }
-                    actX[m * A.lda + d] = A.norm_s ? (sn - om) / os : sn;
+                    actX[m * lda + d] = A.norm_s ? (sn - om) / os : sn;
                     if (A.states_out != nullptr && n < A.N && (!PAIR || half == 0))
                         A.states_out[(((size_t)e * A.H + t) * A.N + n) * A.s + d] = sn;
                 };
@@ -994,15 +1003,15 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
                     for (int d = j; d < A.s; d += 16)
                         slot(d, L.obs_mean[d], L.obs_std[d], L.goal[d], L.cw[d], bout[d]);
                 }
-                for (int d = A.s + A.a + j; d < A.s + A.a + A.k0pad_extra; d += 16) actX[m * A.lda + d] = 0.f;
+                for (int d = A.s + A.a + j; d < A.s + A.a + A.k0pad_extra; d += 16) actX[m * lda + d] = 0.f;
                 sc = rowsum16(sc);
                 const float ac = split ? acs[(t & 1) * M + m] : rowsum16(acp[r]);
                 total[r] += sc + A.alpha_a2 * (ac / (float)A.a);
             }
-            if (!split && t + 1 < A.H) stage_actions<R, SS, EREG>(A, P, L, actX, wave, lane, av, acp);
+            if (!split && t + 1 < A.H) stage_actions<R, SS, EREG>(A, P, L, actX, wave, lane, av, acp, lda);
         } else if (split && actw && t + 1 < A.H) {
             // waves 4-7, concurrently: a_{t+1} into the next MLP input, its CoshLoss row sum into LDS
-            stage_actions<R, SS, EREG>(A, P, L, actX, awave, lane, av, acp);
+            stage_actions<R, SS, EREG>(A, P, L, actX, awave, lane, av, acp, lda);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const float v = rowsum16(acp[r]);
@@ -1031,10 +1040,19 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
     }
 }
 
+// The ring instances compile the LDS row strides in (rollout_kernel LDAC / PWC): the geometry must
+// agree (make_geometry computes the same two numbers).
+template <int T, int K0C_T, int NOT_T>
+static bool ring_strides_ok(const RolloutArgs& A) {
+    if constexpr (K0C_T == 0) return true;
+    else return A.lda == (64 * T > 16 * K0C_T ? 64 * T : 16 * K0C_T) + 4 && A.pw == 16 * NOT_T + 4;
+}
+
 template <int T, int R, int K0C_T, int NOT_T, int NW>
 static hipError_t launch_rollout_tr(const RolloutArgs& A_in, hipStream_t stream) {
     RolloutArgs A = A_in;
     A.nw = NW;
+    if (!ring_strides_ok<T, K0C_T, NOT_T>(A)) return hipErrorInvalidValue;
     const int M = 16 * R;
     const int ntiles = (A.N + M - 1) / M;
     const dim3 grid = A.xcd_map ? dim3(ntiles * A.E) : dim3(ntiles, A.E);
@@ -1095,6 +1113,7 @@ static hipError_t launch_pair_tr(const RolloutArgs& A_in, hipStream_t stream) {
     RolloutArgs A = A_in;
     A.nw = 8;
     A.part_alias = 0;
+    if (!ring_strides_ok<T, K0C_T, NOT_T>(A)) return hipErrorInvalidValue;
     const int ntiles = (A.N + 15) / 16;
     const dim3 grid(16 * ((ntiles + 7) / 8), A.E);
     const size_t lds = rollout_lds_bytes(A, 16);
@@ -1158,6 +1177,9 @@ constexpr int m8_waves(int T, int NOT) { return m8_kp(T, NOT) ? 8 : T; }
 template <int T, int K0C_T, int NOT_T, int K0L = 0>
 __global__ void __launch_bounds__(64 * m8_waves(T, NOT_T), 1) rollout_m8_kernel(const RolloutArgs A) {
     constexpr int M = 8;
+    // compile-time LDS row strides (rollout_kernel LDAC / PWC; the launcher checks the geometry)
+    const int lda = (64 * T > 16 * K0C_T ? 64 * T : 16 * K0C_T) + 4;
+    const int pw = 16 * NOT_T + 4;
     constexpr bool KP = m8_kp(T, NOT_T);
     constexpr int NW = m8_waves(T, NOT_T);
     constexpr int TPW = KP ? 1 : 2;          // 32-row tiles per wave
@@ -1233,16 +1255,16 @@ __global__ void __launch_bounds__(64 * m8_waves(T, NOT_T), 1) rollout_m8_kernel(
         const int m = i / A.s, d = i - (i / A.s) * A.s;
         const int n = min(tile * M + m, A.N - 1);
         const float sv = A.s0_per_cand ? A.s0[(size_t)n * A.s + d] : A.s0[d];
-        actX[m * A.lda + d] = A.norm_s ? (sv - L.obs_mean[d]) / L.obs_std[d] : sv;
+        actX[m * lda + d] = A.norm_s ? (sv - L.obs_mean[d]) / L.obs_std[d] : sv;
     }
     for (int i = tid; i < M * A.k0pad_extra; i += NT) {
         const int m = i / A.k0pad_extra, j = i - (i / A.k0pad_extra) * A.k0pad_extra;
-        actX[m * A.lda + A.s + A.a + j] = 0.f;
+        actX[m * lda + A.s + A.a + j] = 0.f;
     }
     EpiParams<SS> P;
     load_epi_params<SS>(A, L, lane, P);
     if (actw) {
-        stage_actions<1, SS>(A, P, L, actX, awave, lane, av, acp);
+        stage_actions<1, SS>(A, P, L, actX, awave, lane, av, acp, lda);
         const float v = rowsum16(acp[0]);
         if ((lane & 15) == 0) acs[epi_row(0, awave, lane)] = v;
     }
@@ -1278,7 +1300,7 @@ __global__ void __launch_bounds__(64 * m8_waves(T, NOT_T), 1) rollout_m8_kernel(
 #endif
     auto read_b = [&](f32x4 (&b)[4], const float* in, int col) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) b[q] = *reinterpret_cast<const f32x4*>(in + cand * A.lda + col + 4 * q);
+        for (int q = 0; q < 4; ++q) b[q] = *reinterpret_cast<const f32x4*>(in + cand * lda + col + 4 * q);
     };
     auto mma_pair = [&](const f32x4 (&w)[RSL], const f32x4 (&b)[4]) {
         if constexpr (KP) {
@@ -1328,7 +1350,7 @@ __global__ void __launch_bounds__(64 * m8_waves(T, NOT_T), 1) rollout_m8_kernel(
         for (int u = 0; u < TPW; ++u) {
             f32x4 v = acc[u] + bias[u];
             v = __builtin_elementwise_max(v, zero);
-            *reinterpret_cast<f32x4*>(out + cand * A.lda + FPW * wave + 32 * u + 4 * (lane >> 3)) = v;
+            *reinterpret_cast<f32x4*>(out + cand * lda + FPW * wave + 32 * u + 4 * (lane >> 3)) = v;
         }
     };
     // a stored layer another wave reads: publish it (flags) or wait for every wave (barrier)
@@ -1505,7 +1527,7 @@ __global__ void __launch_bounds__(64 * m8_waves(T, NOT_T), 1) rollout_m8_kernel(
 #pragma unroll
                 for (int u = 0; u < NOT8; ++u) {
                     const f32x4 v = (ch[j][u][0] + ch[j][u][1]) + (ch[j][u][2] + ch[j][u][3]);
-                    *reinterpret_cast<f32x4*>(L.part + (wave * NPW + j) * (M * A.pw) + cand * A.pw + 32 * u +
+                    *reinterpret_cast<f32x4*>(L.part + (wave * NPW + j) * (M * pw) + cand * pw + 32 * u +
                                               4 * (lane >> 3)) = v;
                 }
         }
@@ -1514,13 +1536,13 @@ __global__ void __launch_bounds__(64 * m8_waves(T, NOT_T), 1) rollout_m8_kernel(
         STAMP(5);
         // ---- epilogue: the 8-wave kernel's split-mode goal-state epilogue for rows 0..7
         if (epi) {
-            const int ws = M * A.pw;
+            const int ws = M * pw;
             const int j = lane & 15;
             const int m = epi_row(0, wave, lane);
             const int n = tile * M + m;
             float sc = 0.f;
             auto slot = [&](int d, float om, float os, float goal, float cw, float bo) {
-                const int ro = m * A.pw + d;
+                const int ro = m * pw + d;
                 float o = sum_partials<8>(L.part, ws, ro);
                 o = o + bo;
                 const float sn = A.unnorm_s ? o * os + om : o;
@@ -1528,7 +1550,7 @@ __global__ void __launch_bounds__(64 * m8_waves(T, NOT_T), 1) rollout_m8_kernel(
                     const float x = (sn - goal) * cw;
                     sc += sqrtf(x * x + A.alpha_s2) - A.alpha_s;
                 }
-                actX[m * A.lda + d] = A.norm_s ? (sn - om) / os : sn;
+                actX[m * lda + d] = A.norm_s ? (sn - om) / os : sn;
                 if (A.states_out != nullptr && n < A.N)
                     A.states_out[(((size_t)e * A.H + t) * A.N + n) * A.s + d] = sn;
             };
@@ -1545,12 +1567,12 @@ __global__ void __launch_bounds__(64 * m8_waves(T, NOT_T), 1) rollout_m8_kernel(
                     if (d < A.s) slot(d, L.obs_mean[d], L.obs_std[d], L.goal[d], L.cw[d], bout[d]);
                 }
             }
-            for (int d = A.s + A.a + j; d < A.s + A.a + A.k0pad_extra; d += 16) actX[m * A.lda + d] = 0.f;
+            for (int d = A.s + A.a + j; d < A.s + A.a + A.k0pad_extra; d += 16) actX[m * lda + d] = 0.f;
             sc = rowsum16(sc);
             const float ac = acs[(t & 1) * M + m];
             total += sc + A.alpha_a2 * (ac / (float)A.a);
         } else if (actw && t + 1 < A.H) {
-            stage_actions<1, SS>(A, P, L, actX, awave, lane, av, acp);
+            stage_actions<1, SS>(A, P, L, actX, awave, lane, av, acp, lda);
             const float v = rowsum16(acp[0]);
             if ((lane & 15) == 0) acs[((t + 1) & 1) * M + epi_row(0, awave, lane)] = v;
         }
@@ -1583,6 +1605,7 @@ template <int T, int K0C_T, int NOT_T, int K0L = 0>
 static hipError_t launch_m8_tr(const RolloutArgs& A_in, hipStream_t stream) {
     RolloutArgs A = A_in;
     A.nw = 8;   // output partials: the 8-wave kernel's count
+    if (!ring_strides_ok<T, K0C_T, NOT_T>(A)) return hipErrorInvalidValue;
     const dim3 grid = A.xcd_map ? dim3((A.N + 7) / 8 * A.E) : dim3((A.N + 7) / 8, A.E);
     const size_t lds = rollout_lds_bytes(A, 8);
     const auto fn = &rollout_m8_kernel<T, K0C_T, NOT_T, K0L>;
@@ -1629,6 +1652,9 @@ hipError_t launch_rollout_m8(const RolloutArgs& A, int T, hipStream_t stream) {
 template <int T, int K0C_T, int NG, int K0L = 0>
 __global__ void __launch_bounds__(64 * T, 1) rollout_m4_kernel(const RolloutArgs A) {
     constexpr int M = 4;
+    // compile-time LDS row strides (rollout_kernel LDAC / PWC; the launcher checks the geometry)
+    const int lda = (64 * T > 16 * K0C_T ? 64 * T : 16 * K0C_T) + 4;
+    const int pw = 16 * ((NG + 1) & ~1) + 4;
     constexpr int NW = T;
     constexpr int NT = 64 * NW;
     constexpr int KH = 4 * T;
@@ -1680,16 +1706,16 @@ __global__ void __launch_bounds__(64 * T, 1) rollout_m4_kernel(const RolloutArgs
         const int m = i / A.s, d = i - (i / A.s) * A.s;
         const int n = min(tile * M + m, A.N - 1);
         const float sv = A.s0_per_cand ? A.s0[(size_t)n * A.s + d] : A.s0[d];
-        actX[m * A.lda + d] = A.norm_s ? (sv - L.obs_mean[d]) / L.obs_std[d] : sv;
+        actX[m * lda + d] = A.norm_s ? (sv - L.obs_mean[d]) / L.obs_std[d] : sv;
     }
     for (int i = tid; i < M * A.k0pad_extra; i += NT) {
         const int m = i / A.k0pad_extra, j = i - (i / A.k0pad_extra) * A.k0pad_extra;
-        actX[m * A.lda + A.s + A.a + j] = 0.f;
+        actX[m * lda + A.s + A.a + j] = 0.f;
     }
     EpiParams<SS> P;
     load_epi_params<SS>(A, L, lane, P);
     if (actw) {
-        stage_actions<1, SS>(A, P, L, actX, awave, lane, av, acp);
+        stage_actions<1, SS>(A, P, L, actX, awave, lane, av, acp, lda);
         const float v = rowsum16(acp[0]);
         if ((lane & 15) == 0) acs[epi_row(0, awave, lane)] = v;
     }
@@ -1720,7 +1746,7 @@ __global__ void __launch_bounds__(64 * T, 1) rollout_m4_kernel(const RolloutArgs
     const int row0 = 64 * wave + 32 * ((lane >> 2) & 1) + 4 * (lane >> 3);   // this lane's 4 D rows
     auto read_b = [&](f32x4 (&b)[4], const float* in, int col) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) b[q] = *reinterpret_cast<const f32x4*>(in + cand * A.lda + col + 4 * q);
+        for (int q = 0; q < 4; ++q) b[q] = *reinterpret_cast<const f32x4*>(in + cand * lda + col + 4 * q);
     };
     auto mma_chunk = [&](const f32x4 (&w)[4], const f32x4 (&b)[4]) {
 #pragma unroll
@@ -1739,7 +1765,7 @@ __global__ void __launch_bounds__(64 * T, 1) rollout_m4_kernel(const RolloutArgs
     auto store_layer = [&](float* out) {
         f32x4 v = acc + bias;
         v = __builtin_elementwise_max(v, f32x4{0.f, 0.f, 0.f, 0.f});
-        *reinterpret_cast<f32x4*>(out + cand * A.lda + row0) = v;
+        *reinterpret_cast<f32x4*>(out + cand * lda + row0) = v;
     };
 #define M4_CHUNK(SLOT, KC, NK, IN)                                          \
     do {                                                                    \
@@ -1803,7 +1829,7 @@ __global__ void __launch_bounds__(64 * T, 1) rollout_m4_kernel(const RolloutArgs
                 f32x4 hq[4];
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
-                    hq[q] = *reinterpret_cast<const f32x4*>(in + cand * A.lda + 64 * wave + 16 * o + 4 * q);
+                    hq[q] = *reinterpret_cast<const f32x4*>(in + cand * lda + 64 * wave + 16 * o + 4 * q);
                 constexpr int base = K0C_T;   // output chunk o sits in slot (K0C + KH + o) % NB
                 M4_LOAD(((base + o) + NB - 1) % NB, g + NB - 1);
                 const int h = o / KPH;
@@ -1833,20 +1859,20 @@ __global__ void __launch_bounds__(64 * T, 1) rollout_m4_kernel(const RolloutArgs
 #pragma unroll
                     for (int i = 0; i < 4; ++i) y[i] = x[i] + __shfl_xor(x[i], 8);
                     if (chain == 0)
-                        *reinterpret_cast<f32x4*>(L.part + (wave * NHW + h) * (M * A.pw) + cand * A.pw + 16 * gr +
+                        *reinterpret_cast<f32x4*>(L.part + (wave * NHW + h) * (M * pw) + cand * pw + 16 * gr +
                                                   4 * (lane >> 4)) = y;
                 }
         }
         __syncthreads();
         // ---- epilogue: the 8-wave kernel's split-mode goal-state epilogue for rows 0..3
         if (epi) {
-            const int ws = M * A.pw;
+            const int ws = M * pw;
             const int j = lane & 15;
             const int m = epi_row(0, 0, lane);
             const int n = tile * M + m;
             float sc = 0.f;
             auto slot = [&](int d, float om, float os, float goal, float cw, float bo) {
-                const int ro = m * A.pw + d;
+                const int ro = m * pw + d;
                 float o = sum_partials<8>(L.part, ws, ro);
                 o = o + bo;
                 const float sn = A.unnorm_s ? o * os + om : o;
@@ -1854,7 +1880,7 @@ __global__ void __launch_bounds__(64 * T, 1) rollout_m4_kernel(const RolloutArgs
                     const float x = (sn - goal) * cw;
                     sc += sqrtf(x * x + A.alpha_s2) - A.alpha_s;
                 }
-                actX[m * A.lda + d] = A.norm_s ? (sn - om) / os : sn;
+                actX[m * lda + d] = A.norm_s ? (sn - om) / os : sn;
                 if (A.states_out != nullptr && n < A.N)
                     A.states_out[(((size_t)e * A.H + t) * A.N + n) * A.s + d] = sn;
             };
@@ -1870,12 +1896,12 @@ __global__ void __launch_bounds__(64 * T, 1) rollout_m4_kernel(const RolloutArgs
                     if (d < A.s) slot(d, L.obs_mean[d], L.obs_std[d], L.goal[d], L.cw[d], bout[d]);
                 }
             }
-            for (int d = A.s + A.a + j; d < A.s + A.a + A.k0pad_extra; d += 16) actX[m * A.lda + d] = 0.f;
+            for (int d = A.s + A.a + j; d < A.s + A.a + A.k0pad_extra; d += 16) actX[m * lda + d] = 0.f;
             sc = rowsum16(sc);
             const float ac = acs[(t & 1) * M + m];
             total += sc + A.alpha_a2 * (ac / (float)A.a);
         } else if (actw && t + 1 < A.H) {
-            stage_actions<1, SS>(A, P, L, actX, awave, lane, av, acp);
+            stage_actions<1, SS>(A, P, L, actX, awave, lane, av, acp, lda);
             const float v = rowsum16(acp[0]);
             if ((lane & 15) == 0) acs[((t + 1) & 1) * M + epi_row(0, awave, lane)] = v;
         }
@@ -1899,6 +1925,7 @@ template <int T, int K0C_T, int NG, int K0L = 0>
 static hipError_t launch_m4_tr(const RolloutArgs& A_in, hipStream_t stream) {
     RolloutArgs A = A_in;
     A.nw = 8;   // output partials: the canonical 8
+    if (!ring_strides_ok<T, K0C_T, (NG + 1) & ~1>(A)) return hipErrorInvalidValue;
     const int ntiles = (A.N + 3) / 4;
     const dim3 grid = A.xcd_map ? dim3(ntiles * A.E) : dim3(ntiles, A.E);
     const size_t lds = rollout_lds_bytes(A, 4);
