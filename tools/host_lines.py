@@ -1,0 +1,96 @@
+"""Diagnostic: the host side of one bench plan (CEMPlanner.plan_detailed on a host s0, the bench's
+kwargs) statement by statement -- the same calls planners.plan_detailed / _cem_fused_single /
+_cem_plan_host make, in order, with a perf_counter stamp after each -- mean microseconds per segment
+over many plans. Usage: python tools/host_lines.py [config_id] [plans] [candidates]"""
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "mujoco-mbrl_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from mbrl_amd import CEMPlanner, _lib, fused, planners, synthetic  # noqa: E402
+
+
+def main():
+    cid = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    n = int(sys.argv[2]) if len(sys.argv) > 2 else 300
+    prob0 = synthetic.make_problem(cid)
+    cfg = prob0["cfg"]
+    N = int(sys.argv[3]) if len(sys.argv) > 3 else cfg["N"]
+    dev = torch.device("cuda:0")
+    kw = dict(num_candidates=N, num_elites=N // 10, num_iterations=5, alpha=0.1, seed=prob0["rng_seed"],
+              distributed=False, device=dev, precision="f32")
+    s0, model, cost, sa, H = prob0["s0"], prob0["model"], prob0["cost"], prob0["sample_action"], cfg["H"]
+    lib = _lib.load()
+    seg = {}
+
+    def one():
+        t = [time.perf_counter()]
+        stamp = lambda name: (t.append(time.perf_counter()), seg.setdefault(name, []).append(t[-1] - t[-2]))  # noqa: E731
+        d = planners._device(kw)
+        stamp("device")
+        st = CEMPlanner._settings(sa, H, kw)
+        stamp("settings")
+        ctx = torch.cuda.device(d)
+        ctx.__enter__()
+        stamp("cuda.device enter")
+        mdesc = fused.describe_model(model)
+        stamp("describe_model")
+        cdesc = fused.describe_cost(cost, mdesc["s"], mdesc)
+        stamp("describe_cost")
+        prob = fused.device_problem(mdesc, cdesc, d)
+        stamp("device_problem")
+        ok = fused.semantic_check(model, cost, mdesc, cdesc, d, prob)
+        stamp("semantic_check (cached)")
+        assert ok
+        Nn, K, Hh, I = st["N"], st["K"], st["H"], st["I"]
+        pkey = (Nn, Hh, K, I, st["alpha"], st["lo"], st["hi"], st["init_std"], int(st["seed"]) & 0xFFFFFFFFFFFFFFFF)
+        params, pref, need = prob.plan_cache[pkey]
+        stamp("plan_cache")
+        ws = planners._workspace(("cem", str(d)), need, d)
+        stamp("workspace")
+        md = prob.mdesc
+        a, s = md["a"], md["s"]
+        stage = planners._staging(d, Hh * (s + 3 * a) + s)
+        stamp("staging lookup")
+        arr = stage.array
+        o_s0 = Hh * (s + 3 * a)
+        arr[o_s0:o_s0 + s] = s0.detach().reshape(-1).to(torch.float32).numpy()
+        stamp("s0 into staging")
+        o_act, o_mu, o_sg = Hh * s, Hh * (s + a), Hh * (s + 2 * a)
+        at = stage.cached_at((Hh, s, a), (o_s0, o_mu, o_sg, o_act, 0))
+        ev = planners._events(st, I)
+        wsp = _lib.ptr(ws)
+        sh = _lib.stream_handle(d)
+        stamp("pointers + stream handle")
+        rc = lib.mbrl_cem_plan(*prob.refs, at[0], pref, at[1], at[2], at[3], at[4], None, None, None, ev, wsp,
+                               ws.numel(), sh)
+        stamp("mbrl_cem_plan (C enqueue)")
+        _lib.check(rc, "mbrl_cem_plan")
+        torch.cuda.current_stream(d).synchronize()
+        stamp("sync (GPU plan)")
+        out = torch.from_numpy(arr[:o_s0].copy())
+        res = dict(states=out[:o_act].view(Hh, s), actions=out[o_act:o_mu].view(Hh, a))
+        stamp("copy-out")
+        ctx.__exit__(None, None, None)
+        stamp("cuda.device exit")
+        return res
+
+    for _ in range(20):
+        CEMPlanner.plan_detailed(s0, model, cost, sa, H, **kw)   # warm every cache
+        one()
+    seg.clear()
+    for _ in range(n):
+        one()
+    out = {k: round(float(np.mean(v)) * 1e6, 2) for k, v in seg.items()}
+    out["host_total_excl_sync_us"] = round(sum(v for k, v in out.items() if not k.startswith("sync")), 2)
+    print(json.dumps(dict(config=cfg["name"], candidates=N, plans=n, us=out)))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,7 +1,7 @@
 """Where a bench plan's host time goes (bench.py's timed loop, same kwargs and events): per plan the
 Python before the C call, the C call (enqueue), the sync + copy-out, the rest of plan_detailed, the
 bench loop between plans, the garbage collector's pauses, and the device span from the plan events.
-Usage: python tools/host_split.py [config_id] [plans]"""
+Usage: python tools/host_split.py [config_id] [plans] [candidates]"""
 import gc
 import json
 import os
@@ -23,8 +23,9 @@ def main():
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 100
     prob = synthetic.make_problem(cid)
     cfg = prob["cfg"]
+    N = int(sys.argv[3]) if len(sys.argv) > 3 else cfg["N"]
     dev = torch.device("cuda:0")
-    kw = dict(num_candidates=cfg["N"], num_elites=cfg["N"] // 10, num_iterations=5, alpha=0.1,
+    kw = dict(num_candidates=N, num_elites=N // 10, num_iterations=5, alpha=0.1,
               seed=prob["rng_seed"], distributed=False, device=dev, precision="f32")
     stamps = {}
     lib = _lib.load()
@@ -43,6 +44,23 @@ def main():
         stamps.setdefault("host_out", []).append(time.perf_counter())
         return r
     planners._cem_plan_host = host
+    from mbrl_amd import fused
+    real_dp = fused.describe_problem
+
+    def dp(*a, **k):
+        t = time.perf_counter()
+        r = real_dp(*a, **k)
+        stamps.setdefault("describe", []).append(time.perf_counter() - t)
+        return r
+    fused.describe_problem = dp
+    real_settings = planners.CEMPlanner._settings
+
+    def settings(*a, **k):
+        t = time.perf_counter()
+        r = real_settings(*a, **k)
+        stamps.setdefault("settings", []).append(time.perf_counter() - t)
+        return r
+    planners.CEMPlanner._settings = staticmethod(settings)
     gc_time = [0.0, 0, None]
 
     def gc_cb(phase, info):
@@ -83,7 +101,8 @@ def main():
                host_us=wall * 1e6 - span, python_before_c_us=us(ci - ti), c_enqueue_us=us(co - ci),
                sync_and_copy_us=us(ho - co), after_host_us=us(to - ho), between_plans_us=us(ti[1:] - to[:-1]),
                gc_us_per_plan=gc_time[0] / n * 1e6, gc_runs=gc_time[1],
-               python_before_c_max_us=float(np.max(ci - ti) * 1e6))
+               python_before_c_max_us=float(np.max(ci - ti) * 1e6),
+               describe_problem_us=us(stamps["describe"]), settings_us=us(stamps["settings"]), candidates=N)
     print(json.dumps(out))
 
 
