@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MBRL_ABI_VERSION 10
+#define MBRL_ABI_VERSION 11
 
 typedef struct ihipStream_t* mbrl_stream_t; /* == hipStream_t */
 typedef struct ihipEvent_t* mbrl_event_t;   /* == hipEvent_t  */
@@ -172,7 +172,9 @@ enum {
     MBRL_OPT_TRAIN_XCD = 16,        /* training launches: 1 row bands in XCD order (A/B; same bits)           */
     MBRL_OPT_TRAIN_SPLIT = 17,      /* 1: two-hidden-layer training in the five-launch layout instead of the
                                        fused three-launch step (A/B, tests; same bits)                    */
-    MBRL_OPT_COUNT = 18
+    MBRL_OPT_DEBUG_SHARD_FAIL = 18, /* i + 1 (tests): mbrl_cem_plan_sharded reports a failed launch at
+                                       iteration i (the rank then keeps joining the all-gathers); 0 off */
+    MBRL_OPT_COUNT = 19
 };
 int mbrl_set_option(int32_t option, int32_t value);
 int mbrl_get_option(int32_t option);
@@ -275,8 +277,10 @@ int mbrl_cem_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_no
  * bit-identical on every rank and to mbrl_cem_plan's for any nranks (records as mbrl_cem_plan's, over
  * all N). Replaces planners.cem_sharded_protocol's per-iteration Python loop. N % nranks == 0.
  * Every argument check runs before the first collective (the ranks pass the same shape, params and
- * nranks, so they agree on it). A nonzero return with nranks > 1 has ABORTED `comm` (ncclCommAbort), so
- * the other ranks' collectives fail instead of waiting for this one: drop it, do not destroy it.
+ * nranks, so they agree on it). A launch that fails later does not end the call early: the rank skips
+ * its remaining compute launches but still joins every remaining all-gather (its local costs poisoned
+ * to NaN, which every rank ranks last), so no peer waits on it, `comm` stays usable, and the error is
+ * returned at the end. The peers are not told: their plan completes without that rank's candidates.
  * comm == NULL is allowed only under MBRL_OPT_SHARD_EMULATE (tests): each call then rolls out every
  * rank's shard itself and fills the all-gather's rank-major buffer, so one GPU runs any nranks. */
 size_t mbrl_cem_plan_sharded_workspace_bytes(const mbrl_mlp_shape* shape, const mbrl_cem_params* params,

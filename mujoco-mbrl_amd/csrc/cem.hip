@@ -1444,6 +1444,7 @@ int mbrl_set_option(int32_t option, int32_t value) {
         case MBRL_OPT_TRAJ_HOP: ok = value >= 0 && value <= 3; break;
         case MBRL_OPT_GD_HOP: ok = value >= 0 && value <= 3; break;
         case MBRL_OPT_PAIR_L2: ok = value >= 0 && value <= 2; break;
+        case MBRL_OPT_DEBUG_SHARD_FAIL: ok = value >= 0 && value <= 1 << 20; break;
         default: ok = value == 0 || value == 1; break;
     }
     if (!ok) return fail(MBRL_EINVAL, "option %d: value %d not allowed", option, value);
@@ -1950,7 +1951,6 @@ struct Rccl {
     ncclResult_t (*get_unique_id)(ncclUniqueId*);
     ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int);
     ncclResult_t (*comm_destroy)(ncclComm_t);
-    ncclResult_t (*comm_abort)(ncclComm_t);
     ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t);
     std::string error;   // why the library could not be loaded ("" when it was)
 };
@@ -1975,7 +1975,6 @@ static const Rccl& rccl() {
         r.get_unique_id = reinterpret_cast<decltype(r.get_unique_id)>(sym("ncclGetUniqueId"));
         r.comm_init_rank = reinterpret_cast<decltype(r.comm_init_rank)>(sym("ncclCommInitRank"));
         r.comm_destroy = reinterpret_cast<decltype(r.comm_destroy)>(sym("ncclCommDestroy"));
-        r.comm_abort = reinterpret_cast<decltype(r.comm_abort)>(sym("ncclCommAbort"));
         r.all_gather = reinterpret_cast<decltype(r.all_gather)>(sym("ncclAllGather"));
     });
     return r;
@@ -2070,7 +2069,7 @@ size_t mbrl_cem_plan_sharded_workspace_bytes(const mbrl_mlp_shape* shape, const 
 // The body of mbrl_cem_plan_sharded. Every check that can reject the call runs before the first
 // collective, and each is a function of arguments every rank passes alike (shape, params, nranks,
 // the workspace size the same query gives), so the ranks agree on it; what can still fail later is a
-// HIP launch, after which the caller aborts the communicator.
+// HIP launch, and then the rank keeps its place in every remaining all-gather (below).
 static int plan_sharded_body(const mbrl_mlp_shape* shape, const void* packed, const mbrl_norm* norm,
                              const mbrl_cost* cost, const float* s0_in, const mbrl_cem_params* p, mbrl_comm_t comm,
                              int32_t nranks, int32_t rank, float* mu, float* sigma, float* actions_out,
@@ -2098,64 +2097,81 @@ static int plan_sharded_body(const mbrl_mlp_shape* shape, const void* packed, co
     const int off = rank * Nl;   // this rank's global candidates [off, off + Nl)
     const bool fuse = update_kpt(N, p->K, a) != 0 && g_opt[MBRL_OPT_UNFUSED_UPDATE].load(std::memory_order_relaxed) == 0;
     const bool fuse_draw = fuse && update_samples(Nl, a);
+    // From here on the ranks must issue the same collectives: a launch that fails on this rank does not
+    // end the call. Its remaining compute launches are skipped, but it still joins every remaining
+    // all-gather -- with its local costs poisoned to NaN (all bits set), so its peers neither wait on it
+    // nor take its shard's candidates as elites -- and the first error is returned at the end. (An
+    // abort of the communicator would not help: ncclCommAbort acts on the calling rank only, and peers
+    // already inside an all-gather would wait on it.)
+    int err = MBRL_OK;
+    std::string err_msg;
+    auto step = [&](int r) {
+        if (r != MBRL_OK && err == MBRL_OK) {
+            err = r;
+            err_msg = g_err;
+        }
+        return err == MBRL_OK;
+    };
     // one first launch: distribution rows, the workspace copy of s0, iteration 0's proposals of this
     // shard (global candidates [off, off + Nl)), the hand-off words zeroed (mbrl_cem_plan)
     const InitZero z = plan_zero(g, Nl, w.pair, w.xchg, w.xchg_bytes, w.status);
     hipLaunchKernelGGL(cem_init_kernel, dim3(H * (fuse_draw ? draw_slices(H, 1, Nl, a) : 1), 1), dim3(1024), 0, stream,
                        p->seed, p->init_mu, p->init_sigma, p->lo, p->hi, H, a, Nl, w.mu[0], w.sigma[0],
                        fuse_draw ? w.actions : nullptr, s0_in, g.s, w.s0, off, z);
-    if (!fuse_draw) {
+    step(hip_check(hipGetLastError(), "init launch"));
+    if (!fuse_draw && err == MBRL_OK) {
         mbrl_sampler sp0{};
         sp0.seed = p->seed; sp0.iteration = 0; sp0.mu = w.mu[0]; sp0.sigma = w.sigma[0]; sp0.lo = p->lo; sp0.hi = p->hi;
-        if ((rc = sample_impl(&sp0, H, a, Nl, off, w.actions, stream))) return rc;
+        step(sample_impl(&sp0, H, a, Nl, off, w.actions, stream));
     }
     unsigned pair_epoch = 0;
     int cur = 0;
     for (int it = 0; it < p->iterations; ++it) {
         mbrl_sampler sp{};
         sp.seed = p->seed; sp.iteration = it; sp.mu = w.mu[cur]; sp.sigma = w.sigma[cur]; sp.lo = p->lo; sp.hi = p->hi;
-        if (rollout_events && rollout_events[2 * it] &&
-            (rc = hip_check(hipEventRecord(reinterpret_cast<hipEvent_t>(rollout_events[2 * it]), stream), "event")))
-            return rc;
-        rc = rollout_impl(g, packed, norm, cost, w.s0, 0, w.actions, nullptr, Nl, H, 0, w.local, nullptr, nullptr,
-                          stream, pair_area_bytes(g, Nl) ? w.pair : nullptr, z.ptr[0] ? &pair_epoch : nullptr);
-        if (rc) return rc;
-        if (rollout_events && rollout_events[2 * it + 1] &&
-            (rc = hip_check(hipEventRecord(reinterpret_cast<hipEvent_t>(rollout_events[2 * it + 1]), stream), "event")))
-            return rc;
+        if (err == MBRL_OK && rollout_events && rollout_events[2 * it])
+            step(hip_check(hipEventRecord(reinterpret_cast<hipEvent_t>(rollout_events[2 * it]), stream), "event"));
+        if (err == MBRL_OK)
+            step(rollout_impl(g, packed, norm, cost, w.s0, 0, w.actions, nullptr, Nl, H, 0, w.local, nullptr, nullptr,
+                              stream, pair_area_bytes(g, Nl) ? w.pair : nullptr, z.ptr[0] ? &pair_epoch : nullptr));
+        if (err == MBRL_OK && g_opt[MBRL_OPT_DEBUG_SHARD_FAIL].load(std::memory_order_relaxed) == it + 1)
+            step(fail(MBRL_EHIP, "plan_sharded: injected launch failure at iteration %d (MBRL_OPT_DEBUG_SHARD_FAIL)", it));
+        if (err == MBRL_OK && rollout_events && rollout_events[2 * it + 1])
+            step(hip_check(hipEventRecord(reinterpret_cast<hipEvent_t>(rollout_events[2 * it + 1]), stream), "event"));
         // the one collective of an iteration: every rank's [E][Nl] costs, rank-major
         if (!emulate) {
-            if ((rc = nccl_check(rccl().all_gather(w.local, w.gathered, (size_t)E * Nl, ncclFloat,
-                                                   reinterpret_cast<ncclComm_t>(comm), stream), "ncclAllGather")))
-                return rc;
-        } else {
+            if (err != MBRL_OK)   // NaN costs sort last on every rank (MBRL_NAN_LAST)
+                (void)hipMemsetAsync(w.local, 0xFF, (size_t)E * Nl * 4, stream);
+            step(nccl_check(rccl().all_gather(w.local, w.gathered, (size_t)E * Nl, ncclFloat,
+                                              reinterpret_cast<ncclComm_t>(comm), stream), "ncclAllGather"));
+        } else if (err == MBRL_OK) {
             // rank r's slot: its proposals of this iteration (drawn at its global offset from this
             // iteration's mu / sigma, as its own previous update or initial draw made them) rolled out
-            for (int r = 0; r < nranks; ++r) {
+            for (int r = 0; r < nranks && err == MBRL_OK; ++r) {
                 float* slot = w.gathered + (size_t)r * E * Nl;
                 if (r == rank) {
-                    rc = hip_check(hipMemcpyAsync(slot, w.local, (size_t)E * Nl * 4, hipMemcpyDeviceToDevice, stream),
-                                   "emulated gather");
-                } else {
-                    if ((rc = sample_impl(&sp, H, a, Nl, r * Nl, w.emu_actions, stream))) return rc;
-                    rc = rollout_impl(g, packed, norm, cost, w.s0, 0, w.emu_actions, nullptr, Nl, H, 0, slot, nullptr,
+                    step(hip_check(hipMemcpyAsync(slot, w.local, (size_t)E * Nl * 4, hipMemcpyDeviceToDevice, stream),
+                                   "emulated gather"));
+                } else if (step(sample_impl(&sp, H, a, Nl, r * Nl, w.emu_actions, stream))) {
+                    step(rollout_impl(g, packed, norm, cost, w.s0, 0, w.emu_actions, nullptr, Nl, H, 0, slot, nullptr,
                                       nullptr, stream, pair_area_bytes(g, Nl) ? w.pair : nullptr,
-                                      z.ptr[0] ? &pair_epoch : nullptr);
+                                      z.ptr[0] ? &pair_epoch : nullptr));
                 }
-                if (rc) return rc;
             }
         }
+        if (err != MBRL_OK) continue;   // only the all-gathers remain for this rank
         float* costs = w.gathered;
         if (E > 1) {   // (one rank: the identity)
             hipLaunchKernelGGL(shard_costs_kernel, dim3(256), dim3(256), 0, stream, w.gathered, nranks, E, Nl, w.costs);
             costs = w.costs;
         }
-        if (cost_hist && (rc = hip_check(hipMemcpyAsync(cost_hist + (size_t)it * E * N, costs, (size_t)E * N * 4,
-                                                        hipMemcpyDeviceToDevice, stream), "cost record")))
-            return rc;
+        if (cost_hist)
+            step(hip_check(hipMemcpyAsync(cost_hist + (size_t)it * E * N, costs, (size_t)E * N * 4,
+                                          hipMemcpyDeviceToDevice, stream), "cost record"));
         int64_t* elites = elite_hist ? elite_hist + (size_t)it * p->K : w.elites;
         float* rets = returns_hist ? returns_hist + (size_t)it * N : nullptr;
         const bool last = it + 1 == p->iterations;
+        if (err != MBRL_OK) continue;
         if (fuse) {
             UpdateArgs U{};
             U.costs = costs; U.E = E; U.N = N; U.K = p->K; U.member_stride = N; U.H = H; U.a = a;
@@ -2166,21 +2182,20 @@ static int plan_sharded_body(const mbrl_mlp_shape* shape, const void* packed, co
             U.fin_mu = last ? mu : nullptr; U.fin_sigma = last ? sigma : nullptr; U.fin_actions = last ? actions_out : nullptr;
             U.next_actions = (fuse_draw && !last) ? w.actions : nullptr;   // this rank's shard of iteration it + 1
             U.draw_off = off; U.draw_n = Nl;
-            rc = update_impl(U, 1, stream);
-        } else {
-            rc = select_impl(costs, E, N, p->K, MBRL_NAN_LAST, elites, rets, w.keys, align256((size_t)N * 4), stream);
-            if (rc) return rc;
-            rc = refit_impl(&sp, H, a, elites, p->K, p->alpha, w.aelite, w.mu[cur ^ 1], w.sigma[cur ^ 1], stream,
-                            last ? mu : nullptr, last ? sigma : nullptr, last ? actions_out : nullptr);
+            step(update_impl(U, 1, stream));
+        } else if (step(select_impl(costs, E, N, p->K, MBRL_NAN_LAST, elites, rets, w.keys, align256((size_t)N * 4),
+                                    stream))) {
+            step(refit_impl(&sp, H, a, elites, p->K, p->alpha, w.aelite, w.mu[cur ^ 1], w.sigma[cur ^ 1], stream,
+                            last ? mu : nullptr, last ? sigma : nullptr, last ? actions_out : nullptr));
         }
-        if (rc) return rc;
         cur ^= 1;
-        if (!last && !fuse_draw) {
+        if (!last && !fuse_draw && err == MBRL_OK) {
             mbrl_sampler sn = sp;
             sn.iteration = it + 1; sn.mu = w.mu[cur]; sn.sigma = w.sigma[cur];
-            if ((rc = sample_impl(&sn, H, a, Nl, off, w.actions, stream))) return rc;
+            step(sample_impl(&sn, H, a, Nl, off, w.actions, stream));
         }
     }
+    if (err != MBRL_OK) return fail(err, "%s (this rank still joined every all-gather of the plan)", err_msg.c_str());
     // the final mean's states, on every rank (the same on each)
     float* per_member = E == 1 ? states_out : w.states;
     rc = traj_impl(g, packed, norm, w.s0, actions_out, H, per_member, w.xchg, w.xchg_bytes, w.status, stream,
@@ -2199,17 +2214,9 @@ int mbrl_cem_plan_sharded(const mbrl_mlp_shape* shape, const void* packed, const
                           int32_t nranks, int32_t rank, float* mu, float* sigma, float* actions_out,
                           float* states_out, float* cost_hist, float* returns_hist, int64_t* elite_hist,
                           mbrl_event_t* rollout_events, void* workspace, size_t ws_bytes, mbrl_stream_t stream) {
-    const int rc = plan_sharded_body(shape, packed, norm, cost, s0_in, p, comm, nranks, rank, mu, sigma, actions_out,
-                                     states_out, cost_hist, returns_hist, elite_hist, rollout_events, workspace,
-                                     ws_bytes, reinterpret_cast<hipStream_t>(stream));
-    // A rank that stops early would leave the others waiting in an all-gather it never joins: abort the
-    // communicator, so their collectives fail instead (the caller must drop it; include/mbrl_cem.h).
-    if (rc != MBRL_OK && comm && nranks > 1 && rccl().error.empty()) {
-        const std::string msg = g_err;
-        (void)rccl().comm_abort(reinterpret_cast<ncclComm_t>(comm));
-        fail(rc, "%s (communicator aborted)", msg.c_str());
-    }
-    return rc;
+    return plan_sharded_body(shape, packed, norm, cost, s0_in, p, comm, nranks, rank, mu, sigma, actions_out,
+                             states_out, cost_hist, returns_hist, elite_hist, rollout_events, workspace, ws_bytes,
+                             reinterpret_cast<hipStream_t>(stream));
 }
 
 #ifdef MBRL_STAMPS

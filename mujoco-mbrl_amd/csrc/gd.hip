@@ -870,10 +870,15 @@ static hipError_t launch_gd_coop_w(const GdArgs& A, gc_u64* xchg, unsigned* stat
     const int P = A.Wpad / GC_ROWS;
     if (!grid_fits(reinterpret_cast<const void*>(fn), GC_THREADS, lds, P * A.batch))
         return hipErrorCooperativeLaunchTooLarge;
-    if (A.hop_mode >= 1)   // plan b on the blocks with blockIdx.x % 8 == b % 8 (grid.y: groups of 8 plans)
-        hipLaunchKernelGGL(fn, dim3(8 * P, (A.batch + 7) / 8), dim3(GC_THREADS), lds, stream, A, xchg, status);
+    // the per-XCD grid puts ceil(batch / 8) plans' P workgroups on each XCD: they must fit one XCD's
+    // share of the device (an eighth of the capacity), else the (P, batch) grid
+    GdArgs B = A;
+    if (B.hop_mode >= 1 && !grid_fits(reinterpret_cast<const void*>(fn), GC_THREADS, lds, 8 * P * ((B.batch + 7) / 8)))
+        B.hop_mode = 0;
+    if (B.hop_mode >= 1)   // plan b on the blocks with blockIdx.x % 8 == b % 8 (grid.y: groups of 8 plans)
+        hipLaunchKernelGGL(fn, dim3(8 * P, (B.batch + 7) / 8), dim3(GC_THREADS), lds, stream, B, xchg, status);
     else
-        hipLaunchKernelGGL(fn, dim3(P, A.batch), dim3(GC_THREADS), lds, stream, A, xchg, status);
+        hipLaunchKernelGGL(fn, dim3(P, B.batch), dim3(GC_THREADS), lds, stream, B, xchg, status);
     return hipGetLastError();
 }
 

@@ -434,7 +434,9 @@ static hipError_t launch_coop_variant(const TrajArgs& A_in, int E, u64* xchg, un
         return hipErrorCooperativeLaunchTooLarge;
     TrajArgs A = A_in;
     A.E = E;
-    if (A.hop_mode >= 1 && E <= 8) {
+    // the per-XCD grid puts each member's P workgroups on one XCD: P must fit an eighth of the capacity
+    const bool xcd_fits = grid_fits(reinterpret_cast<const void*>(&traj_coop_kernel<K0R, SM, WI>), COOP_THREADS, lds, 8 * P);
+    if (A.hop_mode >= 1 && E <= 8 && xcd_fits) {
         hipLaunchKernelGGL((traj_coop_kernel<K0R, SM, WI>), dim3(8 * P), dim3(COOP_THREADS), lds, stream, A, xchg,
                            status);
     } else {

@@ -26,7 +26,7 @@ MBRL_EHIP = -3
 MBRL_EWORKSPACE = -4
 MBRL_COST_GOAL_STATE = 0
 MBRL_COST_MODEL_REWARD = 1
-ABI_VERSION = 10
+ABI_VERSION = 11
 MBRL_NAN_LAST = 0
 MBRL_NAN_FIRST = 1
 MBRL_PRECISION_F32 = 0
@@ -38,7 +38,7 @@ OPTIONS = {"rollout_tile": 0, "split_tile": 1, "debug_traj_abort": 2, "gd_single
            "unfused_update": 5, "adam_arith": 6, "xcd_map": 7, "train_tile": 8, "train_no_fold": 9,
            "rollout_pair": 10, "shard_emulate": 11, "debug_pair_abort": 12,
            "traj_hop": 13, "gd_hop": 14, "pair_l2": 15,
-           "train_xcd": 16, "train_split": 17}
+           "train_xcd": 16, "train_split": 17, "debug_shard_fail": 18}
 
 
 def precision_code(name):
@@ -231,6 +231,14 @@ class HostStaging:
     def at(self, offset):
         """Device address of element `offset`."""
         return c_void_p(self.device.value + 4 * int(offset))
+
+    def cached_at(self, key, offsets):
+        """at() of each offset, built once per `key` (a plan's fixed layout of this buffer)."""
+        cache = self.__dict__.setdefault("_at", {})
+        hit = cache.get(key)
+        if hit is None:
+            hit = cache[key] = tuple(self.at(o) for o in offsets)
+        return hit
 
     def __del__(self):
         if getattr(self, "host", None):

@@ -347,8 +347,15 @@ _PACKED = weakref.WeakKeyDictionary()   # module -> (key, packed tensor)
 
 
 def _param_key(members, device):
-    return (str(device),) + tuple((p.data_ptr(), p._version) for lins in members for lin in lins
-                                  for p in (lin.weight, lin.bias))
+    # Linear._parameters directly (a replaced Parameter shows up; Module.__getattr__ and a nested
+    # generator cost ~8x as much per plan)
+    key = [str(device)]
+    for lins in members:
+        for lin in lins:
+            prm = lin._parameters
+            w, b = prm["weight"], prm["bias"]
+            key.append((w.data_ptr(), w._version, b.data_ptr(), b._version))
+    return tuple(key)
 
 
 def mlp_shape(desc, precision=_lib.MBRL_PRECISION_F32):
@@ -421,6 +428,9 @@ class DeviceProblem:
         else:
             self._cost_t = []
             self.cost = _lib.Cost(_lib.MBRL_COST_GOAL_STATE, 0, 0, 0, None, None, 0.0, 0.0)
+        # the C-call arguments that never change for this problem (built once, not per plan)
+        self.refs = (ctypes_ref(self.shape), _lib.ptr(self.packed), ctypes_ref(self.norm), ctypes_ref(self.cost))
+        self.plan_cache = {}   # planners: per (CEM settings) the params struct and workspace size
 
 
 def _tensor_key(t):

@@ -198,6 +198,22 @@ class _NativeGrads:
             raise RuntimeError("mbrl_amd: a fused training step's bounded wait timed out (status word "
                                f"{word:#x}); the parameters of that step may be wrong")
 
+    def stage_status(self, staged, e):
+        """staged[e] |= the (sticky) status word, on the device behind epoch e's launches: one small
+        elementwise kernel, no copy engine and no sync (a 4-byte device-to-host copy per epoch stalled
+        the stream ~80 us)."""
+        staged[e:e + 1].bitwise_or_(self.ws[self.status_at:self.status_at + 4].view(torch.int32))
+
+    @staticmethod
+    def check_staged(staged):
+        """Raise naming the first epoch whose status word was set (check_status); one read."""
+        words = staged.cpu().numpy()
+        bad = np.flatnonzero(words & 1)
+        if bad.size:
+            raise RuntimeError("mbrl_amd: a fused training step's bounded wait timed out in epoch "
+                               f"{int(bad[0])} of this train_model call (status word {int(words[bad[0]]):#x}); "
+                               "the parameters of that epoch may be wrong")
+
     def run(self, idx):
         """The batch gradient for the rows `idx` (int64, on the device) into p.grad."""
         for p, g in zip(self.params, self.grads):
@@ -251,22 +267,37 @@ def _train_loop_on(dev, model, dataset, optimizer, batch_size, num_epochs, step_
     own = set() if native is None else {id(p) for p in native.params}
     extra = [p for g in optimizer.param_groups for p in g["params"] if id(p) not in own] if native is not None else []
     num_iters = 0
-    for _ in range(num_epochs):
-        host = _epoch_order(dataset)
-        order = torch.from_numpy(host).to(dev)
-        losses = native.epoch(order, batch_size, fast) if native is not None and fast is not None else None
+    whole = native is not None and fast is not None
+    if whole and num_epochs > 0:
+        # The device path issues the epochs back to back with no host round trip between them (a
+        # per-epoch copy of the row order from pageable memory waited for the previous epoch to drain).
+        # Epoch 0's order is drawn and copied first; the other epochs' orders are drawn while epoch 0
+        # runs -- the same np.random draws in the same order (nothing else in this loop draws from the
+        # global RNG) -- and copied on a side stream the training stream waits on before epoch 1. Each
+        # epoch's status word is staged on the device behind its launches; all are read after the last.
+        orders_host, orders_pinned, orders, side = _order_buffers(dev, num_epochs, dataset.num_transitions())
+        orders_host[0] = _epoch_order(dataset)
+        orders[0].copy_(orders_pinned[0], non_blocking=False)
+        status_staged = torch.zeros(num_epochs, dtype=torch.int32, device=dev)
+    epoch_losses = []
+    for ep in range(num_epochs):
+        if whole and ep == 1:
+            for e in range(1, num_epochs):
+                orders_host[e] = _epoch_order(dataset)
+            main = torch.cuda.current_stream(dev)
+            # (no earlier call still reads the buffers: each train_model call ends with a sync)
+            with torch.cuda.stream(side):
+                orders[1:].copy_(orders_pinned[1:], non_blocking=True)
+            main.wait_stream(side)
+        host = orders_host[ep] if whole else _epoch_order(dataset)
+        order = orders[ep] if whole else torch.from_numpy(host).to(dev)
+        losses = native.epoch(order, batch_size, fast) if whole else None
         if losses is not None:            # the whole epoch in one call; the writer gets its values after
-            if writer is not None:
-                for row in losses.cpu().tolist():
-                    num_iters += 1
-                    parts = [row[1], row[2]][:n_parts]
-                    for tag, val in zip(tags, parts if n_parts > 1 else [row[0]]):
-                        writer.add_scalar(tag.format(model.train_iterations), val, num_iters)
-                    if n_parts > 1:
-                        writer.add_scalar("loss/total/{}".format(model.train_iterations), row[0], num_iters)
-            else:
-                num_iters += losses.shape[0]
+            native.stage_status(status_staged, ep)
+            epoch_losses.append(losses)
             continue
+        num_iters = _write_epoch_losses(epoch_losses, writer, tags, n_parts, model, num_iters)
+        epoch_losses = []
         for i in range(0, len(host), batch_size):
             idx = order[i:i + batch_size]
             if native is not None:
@@ -288,13 +319,51 @@ def _train_loop_on(dev, model, dataset, optimizer, batch_size, num_epochs, step_
                     writer.add_scalar(tag.format(model.train_iterations), val, num_iters)
                 if n_parts > 1:
                     writer.add_scalar("loss/total/{}".format(model.train_iterations), loss, num_iters)
+    num_iters = _write_epoch_losses(epoch_losses, writer, tags, n_parts, model, num_iters)
     if graph is not None:
         for p in model.parameters():      # release the graph-pool grads; the eager path re-allocates
             p.grad = None
     # (the native path leaves the last batch's gradients in .grad, as the reference's loop does)
-    if native is not None:
+    if whole and num_epochs > 0:
+        _NativeGrads.check_staged(status_staged)
+    elif native is not None:
         native.check_status()
     model.train_iterations += 1
+
+
+_ORDER_BUFFERS = {}
+
+
+def _order_buffers(dev, epochs, n):
+    """Pinned host rows, device rows and a copy stream for `epochs` row orders of n transitions, kept for
+    later train_model calls on datasets of n transitions (rows for at least 16 epochs: a pinned
+    allocation costs milliseconds, so a later call with more epochs should not pay it again)."""
+    key = (str(dev), n)
+    hit = _ORDER_BUFFERS.get(key)
+    if hit is None or hit[0].shape[0] < epochs:
+        if len(_ORDER_BUFFERS) > 8:
+            _ORDER_BUFFERS.clear()
+        rows = max(epochs, 16)
+        pinned = torch.empty((rows, n), dtype=torch.int64, pin_memory=True)
+        hit = _ORDER_BUFFERS[key] = (pinned, torch.empty((rows, n), dtype=torch.int64, device=dev),
+                                     torch.cuda.Stream(dev))
+    return hit[0].numpy()[:epochs], hit[0][:epochs], hit[1][:epochs], hit[2]
+
+
+def _write_epoch_losses(epoch_losses, writer, tags, n_parts, model, num_iters):
+    """The writer's per-batch values of whole-epoch device calls (in batch order), after the epochs ran."""
+    for losses in epoch_losses:
+        if writer is None:
+            num_iters += losses.shape[0]
+            continue
+        for row in losses.cpu().tolist():
+            num_iters += 1
+            parts = [row[1], row[2]][:n_parts]
+            for tag, val in zip(tags, parts if n_parts > 1 else [row[0]]):
+                writer.add_scalar(tag.format(model.train_iterations), val, num_iters)
+            if n_parts > 1:
+                writer.add_scalar("loss/total/{}".format(model.train_iterations), row[0], num_iters)
+    return num_iters
 
 
 class DynamicsModel(nn.Module):

@@ -410,7 +410,7 @@ def _staging(dev, n):
     return buf
 
 
-def _cem_plan_host(lib, prob, initial_state, st, params, ws):
+def _cem_plan_host(lib, prob, initial_state, st, params, ws, pref):
     """mbrl_cem_plan with host staging (_lib.HostStaging): the plan's first launch reads the initial
     state from mapped host memory and its last launches write states, actions, mu and sigma there, so
     no copy launch precedes or follows the plan; one stream sync, then host tensors."""
@@ -422,12 +422,11 @@ def _cem_plan_host(lib, prob, initial_state, st, params, ws):
     o_s0 = H * (s + 3 * a)
     arr[o_s0:o_s0 + s] = initial_state.detach().reshape(-1).to(torch.float32).numpy()
     o_act, o_mu, o_sg = H * s, H * (s + a), H * (s + 2 * a)
+    at = stage.cached_at((H, s, a), (o_s0, o_mu, o_sg, o_act, 0))
     pev = st["plan_events"]
     if pev is not None:
         pev[0].record()
-    _lib.check(lib.mbrl_cem_plan(fused.ctypes_ref(prob.shape), _lib.ptr(prob.packed), fused.ctypes_ref(prob.norm),
-                                 fused.ctypes_ref(prob.cost), stage.at(o_s0), fused.ctypes_ref(params), stage.at(o_mu),
-                                 stage.at(o_sg), stage.at(o_act), stage.at(0), None, None, None,
+    _lib.check(lib.mbrl_cem_plan(*prob.refs, at[0], pref, at[1], at[2], at[3], at[4], None, None, None,
                                  _events(st, params.iterations), _lib.ptr(ws), ws.numel(), _lib.stream_handle(dev)),
                "mbrl_cem_plan")
     if pev is not None:
@@ -453,12 +452,19 @@ def _cem_fused_single(prob, initial_state, st):
     md = prob.mdesc
     N, K, H, I = st["N"], st["K"], st["H"], st["I"]
     a, s, E = md["a"], md["s"], md["E"]
-    params = _lib.CemParams(N, H, K, I, st["alpha"], st["lo"], st["hi"], 0.0, st["init_std"], 0,
-                            int(st["seed"]) & 0xFFFFFFFFFFFFFFFF)
-    need = lib.mbrl_cem_workspace_bytes(fused.ctypes_ref(prob.shape), fused.ctypes_ref(params))
+    # the params struct and the workspace size per settings, built once per problem (host turn)
+    pkey = (N, H, K, I, st["alpha"], st["lo"], st["hi"], st["init_std"], int(st["seed"]) & 0xFFFFFFFFFFFFFFFF)
+    hit = prob.plan_cache.get(pkey)
+    if hit is None:
+        params = _lib.CemParams(N, H, K, I, st["alpha"], st["lo"], st["hi"], 0.0, st["init_std"], 0, pkey[-1])
+        need = lib.mbrl_cem_workspace_bytes(fused.ctypes_ref(prob.shape), fused.ctypes_ref(params))
+        if len(prob.plan_cache) > 64:
+            prob.plan_cache.clear()
+        hit = prob.plan_cache[pkey] = (params, fused.ctypes_ref(params), need)
+    params, pref, need = hit
     ws = _workspace(("cem", str(dev)), need, dev)
     if HOST_STAGING and not st["keep"] and not st["record"] and not initial_state.is_cuda:
-        return _cem_plan_host(lib, prob, initial_state, st, params, ws)
+        return _cem_plan_host(lib, prob, initial_state, st, params, ws, pref)
     s0 = initial_state.to(device=dev, dtype=torch.float32).contiguous()
     # one allocation for the outputs; states and actions side by side, so that plan() hands both
     # back to the host in ONE copy
@@ -694,11 +700,8 @@ def _cem_sharded_native(prob, s0, st, world, rank, comm=_OWN_COMM):
                                    _lib.ptr(ws), ws.numel(), _lib.stream_handle(dev))
     if pev is not None and rc == _lib.MBRL_OK:
         pev[1].record()
-    if rc != _lib.MBRL_OK and comm and world > 1:
-        # the library aborted the communicator (so no other rank waits on this one): forget it, and
-        # the next plan builds a new one
-        for k in [k for k, v in _COMMS.items() if v is comm]:
-            del _COMMS[k]
+    # a failure after the argument checks still joined every all-gather of the plan (include/mbrl_cem.h),
+    # so the communicator stays in step with the other ranks and is kept
     _lib.check(rc, "mbrl_cem_plan_sharded")
     out = dict(states=states, actions=actions, mu=mu, sigma=sigma, _both=both)
     if rec:

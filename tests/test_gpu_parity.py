@@ -754,6 +754,28 @@ def _rccl_worker(rank, world, init_file, out_dir):
                          returns=torch.stack(list(res["returns"])).cpu().numpy(),
                          costs=torch.stack(list(res["costs"])).cpu().numpy(),
                          actions=res["actions"].cpu().numpy(), states=res["states"].cpu().numpy())
+        # a launch failure after the first collective (injected at iteration 1): the rank keeps joining
+        # the remaining all-gathers and reports the error at the end, so the communicator stays in step
+        # -- the next plan over the same communicator runs and equals the first one
+        cid, over = RCCL_CASES[0]
+        p = oc.synth_problem(cid, **over)
+        _, model_fn, cost_fn, sample_action = build(p)
+        md = fused.describe_model(model_fn)
+        prob = fused.device_problem(md, fused.describe_cost(cost_fn, md["s"], md), dev)
+        st = CEMPlanner._settings(sample_action, over["H"], dict(num_candidates=over["N"], num_iterations=3,
+                                                                 seed=p["rng_seed"], record=True))
+        s0 = torch.from_numpy(p["s0"]).to(dev)
+        planners.SHARDED_NATIVE = True
+        with planners._lib.option("debug_shard_fail", 2):
+            try:
+                planners._cem_fused_sharded(prob, s0, st, world)
+                raised = ""
+            except RuntimeError as e:
+                raised = str(e)
+        torch.cuda.synchronize()
+        again = planners._cem_fused_sharded(prob, s0, st, world)
+        np.savez(os.path.join(out_dir, f"c{cid}_nagain_r{rank}.npz"), mu=again["mu"].cpu().numpy(),
+                 elites=torch.stack(list(again["elites"])).cpu().numpy(), raised=np.array(raised))
         # a communicator that cannot be created (simulated: mbrl_comm_init fails) sends every rank to
         # the protocol, with a warning, instead of failing the plan
         real_load = planners._lib.load
@@ -812,8 +834,14 @@ def test_sharded_plan_over_rccl():
                            start_method="spawn")
         got = {(cid, n): dict(np.load(os.path.join(d, f"c{cid}_n{n}_r0.npz"))) for cid, _ in RCCL_CASES for n in (0, 1)}
         fail = dict(np.load(os.path.join(d, f"c{RCCL_CASES[0][0]}_nfail_r0.npz")))
+        again = dict(np.load(os.path.join(d, f"c{RCCL_CASES[0][0]}_nagain_r0.npz")))
     assert np.array_equal(fail["mu"], got[(RCCL_CASES[0][0], 0)]["mu"])
     assert np.array_equal(fail["elites"], got[(RCCL_CASES[0][0], 0)]["elites"])
+    # the injected in-loop failure was reported, and the same communicator then ran the next plan exactly
+    assert "injected launch failure at iteration 1" in str(again["raised"]), str(again["raised"])
+    assert "still joined every all-gather" in str(again["raised"])
+    assert np.array_equal(again["mu"], got[(RCCL_CASES[0][0], 1)]["mu"])
+    assert np.array_equal(again["elites"], got[(RCCL_CASES[0][0], 1)]["elites"])
     for cid, over in RCCL_CASES:
         p = ocem.synth_problem(cid, **over)
         _, model_fn, cost_fn, sample_action = build(p)
