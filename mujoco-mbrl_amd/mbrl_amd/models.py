@@ -271,27 +271,28 @@ def _train_loop_on(dev, model, dataset, optimizer, batch_size, num_epochs, step_
     if whole and num_epochs > 0:
         # The device path issues the epochs back to back with no host round trip between them (a
         # per-epoch copy of the row order from pageable memory waited for the previous epoch to drain).
-        # Epoch 0's order is drawn and copied first; the other epochs' orders are drawn while epoch 0
-        # runs -- the same np.random draws in the same order (nothing else in this loop draws from the
-        # global RNG) -- and copied on a side stream the training stream waits on before epoch 1. Each
-        # epoch's status word is staged on the device behind its launches; all are read after the last.
+        # Epoch k + 1's order is drawn while epoch k runs -- the same np.random draws in the same order
+        # (nothing else in this loop draws from the global RNG) -- and copied from pinned memory on a
+        # side stream that the training stream waits on before epoch k + 1 (the copy lands while epoch k
+        # computes). Each epoch's status word is staged on the device behind its launches; all are read
+        # after the last epoch.
         orders_host, orders_pinned, orders, side = _order_buffers(dev, num_epochs, dataset.num_transitions())
         orders_host[0] = _epoch_order(dataset)
         orders[0].copy_(orders_pinned[0], non_blocking=False)
         status_staged = torch.zeros(num_epochs, dtype=torch.int32, device=dev)
+        main = torch.cuda.current_stream(dev)
     epoch_losses = []
     for ep in range(num_epochs):
-        if whole and ep == 1:
-            for e in range(1, num_epochs):
-                orders_host[e] = _epoch_order(dataset)
-            main = torch.cuda.current_stream(dev)
-            # (no earlier call still reads the buffers: each train_model call ends with a sync)
-            with torch.cuda.stream(side):
-                orders[1:].copy_(orders_pinned[1:], non_blocking=True)
-            main.wait_stream(side)
+        if whole and ep >= 1:
+            main.wait_stream(side)        # epoch ep's order has landed (copied while epoch ep - 1 ran)
         host = orders_host[ep] if whole else _epoch_order(dataset)
         order = orders[ep] if whole else torch.from_numpy(host).to(dev)
         losses = native.epoch(order, batch_size, fast) if whole else None
+        if whole and ep + 1 < num_epochs:
+            orders_host[ep + 1] = _epoch_order(dataset)
+            # (no earlier call still reads these rows: each train_model call ends with a sync)
+            with torch.cuda.stream(side):
+                orders[ep + 1].copy_(orders_pinned[ep + 1], non_blocking=True)
         if losses is not None:            # the whole epoch in one call; the writer gets its values after
             native.stage_status(status_staged, ep)
             epoch_losses.append(losses)
@@ -347,6 +348,10 @@ def _order_buffers(dev, epochs, n):
         pinned = torch.empty((rows, n), dtype=torch.int64, pin_memory=True)
         hit = _ORDER_BUFFERS[key] = (pinned, torch.empty((rows, n), dtype=torch.int64, device=dev),
                                      torch.cuda.Stream(dev))
+        # a stream's first operation sets up its hardware queue (~6 ms): pay it here, once
+        with torch.cuda.stream(hit[2]):
+            hit[1][:1].copy_(pinned[:1], non_blocking=True)
+        hit[2].synchronize()
     return hit[0].numpy()[:epochs], hit[0][:epochs], hit[1][:epochs], hit[2]
 
 
