@@ -252,7 +252,17 @@ def ptr(t):
 
 
 def stream_handle(device=None):
-    return c_void_p(torch.cuda.current_stream(device).cuda_stream)
+    """The current HIP stream of `device` (a torch.device, an index or None: the current device) as
+    the hipStream_t every entry point takes (the raw-pointer query: no Stream object per call)."""
+    if device is None:
+        idx = torch.cuda.current_device()
+    elif isinstance(device, int):
+        idx = device
+    else:
+        if not isinstance(device, torch.device):
+            device = torch.device(device)
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+    return c_void_p(torch._C._cuda_getCurrentRawStream(idx))
 
 
 def require_gpu(t):

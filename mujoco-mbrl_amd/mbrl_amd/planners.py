@@ -420,7 +420,8 @@ def _cem_plan_host(lib, prob, initial_state, st, params, ws, pref):
     stage = _staging(dev, H * (s + 3 * a) + s)
     arr = stage.array
     o_s0 = H * (s + 3 * a)
-    arr[o_s0:o_s0 + s] = initial_state.detach().reshape(-1).to(torch.float32).numpy()
+    x = initial_state.detach() if initial_state.requires_grad else initial_state
+    arr[o_s0:o_s0 + s] = x.numpy().reshape(-1) if x.dtype == torch.float32 else x.reshape(-1).to(torch.float32).numpy()
     o_act, o_mu, o_sg = H * s, H * (s + a), H * (s + 2 * a)
     at = stage.cached_at((H, s, a), (o_s0, o_mu, o_sg, o_act, 0))
     pev = st["plan_events"]
