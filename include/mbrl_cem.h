@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MBRL_ABI_VERSION 11
+#define MBRL_ABI_VERSION 12
 
 typedef struct ihipStream_t* mbrl_stream_t; /* == hipStream_t */
 typedef struct ihipEvent_t* mbrl_event_t;   /* == hipEvent_t  */
@@ -174,7 +174,8 @@ enum {
                                        fused three-launch step (A/B, tests; same bits)                    */
     MBRL_OPT_DEBUG_SHARD_FAIL = 18, /* i + 1 (tests): mbrl_cem_plan_sharded reports a failed launch at
                                        iteration i (the rank then keeps joining the all-gathers); 0 off */
-    MBRL_OPT_COUNT = 19
+    MBRL_OPT_TRAIN_FO = 19,         /* 1: the fused training step's F and O as two launches (A/B; same bits) */
+    MBRL_OPT_COUNT = 20
 };
 int mbrl_set_option(int32_t option, int32_t value);
 int mbrl_get_option(int32_t option);

@@ -1659,6 +1659,7 @@ static int train_shape(const mbrl_train_model* m, TrainShape* t) {
     t->fold = g_opt[MBRL_OPT_TRAIN_NO_FOLD].load(std::memory_order_relaxed) == 0 ? 1 : 0;
     t->xcd = g_opt[MBRL_OPT_TRAIN_XCD].load(std::memory_order_relaxed) == 1 ? 1 : 0;
     t->split = g_opt[MBRL_OPT_TRAIN_SPLIT].load(std::memory_order_relaxed) == 1 ? 1 : 0;
+    t->fo_split = g_opt[MBRL_OPT_TRAIN_FO].load(std::memory_order_relaxed) == 1 ? 1 : 0;
     return MBRL_OK;
 }
 

@@ -404,6 +404,7 @@ struct TrainShape {
     int fold;                    // 1: the layer-0 weight gradient folds into the dH_0 launch (same bits)
     int xcd;                     // 1: row-band tiles in XCD order in every launch (MBRL_OPT_TRAIN_XCD; same bits)
     int split;                   // 1: the five-launch layout where the fused step applies (MBRL_OPT_TRAIN_SPLIT; same bits)
+    int fo_split;                // 1: the fused step's F and O as two launches (MBRL_OPT_TRAIN_FO; same bits)
 };
 struct TrainTensors {
     const float* const* weight;  // L + 1 (+ 1 reward head) nn.Linear weights [out][in]

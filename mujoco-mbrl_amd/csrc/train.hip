@@ -850,10 +850,19 @@ struct FusedArgs {
     mbrl_adam_tensor ab1;
     mbrl_adam_hparams hp;
     int arith;
-    unsigned* zero_words;               // F's workgroup 0 zeroes zero_n words (both folds' tickets)
+    unsigned* zero_words;               // F's workgroup 0 zeroes zero_n words (the tickets of later launches)
     int zero_n;
     float scale_s, scale_r, inv_s, inv_r;
+    // F and O in one launch (train_fused_fo_kernel): per 32-row band of the batch a counter (own 128-B
+    // line) that the band's F tiles add to once their H_1 columns are written through; each O tile
+    // waits for all tiles_n, then adds again, and the last add of the band resets it (zero between
+    // launches, as the caller's once-zeroed workspace starts). status: bit 0 = a bounded wait timed out.
+    unsigned* band;
+    unsigned* status;
 };
+
+constexpr int TRAIN_SC1 = 16;   // buffer-op aux bit: sc1 (write-through stores, L1-bypassing loads)
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 // A wave's K range in a launch of nw waves (gemm_tile's split: contiguous 16-deep chunks).
 __device__ __forceinline__ void wave_k_range(int K, int nw, int w, int& kb0, int& kb1) {
@@ -874,15 +883,17 @@ __device__ __forceinline__ f32x4 row4(const float* row, bool valid, int k0, int 
     return v;
 }
 
-// KCH: 16-deep chunks of K0 (2: K0 <= 32, 4: K0 <= 64), one per wave of the layer-0 launch (4 waves)
-template <int NW, int KCH>
-__global__ __launch_bounds__(64 * NW) void train_fused_fwd_kernel(const FusedArgs F) {
+constexpr int FUSED_HLD = FUSED_WMAX + 4, FUSED_XLD = FUSED_K0MAX + 4;
+
+// F's body. KCH: 16-deep chunks of K0 (2: K0 <= 32, 4: K0 <= 64), one per wave of the layer-0 launch
+// (4 waves). FO (one launch with O): the batch's targets and the H_1 tile leave as write-through (sc1)
+// stores, the tile also stays in LDS (hm: O's ReLU mask and dW_out operand), and the workgroup then
+// adds to its band's counter.
+template <int NW, int KCH, bool FO>
+__device__ __forceinline__ void fused_fwd(const FusedArgs& F, float (*red)[TT][TT + 1], float (*h0)[FUSED_HLD],
+                                          float (*xr)[FUSED_XLD], float (*hm)[TT + 1]) {
     constexpr int NT = 64 * NW, EPT = TT * TT / NT, MAXPER = NW == 16 ? 2 : 4, MAXY = NW == 16 ? 2 : 4;
     constexpr int NW0 = 4;   // the layer-0 launch's waves (K0 < 256)
-    constexpr int HLD = FUSED_WMAX + 4, XLD = FUSED_K0MAX + 4;
-    __shared__ float red[NW][TT][TT + 1];
-    __shared__ __attribute__((aligned(16))) float h0[TT][HLD];
-    __shared__ __attribute__((aligned(16))) float xr[TT][XLD];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, q = lane >> 4, c = lane & 15;
     const int tm = blockIdx.x / F.tiles_n, tn = blockIdx.x - tm * F.tiles_n, m0 = tm * TT, n0 = tn * TT;
     const int W = F.W, K0 = F.K0, R = F.R;
@@ -954,11 +965,20 @@ __global__ __launch_bounds__(64 * NW) void train_fused_fwd_kernel(const FusedArg
             const int n = n0 + 16 * y + c, kb = kb0 + 16 * u;
             bw[u][y] = row4(F.w1 + (int64_t)min(n, W - 1) * W, n < W && kb < kb1, kb + 4 * q, W, vec1);
         }
-    float pre[EPT];
+    float pre[FO ? 1 : EPT];
+    f32x4 pre4 = {0.0f, 0.0f, 0.0f, 0.0f};   // FO: thread t < 256 finishes 4 consecutive columns
+    if constexpr (FO) {
 #pragma unroll
-    for (int j = 0; j < EPT; ++j) {
-        const int e = tid + j * NT, n = n0 + (e & 31);
-        pre[j] = n < W ? F.b1[n] : 0.0f;
+        for (int i = 0; i < 4; ++i) {
+            const int n = n0 + (tid & 7) * 4 + i;
+            pre4[i] = (tid < TT * TT / 4 && n < W) ? F.b1[n] : 0.0f;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) {
+            const int e = tid + j * NT, n = n0 + (e & 31);
+            pre[j] = n < W ? F.b1[n] : 0.0f;
+        }
     }
     // W_0's rows for this wave's 16-column blocks of H_0 (y = wave, wave + NW, ...), every chunk
     const int ny = (W + 15) >> 4, nch0 = (K0 + 15) >> 4;
@@ -983,7 +1003,10 @@ __global__ __launch_bounds__(64 * NW) void train_fused_fwd_kernel(const FusedArg
 #pragma unroll
     for (int j = 0; j < TPT; ++j) {
         const int e = tid + j * NT, r = e >> 5, o = e & 31;
-        if (tsrc[j] >= 0) (nx ? F.tnext : F.tgt)[(int64_t)(m0 + r) * F.J + o] = tv[j];
+        if (tsrc[j] < 0) continue;
+        float* dst = (nx ? F.tnext : F.tgt) + (int64_t)(m0 + r) * F.J + o;
+        if (FO && !nx) __hip_atomic_store(dst, tv[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // O reads it
+        else *dst = tv[j];
     }
     __syncthreads();
     FSTAMP(0, 1);
@@ -1057,26 +1080,109 @@ __global__ __launch_bounds__(64 * NW) void train_fused_fwd_kernel(const FusedArg
 #pragma unroll
             for (int v = 0; v < 4; ++v) red[wave][16 * x + 4 * q + v][16 * y + c] = acc[x][y][v];
     __syncthreads();
+    if constexpr (!FO) {
 #pragma unroll
-    for (int j = 0; j < EPT; ++j) {
-        const int e = tid + j * NT, row = e >> 5, col = e & 31, m = m0 + row, n = n0 + col;
-        if (m >= R || n >= W) continue;
-        float v = red[0][row][col];
+        for (int j = 0; j < EPT; ++j) {
+            const int e = tid + j * NT, row = e >> 5, col = e & 31, m = m0 + row, n = n0 + col;
+            if (m >= R || n >= W) continue;
+            float v = red[0][row][col];
 #pragma unroll
-        for (int w = 1; w < NW; ++w) v = v + red[w][row][col];
-        v = v + pre[j];
-        F.act1[(int64_t)m * W + n] = v > 0.0f ? v : 0.0f;
+            for (int w = 1; w < NW; ++w) v = v + red[w][row][col];
+            v = v + pre[j];
+            F.act1[(int64_t)m * W + n] = v > 0.0f ? v : 0.0f;
+        }
+    } else {
+        // the same sums, 4 columns per thread: one 16-byte write-through store (4-byte ones at a ragged
+        // or unaligned edge), and the tile into hm
+        if (tid < TT * TT / 4) {
+            const int row = tid >> 3, c4 = (tid & 7) * 4, m = m0 + row;
+            f32x4 h;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float v = red[0][row][c4 + i];
+#pragma unroll
+                for (int w = 1; w < NW; ++w) v = v + red[w][row][c4 + i];
+                v = v + pre4[i];
+                h[i] = (m < R && n0 + c4 + i < W) ? (v > 0.0f ? v : 0.0f) : 0.0f;
+                hm[row][c4 + i] = h[i];
+            }
+            if (m < R) {
+                const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc(
+                    F.act1, 0, (int)((int64_t)R * W * sizeof(float)), 0x00020000);
+                const unsigned off = (unsigned)(((int64_t)m * W + n0 + c4) * sizeof(float));
+                if ((W & 3) == 0 && (reinterpret_cast<uintptr_t>(F.act1) & 15) == 0 && n0 + c4 + 3 < W) {
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, h), ar, off, 0, TRAIN_SC1);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        if (n0 + c4 + i < W)
+                            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, (float)h[i]), ar, off + 4 * i, 0,
+                                                                  TRAIN_SC1);
+                }
+            }
+        }
+        // every storing wave drains its stores, then one lane signals for the workgroup
+        // (MI355X_MICROARCH.md, the first row of the sc1 hand-off table)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) __hip_atomic_fetch_add(F.band + tm * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     FSTAMP(0, 3);
 }
 
-template <int NW>
-__global__ __launch_bounds__(64 * NW) void train_fused_out_kernel(const FusedArgs F) {
-    constexpr int NT = 64 * NW, EPT = TT * TT / NT, MAXPER = NW == 16 ? 2 : 4;
+// KCH: as fused_fwd
+template <int NW, int KCH>
+__global__ __launch_bounds__(64 * NW) void train_fused_fwd_kernel(const FusedArgs F) {
     __shared__ float red[NW][TT][TT + 1];
-    __shared__ float dy[TT][TT + 1];    // the tile's 32 rows of dY (columns past J zero)
-    __shared__ float hm[TT][TT + 1];    // H_1 of the tile: the ReLU mask and the dW_out operand
-    __shared__ unsigned last;
+    __shared__ __attribute__((aligned(16))) float h0[TT][FUSED_HLD];
+    __shared__ __attribute__((aligned(16))) float xr[TT][FUSED_XLD];
+    fused_fwd<NW, KCH, false>(F, red, h0, xr, nullptr);
+}
+
+// Four consecutive k of an H_1 row handed over in this launch: sc1 buffer loads (the row's byte
+// offset `row_off`; row4's zero fill and element fallback)
+__device__ __forceinline__ f32x4 row4_sc1(__amdgpu_buffer_rsrc_t r, unsigned row_off, bool valid, int k0, int K,
+                                          bool vec) {
+    f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (!valid) return v;
+    if (vec && k0 + 3 < K)
+        return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, row_off + 4u * k0, 0, TRAIN_SC1));
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+        if (k0 + e < K)
+            v[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, row_off + 4u * (k0 + e), 0, TRAIN_SC1));
+    return v;
+}
+
+// FO: wait until every F tile of band tm has written its H_1 columns (one lane polls, sc1 loads; a
+// 1 s bound sets bit 0 of *status instead of hanging), then count this tile as past the wait; the
+// band's last such add resets the counter for the next launch. The band's tiles are consecutive
+// workgroup ids, so with in-order dispatch the earliest unfinished band is always fully resident.
+__device__ __forceinline__ void band_wait(const FusedArgs& F, int tm) {
+    if (threadIdx.x == 0) {
+        unsigned* c = F.band + tm * 32;
+        const unsigned need = (unsigned)F.tiles_n;
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {
+                atomicOr(F.status, 1u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (__hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 == 2 * need)
+            __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+}
+
+// O's body. dy: the tile's 32 rows of dY (columns past J zero); hm: H_1 of the tile (the ReLU mask and
+// the dW_out operand). FO (one launch with F): hm is already there, W_out's rows are loaded before
+// the band wait and the band's H_1 rows and targets after it, with sc1 loads.
+template <int NW, bool FO>
+__device__ __forceinline__ void fused_out(const FusedArgs& F, float (*red)[TT][TT + 1], float (*dy)[TT + 1],
+                                          float (*hm)[TT + 1], unsigned& last) {
+    constexpr int NT = 64 * NW, EPT = TT * TT / NT, MAXPER = NW == 16 ? 2 : 4;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, q = lane >> 4, c = lane & 15;
     const int tm = blockIdx.x / F.tiles_n, tn = blockIdx.x - tm * F.tiles_n, m0 = tm * TT, n0 = tn * TT;
     const int W = F.W, J = F.J, R = F.R, S = F.s;
@@ -1099,15 +1205,35 @@ __global__ __launch_bounds__(64 * NW) void train_fused_out_kernel(const FusedArg
     for (int u = 0; u < MAXPER; ++u) {
         const int kb = kb0 + 16 * u;
 #pragma unroll
-        for (int x = 0; x < 2; ++x) {
-            const int m = m0 + 16 * x + c;
-            av[u][x] = row4(F.act1 + (int64_t)min(m, R - 1) * W, m < R && kb < kb1, kb + 4 * q, W, veca);
-        }
-#pragma unroll
         for (int y = 0; y < 2; ++y) {
             const int o = 16 * y + c;
             const float* row = o < S ? F.wo + (int64_t)o * W : F.wo_r;
             bv[u][y] = row4(row, o < J && kb < kb1, kb + 4 * q, W, vecb);
+        }
+    }
+    if constexpr (FO) {
+        band_wait(F, tm);
+        const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc(
+            F.act1, 0, (int)((int64_t)R * W * sizeof(float)), 0x00020000);
+#pragma unroll
+        for (int u = 0; u < MAXPER; ++u) {
+            const int kb = kb0 + 16 * u;
+#pragma unroll
+            for (int x = 0; x < 2; ++x) {
+                const int m = m0 + 16 * x + c;
+                av[u][x] = row4_sc1(ar, (unsigned)((int64_t)min(m, R - 1) * W * sizeof(float)), m < R && kb < kb1,
+                                    kb + 4 * q, W, veca);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < MAXPER; ++u) {
+            const int kb = kb0 + 16 * u;
+#pragma unroll
+            for (int x = 0; x < 2; ++x) {
+                const int m = m0 + 16 * x + c;
+                av[u][x] = row4(F.act1 + (int64_t)min(m, R - 1) * W, m < R && kb < kb1, kb + 4 * q, W, veca);
+            }
         }
     }
     // the loss epilogue's y - t = acc - (t - bias), and the tile's H_1 block (mask, dW_out operand)
@@ -1117,12 +1243,15 @@ __global__ __launch_bounds__(64 * NW) void train_fused_out_kernel(const FusedArg
         const int e = tid + j * NT, m = m0 + (e >> 5), o = e & 31;
         pre[j] = 0.0f;
         if (m >= R || o >= J) continue;
-        pre[j] = F.tgt[(int64_t)m * J + o] - (o < S ? F.bo[o] : F.bo_r[o - S]);
+        const float* tg = F.tgt + (int64_t)m * J + o;
+        pre[j] = (FO ? __hip_atomic_load(tg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *tg) -
+                 (o < S ? F.bo[o] : F.bo_r[o - S]);
     }
-    for (int e = tid; e < TT * TT; e += NT) {
-        const int r = e >> 5, col = e & 31, m = m0 + r, n = n0 + col;
-        hm[r][col] = (m < R && n < W) ? F.act1[(int64_t)m * W + n] : 0.0f;
-    }
+    if constexpr (!FO)
+        for (int e = tid; e < TT * TT; e += NT) {
+            const int r = e >> 5, col = e & 31, m = m0 + r, n = n0 + col;
+            hm[r][col] = (m < R && n < W) ? F.act1[(int64_t)m * W + n] : 0.0f;
+        }
     f32x4 acc[2][2];
 #pragma unroll
     for (int x = 0; x < 2; ++x)
@@ -1258,6 +1387,9 @@ __global__ __launch_bounds__(64 * NW) void train_fused_out_kernel(const FusedArg
     if (tid == 0) {
         const unsigned t = __hip_atomic_fetch_add(&F.out_ticket[tn], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         last = (t + 1 == (unsigned)F.tiles_r) ? 1u : 0u;
+        // every arrival is in: reset the ticket for the next launch (in one launch with F, nothing
+        // zeroes it at the start)
+        if (last) __hip_atomic_store(&F.out_ticket[tn], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
     FSTAMP(1, 3);
@@ -1309,6 +1441,31 @@ __global__ __launch_bounds__(64 * NW) void train_fused_out_kernel(const FusedArg
             }
         }
     }
+}
+
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void train_fused_out_kernel(const FusedArgs F) {
+    __shared__ float red[NW][TT][TT + 1];
+    __shared__ float dy[TT][TT + 1];
+    __shared__ float hm[TT][TT + 1];
+    __shared__ unsigned last;
+    fused_out<NW, false>(F, red, dy, hm, last);
+}
+
+// F and O as one launch: the O tiles of a 32-row band wait (band_wait) for that band's F tiles only,
+// instead of the whole grid at a kernel boundary, and W_out's rows load during the wait. The same
+// bodies, so the same bits as the two launches (MBRL_OPT_TRAIN_FO = 1 keeps them apart).
+template <int NW, int KCH>
+__global__ __launch_bounds__(64 * NW) void train_fused_fo_kernel(const FusedArgs F) {
+    __shared__ float red[NW][TT][TT + 1];
+    __shared__ __attribute__((aligned(16))) float h0[TT][FUSED_HLD];
+    __shared__ __attribute__((aligned(16))) float xr[TT][FUSED_XLD];
+    __shared__ unsigned last;
+    // hm and dy alias h0, which F no longer reads once its H_1 products are in red
+    float(*hm)[TT + 1] = reinterpret_cast<float(*)[TT + 1]>(&h0[0][0]);
+    float(*dy)[TT + 1] = hm + TT;
+    fused_fwd<NW, KCH, true>(F, red, h0, xr, hm);
+    fused_out<NW, true>(F, red, dy, hm, last);
 }
 
 static Operand direct(const float* p0, const float* p1, int split, int ld, int rows) {
@@ -1376,9 +1533,10 @@ struct TrainWs {
     float *xbuf2, *tgt2;  // the fused step's second gather slot (the next batch's rows and targets)
     float* out_part;      // fused step: the output layer's weight-gradient partials [row tile][J][W]
     float* tgt;           // fused step: the batch's targets [R][J] (F gathers, O reads)
-    unsigned* tickets;    // [ceil(W / 32)] each: the dW_0 fold's, the fused dW_out fold's, the fused dH_0
-                          // tiles' W_1-read arrivals
+    unsigned* tickets;    // [ceil(W / 32)] each: the dW_0 fold's, the fused dH_0 tiles' W_1-read arrivals,
+                          // the fused dW_out fold's
     unsigned* status;     // fused step: bit 0 = a bounded wait timed out (never expected)
+    unsigned* bands;      // fused step, F and O in one launch: [row tiles][32] band counters (one line each)
     size_t floats;
 };
 
@@ -1405,6 +1563,7 @@ static TrainWs train_ws(const TrainShape& t, int batch, float* base) {
     w.tgt2 = take(R * J);
     w.tickets = reinterpret_cast<unsigned*>(take(3 * ((W + TT - 1) / TT)));
     w.status = reinterpret_cast<unsigned*>(take(1));
+    w.bands = reinterpret_cast<unsigned*>(take(32 * tiles_r));
     w.floats = off;
     return w;
 }
@@ -1493,17 +1652,27 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
         F.out_part = B.out_part;
         F.dwo = w.weight_grad[L]; F.dwo_r = t.reward ? w.weight_grad[L + 1] : w.weight_grad[L];
         F.dbo = w.bias_grad[L]; F.dbo_r = t.reward ? w.bias_grad[L + 1] : w.bias_grad[L];
-        F.out_ticket = B.tickets + tiles_n;
+        F.out_ticket = B.tickets + 2 * tiles_n;
+        F.band = B.bands; F.status = B.status;
         F.db1 = w.bias_grad[1];
         if (adam) {
             F.adam = 1; F.ab1 = adam[3]; F.hp = *hp; F.arith = arith;
         }
-        F.zero_words = B.tickets; F.zero_n = 3 * tiles_n;
+        // F zeroes the later launches' tickets (in one launch with O, not O's own: its last arrivers
+        // reset them)
+        const bool fo = t.fo_split == 0;
+        F.zero_words = B.tickets; F.zero_n = (fo ? 2 : 3) * tiles_n;
         F.scale_s = 2.0f / (float)((int64_t)batch * t.s); F.scale_r = 2.0f / (float)batch;
         F.inv_s = 1.0f / (float)((int64_t)batch * t.s); F.inv_r = 1.0f / (float)batch;
         const dim3 grid(tiles_r * tiles_n);
         // the wave count of the separate launches whose K is W; K0's chunks
-        if (W >= 256) {
+        if (fo && W >= 256) {
+            if (K0 <= 32) hipLaunchKernelGGL((train_fused_fo_kernel<16, 2>), grid, dim3(64 * 16), 0, stream, F);
+            else hipLaunchKernelGGL((train_fused_fo_kernel<16, 4>), grid, dim3(64 * 16), 0, stream, F);
+        } else if (fo) {
+            if (K0 <= 32) hipLaunchKernelGGL((train_fused_fo_kernel<4, 2>), grid, dim3(64 * 4), 0, stream, F);
+            else hipLaunchKernelGGL((train_fused_fo_kernel<4, 4>), grid, dim3(64 * 4), 0, stream, F);
+        } else if (W >= 256) {
             if (K0 <= 32) hipLaunchKernelGGL((train_fused_fwd_kernel<16, 2>), grid, dim3(64 * 16), 0, stream, F);
             else hipLaunchKernelGGL((train_fused_fwd_kernel<16, 4>), grid, dim3(64 * 16), 0, stream, F);
             hipLaunchKernelGGL(train_fused_out_kernel<16>, grid, dim3(64 * 16), 0, stream, F);
@@ -1622,10 +1791,10 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
             // once those tiles' K loops are done (dH_0 tiles have the lower ids)
             Output& O = G.d[G.nd - 1].out;
             O.adam = 1; O.aw = adam[2];
-            O.wait_ticket = B.tickets + 2 * tiles_n;
+            O.wait_ticket = B.tickets + tiles_n;
             O.wait_count = (unsigned)((R + TT * tmx - 1) / (TT * tmx));
             O.wait_status = B.status;
-            G.d[0].out.arrive_ticket = B.tickets + 2 * tiles_n;
+            G.d[0].out.arrive_ticket = B.tickets + tiles_n;
         }
         // layer l + 1's gradient is complete (previous launch) and this launch does not read its
         // parameters: its Adam step rides along (with the reward head when l + 1 is the output layer)

@@ -26,7 +26,7 @@ MBRL_EHIP = -3
 MBRL_EWORKSPACE = -4
 MBRL_COST_GOAL_STATE = 0
 MBRL_COST_MODEL_REWARD = 1
-ABI_VERSION = 11
+ABI_VERSION = 12
 MBRL_NAN_LAST = 0
 MBRL_NAN_FIRST = 1
 MBRL_PRECISION_F32 = 0
@@ -38,7 +38,7 @@ OPTIONS = {"rollout_tile": 0, "split_tile": 1, "debug_traj_abort": 2, "gd_single
            "unfused_update": 5, "adam_arith": 6, "xcd_map": 7, "train_tile": 8, "train_no_fold": 9,
            "rollout_pair": 10, "shard_emulate": 11, "debug_pair_abort": 12,
            "traj_hop": 13, "gd_hop": 14, "pair_l2": 15,
-           "train_xcd": 16, "train_split": 17, "debug_shard_fail": 18}
+           "train_xcd": 16, "train_split": 17, "debug_shard_fail": 18, "train_fo": 19}
 
 
 def precision_code(name):

@@ -8,6 +8,7 @@ reference's arithmetic.
 """
 import ctypes
 import functools
+import weakref
 
 import numpy as np
 import torch
@@ -95,6 +96,9 @@ class _GraphStep:
 # gradient from mbrl_train_grads (csrc/train.hip) instead of autograd. False: autograd in a HIP graph.
 NATIVE_TRAINING = True
 
+# model -> (binding key, _NativeGrads) of its last native train_model call (_NativeGrads.cached)
+_NATIVE_CACHE = weakref.WeakKeyDictionary()
+
 
 class _NativeGrads:
     """mbrl_train_grads for Model (noise None) / ModelWithReward with MSELoss(reduction='mean'):
@@ -131,6 +135,32 @@ class _NativeGrads:
         self.ptrs = [t.data_ptr() for t in self.params]
         self.dev = dev
         self._lib = _lib
+
+    @classmethod
+    def cached(cls, model, ins, outs, horizon, batch_size, reward):
+        """The object of the model's previous train_model call when nothing it binds has changed (the
+        parameter and gradient storage, the stacked transitions, the batch size), else a new one. A
+        call then starts its first launch without allocating and zeroing the gradients and the
+        workspace (host time the GPU idles through at the start of every call,
+        tools/train_startup.py). Rebuilt when a non-contiguous input would need a fresh contiguous
+        copy."""
+        key = (str(_device_of(model)), int(horizon), int(batch_size), bool(reward),
+               tuple(t.data_ptr() for lin in model.linears() for t in (lin.weight, lin.bias)),
+               tuple((x.data_ptr(), tuple(x.shape), x.is_contiguous()) for x in (*ins, *outs)))
+        hit = _NATIVE_CACHE.get(model)
+        if hit is not None and hit[0] == key:
+            return hit[1]
+        obj = cls(model, ins, outs, horizon, batch_size, reward)
+        if all(x.is_contiguous() for x in (*ins, *outs)):
+            _NATIVE_CACHE[model] = (key, obj)
+        else:
+            _NATIVE_CACHE.pop(model, None)
+        return obj
+
+    @staticmethod
+    def forget(model):
+        """Drop the model's cached object (after a failed status check: its sticky word is set)."""
+        _NATIVE_CACHE.pop(model, None)
 
     @staticmethod
     def supported(model, dataset, ins, outs, criterion):
@@ -192,27 +222,13 @@ class _NativeGrads:
 
     def check_status(self):
         """Raise if an in-launch wait of the fused step timed out (the workgroup dispatch order its
-        Adam placement relies on was not kept): the parameters may then be off. Never expected."""
+        Adam placement relies on was not kept): the parameters may then be off. Never expected. The
+        word is sticky (set by any launch since the workspace was zeroed), so one read after the last
+        epoch of a train_model call covers every epoch of it: no per-epoch copy or kernel."""
         word = int(self.ws[self.status_at:self.status_at + 4].view(torch.int32).item())
         if word & 1:
             raise RuntimeError("mbrl_amd: a fused training step's bounded wait timed out (status word "
                                f"{word:#x}); the parameters of that step may be wrong")
-
-    def stage_status(self, staged, e):
-        """staged[e] |= the (sticky) status word, on the device behind epoch e's launches: one small
-        elementwise kernel, no copy engine and no sync (a 4-byte device-to-host copy per epoch stalled
-        the stream ~80 us)."""
-        staged[e:e + 1].bitwise_or_(self.ws[self.status_at:self.status_at + 4].view(torch.int32))
-
-    @staticmethod
-    def check_staged(staged):
-        """Raise naming the first epoch whose status word was set (check_status); one read."""
-        words = staged.cpu().numpy()
-        bad = np.flatnonzero(words & 1)
-        if bad.size:
-            raise RuntimeError("mbrl_amd: a fused training step's bounded wait timed out in epoch "
-                               f"{int(bad[0])} of this train_model call (status word {int(words[bad[0]]):#x}); "
-                               "the parameters of that epoch may be wrong")
 
     def run(self, idx):
         """The batch gradient for the rows `idx` (int64, on the device) into p.grad."""
@@ -254,7 +270,7 @@ def _train_loop_on(dev, model, dataset, optimizer, batch_size, num_epochs, step_
     if dev.type == "cuda":
         reward = _NativeGrads.supported(model, dataset, ins, outs, criterion)
         if reward is not None:
-            native = _NativeGrads(model, ins, outs, dataset.horizon, batch_size, reward)
+            native = _NativeGrads.cached(model, ins, outs, dataset.horizon, batch_size, reward)
     if native is None and dev.type == "cuda" and dataset.num_transitions() >= batch_size:
         try:
             graph = _GraphStep(model, dataset, ins, outs, batch_size, step_loss, n_parts)
@@ -274,12 +290,12 @@ def _train_loop_on(dev, model, dataset, optimizer, batch_size, num_epochs, step_
         # Epoch k + 1's order is drawn while epoch k runs -- the same np.random draws in the same order
         # (nothing else in this loop draws from the global RNG) -- and copied from pinned memory on a
         # side stream that the training stream waits on before epoch k + 1 (the copy lands while epoch k
-        # computes). Each epoch's status word is staged on the device behind its launches; all are read
-        # after the last epoch.
+        # computes). The sticky status word is read once, after the last epoch.
         orders_host, orders_pinned, orders, side = _order_buffers(dev, num_epochs, dataset.num_transitions())
         orders_host[0] = _epoch_order(dataset)
-        orders[0].copy_(orders_pinned[0], non_blocking=False)
-        status_staged = torch.zeros(num_epochs, dtype=torch.int32, device=dev)
+        # stream-ordered before epoch 0's launches (the pinned row is not rewritten before the sync
+        # that ends this call)
+        orders[0].copy_(orders_pinned[0], non_blocking=True)
         main = torch.cuda.current_stream(dev)
     epoch_losses = []
     for ep in range(num_epochs):
@@ -294,7 +310,6 @@ def _train_loop_on(dev, model, dataset, optimizer, batch_size, num_epochs, step_
             with torch.cuda.stream(side):
                 orders[ep + 1].copy_(orders_pinned[ep + 1], non_blocking=True)
         if losses is not None:            # the whole epoch in one call; the writer gets its values after
-            native.stage_status(status_staged, ep)
             epoch_losses.append(losses)
             continue
         num_iters = _write_epoch_losses(epoch_losses, writer, tags, n_parts, model, num_iters)
@@ -325,10 +340,12 @@ def _train_loop_on(dev, model, dataset, optimizer, batch_size, num_epochs, step_
         for p in model.parameters():      # release the graph-pool grads; the eager path re-allocates
             p.grad = None
     # (the native path leaves the last batch's gradients in .grad, as the reference's loop does)
-    if whole and num_epochs > 0:
-        _NativeGrads.check_staged(status_staged)
-    elif native is not None:
-        native.check_status()
+    try:
+        if native is not None:
+            native.check_status()
+    except RuntimeError:
+        _NativeGrads.forget(model)        # the workspace's sticky status word is set: start afresh
+        raise
     model.train_iterations += 1
 
 

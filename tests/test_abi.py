@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     assert decl == sorted(_lib.EXPORTED)
     for name in decl:
         assert hasattr(lib, name), name
-    assert lib.mbrl_abi_version() == _lib.ABI_VERSION == 11
+    assert lib.mbrl_abi_version() == _lib.ABI_VERSION == 12
 
 
 def test_no_gpu_needed_for_sizing_calls():

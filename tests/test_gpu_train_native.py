@@ -172,6 +172,34 @@ def test_native_training_leaves_the_last_batch_gradient():
         assert torch.allclose(x, y, rtol=1e-4, atol=1e-4 * float(y.abs().max()) + 1e-12)
 
 
+def test_cached_native_object_trains_like_a_fresh_one():
+    """train_model reuses the model's _NativeGrads (gradients, workspace) across calls while nothing it
+    binds changed. Three calls with the cache equal three calls that each start from a fresh object,
+    bit for bit; growing the dataset (new stacked tensors) or the batch size rebuilds it."""
+    from mbrl_amd import models
+    out = {}
+    for cached in (True, False):
+        ds = _dataset(17, 6, 1, 700, seed=11)
+        m = _model("model", 17, 6, 512, 2, seed=3)
+        opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+        np.random.seed(8)
+        objs = []
+        for call, bs in enumerate((512, 512, 256, 512)):
+            if not cached:
+                models._NativeGrads.forget(m)
+            if call == 3:   # a grown dataset: new stacked tensors
+                extra = _dataset(17, 6, 1, 90, seed=12)
+                ds.add_rollouts(extra.rollouts)
+            m.train_model(ds, opt, batch_size=bs, num_epochs=2)
+            objs.append(models._NATIVE_CACHE.get(m, (None, None))[1])
+        out[cached] = [p.detach().cpu() for p in m.parameters()]
+        if cached:
+            assert objs[0] is objs[1]            # same binding: reused
+            assert objs[2] is not objs[1]        # batch size changed
+            assert objs[3] is not objs[2]        # dataset grew
+    assert all(torch.equal(x, y) for x, y in zip(out[True], out[False]))
+
+
 @pytest.mark.parametrize("case", range(24))
 def test_native_gradients_random_shapes(case):
     """mbrl_train_grads at random shapes (dims, widths off the tile grid, depth, horizon, batch sizes
@@ -274,15 +302,20 @@ def test_fused_step_is_bitwise_neutral(kind, s, a, W, H, B):
     read it) instead of five (MBRL_OPT_TRAIN_SPLIT = 1). The same chains in the same order: equal
     gradients and losses from mbrl_train_grads, and equal parameters, optimizer state and losses
     after three epochs of mbrl_train_epoch whose last batch is short (and takes the five-launch
-    path); the status word of the bounded in-launch waits stays clear."""
+    path); the status word of the bounded in-launch waits stays clear. The fused step is checked both
+    as the default single F+O launch (band waits) and with F and O as two launches
+    (MBRL_OPT_TRAIN_FO = 1)."""
+    import contextlib
     from mbrl_amd import _lib, models
     ds = _dataset(s, a, H, 3 * B + 37, seed=W + s)
     _, ins, outs = ds.stacked(DEV)
     reward = kind == "reward"
     idx = torch.randperm(ds.num_transitions(), generator=torch.Generator().manual_seed(B))[:B].to(DEV)
     grads, trained = {}, {}
-    for split in (1, 0):
-        with _lib.option("train_split", split):
+    for split in (1, 0, "fo_split"):
+        with contextlib.ExitStack() as opts:
+            opts.enter_context(_lib.option("train_split", 1 if split == 1 else 0))
+            opts.enter_context(_lib.option("train_fo", 1 if split == "fo_split" else 0))
             m = _model(kind, s, a, W, 2, seed=W)
             nat = models._NativeGrads(m, ins, outs, ds.horizon, B, reward)
             loss, parts = nat.run(idx)
@@ -298,14 +331,15 @@ def test_fused_step_is_bitwise_neutral(kind, s, a, W, H, B):
             trained[split] = ([p.detach().clone() for p in m.parameters()],
                               [(float(st["step"]), st["exp_avg"].clone(), st["exp_avg_sq"].clone())
                                for st in opt.state.values()], w.rows)
-    for i, (x, y) in enumerate(zip(grads[0], grads[1])):
-        assert torch.equal(x, y), (i, float((x - y).abs().max()))
-    (pa, sa, ra), (pb, sb, rb) = trained[0], trained[1]
-    for i, (x, y) in enumerate(zip(pa, pb)):
-        assert torch.equal(x, y), (i, float((x - y).abs().max()))
-    for (ka, ma, va), (kb, mb, vb) in zip(sa, sb):
-        assert ka == kb and torch.equal(ma, mb) and torch.equal(va, vb)
-    assert ra == rb and len(ra) > 0
+    for mode in (0, "fo_split"):
+        for i, (x, y) in enumerate(zip(grads[mode], grads[1])):
+            assert torch.equal(x, y), (mode, i, float((x - y).abs().max()))
+        (pa, sa, ra), (pb, sb, rb) = trained[mode], trained[1]
+        for i, (x, y) in enumerate(zip(pa, pb)):
+            assert torch.equal(x, y), (mode, i, float((x - y).abs().max()))
+        for (ka, ma, va), (kb, mb, vb) in zip(sa, sb):
+            assert ka == kb and torch.equal(ma, mb) and torch.equal(va, vb)
+        assert ra == rb and len(ra) > 0
 
 
 @pytest.mark.parametrize("case", range(12))

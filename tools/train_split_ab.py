@@ -1,6 +1,7 @@
 """A/B of the training step's launch structure: train_model (2 x W, batch 512, Adam,
-cheetah-shaped data, 10k transitions) in the r04 fused three-launch step against the r03 five-launch
-layout (MBRL_OPT_TRAIN_SPLIT = 1), interleaved on one GPU; wall-clock steps/s of whole epochs (the
+cheetah-shaped data, 10k transitions) in the r05 two-launch step (F and O in one launch) against the
+r04 three-launch step (MBRL_OPT_TRAIN_FO = 1) and the r03 five-launch layout (MBRL_OPT_TRAIN_SPLIT = 1),
+interleaved on one GPU, with the trained parameters required equal bit for bit; wall-clock steps/s of whole epochs (the
 step is GPU-bound: one host call per epoch). Usage: python tools/train_split_ab.py [W ...] [--epochs E]"""
 import json
 import os
@@ -17,8 +18,8 @@ from mbrl_amd import _lib, models  # noqa: E402
 from train_bench import dataset  # noqa: E402
 
 
-def run(W, epochs, ds, split):
-    with _lib.option("train_split", split):
+def run(W, epochs, ds, split, fo_split):
+    with _lib.option("train_split", split), _lib.option("train_fo", fo_split):
         torch.manual_seed(0)
         m = models.Model(17, 6, hidden_units=W).to("cuda:0")
         opt = torch.optim.Adam(m.parameters(), lr=1e-3)
@@ -31,7 +32,7 @@ def run(W, epochs, ds, split):
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
     steps = epochs * ((len(ds.transition_index()) + 511) // 512)
-    return steps / dt
+    return steps / dt, torch.cat([p.detach().reshape(-1) for p in m.parameters()])
 
 
 def main():
@@ -45,8 +46,12 @@ def main():
     for W in widths:
         out = {"workload": f"train_model s=17 a=6 2x{W} batch 512, 10k transitions, Adam", "unit": "steps/s"}
         for _ in range(3):
-            for name, split in (("split5 (r03)", 1), ("fused3 (r04)", 0)):
-                out.setdefault(name, []).append(round(run(W, epochs, ds, split), 1))
+            ref = None
+            for name, split, fo in (("split5 (r03)", 1, 0), ("fused3 (r04)", 0, 1), ("fused2 (r05)", 0, 0)):
+                rate, params = run(W, epochs, ds, split, fo)
+                ref = params if ref is None else ref
+                assert torch.equal(params, ref), f"{name}: parameters differ from the five-launch layout's"
+                out.setdefault(name, []).append(round(rate, 1))
         out["us_per_step"] = {k: round(1e6 / float(np.median(v)), 2) for k, v in out.items() if isinstance(v, list)}
         print(json.dumps(out), flush=True)
 

@@ -1,0 +1,93 @@
+"""Diagnostic: the host's turn at the start of a train_model call on the device path (what the GPU
+waits for before the first training launch), statement by statement -- the calls
+models._train_loop_on makes before its first mbrl_train_epoch, in order, with a perf_counter stamp
+after each -- plus the device span of whole calls (fence-free events around train_model, as bench.py's
+`train` object measures them) for 1 and 10 epochs, so the fixed cost per call is
+span(10) - 10 (span(10) - span(1)) / 9. Usage: python tools/train_startup.py [calls]"""
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "mujoco-mbrl_amd"), os.path.join(REPO, "tools")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import train_bench  # noqa: E402
+from mbrl_amd import models  # noqa: E402
+from mbrl_amd.optim import AdamStep  # noqa: E402
+
+
+def main():
+    calls = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    dev = torch.device("cuda:0")
+    ds = train_bench.dataset()
+    torch.manual_seed(0)
+    m = models.Model(17, 6, hidden_units=512).to(dev)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    np.random.seed(1)
+    m.train_model(ds, opt, batch_size=512, num_epochs=1)
+    torch.cuda.synchronize()
+    seg = {}
+
+    def startup():
+        t = [time.perf_counter()]
+        stamp = lambda name: (t.append(time.perf_counter()), seg.setdefault(name, []).append(t[-1] - t[-2]))  # noqa: E731
+        ctx = torch.cuda.device(dev)
+        ctx.__enter__()
+        stamp("cuda.device enter")
+        ds.num_transitions()
+        _, ins, outs = ds.stacked(dev)
+        stamp("num_transitions + stacked")
+        reward = models._NativeGrads.supported(m, ds, ins, outs, torch.nn.MSELoss())
+        stamp("supported")
+        native = models._NativeGrads.cached(m, ins, outs, ds.horizon, 512, reward) \
+            if hasattr(models._NativeGrads, "cached") else models._NativeGrads(m, ins, outs, ds.horizon, 512, reward)
+        stamp("native grads object")
+        fast = AdamStep.maybe(opt)
+        stamp("AdamStep.maybe")
+        own = {id(p) for p in native.params}
+        [p for g in opt.param_groups for p in g["params"] if id(p) not in own]
+        stamp("extra params")
+        oh, op, od, side = models._order_buffers(dev, 10, ds.num_transitions())
+        stamp("_order_buffers")
+        oh[0] = models._epoch_order(ds)
+        stamp("_epoch_order")
+        od[0].copy_(op[0], non_blocking=True)
+        stamp("order copy (enqueue)")
+        torch.zeros(10, dtype=torch.int32, device=dev)
+        stamp("status zeros")
+        losses = native.epoch(od[0], 512, fast)
+        stamp("epoch call (plan + enqueue)")
+        torch.cuda.synchronize()
+        stamp("sync")
+        ctx.__exit__(None, None, None)
+        return losses
+
+    for _ in range(3):
+        startup()
+    seg.clear()
+    for _ in range(calls):
+        startup()
+    out = {k: round(float(np.median(v)) * 1e6, 1) for k, v in seg.items()}
+    out["before_first_launch_us"] = round(sum(v for k, v in out.items() if k not in ("sync", "epoch call (plan + enqueue)")), 1)
+
+    def span(epochs):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        m.train_model(ds, opt, batch_size=512, num_epochs=epochs)
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) * 1e3
+
+    sp = {e: float(np.median([span(e) for _ in range(7)])) for e in (1, 10)}
+    per_epoch = (sp[10] - sp[1]) / 9
+    print(json.dumps(dict(startup_us=out, span_us={str(k): round(v, 1) for k, v in sp.items()},
+                          per_epoch_us=round(per_epoch, 1), fixed_per_call_us=round(sp[10] - 10 * per_epoch, 1),
+                          us_per_step_10=round(sp[10] / 200, 2))))
+
+
+if __name__ == "__main__":
+    main()
