@@ -1540,6 +1540,9 @@ struct TrainWs {
     size_t floats;
 };
 
+// The fused step needs the dW_0 fold, whose 32-row waves bound its rows: R <= 512, 16 bands of 32.
+constexpr int FUSED_MAX_BANDS = 16;
+
 static TrainWs train_ws(const TrainShape& t, int batch, float* base) {
     const size_t R = (size_t)batch * t.H, J = t.s + (t.reward ? 1 : 0), W = t.W, tiles_r = (R + TT - 1) / TT;
     const size_t tiles_out = tiles_r * ((J + TT - 1) / TT);
@@ -1547,6 +1550,13 @@ static TrainWs train_ws(const TrainShape& t, int batch, float* base) {
     TrainWs w{};
     size_t off = 0;
     auto take = [&](size_t n) { float* p = base ? base + off : nullptr; off += up(n); return p; };
+    // the control words first, at offsets that depend on the model only: every batch of an epoch
+    // (the short last one lays out its data areas for its own size) finds the tickets, the sticky
+    // status word and the band counters where the others left them, zero between launches; the band
+    // counters sized for the fused step's largest batch (FUSED_MAX_BANDS)
+    w.tickets = reinterpret_cast<unsigned*>(take(3 * ((W + TT - 1) / TT)));
+    w.status = reinterpret_cast<unsigned*>(take(1));
+    w.bands = reinterpret_cast<unsigned*>(take(32 * FUSED_MAX_BANDS));
     for (int l = 0; l < t.L; ++l) w.act[l] = take(R * W);
     w.dh[0] = take(R * W);
     w.dh[1] = take(R * W);
@@ -1561,9 +1571,6 @@ static TrainWs train_ws(const TrainShape& t, int batch, float* base) {
     w.tgt = take(R * J);
     w.xbuf2 = take(R * (t.s + t.a));
     w.tgt2 = take(R * J);
-    w.tickets = reinterpret_cast<unsigned*>(take(3 * ((W + TT - 1) / TT)));
-    w.status = reinterpret_cast<unsigned*>(take(1));
-    w.bands = reinterpret_cast<unsigned*>(take(32 * tiles_r));
     w.floats = off;
     return w;
 }
@@ -1590,8 +1597,13 @@ static bool fused_step(const TrainShape& t, int fold_nw) {
     const int J = t.s + (t.reward ? 1 : 0), K0 = t.s + t.a;
     return t.split == 0 && t.L == 2 && fold_nw > 0 && J <= TT && K0 <= FUSED_K0MAX && t.W <= FUSED_WMAX;
 }
+static bool fused_step(const TrainShape& t, int fold_nw, int R) {
+    return fused_step(t, fold_nw) && (R + TT - 1) / TT <= FUSED_MAX_BANDS;   // (fold_nw > 0 implies it)
+}
 
-bool train_fused_applies(const TrainShape& t, int batch) { return fused_step(t, fold_waves(t, batch * t.H)); }
+bool train_fused_applies(const TrainShape& t, int batch) {
+    return fused_step(t, fold_waves(t, batch * t.H), batch * t.H);
+}
 
 hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const int64_t* idx, int batch,
                               float* loss_out, float* ws, hipStream_t stream, const mbrl_adam_tensor* adam,
@@ -1600,7 +1612,7 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
     const int R = batch * t.H, W = t.W, K0 = t.s + t.a, J = t.s + (t.reward ? 1 : 0), L = t.L;
     const int tiles_r = (R + TT - 1) / TT;
     const int fold_nw = fold_waves(t, R);
-    const bool fused = fused_step(t, fold_nw);
+    const bool fused = fused_step(t, fold_nw, R);
     if (pending_n) *pending_n = 0;
     if ((prior_n > 0 && !prior) || prior_n > ADAM_FUSED_MAX || (adam && fold_nw && (!pending || !pending_n)))
         return hipErrorInvalidValue;

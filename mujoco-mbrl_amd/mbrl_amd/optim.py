@@ -147,17 +147,13 @@ class AdamStep:
             return None
         lr, (b1, b2), eps, wd = g["lr"], g["betas"], g["eps"], g["weight_decay"]
         n = len(params)
-        ss, bc = (ctypes.c_float * (steps * n))(), (ctypes.c_float * (steps * n))()
+        va, vb = [], []
         for s in range(steps):                    # adam.py _multi_tensor_adam, capturable = False
-            k = k0 + s + 1
-            a, b = (lr / (1 - b1 ** k)) * -1, (1 - b2 ** k) ** 0.5
-            for i in range(n):
-                ss[s * n + i], bc[s * n + i] = a, b
-        table = (_lib.AdamTensor * n)()
-        for i, p in enumerate(params):
-            table[i].param, table[i].grad = p.data_ptr(), p.grad.data_ptr()
-            table[i].exp_avg, table[i].exp_avg_sq = state[p]["exp_avg"].data_ptr(), state[p]["exp_avg_sq"].data_ptr()
-            table[i].numel = p.numel()
+            k = k0 + s + 1                        # (Python floats, as torch computes them; c_float rounds)
+            va += [(lr / (1 - b1 ** k)) * -1] * n
+            vb += [(1 - b2 ** k) ** 0.5] * n
+        ss, bc = (ctypes.c_float * (steps * n))(*va), (ctypes.c_float * (steps * n))(*vb)
+        table = self._table(0, params)            # (rebuilt only when a tensor moved)
         self._pending = (counters, steps)
         return table, _lib.AdamHparams(1 - b1, b2, 1 - b2, eps, wd), ss, bc
 
