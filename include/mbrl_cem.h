@@ -199,6 +199,16 @@ int mbrl_comm_destroy(mbrl_comm_t comm);
 int mbrl_host_alloc(size_t bytes, void** host_ptr, void** device_ptr);
 int mbrl_host_free(void* host_ptr);
 
+/* ---- stream plumbing (no reference counterpart; ABI v12): events for ordering work between streams
+ * and for the host to wait on, created without timing and without the system-scope fence a default
+ * event's record ends in (which idles the GPU ~5.5 us per record). train_model's epoch loop orders its
+ * row-order copies with them (mbrl_amd/models.py _OrderRing). A never-recorded event is complete. */
+int mbrl_event_create(mbrl_event_t* event);
+int mbrl_event_record(mbrl_event_t event, mbrl_stream_t stream);
+int mbrl_stream_wait_event(mbrl_stream_t stream, mbrl_event_t event);
+int mbrl_event_synchronize(mbrl_event_t event);
+int mbrl_event_destroy(mbrl_event_t event);
+
 /* ---- model upload: replaces the per-call nn.Linear weight reads of Model._forward (models.py:106-110) */
 size_t mbrl_mlp_packed_bytes(const mbrl_mlp_shape* shape);
 /* weights[e*NL+l] / biases[...], NL = L + 1 + reward_head: DEVICE pointers to nn.Linear weight

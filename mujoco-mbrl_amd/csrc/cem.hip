@@ -1473,6 +1473,37 @@ int mbrl_host_free(void* host_ptr) {
     return host_ptr ? hip_check(hipHostFree(host_ptr), "hipHostFree") : MBRL_OK;
 }
 
+int mbrl_event_create(mbrl_event_t* event) {
+    if (!event) return fail(MBRL_EINVAL, "event_create: NULL");
+    hipEvent_t e = nullptr;
+    if (int rc = hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence),
+                           "hipEventCreateWithFlags"))
+        return rc;
+    *event = reinterpret_cast<mbrl_event_t>(e);
+    return MBRL_OK;
+}
+
+int mbrl_event_record(mbrl_event_t event, mbrl_stream_t stream) {
+    if (!event) return fail(MBRL_EINVAL, "event_record: NULL event");
+    return hip_check(hipEventRecord(reinterpret_cast<hipEvent_t>(event), reinterpret_cast<hipStream_t>(stream)),
+                     "hipEventRecord");
+}
+
+int mbrl_stream_wait_event(mbrl_stream_t stream, mbrl_event_t event) {
+    if (!event) return fail(MBRL_EINVAL, "stream_wait_event: NULL event");
+    return hip_check(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), reinterpret_cast<hipEvent_t>(event), 0),
+                     "hipStreamWaitEvent");
+}
+
+int mbrl_event_synchronize(mbrl_event_t event) {
+    if (!event) return fail(MBRL_EINVAL, "event_synchronize: NULL event");
+    return hip_check(hipEventSynchronize(reinterpret_cast<hipEvent_t>(event)), "hipEventSynchronize");
+}
+
+int mbrl_event_destroy(mbrl_event_t event) {
+    return event ? hip_check(hipEventDestroy(reinterpret_cast<hipEvent_t>(event)), "hipEventDestroy") : MBRL_OK;
+}
+
 int mbrl_get_option(int32_t option) {
     if (option < 0 || option >= MBRL_OPT_COUNT) return fail(MBRL_EINVAL, "unknown option %d", option);
     return g_opt[option].load();

@@ -62,6 +62,8 @@ EXPORTED = (
     "mbrl_train_epoch", "mbrl_gd_batch_workspace_bytes", "mbrl_gd_plan_batch", "mbrl_host_alloc",
     "mbrl_host_free", "mbrl_comm_unique_id", "mbrl_comm_init", "mbrl_comm_destroy",
     "mbrl_cem_plan_sharded_workspace_bytes", "mbrl_cem_plan_sharded",
+    "mbrl_event_create", "mbrl_event_record", "mbrl_stream_wait_event", "mbrl_event_synchronize",
+    "mbrl_event_destroy",
 )
 
 
@@ -140,6 +142,11 @@ def load():
         "mbrl_get_option": (c_int32, [c_int32]),
         "mbrl_host_alloc": (c_int32, [c_size_t, POINTER(c_void_p), POINTER(c_void_p)]),
         "mbrl_host_free": (c_int32, [c_void_p]),
+        "mbrl_event_create": (c_int32, [POINTER(c_void_p)]),
+        "mbrl_event_record": (c_int32, [c_void_p, c_void_p]),
+        "mbrl_stream_wait_event": (c_int32, [c_void_p, c_void_p]),
+        "mbrl_event_synchronize": (c_int32, [c_void_p]),
+        "mbrl_event_destroy": (c_int32, [c_void_p]),
         "mbrl_mlp_packed_bytes": (c_size_t, [POINTER(MlpShape)]),
         "mbrl_mlp_pack": (c_int32, [POINTER(MlpShape), POINTER(c_void_p), POINTER(c_void_p), P, P]),
         "mbrl_rollout_cost": (c_int32, [POINTER(MlpShape), P, POINTER(Norm), POINTER(Cost), P, c_int32, P,
@@ -244,6 +251,37 @@ class HostStaging:
         if getattr(self, "host", None):
             self._lib.mbrl_host_free(c_void_p(self.host))
             self.host = None
+
+
+class StreamEvent:
+    """A fence-free HIP event (mbrl_event_create: no timing, no system-scope fence at its record) for
+    ordering one stream after another or letting the host wait: torch.cuda.Event's record idles the
+    GPU ~5.5 us behind its system-scope fence. `record(stream)`, `wait(stream)` and `synchronize()` take
+    torch streams; a never-recorded event is complete."""
+
+    def __init__(self):
+        lib = load()
+        h = c_void_p()
+        check(lib.mbrl_event_create(ctypes.byref(h)), "mbrl_event_create")
+        self._lib, self.handle, self.recorded = lib, h, False
+
+    def record(self, stream):
+        check(self._lib.mbrl_event_record(self.handle, c_void_p(stream.cuda_stream)), "mbrl_event_record")
+        self.recorded = True
+
+    def wait(self, stream):
+        if self.recorded:
+            check(self._lib.mbrl_stream_wait_event(c_void_p(stream.cuda_stream), self.handle),
+                  "mbrl_stream_wait_event")
+
+    def synchronize(self):
+        if self.recorded:
+            check(self._lib.mbrl_event_synchronize(self.handle), "mbrl_event_synchronize")
+
+    def __del__(self):
+        if getattr(self, "handle", None):
+            self._lib.mbrl_event_destroy(self.handle)
+            self.handle = None
 
 
 def ptr(t):

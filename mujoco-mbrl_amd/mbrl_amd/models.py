@@ -288,28 +288,28 @@ def _train_loop_on(dev, model, dataset, optimizer, batch_size, num_epochs, step_
         # The device path issues the epochs back to back with no host round trip between them (a
         # per-epoch copy of the row order from pageable memory waited for the previous epoch to drain).
         # Epoch k + 1's order is drawn while epoch k runs -- the same np.random draws in the same order
-        # (nothing else in this loop draws from the global RNG) -- and copied from pinned memory on a
-        # side stream that the training stream waits on before epoch k + 1 (the copy lands while epoch k
-        # computes). The sticky status word is read once, after the last epoch.
-        orders_host, orders_pinned, orders, side = _order_buffers(dev, num_epochs, dataset.num_transitions())
-        orders_host[0] = _epoch_order(dataset)
-        # stream-ordered before epoch 0's launches (the pinned row is not rewritten before the sync
-        # that ends this call)
-        orders[0].copy_(orders_pinned[0], non_blocking=True)
+        # (nothing else in this loop draws from the global RNG) -- into a ring of pinned rows and copied
+        # on a side stream that the training stream waits on before epoch k + 1 (the copy lands while
+        # epoch k computes). The sticky status word is read once, after the last epoch.
+        ring = _order_ring(dev, dataset.num_transitions())
         main = torch.cuda.current_stream(dev)
+        ring.draw(0)
+        ring.copy(0, main)
     epoch_losses = []
     for ep in range(num_epochs):
-        if whole and ep >= 1:
-            main.wait_stream(side)        # epoch ep's order has landed (copied while epoch ep - 1 ran)
-        host = orders_host[ep] if whole else _epoch_order(dataset)
-        order = orders[ep] if whole else torch.from_numpy(host).to(dev)
+        if whole:
+            host, order = ring.rows(ep)
+            if ep >= 1:
+                ring.copied[ep % ring.K].wait(main)   # epoch ep's order has landed
+        else:
+            host = _epoch_order(dataset)
+            order = torch.from_numpy(host).to(dev)
         losses = native.epoch(order, batch_size, fast) if whole else None
         if whole and ep + 1 < num_epochs:
-            orders_host[ep + 1] = _epoch_order(dataset)
-            # (no earlier call still reads these rows: each train_model call ends with a sync)
-            with torch.cuda.stream(side):
-                orders[ep + 1].copy_(orders_pinned[ep + 1], non_blocking=True)
+            ring.draw(ep + 1)
+            ring.copy(ep + 1, ring.side)
         if losses is not None:            # the whole epoch in one call; the writer gets its values after
+            ring.consumed[ep % ring.K].record(main)   # the ring row is free once this epoch has run
             epoch_losses.append(losses)
             continue
         num_iters = _write_epoch_losses(epoch_losses, writer, tags, n_parts, model, num_iters)
@@ -335,6 +335,8 @@ def _train_loop_on(dev, model, dataset, optimizer, batch_size, num_epochs, step_
                     writer.add_scalar(tag.format(model.train_iterations), val, num_iters)
                 if n_parts > 1:
                     writer.add_scalar("loss/total/{}".format(model.train_iterations), loss, num_iters)
+        if whole:
+            ring.consumed[ep % ring.K].record(torch.cuda.current_stream(dev))
     num_iters = _write_epoch_losses(epoch_losses, writer, tags, n_parts, model, num_iters)
     if graph is not None:
         for p in model.parameters():      # release the graph-pool grads; the eager path re-allocates
@@ -349,27 +351,60 @@ def _train_loop_on(dev, model, dataset, optimizer, batch_size, num_epochs, step_
     model.train_iterations += 1
 
 
-_ORDER_BUFFERS = {}
+class _OrderRing:
+    """K pinned host rows and K device rows of n row indices, a copy stream and per-row events, reused
+    by every train_model call on datasets of n transitions: epoch e's order lives in row e % K. The
+    host draws into a pinned row only once the copy that last read it has finished (`copied`), and
+    the side stream copies into a device row only once the epoch that last read it has run
+    (`consumed`), so the host may run up to ~2K epochs ahead and no call allocates (a pinned
+    allocation costs milliseconds, a new stream's first use ~6 ms of queue set-up)."""
+    K = 4
+
+    def __init__(self, dev, n):
+        self.n = n
+        self.pinned = torch.empty((self.K, n), dtype=torch.int64, pin_memory=True)
+        self.host = self.pinned.numpy()
+        self.arange = np.arange(n, dtype=np.int64)
+        self.dev = torch.empty((self.K, n), dtype=torch.int64, device=dev)
+        self.side = torch.cuda.Stream(dev)
+        with torch.cuda.stream(self.side):          # set up the side stream's queue here, once
+            self.dev[:1].copy_(self.pinned[:1], non_blocking=True)
+        self.side.synchronize()
+        from . import _lib
+        self.copied = [_lib.StreamEvent() for _ in range(self.K)]      # fence-free: a torch.cuda.Event
+        self.consumed = [_lib.StreamEvent() for _ in range(self.K)]    # record idles the GPU ~5.5 us
+
+    def draw(self, e):
+        """Epoch e's order (models._epoch_order's draws: NumPy's shuffle of arange(n), in place)."""
+        r = e % self.K
+        self.copied[r].synchronize()                # the copy that last read this pinned row is done
+        row = self.host[r]
+        np.copyto(row, self.arange)
+        np.random.shuffle(row)
+
+    def copy(self, e, stream):
+        r = e % self.K
+        with torch.cuda.stream(stream):
+            self.consumed[r].wait(stream)           # (an event never recorded is complete)
+            self.dev[r].copy_(self.pinned[r], non_blocking=True)
+            self.copied[r].record(stream)
+
+    def rows(self, e):
+        r = e % self.K
+        return self.host[r], self.dev[r]
 
 
-def _order_buffers(dev, epochs, n):
-    """Pinned host rows, device rows and a copy stream for `epochs` row orders of n transitions, kept for
-    later train_model calls on datasets of n transitions (rows for at least 16 epochs: a pinned
-    allocation costs milliseconds, so a later call with more epochs should not pay it again)."""
+_ORDER_RINGS = {}
+
+
+def _order_ring(dev, n):
     key = (str(dev), n)
-    hit = _ORDER_BUFFERS.get(key)
-    if hit is None or hit[0].shape[0] < epochs:
-        if len(_ORDER_BUFFERS) > 8:
-            _ORDER_BUFFERS.clear()
-        rows = max(epochs, 16)
-        pinned = torch.empty((rows, n), dtype=torch.int64, pin_memory=True)
-        hit = _ORDER_BUFFERS[key] = (pinned, torch.empty((rows, n), dtype=torch.int64, device=dev),
-                                     torch.cuda.Stream(dev))
-        # a stream's first operation sets up its hardware queue (~6 ms): pay it here, once
-        with torch.cuda.stream(hit[2]):
-            hit[1][:1].copy_(pinned[:1], non_blocking=True)
-        hit[2].synchronize()
-    return hit[0].numpy()[:epochs], hit[0][:epochs], hit[1][:epochs], hit[2]
+    ring = _ORDER_RINGS.get(key)
+    if ring is None:
+        if len(_ORDER_RINGS) > 8:
+            _ORDER_RINGS.clear()
+        ring = _ORDER_RINGS[key] = _OrderRing(dev, n)
+    return ring
 
 
 def _write_epoch_losses(epoch_losses, writer, tags, n_parts, model, num_iters):

@@ -51,15 +51,13 @@ def main():
         own = {id(p) for p in native.params}
         [p for g in opt.param_groups for p in g["params"] if id(p) not in own]
         stamp("extra params")
-        oh, op, od, side = models._order_buffers(dev, 10, ds.num_transitions())
-        stamp("_order_buffers")
-        oh[0] = models._epoch_order(ds)
-        stamp("_epoch_order")
-        od[0].copy_(op[0], non_blocking=True)
+        ring = models._order_ring(dev, ds.num_transitions())
+        stamp("_order_ring")
+        ring.draw(0)
+        stamp("epoch 0 draw")
+        ring.copy(0, torch.cuda.current_stream(dev))
         stamp("order copy (enqueue)")
-        torch.zeros(10, dtype=torch.int32, device=dev)
-        stamp("status zeros")
-        losses = native.epoch(od[0], 512, fast)
+        losses = native.epoch(ring.rows(0)[1], 512, fast)
         stamp("epoch call (plan + enqueue)")
         torch.cuda.synchronize()
         stamp("sync")
@@ -82,11 +80,11 @@ def main():
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) * 1e3
 
-    sp = {e: float(np.median([span(e) for _ in range(7)])) for e in (1, 10)}
-    per_epoch = (sp[10] - sp[1]) / 9
+    sp = {e: float(np.median([span(e) for _ in range(5)])) for e in (1, 10, 50)}
+    per_epoch = (sp[50] - sp[10]) / 40
     print(json.dumps(dict(startup_us=out, span_us={str(k): round(v, 1) for k, v in sp.items()},
                           per_epoch_us=round(per_epoch, 1), fixed_per_call_us=round(sp[10] - 10 * per_epoch, 1),
-                          us_per_step_10=round(sp[10] / 200, 2))))
+                          us_per_step_10=round(sp[10] / 200, 2), us_per_step_50=round(sp[50] / 1000, 2))))
 
 
 if __name__ == "__main__":
