@@ -220,13 +220,20 @@ def describe(model, cost, device):
     return mdesc, cdesc
 
 
+_PLAIN = frozenset((dict, str, int, bool, type(None), functools.partial))
+
+
 def _value_stamp(v, out):
     """Identity of a value recognition reads, plus a tensor's storage and version (in-place updates)."""
-    out.append(id(v))
-    if torch.is_tensor(v):
-        out.append((v.data_ptr(), v._version))
-    elif isinstance(v, float):
+    t = type(v)
+    if t in _PLAIN:                       # (the common cases first: this runs on every plan's host turn)
+        out.append(id(v))
+    elif t is float:
         out.append(v)
+    elif isinstance(v, torch.Tensor):
+        out.append((id(v), v.data_ptr(), v._version))
+    else:
+        out.append(id(v))
 
 
 def _callable_stamp(fn, out):

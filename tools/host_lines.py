@@ -39,15 +39,9 @@ def main():
         ctx = torch.cuda.device(d)
         ctx.__enter__()
         stamp("cuda.device enter")
-        mdesc = fused.describe_model(model)
-        stamp("describe_model")
-        cdesc = fused.describe_cost(cost, mdesc["s"], mdesc)
-        stamp("describe_cost")
-        prob = fused.device_problem(mdesc, cdesc, d)
-        stamp("device_problem")
-        ok = fused.semantic_check(model, cost, mdesc, cdesc, d, prob)
-        stamp("semantic_check (cached)")
-        assert ok
+        mdesc, cdesc, prob = fused.describe_problem(model, cost, d, st["precision"])
+        stamp("describe_problem (stamp fast path)")
+        assert prob is not None
         Nn, K, Hh, I = st["N"], st["K"], st["H"], st["I"]
         pkey = (Nn, Hh, K, I, st["alpha"], st["lo"], st["hi"], st["init_std"], int(st["seed"]) & 0xFFFFFFFFFFFFFFFF)
         params, pref, need = prob.plan_cache[pkey]
@@ -74,8 +68,9 @@ def main():
         _lib.check(rc, "mbrl_cem_plan")
         torch.cuda.current_stream(d).synchronize()
         stamp("sync (GPU plan)")
-        out = torch.from_numpy(arr[:o_s0].copy())
-        res = dict(states=out[:o_act].view(Hh, s), actions=out[o_act:o_mu].view(Hh, a))
+        x = arr[:o_s0].copy()
+        res = dict(states=torch.from_numpy(x[:o_act].reshape(Hh, s)), actions=torch.from_numpy(x[o_act:o_mu].reshape(Hh, a)),
+                   mu=torch.from_numpy(x[o_mu:o_sg].reshape(Hh, a)), sigma=torch.from_numpy(x[o_sg:].reshape(Hh, a)))
         stamp("copy-out")
         ctx.__exit__(None, None, None)
         stamp("cuda.device exit")
