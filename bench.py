@@ -302,7 +302,7 @@ def train_line(dev, W=512, epochs=50):
     """the reference's train_model (models.py:53-93; Adam, experiment.py:55-62)
     for a 2 x W Model on 10k synthetic cheetah-shaped transitions (s = 17, a = 6), batch 512 -- on this
     GPU through mbrl_train_epoch (csrc/train.hip: the fused two-launch step, Adam in its launches).
-    One warm-up epoch, then one train_model call of `epochs` epochs timed between two events on the
+    A 10-epoch warm-up call, then one train_model call of `epochs` epochs timed between two events on the
     training stream (GPU-bound: one host call per epoch; the call's own start-up -- the first epoch's
     shuffle, the checks before the first launch, the final status read -- inside the span). 50 is the
     reference's num_epochs default, which its agent's training loop uses (agents.py:292); a 10-epoch
@@ -322,8 +322,9 @@ def train_line(dev, W=512, epochs=50):
     m = models.Model(17, 6, hidden_units=W).to(dev)
     opt = torch.optim.Adam(m.parameters(), lr=1e-3)
     np.random.seed(1)
-    m.train_model(ds, opt, batch_size=512, num_epochs=1)
+    m.train_model(ds, opt, batch_size=512, num_epochs=10)   # warm-up: the ring rows, the copy stream, events
     torch.cuda.synchronize(dev)
+    gc.collect()    # the set-up's garbage (tens of thousands of per-step tensors) before the timed calls
     def timed(n_epochs):
         np.random.seed(2)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

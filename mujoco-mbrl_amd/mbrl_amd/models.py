@@ -356,9 +356,10 @@ class _OrderRing:
     by every train_model call on datasets of n transitions: epoch e's order lives in row e % K. The
     host draws into a pinned row only once the copy that last read it has finished (`copied`), and
     the side stream copies into a device row only once the epoch that last read it has run
-    (`consumed`), so the host may run up to ~2K epochs ahead and no call allocates (a pinned
+    (`consumed`), so the host may run up to ~2K epochs ahead -- ~35 ms of 2x512 training at K = 16,
+    room for a garbage-collector pause of the host thread -- and no call allocates (a pinned
     allocation costs milliseconds, a new stream's first use ~6 ms of queue set-up)."""
-    K = 4
+    K = 16
 
     def __init__(self, dev, n):
         self.n = n
@@ -373,6 +374,13 @@ class _OrderRing:
         from . import _lib
         self.copied = [_lib.StreamEvent() for _ in range(self.K)]      # fence-free: a torch.cuda.Event
         self.consumed = [_lib.StreamEvent() for _ in range(self.K)]    # record idles the GPU ~5.5 us
+        # a host wait on an event that is still pending takes a slow first-use path (~2 ms, measured
+        # on the first long train_model call of a process, tools/train_after_load.py): take it here
+        for r in range(self.K):
+            with torch.cuda.stream(self.side):
+                self.dev[r].copy_(self.pinned[r], non_blocking=True)
+                self.copied[r].record(self.side)
+            self.copied[r].synchronize()
 
     def draw(self, e):
         """Epoch e's order (models._epoch_order's draws: NumPy's shuffle of arange(n), in place)."""
