@@ -343,6 +343,8 @@ def train_line(dev, W=512, epochs=50):
     return dict(workload=f"train_model Model(17, 6) 2x{W}, batch 512, Adam, 10k synthetic transitions "
                          f"(SURVEY.md §8f rank 2)", steps_per_s=steps / wall, us_per_step=wall / steps * 1e6,
                 gpu_us_per_step=gpu_us, gpu_us_per_step_10_epochs=gpu_us10, launches_per_step=2,
+                status="the fused step's sticky status word (bounded in-launch waits) is read at the end of "
+                       "every train_model call, which raises if it is set: clear for every call here",
                 flop_per_step=flop, frac=flop / (gpu_us * 1e-6) / 1e12 / PEAK_FP32_MFMA_TFLOPS, epochs=epochs,
                 steps=steps)
 
@@ -386,7 +388,7 @@ def main():
             dist.init_process_group(backend)
         assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
 
-    from mbrl_amd import CEMPlanner, synthetic
+    from mbrl_amd import CEMPlanner, _lib, synthetic
     prob = synthetic.make_problem(args.config)
     prob["cfg_id"] = args.config
     cfg = prob["cfg"]
@@ -521,6 +523,9 @@ def main():
                      "kernel": "rollout_kernel", "avg_launch_ms": avg_rollout_s * 1e3,
                      "flop_per_launch": flop_launch},
     }
+    built, same = _lib.build_info()
+    out["build"] = {"library": "mujoco-mbrl_amd/mbrl_amd/libmbrl_cem.so", "source_digest": built,
+                    "matches_tree": same}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["parity"] = parity_sample(prob, first)
     if not args.no_variants:

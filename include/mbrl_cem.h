@@ -140,6 +140,9 @@ typedef struct {
 } mbrl_cem_params;
 
 int mbrl_abi_version(void);
+/* "src=<16 hex digits> arch=gfx950": the sha256 prefix of the sources the library was built from
+ * (mujoco-mbrl_amd/Makefile DIGEST_FILES), so a caller can check a prebuilt library against a tree. */
+const char* mbrl_build_info(void);
 const char* mbrl_last_error(void);
 
 /* ---- process-wide switches for A/B runs and for tests that force a fallback. Every option starts

@@ -1429,6 +1429,13 @@ extern "C" {
 
 int mbrl_abi_version(void) { return MBRL_ABI_VERSION; }
 
+#if __has_include("src_digest.h")
+#include "src_digest.h"
+#else
+#define MBRL_SRC_DIGEST "unknown"
+#endif
+const char* mbrl_build_info(void) { return "src=" MBRL_SRC_DIGEST " arch=gfx950"; }
+
 const char* mbrl_last_error(void) { return g_err.c_str(); }
 
 int mbrl_set_option(int32_t option, int32_t value) {

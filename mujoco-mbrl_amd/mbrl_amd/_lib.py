@@ -62,7 +62,7 @@ EXPORTED = (
     "mbrl_train_epoch", "mbrl_gd_batch_workspace_bytes", "mbrl_gd_plan_batch", "mbrl_host_alloc",
     "mbrl_host_free", "mbrl_comm_unique_id", "mbrl_comm_init", "mbrl_comm_destroy",
     "mbrl_cem_plan_sharded_workspace_bytes", "mbrl_cem_plan_sharded",
-    "mbrl_event_create", "mbrl_event_record", "mbrl_stream_wait_event", "mbrl_event_synchronize",
+    "mbrl_build_info", "mbrl_event_create", "mbrl_event_record", "mbrl_stream_wait_event", "mbrl_event_synchronize",
     "mbrl_event_destroy",
 )
 
@@ -137,6 +137,7 @@ def load():
     P = c_void_p
     sig = {
         "mbrl_abi_version": (c_int32, []),
+        "mbrl_build_info": (ctypes.c_char_p, []),
         "mbrl_last_error": (ctypes.c_char_p, []),
         "mbrl_set_option": (c_int32, [c_int32, c_int32]),
         "mbrl_get_option": (c_int32, [c_int32]),
@@ -195,6 +196,31 @@ def load():
         raise ImportError(f"mbrl_amd ABI version mismatch: {lib.mbrl_abi_version()} != {ABI_VERSION}")
     _lib = lib
     return lib
+
+
+def source_digest():
+    """The digest mujoco-mbrl_amd/Makefile compiles into mbrl_build_info(), recomputed from the tree's
+    sources (None where they are absent)."""
+    import glob
+    import hashlib
+    pkg = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    files = sorted(glob.glob(os.path.join(pkg, "csrc", "*.hip")) + glob.glob(os.path.join(pkg, "csrc", "*.h")),
+                   key=lambda f: os.path.relpath(f, pkg))
+    files.append(os.path.join(os.path.dirname(pkg), "include", "mbrl_cem.h"))
+    if not all(os.path.exists(f) for f in files):
+        return None
+    h = hashlib.sha256()
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def build_info():
+    """(the loaded library's source digest, whether it equals the tree's)."""
+    info = load().mbrl_build_info().decode()
+    built = dict(kv.split("=", 1) for kv in info.split())["src"]
+    return built, built == source_digest()
 
 
 def check(rc, what):

@@ -194,3 +194,12 @@ def test_training_workspace_and_status_word_sizing():
     bad.state_dim, bad.action_dim, bad.hidden, bad.n_hidden, bad.reward_head, bad.horizon = 17, 6, 512, 0, 0, 1
     assert lib.mbrl_train_workspace_bytes(ctypes.byref(bad), 512) == 0
     assert lib.mbrl_train_status_offset(ctypes.byref(bad), 512) == ctypes.c_size_t(-1).value
+
+
+def test_library_was_built_from_this_tree():
+    """mbrl_build_info() carries the sha256 prefix of the sources the .so was compiled from
+    (mujoco-mbrl_amd/Makefile DIGEST_FILES); it must equal the digest of the sources in this tree,
+    so a prebuilt library that travels with the tree is known to be these sources' build."""
+    from mbrl_amd import _lib
+    built, same = _lib.build_info()
+    assert same, f"libmbrl_cem.so was built from sources {built}, the tree holds {_lib.source_digest()}: rebuild"
