@@ -429,7 +429,7 @@ __device__ __forceinline__ void gemm_tile(const GemmLaunch& L, int tile, float (
     // (stamp slots: 0 entry, 1 K loop done, 2 after the reduction barrier / arrival wait, 3 exit)
     // up to GROUP chunks' operands in flight at once, then their MFMAs: with the usual 1-4 chunks
     // per wave the loads' latency is paid once
-    constexpr int GROUP = NW == 16 ? (TMX == 2 ? 1 : 2) : 4;   // TMX 2 at 16 waves: the 128-VGPR budget
+    constexpr int GROUP = NW == 16 ? (TMX == 2 ? 1 : 2) : NW == 8 ? 2 : 4;   // TMX 2 at 16 waves: the 128-VGPR budget
     for (int g0 = kb0; g0 < kb1; g0 += 16 * GROUP) {
         f32x4 a[GROUP][2 * TMX], b[GROUP][2];
 #pragma unroll
@@ -1489,17 +1489,25 @@ static void finish(GemmDesc& D, int M, int N, int K, int tmx = 1) {
     D.tiles = ((M + TT * tmx - 1) / (TT * tmx)) * D.tiles_n;
 }
 
-// 16 waves split a long K (the hidden layers, every weight gradient); 4 suffice for short ones.
+// 16 waves split a long K (the hidden layers, every weight gradient); 4 suffice for short ones; 8 where
+// the longest K is a weight gradient's batch rows in (128, 256) -- each wave then sums 32 rows, the
+// row tile of the fused step's folds (launch_waves; fold_waves follows the same rule).
 // TMX: the C tile height of every product of the launch (finish() with the same tmx).
+static int launch_waves(const GemmLaunch& L) {
+    int kmax = 0;
+    bool grad_rows = false;
+    for (int i = 0; i < L.nd; ++i) kmax = max(kmax, L.d[i].K);
+    for (int i = 0; i < L.nd; ++i) grad_rows = grad_rows || (L.d[i].out.mode == EPI_GRAD && L.d[i].K == kmax);
+    return kmax >= 256 ? 16 : (kmax > 128 && grad_rows) ? 8 : 4;
+}
+
 template <int A0, int B0, int A1 = -1, int B1 = -1, int TMX = 1>
 static hipError_t launch_gemm(GemmLaunch& L, bool loss_wg, hipStream_t stream) {
-    int blocks = loss_wg ? 1 : 0, kmax = 0;
-    for (int i = 0; i < L.nd; ++i) {
-        blocks += L.d[i].tiles;
-        kmax = max(kmax, L.d[i].K);
-    }
+    int blocks = loss_wg ? 1 : 0;
+    for (int i = 0; i < L.nd; ++i) blocks += L.d[i].tiles;
+    const int nw = launch_waves(L);
     // fused Adam blocks: chunks of 4 elements per thread of the launch's workgroup size
-    const int chunk = 64 * (kmax >= 256 ? 16 : 4) * 4;
+    const int chunk = 64 * nw * 4;
     L.adam_chunk = chunk;
     L.adam_blocks = 0;
     for (int i = 0; i < L.adam_count; ++i) {
@@ -1514,10 +1522,12 @@ static hipError_t launch_gemm(GemmLaunch& L, bool loss_wg, hipStream_t stream) {
     const int tiles_m0 = L.d[0].tiles / L.d[0].tiles_n;
     L.xcd = L.xcd && (tiles_m0 % (8 * (2 / TMX)) == 0);
     if constexpr (TMX == 2) {   // chosen only for long K (launch_train_grads): 16 waves
-        if (kmax < 256) return hipErrorInvalidValue;
+        if (nw != 16) return hipErrorInvalidValue;
         hipLaunchKernelGGL((train_gemm_kernel<16, A0, B0, A1, B1, TMX>), dim3(blocks), dim3(64 * 16), 0, stream, L);
-    } else if (kmax >= 256) {
+    } else if (nw == 16) {
         hipLaunchKernelGGL((train_gemm_kernel<16, A0, B0, A1, B1, TMX>), dim3(blocks), dim3(64 * 16), 0, stream, L);
+    } else if (nw == 8) {
+        hipLaunchKernelGGL((train_gemm_kernel<8, A0, B0, A1, B1, TMX>), dim3(blocks), dim3(64 * 8), 0, stream, L);
     } else {
         hipLaunchKernelGGL((train_gemm_kernel<4, A0, B0, A1, B1, TMX>), dim3(blocks), dim3(64 * 4), 0, stream, L);
     }
@@ -1583,10 +1593,11 @@ size_t train_status_offset(const TrainShape& t, int batch) {
 }
 
 // Whether the layer-0 weight gradient folds into the dH_0 launch bit-identically: its separate launch
-// (M = W, K = R) gives each of its waves one 32-row block of the batch (16 waves at R >= 256, else 4).
+// (M = W, K = R) gives each of its waves one 32-row block of the batch (16 waves at R >= 256, 8 in
+// (128, 256), else 4: launch_waves).
 static int fold_waves(const TrainShape& t, int R) {
     if (t.fold == 0 || t.L < 1) return 0;
-    const int nw = R >= 256 ? 16 : 4, chunks = (R + 15) / 16, per = (chunks + nw - 1) / nw;
+    const int nw = R >= 256 ? 16 : R > 128 ? 8 : 4, chunks = (R + 15) / 16, per = (chunks + nw - 1) / nw;
     return per == 2 ? nw : 0;
 }
 

@@ -58,7 +58,7 @@ def _autograd(m, ds, ins, outs, idx, reward):
 
 CASES = [("model", 17, 6, 512, 2, 1, 512), ("model", 17, 6, 50, 2, 1, 512), ("model", 5, 1, 64, 1, 2, 37),
          ("model", 24, 8, 200, 3, 3, 300), ("model", 3, 2, 33, 2, 1, 1), ("reward", 17, 6, 200, 2, 1, 512),
-         ("reward", 11, 3, 96, 2, 2, 129), ("model", 67, 21, 128, 2, 1, 256)]
+         ("reward", 11, 3, 96, 2, 2, 129), ("model", 67, 21, 128, 2, 1, 256), ("model", 17, 6, 512, 2, 1, 200)]
 
 
 @pytest.mark.parametrize("kind,s,a,W,L,H,B", CASES)
@@ -295,7 +295,8 @@ def test_layer0_gradient_fold_is_bitwise_neutral(kind, W, L, H, B):
 @pytest.mark.parametrize("kind,s,a,W,H,B", [("model", 17, 6, 512, 1, 512), ("reward", 17, 6, 512, 1, 512),
                                            ("reward", 17, 6, 200, 1, 400), ("model", 17, 6, 50, 1, 512),
                                            ("model", 24, 8, 333, 2, 150), ("model", 5, 1, 96, 1, 100),
-                                           ("reward", 31, 33, 256, 1, 300), ("model", 11, 2, 512, 3, 171)])
+                                           ("reward", 31, 33, 256, 1, 300), ("model", 11, 2, 512, 3, 171),
+                                           ("model", 17, 6, 512, 1, 252), ("reward", 17, 6, 200, 1, 200)])
 def test_fused_step_is_bitwise_neutral(kind, s, a, W, H, B):
     """Two hidden layers train in three launches (H_0 recomputed per H_1 tile, dY per dH_1 tile, the
     output layer's weight gradient folded; W_1's Adam step in the dH_0 launch after the tiles that
@@ -354,10 +355,10 @@ def test_fused_step_random_shapes_bitwise(case):
     a = int(rng.integers(1, 64 - s + 1))
     W = int(rng.choice([33, 50, 64, 97, 128, 200, 255, 256, 333, 400, 512]))
     H = int(rng.integers(1, 3))
-    lo, hi = [(64, 128), (256, 512)][int(rng.integers(0, 2))]
+    lo, hi = [(64, 128), (128, 255), (256, 512)][int(rng.integers(0, 3))]
     B = int(rng.integers(lo // H + 1, hi // H + 1))
     R = B * H
-    nw = 16 if R >= 256 else 4   # train.hip fold_waves: the fused step needs the dW_0 fold (per == 2)
+    nw = 16 if R >= 256 else 8 if R > 128 else 4   # train.hip fold_waves: the fused step needs per == 2
     assert lo < R <= hi and (((R + 15) // 16 + nw - 1) // nw) == 2
     ds = _dataset(s, a, H, 3 * B + 5, seed=case)
     _, ins, outs = ds.stacked(DEV)
