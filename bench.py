@@ -302,9 +302,10 @@ def train_line(dev, W=512, epochs=50):
     """the reference's train_model (models.py:53-93; Adam, experiment.py:55-62)
     for a 2 x W Model on 10k synthetic cheetah-shaped transitions (s = 17, a = 6), batch 512 -- on this
     GPU through mbrl_train_epoch (csrc/train.hip: the fused two-launch step, Adam in its launches).
-    A 10-epoch warm-up call, then one train_model call of `epochs` epochs timed between two events on the
-    training stream (GPU-bound: one host call per epoch; the call's own start-up -- the first epoch's
-    shuffle, the checks before the first launch, the final status read -- inside the span). 50 is the
+    Warm-up calls of 10, `epochs` and `epochs` epochs, then a 10-epoch and an `epochs`-epoch call, each
+    timed between two events on the training stream (GPU-bound: one host call per epoch; the call's own
+    start-up -- the first epoch's shuffle, the checks before the first launch, the final status read --
+    inside the span). 50 is the
     reference's num_epochs default, which its agent's training loop uses (agents.py:292); a 10-epoch
     call is timed beside it. FLOP per step: forward 2R(K0 W + W^2 + W s), the same for the weight
     gradients, 2R(W s + W^2) for the input gradients (R = 512 rows)."""
@@ -321,10 +322,14 @@ def train_line(dev, W=512, epochs=50):
     torch.manual_seed(0)
     m = models.Model(17, 6, hidden_units=W).to(dev)
     opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    gc.collect()    # the set-up's garbage (tens of thousands of per-step tensors) before the warm-up
     np.random.seed(1)
-    m.train_model(ds, opt, batch_size=512, num_epochs=10)   # warm-up: the ring rows, the copy stream, events
+    # warm-up: the ring rows, the copy stream, events -- and ~120 ms of back-to-back training, which the
+    # GPU needs to reach its steady clock after the host-side set-up above left it idle (the first
+    # 50-epoch call of a process measured 57.1 us per step, the third 54.8: tools/train_gc_probe.py)
+    for n in (10, epochs, epochs):
+        m.train_model(ds, opt, batch_size=512, num_epochs=n)
     torch.cuda.synchronize(dev)
-    gc.collect()    # the set-up's garbage (tens of thousands of per-step tensors) before the timed calls
     def timed(n_epochs):
         np.random.seed(2)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
