@@ -21,6 +21,7 @@ Both take the fused path when fused.describe_* recognise the model / cost closur
 user's callables run on device tensors (reference semantics, planners.py:199-210) and selection /
 refit still run in the HIP extension.
 """
+import contextlib
 import threading
 import warnings
 
@@ -45,6 +46,17 @@ def _device(kwargs):
             raise RuntimeError("mbrl_amd planners need a ROCm GPU (torch.cuda.is_available() is False)")
         dev = torch.device("cuda", torch.cuda.current_device())
     return torch.device(dev)
+
+
+_NULL_CTX = contextlib.nullcontext()
+
+
+def _on_device(dev):
+    """torch.cuda.device(dev), or a no-op when dev is already the current device (the common case:
+    the context manager's enter and exit are a few microseconds of every plan's host turn)."""
+    if dev.index is not None and torch._C._cuda_getDevice() == dev.index:
+        return _NULL_CTX
+    return torch.cuda.device(dev)
 
 
 def _to_host(x, keep_device):
@@ -282,8 +294,33 @@ class CEMPlanner(ModelPlanner):
         """B plans at once, one per row of initial_states [B, s] (see cem_plan_batch)."""
         return cem_plan_batch(initial_states, model, cost, sample_action, horizon, **kwargs)
 
+    _SETTINGS = {}
+
     @staticmethod
     def _settings(sample_action, horizon, kwargs):
+        """The plan's settings; with an explicit seed the dict is built once per (sampler, horizon,
+        kwargs) and reused (part of every plan's host turn). Unhashable kwargs values (the timing hooks'
+        lists) key by identity: the dict holds those objects themselves, so it sees their contents."""
+        if kwargs.get("seed") is not None:
+            try:
+                key = (id(sample_action), horizon,
+                       tuple((k, v if isinstance(v, (int, float, str, bool, torch.device, tuple, type(None)))
+                              else ("id", id(v))) for k, v in kwargs.items()))
+                hit = CEMPlanner._SETTINGS.get(key)
+            except TypeError:          # an unhashable tuple value
+                key, hit = None, None
+            if hit is not None and hit[0] is sample_action:
+                return hit[1]
+            st = CEMPlanner._settings_build(sample_action, horizon, kwargs)
+            if key is not None:
+                if len(CEMPlanner._SETTINGS) > 64:
+                    CEMPlanner._SETTINGS.clear()
+                CEMPlanner._SETTINGS[key] = (sample_action, st)
+            return st
+        return CEMPlanner._settings_build(sample_action, horizon, kwargs)
+
+    @staticmethod
+    def _settings_build(sample_action, horizon, kwargs):
         d = CEMPlanner.defaults
         g = lambda k: kwargs.get(k, d[k])  # noqa: E731
         N = int(g("num_candidates"))
@@ -313,7 +350,7 @@ class CEMPlanner(ModelPlanner):
         """plan() plus diagnostics: dict(states, actions, mu, sigma[, costs, returns, elites per iteration])."""
         dev = _device(kwargs)
         st = CEMPlanner._settings(sample_action, horizon, kwargs)
-        with torch.cuda.device(dev):
+        with _on_device(dev):
             mdesc, cdesc, prob = fused.describe_problem(model, cost, dev, st["precision"])
             ws = None
             if st["distributed"] and torch.distributed.is_available() and torch.distributed.is_initialized() \
@@ -439,12 +476,20 @@ def _cem_plan_host(lib, prob, initial_state, st, params, ws, pref):
                 _host=True)
 
 
+_EVENT_ARRAYS = {}
+
+
 def _events(st, I):
     events = st["events"]
     if events is None:
         return None
-    return (_lib.c_void_p * (2 * I))(*[(e.cuda_event if pair is not None else None)
-                                       for pair in events for e in (pair or (None, None))])
+    handles = tuple((e.cuda_event if pair is not None else None) for pair in events for e in (pair or (None, None)))
+    arr = _EVENT_ARRAYS.get(handles)
+    if arr is None:
+        if len(_EVENT_ARRAYS) > 16:
+            _EVENT_ARRAYS.clear()
+        arr = _EVENT_ARRAYS[handles] = (_lib.c_void_p * (2 * I))(*handles)
+    return arr
 
 
 def _cem_fused_single(prob, initial_state, st):
