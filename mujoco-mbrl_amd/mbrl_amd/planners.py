@@ -295,27 +295,30 @@ class CEMPlanner(ModelPlanner):
         return cem_plan_batch(initial_states, model, cost, sample_action, horizon, **kwargs)
 
     _SETTINGS = {}
+    _HOOKS = ("rollout_events", "plan_events")
 
     @staticmethod
     def _settings(sample_action, horizon, kwargs):
         """The plan's settings; with an explicit seed the dict is built once per (sampler, horizon,
-        kwargs) and reused (part of every plan's host turn). Unhashable kwargs values (the timing hooks'
-        lists) key by identity: the dict holds those objects themselves, so it sees their contents."""
+        kwargs) and reused (part of every plan's host turn). The timing hooks (fresh lists per plan in
+        bench.py) stay out of the key and are set on a copy."""
         if kwargs.get("seed") is not None:
             try:
                 key = (id(sample_action), horizon,
-                       tuple((k, v if isinstance(v, (int, float, str, bool, torch.device, tuple, type(None)))
-                              else ("id", id(v))) for k, v in kwargs.items()))
+                       tuple((k, v) for k, v in kwargs.items() if k not in CEMPlanner._HOOKS))
                 hit = CEMPlanner._SETTINGS.get(key)
-            except TypeError:          # an unhashable tuple value
+            except TypeError:          # an unhashable kwargs value: no caching
                 key, hit = None, None
-            if hit is not None and hit[0] is sample_action:
-                return hit[1]
-            st = CEMPlanner._settings_build(sample_action, horizon, kwargs)
-            if key is not None:
-                if len(CEMPlanner._SETTINGS) > 64:
-                    CEMPlanner._SETTINGS.clear()
-                CEMPlanner._SETTINGS[key] = (sample_action, st)
+            if hit is None or hit[0] is not sample_action:
+                hit = (sample_action, CEMPlanner._settings_build(sample_action, horizon, kwargs))
+                if key is not None:
+                    if len(CEMPlanner._SETTINGS) > 64:
+                        CEMPlanner._SETTINGS.clear()
+                    CEMPlanner._SETTINGS[key] = hit
+            st = hit[1]
+            ev, pev = kwargs.get("rollout_events"), kwargs.get("plan_events")
+            if ev is not st["events"] or pev is not st["plan_events"]:
+                st = dict(st, events=ev, plan_events=pev)
             return st
         return CEMPlanner._settings_build(sample_action, horizon, kwargs)
 
