@@ -274,3 +274,30 @@ def test_cem_planner_on_a_gpu_less_host_raises():
     _, model_fn, cost_fn, sample_action = build(p)
     with pytest.raises(RuntimeError, match="GPU"):
         CEMPlanner.plan(torch.from_numpy(p["s0"]), model_fn, cost_fn, sample_action, 4, num_candidates=64)
+
+
+def test_cem_settings_cache_semantics():
+    """CEMPlanner._settings builds the settings once per (sampler, horizon, kwargs) when the seed is
+    explicit: equal kwargs give the same dict, any changed value a new one, the per-plan timing hooks
+    are set on a copy, unhashable values and seed=None are never cached (seed=None draws from the
+    global NumPy RNG on every call, as the reference's sampler does)."""
+    from mbrl_amd import synthetic
+    from mbrl_amd.planners import CEMPlanner
+    p = synthetic.make_problem(3, N=64, H=4)
+    sa = p["sample_action"]
+    kw = dict(num_candidates=64, num_iterations=2, seed=5)
+    a, b = CEMPlanner._settings(sa, 4, dict(kw)), CEMPlanner._settings(sa, 4, dict(kw))
+    assert a is b and a["N"] == 64 and a["seed"] == 5
+    c = CEMPlanner._settings(sa, 4, dict(kw, num_candidates=128))
+    assert c is not a and c["N"] == 128 and a["N"] == 64
+    assert CEMPlanner._settings(sa, 5, dict(kw))["H"] == 5
+    hooks = [None, None]
+    d = CEMPlanner._settings(sa, 4, dict(kw, rollout_events=hooks))
+    assert d["events"] is hooks and a["events"] is None and d["N"] == 64
+    e = CEMPlanner._settings(sa, 4, dict(kw, action_bounds=[-2.0, 2.0]))   # unhashable: built afresh
+    assert (e["lo"], e["hi"]) == (-2.0, 2.0)
+    np.random.seed(0)
+    s1 = CEMPlanner._settings(sa, 4, dict(num_candidates=64))["seed"]
+    s2 = CEMPlanner._settings(sa, 4, dict(num_candidates=64))["seed"]
+    np.random.seed(0)
+    assert s1 != s2 and s1 == int(np.random.randint(0, 2 ** 62, dtype=np.int64))
