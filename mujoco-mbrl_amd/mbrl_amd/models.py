@@ -358,11 +358,13 @@ class _OrderRing:
     the side stream copies into a device row only once the epoch that last read it has run
     (`consumed`), so the host may run up to ~2K epochs ahead -- ~35 ms of 2x512 training at K = 16,
     room for a garbage-collector pause of the host thread -- and no call allocates (a pinned
-    allocation costs milliseconds, a new stream's first use ~6 ms of queue set-up)."""
-    K = 16
+    allocation costs milliseconds, a new stream's first use ~6 ms of queue set-up). K shrinks with
+    the dataset (16 rows up to 131k transitions, 4 from 524k on: a longer epoch is a longer lead), so
+    the ring holds at most 16 MB of pinned memory up to 524k transitions and 4 rows beyond."""
 
     def __init__(self, dev, n):
         self.n = n
+        self.K = max(4, min(16, (1 << 21) // max(n, 1)))
         self.pinned = torch.empty((self.K, n), dtype=torch.int64, pin_memory=True)
         self.host = self.pinned.numpy()
         self.arange = np.arange(n, dtype=np.int64)
