@@ -8,6 +8,7 @@ reference's arithmetic.
 """
 import ctypes
 import functools
+import threading
 import weakref
 
 import numpy as np
@@ -408,7 +409,8 @@ _ORDER_RINGS = {}
 
 
 def _order_ring(dev, n):
-    key = (str(dev), n)
+    # one ring per thread: two threads training at once must not share pinned rows
+    key = (str(dev), n, threading.get_ident())
     ring = _ORDER_RINGS.get(key)
     if ring is None:
         if len(_ORDER_RINGS) > 8:
