@@ -471,6 +471,12 @@ __global__ void __launch_bounds__(1024) select_kernel(const float* __restrict__ 
 // coalesced (candidate n by thread n % 1024) into LDS keys, then each thread takes its KPT keys from
 // LDS; the LDS key array is reused for the per-wave radix histograms afterwards.
 constexpr int SEL_HIST_WORDS = 2 * 16 * 257;
+// Up to this many keys per thread the returns load as per-thread float4 runs; above it, as coalesced
+// scalar rows transposed through LDS (a thread's float4 run at KPT 32 puts 64 lines under every wave
+// load instruction). A/B: -DMBRL_SELECT_VEC_MAX=64 is the r04 choice.
+#ifndef MBRL_SELECT_VEC_MAX
+#define MBRL_SELECT_VEC_MAX 64
+#endif
 
 // Segmented over blockIdx.x (independent problems of N candidates each, batched planning): segment
 // b reads costs[e * member_stride + b * N + n] and writes elite_idx[b * K ..] (local indices) and
@@ -487,9 +493,10 @@ __device__ __forceinline__ void select_reg_body(const float* __restrict__ costs,
     const int tid = threadIdx.x, wave = tid >> 6;
     const int n0 = tid * KPT;
     uint32_t key[KPT];
-    // KPT >= 4 with 16-byte aligned rows: each thread loads its own contiguous KPT returns as float4
-    // (no LDS transpose); the member sum keeps the same per-candidate order, so the bits are the same
-    const bool vec = KPT >= 4 && (N & 3) == 0 && (member_stride & 3) == 0;
+    // KPT in [4, MBRL_SELECT_VEC_MAX] with 16-byte aligned rows: each thread loads its own contiguous
+    // KPT returns as float4 (no LDS transpose); the member sum keeps the same per-candidate order, so
+    // the bits are the same either way
+    const bool vec = KPT >= 4 && KPT <= MBRL_SELECT_VEC_MAX && (N & 3) == 0 && (member_stride & 3) == 0;
     if (vec) {
         typedef float f4 __attribute__((ext_vector_type(4)));
         constexpr int G4 = KPT >= 4 ? KPT / 4 : 1;
