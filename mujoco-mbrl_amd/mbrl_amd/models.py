@@ -356,8 +356,8 @@ class _OrderRing:
     """K pinned host rows and K device rows of n row indices, a copy stream and per-row events, reused
     by every train_model call on datasets of n transitions: epoch e's order lives in row e % K. The
     host draws into a pinned row only once the copy that last read it has finished (`copied`), and
-    the side stream copies into a device row only once the epoch that last read it has run
-    (`consumed`), so the host may run up to ~2K epochs ahead -- ~35 ms of 2x512 training at K = 16,
+    enqueues the copy into a device row only once the epoch that last read it has run (`consumed`),
+    so the host may run up to ~K epochs ahead -- ~17 ms of 2x512 training at K = 16,
     room for a garbage-collector pause of the host thread -- and no call allocates (a pinned
     allocation costs milliseconds, a new stream's first use ~6 ms of queue set-up). K shrinks with
     the dataset (16 rows up to 131k transitions, 4 from 524k on: a longer epoch is a longer lead), so
@@ -395,8 +395,11 @@ class _OrderRing:
 
     def copy(self, e, stream):
         r = e % self.K
+        # the epoch that last read this device row must have run: the host checks (it is K epochs
+        # back, so this rarely waits) -- a wait of the side stream on the training stream's event cost
+        # the training stream 20-45 us per epoch (tools/train_epoch_plumbing.py)
+        self.consumed[r].synchronize()              # (an event never recorded is complete)
         with torch.cuda.stream(stream):
-            self.consumed[r].wait(stream)           # (an event never recorded is complete)
             self.dev[r].copy_(self.pinned[r], non_blocking=True)
             self.copied[r].record(stream)
 
