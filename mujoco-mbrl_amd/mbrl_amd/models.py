@@ -359,17 +359,20 @@ class _OrderRing:
     enqueues the copy into a device row only once the epoch that last read it has run (`consumed`),
     so the host may run up to ~K epochs ahead -- ~17 ms of 2x512 training at K = 16,
     room for a garbage-collector pause of the host thread -- and no call allocates (a pinned
-    allocation costs milliseconds, a new stream's first use ~6 ms of queue set-up). K shrinks with
-    the dataset (16 rows up to 131k transitions, 4 from 524k on: a longer epoch is a longer lead), so
-    the ring holds at most 16 MB of pinned memory up to 524k transitions and 4 rows beyond."""
+    allocation costs milliseconds, a new stream's first use ~6 ms of queue set-up). Rows hold
+    `cap` indices, n rounded up to a power of two, and an epoch uses the first n: the dataset of an
+    MBRL loop grows every episode, and it reuses one ring until it doubles. K shrinks with the
+    capacity (16 rows up to 131k, 4 from 524k on: a longer epoch is a longer lead), so the ring
+    holds at most 16 MB of pinned memory up to 524k indices and 4 rows beyond."""
 
-    def __init__(self, dev, n):
-        self.n = n
-        self.K = max(4, min(16, (1 << 21) // max(n, 1)))
-        self.pinned = torch.empty((self.K, n), dtype=torch.int64, pin_memory=True)
+    def __init__(self, dev, cap):
+        self.cap = cap
+        self.n = cap
+        self.K = max(4, min(16, (1 << 21) // max(cap, 1)))
+        self.pinned = torch.empty((self.K, cap), dtype=torch.int64, pin_memory=True)
         self.host = self.pinned.numpy()
-        self.arange = np.arange(n, dtype=np.int64)
-        self.dev = torch.empty((self.K, n), dtype=torch.int64, device=dev)
+        self.arange = np.arange(cap, dtype=np.int64)
+        self.dev = torch.empty((self.K, cap), dtype=torch.int64, device=dev)
         self.side = torch.cuda.Stream(dev)
         with torch.cuda.stream(self.side):          # set up the side stream's queue here, once
             self.dev[:1].copy_(self.pinned[:1], non_blocking=True)
@@ -389,9 +392,9 @@ class _OrderRing:
         """Epoch e's order (models._epoch_order's draws: NumPy's shuffle of arange(n), in place)."""
         r = e % self.K
         self.copied[r].synchronize()                # the copy that last read this pinned row is done
-        row = self.host[r]
-        np.copyto(row, self.arange)
-        np.random.shuffle(row)
+        row = self.host[r, :self.n]
+        np.copyto(row, self.arange[:self.n])
+        np.random.shuffle(row)                      # (in place on the view: the draws of a fresh arange(n))
 
     def copy(self, e, stream):
         r = e % self.K
@@ -400,12 +403,12 @@ class _OrderRing:
         # the training stream 20-45 us per epoch (tools/train_epoch_plumbing.py)
         self.consumed[r].synchronize()              # (an event never recorded is complete)
         with torch.cuda.stream(stream):
-            self.dev[r].copy_(self.pinned[r], non_blocking=True)
+            self.dev[r, :self.n].copy_(self.pinned[r, :self.n], non_blocking=True)
             self.copied[r].record(stream)
 
     def rows(self, e):
         r = e % self.K
-        return self.host[r], self.dev[r]
+        return self.host[r, :self.n], self.dev[r, :self.n]
 
 
 _ORDER_RINGS = {}
@@ -413,12 +416,14 @@ _ORDER_RINGS = {}
 
 def _order_ring(dev, n):
     # one ring per thread: two threads training at once must not share pinned rows
-    key = (str(dev), n, threading.get_ident())
+    cap = 1 << max(10, (max(n, 1) - 1).bit_length())
+    key = (str(dev), cap, threading.get_ident())
     ring = _ORDER_RINGS.get(key)
     if ring is None:
         if len(_ORDER_RINGS) > 8:
             _ORDER_RINGS.clear()
-        ring = _ORDER_RINGS[key] = _OrderRing(dev, n)
+        ring = _ORDER_RINGS[key] = _OrderRing(dev, cap)
+    ring.n = n                  # (the previous call's epochs were all enqueued before this one draws)
     return ring
 
 

@@ -175,7 +175,9 @@ def test_native_training_leaves_the_last_batch_gradient():
 def test_cached_native_object_trains_like_a_fresh_one():
     """train_model reuses the model's _NativeGrads (gradients, workspace) across calls while nothing it
     binds changed. Three calls with the cache equal three calls that each start from a fresh object,
-    bit for bit; growing the dataset (new stacked tensors) or the batch size rebuilds it."""
+    bit for bit; growing the dataset (new stacked tensors) or the batch size rebuilds it. The order
+    ring is kept across the grown dataset (same power-of-two capacity), and a fresh ring per call
+    trains to the same bits."""
     from mbrl_amd import models
     out = {}
     for cached in (True, False):
@@ -183,20 +185,23 @@ def test_cached_native_object_trains_like_a_fresh_one():
         m = _model("model", 17, 6, 512, 2, seed=3)
         opt = torch.optim.Adam(m.parameters(), lr=1e-3)
         np.random.seed(8)
-        objs = []
+        objs, rings = [], []
         for call, bs in enumerate((512, 512, 256, 512)):
             if not cached:
                 models._NativeGrads.forget(m)
+                models._ORDER_RINGS.clear()
             if call == 3:   # a grown dataset: new stacked tensors
                 extra = _dataset(17, 6, 1, 90, seed=12)
                 ds.add_rollouts(extra.rollouts)
             m.train_model(ds, opt, batch_size=bs, num_epochs=2)
             objs.append(models._NATIVE_CACHE.get(m, (None, None))[1])
+            rings.append(models._order_ring(DEV, ds.num_transitions()))
         out[cached] = [p.detach().cpu() for p in m.parameters()]
         if cached:
             assert objs[0] is objs[1]            # same binding: reused
             assert objs[2] is not objs[1]        # batch size changed
             assert objs[3] is not objs[2]        # dataset grew
+            assert rings[3] is rings[0] and rings[3].n == ds.num_transitions() < rings[3].cap
     assert all(torch.equal(x, y) for x, y in zip(out[True], out[False]))
 
 
