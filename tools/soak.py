@@ -10,7 +10,8 @@ the path's first result (and, for the pairs, with the 8-candidate tiles that nee
 * the training step's band waits (F -> O inside one launch) and arrival waits (dH_0 -> dW_1), over
   a long train_model call: the sticky status word is read at its end and must be clear, and the
   weights must equal a run of the three-launch layout (MBRL_OPT_TRAIN_FO = 1).
-Usage: python tools/soak.py [seconds_per_part]. Prints one JSON line per part and a summary."""
+Usage: python tools/soak.py [seconds_per_part] [parts: any of cem,gd,train; default all]. Prints one
+JSON line per part and a summary."""
 import json
 import os
 import sys
@@ -96,9 +97,10 @@ def train_part(seconds):
         torch.cuda.synchronize()
         return [p.detach().clone() for p in m.parameters()]
 
+    run(5, 0)                                   # first call: bindings, ring, clocks
     t0 = time.perf_counter()
-    run(5, 0)
-    per_epoch = (time.perf_counter() - t0) / 5
+    run(20, 0)
+    per_epoch = (time.perf_counter() - t0) / 20
     epochs = max(10, int(seconds / max(per_epoch, 1e-4) / 2))
     fused = run(epochs, 0)
     split = run(epochs, 1)
@@ -110,18 +112,22 @@ def train_part(seconds):
 
 def main():
     seconds = float(sys.argv[1]) if len(sys.argv) > 1 else 20.0
+    which = set(sys.argv[2].split(",")) if len(sys.argv) > 2 else {"cem", "gd", "train"}
     parts = []
     pair = {"rollout_pair": 1, "debug_pair_abort": 2}
     m8 = {"rollout_tile": 8, "rollout_pair": 2}
-    for cfg_id, N in ((4, 2048), (3, 2048)):
-        parts.append(cem_part(cfg_id, N, seconds, pair, m8))
+    if "cem" in which:
+        for cfg_id, N in ((4, 2048), (3, 2048)):
+            parts.append(cem_part(cfg_id, N, seconds, pair, m8))
+            print(json.dumps(parts[-1]), flush=True)
+        parts.append(cem_part(3, 4096, seconds, {}, {"traj_hop": 1}))     # the bench plan; trajectory hop modes
         print(json.dumps(parts[-1]), flush=True)
-    parts.append(cem_part(3, 4096, seconds, {}, {"traj_hop": 1}))     # the bench plan; trajectory hop modes
-    print(json.dumps(parts[-1]), flush=True)
-    parts.append(gd_part(seconds))
-    print(json.dumps(parts[-1]), flush=True)
-    parts.append(train_part(seconds))
-    print(json.dumps(parts[-1]), flush=True)
+    if "gd" in which:
+        parts.append(gd_part(seconds))
+        print(json.dumps(parts[-1]), flush=True)
+    if "train" in which:
+        parts.append(train_part(seconds))
+        print(json.dumps(parts[-1]), flush=True)
     bad = sum(p["mismatches"] for p in parts) + sum(1 for p in parts if p.get("first_equals_reference") is False)
     print(json.dumps(dict(summary=True, parts=len(parts), failures=bad, seconds_per_part=seconds)))
     sys.exit(1 if bad else 0)
