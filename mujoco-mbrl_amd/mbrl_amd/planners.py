@@ -422,14 +422,25 @@ def cem_plan_batch(initial_states, model, cost, sample_action, horizon, **kwargs
         return _to_host(states, keep), _to_host(actions, keep)
 
 
-_WS = {}
+_WS = threading.local()
 
 
 def _workspace(key, nbytes, device):
-    buf = _WS.get(key)
+    """Scratch for `key` owned by this thread and the current stream of `device`. A plan enqueues on
+    the current stream and reuses its scratch in stream order; another thread, or this thread on
+    another stream, gets a buffer of its own, so plans in flight never share scratch (the flags,
+    epochs and proposals of one plan are not overwritten by another's launches)."""
+    bufs = getattr(_WS, "bufs", None)
+    if bufs is None:
+        bufs = _WS.bufs = {}
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    k = key + (torch._C._cuda_getCurrentRawStream(idx),)
+    buf = bufs.get(k)
     if buf is None or buf.numel() < nbytes or buf.device != device:
+        if buf is None and len(bufs) > 16:
+            bufs.clear()
         buf = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=device)
-        _WS[key] = buf
+        bufs[k] = buf
     return buf
 
 
