@@ -66,6 +66,7 @@ def main():
         bench_frac=bench["roofline"]["frac"], bench_ms_per_plan=bench["ms_per_step"],
         plan_span_us=span / P, plan_gaps_us=gaps / P,
         between_plans_us=sum(between) / max(1, len(between)),
+        between_plans_median_us=(sorted(between)[len(between) // 2] if between else 0.0),   # (one slow host turn moves the mean)
         busy_us_per_plan={f: busy[f] / P for f in fams}, launches_per_plan={f: count[f] / P for f in fams},
         note=f"rocprofv3 --kernel-trace --stats of bench.py ({steps} timed plans); under the profiler, "
              "so ms_per_plan is a little above the unprofiled bench line")
