@@ -223,16 +223,22 @@ struct Output {
                               // read of the weight block) is done -- what wait_ticket counts
     // EPI_MASK of dH_0 with fold (launch_train_grads): the tile also yields the layer-0 weight
     // gradient's partial over each of its 32-row blocks -- exactly what wave tr of the separate dW_0
-    // launch summed -- into fold_part[tr][W][K0]; the last of a column block's tiles to finish (a
-    // ticket per column block) adds them in wave order into dW_0 / db_0 and takes layer 0's Adam step
+    // launch summed -- as tagged granules (fold_gran below); the dW_1 tiles of row block 0 add them
+    // in wave order into dW_0 / db_0 and take layer 0's Adam step (fold_sum)
     int fold, fold_k0, fold_nw;         // input columns K0, the separate launch's wave count
     const float* fold_x;                // the gathered input [R][K0] (xbuf, written by the forward)
-    float* fold_part;
-    unsigned* fold_ticket;              // [ceil(W / 32)], zeroed by the forward launch
     float *fold_dw, *fold_db;           // dW_0 [W][K0], db_0 [W]
     int fold_cs_tiles;                  // 32-row tiles of the column sums (colsum_out of this product)
     int fold_adam;
     mbrl_adam_tensor fold_aw, fold_ab;
+    // the fold's hand-off as tagged granules {value, tag} (8-byte stores, read untorn): the partials
+    // [tr][W][K0] and the column sums [tr][W] of dH_0, tag = the step's serial (*fold_serial, raised
+    // by the step's first launch); the dW_1 tiles of row block 0 (fold_sum) poll them and finish
+    // dW_0 / db_0 and layer 0's Adam step. No drain, ticket or last arriver on the producers' side.
+    unsigned long long *fold_gran, *cs_gran;
+    const unsigned* fold_serial;
+    unsigned* fold_status;              // bit 0: a bounded wait timed out
+    int fold_sum;                       // EPI_GRAD (dW_1): row block 0's tiles run fold_sum
     float scale_s, scale_r;   // EPI_LOSS: dY scale of the state / reward columns (2 / numel)
     float inv_s, inv_r;       // EPI_LOSS: loss weight of the state / reward columns (1 / numel)
     int s;                    // EPI_LOSS: state columns (n >= s: the reward column)
@@ -267,6 +273,7 @@ struct GemmLaunch {
     mbrl_adam_tensor adam_t[ADAM_FUSED_MAX];
     unsigned* zero_words;   // workgroup 0 zeroes zero_n words first (the fold's tickets; forward launch)
     int zero_n;
+    unsigned* serial;       // workgroup 0 raises the step's serial (the fold's granule tag; forward launch)
     int adam_first[ADAM_FUSED_MAX + 1];
     mbrl_adam_hparams hp;
     int arith;
@@ -325,6 +332,13 @@ __device__ __forceinline__ void stash_input(const GemmLaunch& L, const GemmDesc&
 template <int NW, int TMX, int DI>
 __device__ __forceinline__ void fold_dw0(const GemmLaunch& L, int tm, int n0, float (*red)[TT * TMX][TT + 1],
                                          const float (*xs)[FOLD_K0MAX]);
+template <int NW>
+__device__ __forceinline__ void fold_sum(const GemmLaunch& L, int n0);
+
+// A tagged granule {value, tag}: one 8-byte store, read untorn (MI355X_MICROARCH.md, granules)
+__device__ __forceinline__ unsigned long long granule(float v, unsigned tag) {
+    return ((unsigned long long)tag << 32) | __float_as_uint(v);
+}
 
 // p[0] + p[stride] + ... + p[(n - 1) stride], summed in index order like a plain loop, with the loads
 // of each 16 terms in flight together (a loop that loads one term per iteration pays the memory
@@ -538,14 +552,16 @@ __device__ __forceinline__ void gemm_tile(const GemmLaunch& L, int tile, float (
         if (tid < TM && n0 + col < D.N && m0 + TT * sub < D.M) {
             float t = red[0][TT * sub][col];
             for (int r = 1; r < TT; ++r) t = t + red[0][TT * sub + r][col];
-            float* dst = O.colsum_out + (int64_t)(tm * TMX + sub) * D.N + n0 + col;
-            if (O.fold)   // read back by the fold's last arriver (sc1 hand-off)
-                __hip_atomic_store(dst, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int64_t di = (int64_t)(tm * TMX + sub) * D.N + n0 + col;
+            if (O.fold)   // read by fold_sum (dW_1 tile (0, n0 / 32)) as a tagged granule
+                __hip_atomic_store(O.cs_gran + di, granule(t, *O.fold_serial), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
             else
-                *dst = t;
+                O.colsum_out[di] = t;
         }
         if (O.mode == EPI_MASK && O.fold) fold_dw0<NW, TMX, DI>(L, tm, n0, red, xs);
     }
+    if (O.mode == EPI_GRAD && O.fold_sum && tm == 0) fold_sum<NW>(L, n0);
     if (O.mode == EPI_LOSS) {   // the tile's loss: a butterfly per wave, then the waves in order
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) {
@@ -573,36 +589,19 @@ __device__ __forceinline__ void gemm_tile(const GemmLaunch& L, int tile, float (
 // dW_0 launch (M = W, N = K0, K = R, fold_nw waves of 32 rows each) computed, per wave tr, one 32 x 32
 // block of dW_0 over rows [32 tr, 32 tr + 32) with acc[x][y] over 16-row chunks u, k = 4 q + s: the
 // same loads and MFMAs in the same order run here per 32-row half of the tile, so every partial is
-// the same float, and the last arriver sums them in wave order with the empty waves' +0 -- the
-// separate launch's result bit for bit.
+// the same float; they leave as tagged granules, and fold_sum (a dW_1 tile of the same launch) adds
+// them in wave order with the empty waves' +0 -- the separate launch's result bit for bit.
 template <int NW, int TMX, int DI>
 __device__ __forceinline__ void fold_dw0(const GemmLaunch& L, int tm, int n0, float (*red)[TT * TMX][TT + 1],
                                          const float (*xs)[FOLD_K0MAX]) {
     const GemmDesc& D = L.d[DI];
     constexpr int TM = TT * TMX;
+    (void)TM;
     const Output& O = D.out;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, q = lane >> 4, c = lane & 15;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, q = lane >> 4, c = lane & 15;
     const int R = D.M, W = D.N, K0 = O.fold_k0, m0 = tm * TT * TMX;
     const int kt = (K0 + TT - 1) / TT;
-    // the last arriver's Adam operands for this column block of W_0 / b_0, loaded by every tile now
-    // (one element per thread at K0 <= 32) so that its tail has one memory round trip, not three
-    constexpr int NT = 64 * NW, FPT = (TT * FOLD_K0MAX + NT - 1) / NT;
-    float fp[FPT], fm[FPT], fv[FPT], bp = 0.0f, bm = 0.0f, bv = 0.0f;
-    const bool fpre = O.fold_adam && K0 <= FOLD_K0MAX;
-#pragma unroll
-    for (int u = 0; u < FPT; ++u) {
-        const int e = tid + u * NT, j = n0 + e / max(K0, 1), kk = e - (e / max(K0, 1)) * K0;
-        const bool in = fpre && e < TT * K0 && j < W;
-        const int64_t i = (int64_t)j * K0 + kk;
-        fp[u] = in ? O.fold_aw.param[i] : 0.0f;
-        fm[u] = in ? O.fold_aw.exp_avg[i] : 0.0f;
-        fv[u] = in ? O.fold_aw.exp_avg_sq[i] : 0.0f;
-    }
-    if (fpre && tid < TT && n0 + tid < W) {
-        bp = O.fold_ab.param[n0 + tid];
-        bm = O.fold_ab.exp_avg[n0 + tid];
-        bv = O.fold_ab.exp_avg_sq[n0 + tid];
-    }
+    const unsigned tag = *O.fold_serial;
     for (int task = wave; task < TMX * kt; task += NW) {
         const int h = task / kt, kb = task - (task / kt) * kt;
         const int r0 = m0 + TT * h;
@@ -653,91 +652,116 @@ __device__ __forceinline__ void fold_dw0(const GemmLaunch& L, int tm, int n0, fl
 #pragma unroll
                 for (int v = 0; v < 4; ++v) {
                     const int j = n0 + 16 * x + 4 * q + v, kk = TT * kb + 16 * y + c;
-                    if (j < W && kk < K0)    // sc1 (write-through) stores: no release fence needed
-                        __hip_atomic_store(O.fold_part + ((int64_t)tr * W + j) * K0 + kk, acc[x][y][v],
+                    if (j < W && kk < K0)    // read by fold_sum as a tagged granule: nothing to drain
+                        __hip_atomic_store(O.fold_gran + ((int64_t)tr * W + j) * K0 + kk, granule(acc[x][y][v], tag),
                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
     }
-    // ticket: the last tile of column block n0 / 32 to arrive finishes dW_0 / db_0 of its 32 rows.
-    // Hand-off (MI355X_MICROARCH.md, the sc1 table's first row): every partial and column sum is an sc1
-    // store, every storing wave waits for its stores, one lane adds to the block's ticket after a
-    // barrier, and the workgroup whose add returns the last count reads them back with sc1 loads.
-    __shared__ unsigned last;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    const int tiles_m = (R + TM - 1) / TM;
-    if (tid == 0) {
-        const unsigned t = __hip_atomic_fetch_add(&O.fold_ticket[n0 / TT], 1u, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-        last = (t + 1 == (unsigned)tiles_m) ? 1u : 0u;
+}
+
+// The fold's sums, in the dW_1 tile (0, n0 / 32) of the same launch (higher workgroup ids than every
+// dH_0 tile, so those were dispatched first and always finish): the column block's per-32-row partials
+// added in wave order with the empty waves' +0 -- the separate dW_0 launch's sum, bit for bit -- and
+// db_0 from the column sums over the 32-row tiles, then layer 0's Adam step. Each lane loads all of its
+// granules at once and reloads the ones whose tag is not yet this step's (bounded: 1 s, then bit 0 of
+// the status word).
+template <int NW>
+__device__ __forceinline__ bool poll_granules(const unsigned long long* const* p, int n, unsigned tag, float* out,
+                                              unsigned* status) {
+    unsigned long long g[16];
+    unsigned need = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        out[i] = 0.0f;
+        if (i < n) need |= 1u << i;
     }
-    __syncthreads();
-    if (!last) return;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (need) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            g[i] = ((need >> i) & 1u) ? __hip_atomic_load(p[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            if (((need >> i) & 1u) && (unsigned)(g[i] >> 32) == tag) {
+                out[i] = __uint_as_float((unsigned)g[i]);
+                need &= ~(1u << i);
+            }
+        if (!need) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {
+            if (status) atomicOr(status, 1u);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return true;
+}
+
+template <int NW>
+__device__ __forceinline__ void fold_sum(const GemmLaunch& L, int n0) {
+    const GemmDesc& D = L.d[0];
+    const Output& O = D.out;
+    const int tid = threadIdx.x;
+    const int R = D.M, W = D.N, K0 = O.fold_k0;
     const int ntr = (R + TT - 1) / TT;      // non-empty waves of the separate launch
-    // every load of the tail first (db_0's column sums, then the partials): one round trip
-    float cs[16];
-    const bool csfast = O.fold_cs_tiles <= 16, dbt = tid < TT && n0 + tid < W;
+    const unsigned tag = *O.fold_serial;
+    constexpr int NT = 64 * NW;
+    const bool dbt = tid < TT && n0 + tid < W;
+    // the Adam operands of this column block first: their latency overlaps the polls
+    float bp = 0.0f, bm = 0.0f, bv = 0.0f;
+    if (O.fold_adam && dbt) {
+        bp = O.fold_ab.param[n0 + tid];
+        bm = O.fold_ab.exp_avg[n0 + tid];
+        bv = O.fold_ab.exp_avg_sq[n0 + tid];
+    }
+    for (int e0 = 0; e0 < TT * K0; e0 += NT) {
+        const int e = e0 + tid, j = n0 + e / K0, kk = e - (e / K0) * K0;
+        const bool in = e < TT * K0 && j < W;
+        const int64_t i = (int64_t)j * K0 + kk;
+        float fp = 0.0f, fm = 0.0f, fv = 0.0f;
+        if (in && O.fold_adam) {
+            fp = O.fold_aw.param[i];
+            fm = O.fold_aw.exp_avg[i];
+            fv = O.fold_aw.exp_avg_sq[i];
+        }
+        const unsigned long long* ptr[16];
+        const int np = in ? min(ntr, O.fold_nw) : 0;
 #pragma unroll
-    for (int i = 0; i < 16; ++i)
-        cs[i] = (dbt && csfast && i < O.fold_cs_tiles)
-                    ? __hip_atomic_load(O.colsum_out + (int64_t)i * W + n0 + tid, __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_AGENT)
-                    : 0.0f;
-    auto sum_partials = [&](int j, int kk) {
-        float p[16];                         // fold_nw <= 16: every load in flight before the sum
-#pragma unroll
-        for (int w = 0; w < 16; ++w)
-            p[w] = (w < ntr && w < O.fold_nw)
-                       ? __hip_atomic_load(O.fold_part + ((int64_t)w * W + j) * K0 + kk, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT)
-                       : 0.0f;
+        for (int w = 0; w < 16; ++w) ptr[w] = O.fold_gran + ((int64_t)min(w, max(np - 1, 0)) * W + j) * K0 + kk;
+        float p[16];
+        poll_granules<NW>(ptr, np, tag, p, O.fold_status);
+        if (!in) continue;
         float v = p[0];
 #pragma unroll
         for (int w = 1; w < 16; ++w)
             if (w < O.fold_nw) v = v + p[w];
-        return v;
-    };
-    if (fpre) {                              // the Adam operands are in registers (fp / fm / fv)
-#pragma unroll
-        for (int u = 0; u < FPT; ++u) {
-            const int e = tid + u * NT, j = n0 + e / K0, kk = e - (e / K0) * K0;
-            if (e >= TT * K0 || j >= W) continue;
-            const float v = sum_partials(j, kk);
-            const int64_t i = (int64_t)j * K0 + kk;
-            O.fold_dw[i] = v;
-            adam_element(fp[u], v, fm[u], fv[u], O.fold_aw.step_size, O.fold_aw.bc2_sqrt, L.hp, L.arith);
-            O.fold_aw.param[i] = fp[u];
-            O.fold_aw.exp_avg[i] = fm[u];
-            O.fold_aw.exp_avg_sq[i] = fv[u];
-        }
-    } else {
-        for (int e = tid; e < TT * K0; e += NT) {
-            const int j = n0 + e / K0, kk = e - (e / K0) * K0;
-            if (j >= W) continue;
-            const float v = sum_partials(j, kk);
-            const int64_t i = (int64_t)j * K0 + kk;
-            O.fold_dw[i] = v;
-            if (O.fold_adam)
-                adam_element(O.fold_aw.param[i], v, O.fold_aw.exp_avg[i], O.fold_aw.exp_avg_sq[i],
-                             O.fold_aw.step_size, O.fold_aw.bc2_sqrt, L.hp, L.arith);
+        O.fold_dw[i] = v;
+        if (O.fold_adam) {
+            adam_element(fp, v, fm, fv, O.fold_aw.step_size, O.fold_aw.bc2_sqrt, L.hp, L.arith);
+            O.fold_aw.param[i] = fp;
+            O.fold_aw.exp_avg[i] = fm;
+            O.fold_aw.exp_avg_sq[i] = fv;
         }
     }
-    if (dbt) {                               // db_0: the column sums of dH_0 over the 32-row tiles
+    if (tid < 64) {                          // db_0: the column sums of dH_0 over the 32-row tiles
         const int j = n0 + tid;
-        float g = cs[0];
+        const unsigned long long* ptr[16];
+        const int np = dbt ? min(O.fold_cs_tiles, 16) : 0;
 #pragma unroll
-        for (int i = 1; i < 16; ++i)
-            if (i < O.fold_cs_tiles) g = g + cs[i];
-        if (!csfast) g = ordered_sum<true>(O.colsum_out + j, W, O.fold_cs_tiles);
-        O.fold_db[j] = g;
-        if (fpre) {
-            adam_element(bp, g, bm, bv, O.fold_ab.step_size, O.fold_ab.bc2_sqrt, L.hp, L.arith);
-            O.fold_ab.param[j] = bp;
-            O.fold_ab.exp_avg[j] = bm;
-            O.fold_ab.exp_avg_sq[j] = bv;
-        } else if (O.fold_adam) {
-            adam_element(O.fold_ab.param[j], g, O.fold_ab.exp_avg[j], O.fold_ab.exp_avg_sq[j], O.fold_ab.step_size,
-                         O.fold_ab.bc2_sqrt, L.hp, L.arith);
+        for (int i = 0; i < 16; ++i) ptr[i] = O.cs_gran + (int64_t)min(i, max(np - 1, 0)) * W + min(j, W - 1);
+        float cs[16];
+        poll_granules<NW>(ptr, np, tag, cs, O.fold_status);
+        if (dbt) {
+            float g = cs[0];
+#pragma unroll
+            for (int i = 1; i < 16; ++i)
+                if (i < O.fold_cs_tiles) g = g + cs[i];
+            O.fold_db[j] = g;
+            if (O.fold_adam) {
+                adam_element(bp, g, bm, bv, O.fold_ab.step_size, O.fold_ab.bc2_sqrt, L.hp, L.arith);
+                O.fold_ab.param[j] = bp;
+                O.fold_ab.exp_avg[j] = bm;
+                O.fold_ab.exp_avg_sq[j] = bv;
+            }
         }
     }
 }
@@ -753,6 +777,7 @@ __global__ __launch_bounds__(64 * NW) void train_gemm_kernel(const GemmLaunch L)
     const int b = blockIdx.x;
     if (b == 0 && L.zero_words)
         for (int i = threadIdx.x; i < L.zero_n; i += 64 * NW) L.zero_words[i] = 0u;
+    if (b == 0 && L.serial && threadIdx.x == 0) *L.serial = *L.serial + 1u;
     if (b < L.d[0].tiles) {
         int tile = b;
         if (L.xcd) {   // block b on XCD b % 8 (round-robin dispatch) takes a tile of a 64-row band of that XCD
@@ -820,7 +845,7 @@ __global__ __launch_bounds__(64 * NW) void train_gemm_kernel(const GemmLaunch L)
 //      launch's tile: loss partials and dY column sums from the first column tile), dH_1 =
 //      (dY W_out) * (H_1 > 0), and the output layer's weight-gradient partial over the tile's 32 rows
 //      -- exactly wave tm of the separate dW_out product -- summed in wave order by the column block's
-//      last arriver (the dW_0 fold's hand-off), which also finishes db_out, db_1 and b_1's Adam step.
+//      last arriver (an sc1 hand-off), which also finishes db_out, db_1 and b_1's Adam step.
 //      Removes a launch and the dY round trip.
 //   B  launch_gemm: dH_0 with the folded dW_0 and its Adam step, dW_1 -- whose tiles step W_1 in place
 //      once the dH_0 tiles of their column block have read it -- and the output layer's Adam step as
@@ -852,6 +877,7 @@ struct FusedArgs {
     int arith;
     unsigned* zero_words;               // F's workgroup 0 zeroes zero_n words (the tickets of later launches)
     int zero_n;
+    unsigned* serial;                   // F's workgroup 0 raises the step's serial (B's granule tag)
     float scale_s, scale_r, inv_s, inv_r;
     // F and O in one launch (train_fused_fo_kernel): per 32-row band of the batch a counter (own 128-B
     // line) that the band's F tiles add to once their H_1 columns are written through; each O tile
@@ -900,6 +926,7 @@ __device__ __forceinline__ void fused_fwd(const FusedArgs& F, float (*red)[TT][T
     FSTAMP(0, 0);
     if (blockIdx.x == 0 && F.zero_words)
         for (int i = tid; i < F.zero_n; i += NT) F.zero_words[i] = 0u;
+    if (blockIdx.x == 0 && F.serial && tid == 0) *F.serial = *F.serial + 1u;
     // the batch's 32 input rows are gathered through the row indices: the indices, the rows, then every
     // weight operand of the launch (in-order vmcnt: a wait for the rows then waits for nothing issued
     // after them, and the weights travel while the rows do)
@@ -1539,14 +1566,16 @@ static hipError_t launch_gemm(GemmLaunch& L, bool loss_wg, hipStream_t stream) {
 // per-row-tile column sums of dY [tiles][J] and of the two dH [tiles][W].
 struct TrainWs {
     float* act[MBRL_TRAIN_MAX_LAYERS];
-    float *dh[2], *dy, *loss_part, *xbuf, *cs_dy, *cs_dh[2], *fold_part;
+    float *dh[2], *dy, *loss_part, *xbuf, *cs_dy, *cs_dh[2];
     float *xbuf2, *tgt2;  // the fused step's second gather slot (the next batch's rows and targets)
     float* out_part;      // fused step: the output layer's weight-gradient partials [row tile][J][W]
     float* tgt;           // fused step: the batch's targets [R][J] (F gathers, O reads)
-    unsigned* tickets;    // [ceil(W / 32)] each: the dW_0 fold's, the fused dH_0 tiles' W_1-read arrivals,
-                          // the fused dW_out fold's
+    unsigned* tickets;    // [ceil(W / 32)] each: (unused: the dW_0 fold's before its granules), the fused
+                          // dH_0 tiles' W_1-read arrivals, the fused dW_out fold's
     unsigned* status;     // fused step: bit 0 = a bounded wait timed out (never expected)
     unsigned* bands;      // fused step, F and O in one launch: [row tiles][32] band counters (one line each)
+    unsigned* serial;     // the step's serial: the dW_0 fold's granule tag (raised by each step's first launch)
+    unsigned long long *fold_gran, *cs_gran;   // the fold's tagged partials [tr][W][K0] and column sums [tr][W]
     size_t floats;
 };
 
@@ -1567,6 +1596,7 @@ static TrainWs train_ws(const TrainShape& t, int batch, float* base) {
     w.tickets = reinterpret_cast<unsigned*>(take(3 * ((W + TT - 1) / TT)));
     w.status = reinterpret_cast<unsigned*>(take(1));
     w.bands = reinterpret_cast<unsigned*>(take(32 * FUSED_MAX_BANDS));
+    w.serial = reinterpret_cast<unsigned*>(take(1));
     for (int l = 0; l < t.L; ++l) w.act[l] = take(R * W);
     w.dh[0] = take(R * W);
     w.dh[1] = take(R * W);
@@ -1576,11 +1606,12 @@ static TrainWs train_ws(const TrainShape& t, int batch, float* base) {
     w.cs_dy = take(tiles_r * J);
     w.cs_dh[0] = take(tiles_r * W);
     w.cs_dh[1] = take(tiles_r * W);
-    w.fold_part = take(tiles_r * W * (size_t)(t.s + t.a));   // the folded dW_0's per-32-row partials
     w.out_part = take(tiles_r * J * W);
     w.tgt = take(R * J);
     w.xbuf2 = take(R * (t.s + t.a));
     w.tgt2 = take(R * J);
+    w.fold_gran = reinterpret_cast<unsigned long long*>(take(2 * tiles_r * W * (size_t)(t.s + t.a)));
+    w.cs_gran = reinterpret_cast<unsigned long long*>(take(2 * tiles_r * W));
     w.floats = off;
     return w;
 }
@@ -1685,6 +1716,7 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
         // reset them)
         const bool fo = t.fo_split == 0;
         F.zero_words = B.tickets; F.zero_n = (fo ? 2 : 3) * tiles_n;
+        F.serial = B.serial;
         F.scale_s = 2.0f / (float)((int64_t)batch * t.s); F.scale_r = 2.0f / (float)batch;
         F.inv_s = 1.0f / (float)((int64_t)batch * t.s); F.inv_r = 1.0f / (float)batch;
         const dim3 grid(tiles_r * tiles_n);
@@ -1722,16 +1754,17 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
         finish(D, R, W, l == 0 ? K0 : W);
         G.nd = 1;
         if (l == 0) {
-            // the forward launch zeroes the fold's tickets and takes the previous step's deferred
-            // Adam step (a layer nothing before this step's second forward launch reads)
-            G.zero_words = fold_nw ? B.tickets : nullptr;
-            G.zero_n = (W + TT - 1) / TT;
+            // the forward launch raises the step's serial (the fold's granule tag) and takes the
+            // previous step's deferred Adam step (a layer nothing before this step's second forward
+            // launch reads)
+            G.serial = fold_nw ? B.serial : nullptr;
             G.adam_count = 0;
             for (int i = 0; i < prior_n; ++i) G.adam_t[G.adam_count++] = prior[i];
         }
         G.xcd = xcd_opt;
         e = l == 0 ? launch_gemm<OP_GATHER, OP_DIRECT>(G, false, stream) : launch_gemm<OP_DIRECT, OP_DIRECT>(G, false, stream);
         G.zero_words = nullptr;
+        G.serial = nullptr;
         G.adam_count = 0;
         if (e != hipSuccess) return e;
     }
@@ -1778,9 +1811,10 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
             finish(D, R, W, n_out, tmx);
             if (l == 1 && fold_nw) {
                 Output& O = D.out;
-                O.fold = 1; O.fold_k0 = K0; O.fold_nw = fold_nw; O.fold_x = B.xbuf; O.fold_part = B.fold_part;
-                O.fold_ticket = B.tickets; O.fold_dw = w.weight_grad[0]; O.fold_db = w.bias_grad[0];
-                O.fold_cs_tiles = tiles_r;
+                O.fold = 1; O.fold_k0 = K0; O.fold_nw = fold_nw; O.fold_x = B.xbuf;
+                O.fold_dw = w.weight_grad[0]; O.fold_db = w.bias_grad[0];
+                O.fold_cs_tiles = tiles_r;   // <= 16: the fold's 32-row waves bound R by 512 (fold_waves)
+                O.fold_gran = B.fold_gran; O.cs_gran = B.cs_gran; O.fold_serial = B.serial; O.fold_status = B.status;
                 if (adam) {          // nothing in this launch reads layer 0's parameters
                     O.fold_adam = 1; O.fold_aw = adam[0]; O.fold_ab = adam[1];
                 }
@@ -1803,6 +1837,7 @@ hipError_t launch_train_grads(const TrainShape& t, const TrainTensors& w, const 
                 O.g0 = O.g1 = w.bias_grad[l];
             }
             finish(D, n_out, n_in, R, tmx);
+            if (l == 1 && fold_nw) O.fold_sum = 1;   // row block 0's tiles finish dW_0 / db_0 (fold_sum)
         }
         if (adam && l == 0) {   // nothing in this launch reads layer 0's parameters: step them in place
             G.d[G.nd - 1].out.adam = 1;
