@@ -322,6 +322,95 @@ __device__ __forceinline__ f32x4 load_operand(const GemmLaunch& L, const Operand
     return v;
 }
 
+// The second of a wave's two K chunks through LDS (MBRL_TRAIN_GLDS): load_operand's elements, issued as
+// direct-to-LDS loads (global_load_lds: no VGPR destination) into the wave's own 1 KB fragment slot, so
+// both chunks travel together at the 16-wave budget of 128 VGPRs; read back with the same predicates.
+// A whole-row 16-byte load where load_operand would take one (every lane's 4 columns inside K), else one
+// 4-byte load per element; a lane with nothing to read points at the operand's first element and its
+// value is replaced on the way back. The LDS destination is the slot base + lane x size (wave-uniform base).
+#ifndef MBRL_TRAIN_GLDS
+#define MBRL_TRAIN_GLDS 0
+#endif
+template <int KIND>
+__device__ __forceinline__ bool staged_vec(const Operand& o, int kb, int K) {
+    return KIND == OP_DIRECT && o.vec && kb + 16 <= K;
+}
+
+// Branch-free operand loads (OP_DIRECT / OP_TRANS): every lane loads from a valid address -- its own
+// element, or the operand's first element where it has none -- and the value is masked once all of
+// the chunk's loads are in flight (mask_raw). load_operand's guarded loads compile to divergent
+// branches, and hipcc closes each join with vmcnt(0): one memory round trip per fragment.
+template <int KIND>
+__device__ __forceinline__ f32x4 load_raw(const Operand& o, int i, int kb, int k0, int K) {
+    const bool row_ok = i < o.rows && i != o.ones_row;
+    if (staged_vec<KIND>(o, kb, K)) {
+        const float* g = row_ok ? storage_row(o, i) + k0 : o.p0;
+        return *reinterpret_cast<const f32x4*>(g);
+    }
+    f32x4 v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const float* g = o.p0;
+        if (row_ok && k0 + e < K) {
+            if constexpr (KIND == OP_DIRECT) g = storage_row(o, i) + k0 + e;
+            else g = storage_row(o, k0 + e) + i;
+        }
+        v[e] = *g;
+    }
+    return v;
+}
+
+template <int KIND>
+__device__ __forceinline__ f32x4 mask_raw(const Operand& o, int i, int kb, int k0, int K, f32x4 v) {
+    if (i >= o.rows) return f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    if (i == o.ones_row) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = k0 + e < K ? 1.0f : 0.0f;
+        return v;
+    }
+    if (!staged_vec<KIND>(o, kb, K))
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            if (!(k0 + e < K)) v[e] = 0.0f;
+    return v;
+}
+
+template <int KIND>
+__device__ __forceinline__ void stage_operand(const GemmLaunch& L, const Operand& o, int i, int kb, int k0, int K,
+                                              float* slot) {
+    const bool row_ok = i < o.rows && i != o.ones_row;
+    if (staged_vec<KIND>(o, kb, K)) {
+        const float* g = row_ok ? storage_row(o, i) + k0 : o.p0;
+        __builtin_amdgcn_global_load_lds(g, slot, 16, 0, 0);
+        return;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const float* g = o.p0;
+        if (row_ok && k0 + e < K) {
+            if constexpr (KIND == OP_DIRECT) g = storage_row(o, i) + k0 + e;
+            else g = storage_row(o, k0 + e) + i;
+        }
+        __builtin_amdgcn_global_load_lds(g, slot + 64 * e, 4, 0, 0);
+    }
+}
+
+template <int KIND>
+__device__ __forceinline__ f32x4 read_staged(const Operand& o, int i, int kb, int k0, int K, const float* slot, int lane) {
+    f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (i >= o.rows) return v;
+    if (i == o.ones_row) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = k0 + e < K ? 1.0f : 0.0f;
+        return v;
+    }
+    if (staged_vec<KIND>(o, kb, K)) return *reinterpret_cast<const f32x4*>(slot + 4 * lane);
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+        if (k0 + e < K) v[e] = slot[64 * e + lane];
+    return v;
+}
+
 // The gathered batch input, kept for the layer-0 weight gradient (fwd0 writes it as it loads it).
 __device__ __forceinline__ void stash_input(const GemmLaunch& L, const GemmDesc& D, const f32x4& v, int m, int k0) {
 #pragma unroll
@@ -444,19 +533,86 @@ __device__ __forceinline__ void gemm_tile(const GemmLaunch& L, int tile, float (
     // up to GROUP chunks' operands in flight at once, then their MFMAs: with the usual 1-4 chunks
     // per wave the loads' latency is paid once
     constexpr int GROUP = NW == 16 ? (TMX == 2 ? 1 : 2) : NW == 8 ? 2 : 4;   // TMX 2 at 16 waves: the 128-VGPR budget
-    for (int g0 = kb0; g0 < kb1; g0 += 16 * GROUP) {
+    int g0 = kb0;
+    constexpr bool RAW = AK != OP_GATHER && BK != OP_GATHER;   // branch-free loads (load_raw / mask_raw)
+    if constexpr (NW == 16 && TMX == 2 && RAW && MBRL_TRAIN_GLDS) {
+        if (kb1 - kb0 > 16 && kb1 - kb0 <= 32) {
+            // the wave's two chunks at once: the first into registers, the second into LDS (its own
+            // slot of red, which it overwrites with its partials only after reading it back); the
+            // first chunk's use waits for both (vmcnt(0)), so the two latencies overlap
+            float* const slot = &red[wave][0][0];
+            const int kb = kb0 + 16;
+            // the LDS-bound loads first: they are branch-free, while the register loads' per-element
+            // guards become branches whose join points hipcc closes with vmcnt(0) -- which then also
+            // waits for these, already in flight
+#pragma unroll
+            for (int x = 0; x < 2 * TMX; ++x) stage_operand<AK>(L, D.A, m0 + 16 * x + c, kb, kb + 4 * q, D.K, slot + 256 * x);
+#pragma unroll
+            for (int y = 0; y < 2; ++y)
+                stage_operand<BK>(L, D.B, n0 + 16 * y + c, kb, kb + 4 * q, D.K, slot + 256 * (2 * TMX + y));
+            f32x4 a[2 * TMX], b[2];
+#pragma unroll
+            for (int x = 0; x < 2 * TMX; ++x) a[x] = load_raw<AK>(D.A, m0 + 16 * x + c, kb0, kb0 + 4 * q, D.K);
+#pragma unroll
+            for (int y = 0; y < 2; ++y) b[y] = load_raw<BK>(D.B, n0 + 16 * y + c, kb0, kb0 + 4 * q, D.K);
+#pragma unroll
+            for (int x = 0; x < 2 * TMX; ++x) a[x] = mask_raw<AK>(D.A, m0 + 16 * x + c, kb0, kb0 + 4 * q, D.K, a[x]);
+#pragma unroll
+            for (int y = 0; y < 2; ++y) b[y] = mask_raw<BK>(D.B, n0 + 16 * y + c, kb0, kb0 + 4 * q, D.K, b[y]);
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int x = 0; x < 2 * TMX; ++x)
+#pragma unroll
+                    for (int y = 0; y < 2; ++y)
+                        acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[x][s], b[y][s], acc[x][y], 0, 0, 0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int x = 0; x < 2 * TMX; ++x) a[x] = read_staged<AK>(D.A, m0 + 16 * x + c, kb, kb + 4 * q, D.K, slot + 256 * x, lane);
+#pragma unroll
+            for (int y = 0; y < 2; ++y)
+                b[y] = read_staged<BK>(D.B, n0 + 16 * y + c, kb, kb + 4 * q, D.K, slot + 256 * (2 * TMX + y), lane);
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int x = 0; x < 2 * TMX; ++x)
+#pragma unroll
+                    for (int y = 0; y < 2; ++y)
+                        acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[x][s], b[y][s], acc[x][y], 0, 0, 0);
+            g0 = kb1;
+        }
+    }
+    for (; g0 < kb1; g0 += 16 * GROUP) {
         f32x4 a[GROUP][2 * TMX], b[GROUP][2];
 #pragma unroll
         for (int u = 0; u < GROUP; ++u) {
             const int kb = g0 + 16 * u;
             if (kb >= kb1) break;
+            if constexpr (RAW) {
 #pragma unroll
-            for (int x = 0; x < 2 * TMX; ++x) {
-                a[u][x] = load_operand<AK>(L, D.A, m0 + 16 * x + c, kb + 4 * q, D.K);
-                if (stash) stash_input(L, D, a[u][x], m0 + 16 * x + c, kb + 4 * q);
+                for (int x = 0; x < 2 * TMX; ++x) a[u][x] = load_raw<AK>(D.A, m0 + 16 * x + c, kb, kb + 4 * q, D.K);
+#pragma unroll
+                for (int y = 0; y < 2; ++y) b[u][y] = load_raw<BK>(D.B, n0 + 16 * y + c, kb, kb + 4 * q, D.K);
+            } else {
+#pragma unroll
+                for (int x = 0; x < 2 * TMX; ++x) {
+                    a[u][x] = load_operand<AK>(L, D.A, m0 + 16 * x + c, kb + 4 * q, D.K);
+                    if (stash) stash_input(L, D, a[u][x], m0 + 16 * x + c, kb + 4 * q);
+                }
+#pragma unroll
+                for (int y = 0; y < 2; ++y) b[u][y] = load_operand<BK>(L, D.B, n0 + 16 * y + c, kb + 4 * q, D.K);
             }
+        }
+        if constexpr (RAW) {
 #pragma unroll
-            for (int y = 0; y < 2; ++y) b[u][y] = load_operand<BK>(L, D.B, n0 + 16 * y + c, kb + 4 * q, D.K);
+            for (int u = 0; u < GROUP; ++u) {   // the masks, once every load of the group is in flight
+                const int kb = g0 + 16 * u;
+                if (kb >= kb1) break;
+#pragma unroll
+                for (int x = 0; x < 2 * TMX; ++x) a[u][x] = mask_raw<AK>(D.A, m0 + 16 * x + c, kb, kb + 4 * q, D.K, a[u][x]);
+#pragma unroll
+                for (int y = 0; y < 2; ++y) b[u][y] = mask_raw<BK>(D.B, n0 + 16 * y + c, kb, kb + 4 * q, D.K, b[u][y]);
+            }
         }
 #pragma unroll
         for (int u = 0; u < GROUP; ++u) {
@@ -770,7 +926,7 @@ __device__ __forceinline__ void fold_sum(const GemmLaunch& L, int n0) {
 // at compile time so each instantiation carries only its own load paths.
 template <int NW, int A0, int B0, int A1, int B1, int TMX>
 __global__ __launch_bounds__(64 * NW) void train_gemm_kernel(const GemmLaunch L) {
-    __shared__ float red[NW][TT * TMX][TT + 1];
+    __shared__ __attribute__((aligned(16))) float red[NW][TT * TMX][TT + 1];   // (16-B: the staged chunk's slots)
     __shared__ float xs[TT * TMX][FOLD_K0MAX];   // the dW_0 fold's input rows (dH_0 launches only)
     TSTAMP(0);
     // (constant indices only: a dynamic index into the kernel arguments would copy them to scratch)
@@ -899,6 +1055,9 @@ __device__ __forceinline__ void wave_k_range(int K, int nw, int w, int& kb0, int
 
 // Four consecutive k of one row of a row-major matrix (row stride ld), zero past K or for an absent
 // row: load_operand<OP_DIRECT>'s values (float4 when aligned, else element by element).
+// (The guarded loads here measured faster than load_raw's branch-free form in F and O: 49.2-49.3
+// against 50.0 us per step, late r05 -- unlike the backward launch's K loop, where the branch-free
+// form saves 3.6 us.)
 __device__ __forceinline__ f32x4 row4(const float* row, bool valid, int k0, int K, bool vec) {
     f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
     if (!valid) return v;
