@@ -310,7 +310,8 @@ def test_fused_step_is_bitwise_neutral(kind, s, a, W, H, B):
     after three epochs of mbrl_train_epoch whose last batch is short (and takes the five-launch
     path); the status word of the bounded in-launch waits stays clear. The fused step is checked both
     as the default single F+O launch (band waits) and with F and O as two launches
-    (MBRL_OPT_TRAIN_FO = 1)."""
+    (MBRL_OPT_TRAIN_FO = 1), and with the backward tiles in XCD order (MBRL_OPT_TRAIN_XCD = 1, where
+    the dW_1 tiles, not the last dH_0 row tiles, finish the dW_0 fold)."""
     import contextlib
     from mbrl_amd import _lib, models
     ds = _dataset(s, a, H, 3 * B + 37, seed=W + s)
@@ -318,10 +319,11 @@ def test_fused_step_is_bitwise_neutral(kind, s, a, W, H, B):
     reward = kind == "reward"
     idx = torch.randperm(ds.num_transitions(), generator=torch.Generator().manual_seed(B))[:B].to(DEV)
     grads, trained = {}, {}
-    for split in (1, 0, "fo_split"):
+    for split in (1, 0, "fo_split", "xcd"):
         with contextlib.ExitStack() as opts:
             opts.enter_context(_lib.option("train_split", 1 if split == 1 else 0))
             opts.enter_context(_lib.option("train_fo", 1 if split == "fo_split" else 0))
+            opts.enter_context(_lib.option("train_xcd", 1 if split == "xcd" else 0))
             m = _model(kind, s, a, W, 2, seed=W)
             nat = models._NativeGrads(m, ins, outs, ds.horizon, B, reward)
             loss, parts = nat.run(idx)
@@ -337,7 +339,7 @@ def test_fused_step_is_bitwise_neutral(kind, s, a, W, H, B):
             trained[split] = ([p.detach().clone() for p in m.parameters()],
                               [(float(st["step"]), st["exp_avg"].clone(), st["exp_avg_sq"].clone())
                                for st in opt.state.values()], w.rows)
-    for mode in (0, "fo_split"):
+    for mode in (0, "fo_split", "xcd"):
         for i, (x, y) in enumerate(zip(grads[mode], grads[1])):
             assert torch.equal(x, y), (mode, i, float((x - y).abs().max()))
         (pa, sa, ra), (pb, sb, rb) = trained[mode], trained[1]
