@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define MBRL_ABI_VERSION 12
+#define MBRL_ABI_VERSION 13
 
 typedef struct ihipStream_t* mbrl_stream_t; /* == hipStream_t */
 typedef struct ihipEvent_t* mbrl_event_t;   /* == hipEvent_t  */
@@ -38,7 +38,9 @@ enum {
     MBRL_EINVAL = -1,        /* bad argument (null pointer, non-positive size, K > N, ...) */
     MBRL_EUNSUPPORTED = -2,  /* shape outside what the kernels are built for */
     MBRL_EHIP = -3,          /* a HIP runtime call failed */
-    MBRL_EWORKSPACE = -4     /* workspace too small */
+    MBRL_EWORKSPACE = -4,    /* workspace too small */
+    MBRL_EPEER = -5          /* mbrl_cem_plan_sharded: another rank failed during the plan (ABI v13); this
+                                rank's outputs are void, its communicator stays usable */
 };
 
 /* Cost kinds.
@@ -163,7 +165,14 @@ enum {
     MBRL_OPT_ROLLOUT_PAIR = 10,     /* column-split pairs in plans: 0 auto, 1 forced (MBRL_EUNSUPPORTED where
                                        they cannot run), 2 never; standalone rollouts never use them  */
     MBRL_OPT_SHARD_EMULATE = 11,    /* 1 (tests): mbrl_cem_plan_sharded with comm == NULL computes every
-                                       other rank's shard itself in place of the all-gather (G > 1 on one GPU) */
+                                       other rank's shard itself in place of the all-gather (G > 1 on one GPU)
+                                       and keeps each iteration's gathered costs in the workspace; 2 (timing,
+                                       ABI v13): the other ranks' slots are copied from those kept costs (one
+                                       launch per iteration), so the call runs exactly one rank's work: its
+                                       shard's rollout, the update over all N, its own draw, the trajectory.
+                                       Mode 2 is bit-identical to mode 1 after a mode-1 plan of the same
+                                       problem, seed and N (any rank id); set the option before the
+                                       workspace query (the kept costs live in the workspace) */
     MBRL_OPT_DEBUG_PAIR_ABORT = 12, /* 1: the column-split pair kernel gives up at once (its redo runs);
                                        2: no redo launch behind it (tests of the pair kernel's own results) */
     MBRL_OPT_TRAJ_HOP = 13,         /* cooperative trajectory hand-offs: 0 auto, 1 (P, E) grid + sc1 granules,
@@ -176,9 +185,14 @@ enum {
     MBRL_OPT_TRAIN_SPLIT = 17,      /* 1: two-hidden-layer training in the five-launch layout instead of the
                                        fused three-launch step (A/B, tests; same bits)                    */
     MBRL_OPT_DEBUG_SHARD_FAIL = 18, /* i + 1 (tests): mbrl_cem_plan_sharded reports a failed launch at
-                                       iteration i (the rank then keeps joining the all-gathers); 0 off */
+                                       iteration i on the rank MBRL_OPT_DEBUG_SHARD_FAIL_RANK names (the rank
+                                       then keeps joining the all-gathers); 0 off */
     MBRL_OPT_TRAIN_FO = 19,         /* 1: the fused training step's F and O as two launches (A/B; same bits) */
-    MBRL_OPT_COUNT = 20
+    MBRL_OPT_DEBUG_SHARD_FAIL_RANK = 20, /* (tests, ABI v13) r + 1: the injected failure is rank r's only (the
+                                       other ranks see it as a peer failure; under MBRL_OPT_SHARD_EMULATE a
+                                       call with another rank id fails that rank's emulated slot); 0: the
+                                       calling rank's, whatever its id */
+    MBRL_OPT_COUNT = 21
 };
 int mbrl_set_option(int32_t option, int32_t value);
 int mbrl_get_option(int32_t option);
@@ -293,10 +307,15 @@ int mbrl_cem_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_no
  * Every argument check runs before the first collective (the ranks pass the same shape, params and
  * nranks, so they agree on it). A launch that fails later does not end the call early: the rank skips
  * its remaining compute launches but still joins every remaining all-gather (its local costs poisoned
- * to NaN, which every rank ranks last), so no peer waits on it, `comm` stays usable, and the error is
- * returned at the end. The peers are not told: their plan completes without that rank's candidates.
- * comm == NULL is allowed only under MBRL_OPT_SHARD_EMULATE (tests): each call then rolls out every
- * rank's shard itself and fills the all-gather's rank-major buffer, so one GPU runs any nranks. */
+ * to NaN), so no peer waits on it and `comm` stays usable, and returns its own error at the end.
+ * Failure is visible on every rank (ABI v13): the last iteration's all-gather also gathers one status
+ * word per rank (grouped with the costs in one RCCL call), and a rank whose status word is set makes
+ * every other rank return MBRL_EPEER instead of a plan over N - N / nranks candidates. With nranks > 1
+ * the call therefore returns after the plan has completed on `stream` (one stream synchronisation, at
+ * its end); with nranks == 1 it only enqueues, as mbrl_cem_plan.
+ * comm == NULL is allowed only under MBRL_OPT_SHARD_EMULATE (tests, timing): each call then fills the
+ * all-gather's rank-major buffer itself (mode 1: rolls out every rank's shard; mode 2: copies the other
+ * ranks' costs kept by an earlier mode-1 plan), so one GPU runs any nranks. */
 size_t mbrl_cem_plan_sharded_workspace_bytes(const mbrl_mlp_shape* shape, const mbrl_cem_params* params,
                                              int32_t nranks);
 int mbrl_cem_plan_sharded(const mbrl_mlp_shape* shape, const void* packed, const mbrl_norm* norm,
@@ -422,8 +441,11 @@ size_t mbrl_train_workspace_bytes(const mbrl_train_model* model, int32_t batch);
 /* Byte offset in the workspace of a 32-bit status word the fused training step (two hidden layers)
  * sets bit 0 of if one of its bounded in-launch waits timed out -- a workgroup-dispatch order the
  * kernels rely on was not kept and an Adam step may have raced a read of its weights. Never expected;
- * the word is sticky (the caller zeroes the workspace once and reads the word after training).
- * (size_t)-1 for a bad shape. */
+ * the word is sticky (the caller reads it after training and clears it). The caller zeroes the
+ * workspace once before its first use: the fused step tags its layer-0 fold partials with a serial
+ * kept in the workspace. Each mbrl_train_grads / mbrl_train_epoch call clears the step's arrival
+ * tickets and band counters itself (one memset on entry, ABI v13), so a step that timed out does not
+ * carry stale counts into the next call. (size_t)-1 for a bad shape. */
 size_t mbrl_train_status_offset(const mbrl_train_model* model, int32_t batch);
 int mbrl_train_grads(const mbrl_train_model* model, const mbrl_train_data* data, const int64_t* batch_idx,
                      int32_t batch, float* loss_out, void* workspace, size_t ws_bytes, mbrl_stream_t stream);
@@ -435,9 +457,10 @@ int mbrl_train_grads(const mbrl_train_model* model, const mbrl_train_data* data,
  * step's scalars step_sizes[b * count + i], bc2_sqrt[b * count + i] (host arrays, computed as for
  * mbrl_adam_step). The host issues every launch of the epoch in one call. losses: [batches][3]
  * device floats (total, state, reward per batch) or NULL. workspace as for mbrl_train_grads with
- * batch = batch_size. Two hidden layers (the reference's models): three launches per batch with the
- * Adam step inside them, each batch's launches also gathering the next batch's rows; the result is
- * the per-batch calls' bit for bit (tests/test_gpu_train_native.py). */
+ * batch = batch_size. Two hidden layers (the reference's models): two launches per batch (forward with
+ * the output layer, then the backward with the layer-0 fold) with the Adam step inside them, each
+ * batch's launches also gathering the next batch's rows; the result is the per-batch calls' bit for
+ * bit (tests/test_gpu_train_native.py). */
 int mbrl_train_epoch(const mbrl_train_model* model, const mbrl_train_data* data, const int64_t* order, int64_t rows,
                      int32_t batch_size, const mbrl_adam_tensor* tensors, int32_t count,
                      const mbrl_adam_hparams* hparams, const float* step_sizes, const float* bc2_sqrt, float* losses,

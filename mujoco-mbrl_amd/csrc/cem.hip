@@ -470,7 +470,15 @@ __global__ void __launch_bounds__(1024) select_kernel(const float* __restrict__ 
 // (contiguous, so the compaction scan yields ascending indices). Returns are computed and stored
 // coalesced (candidate n by thread n % 1024) into LDS keys, then each thread takes its KPT keys from
 // LDS; the LDS key array is reused for the per-wave radix histograms afterwards.
-constexpr int SEL_HIST_WORDS = 2 * 16 * 257;
+constexpr int SEL_HIST_WORDS = 2 * 16 * 257;   // two buffers of per-wave 8-bit digit histograms
+constexpr int SEL_WIDE_BITS = 11, SEL_WIDE_BINS = 1 << SEL_WIDE_BITS;   // the first (wide) pass
+constexpr int SEL_LIST = 2048;                  // keys of the wide pass's bucket kept in LDS
+// LDS words of the register-resident selection: the coalesced key staging of the non-vector load,
+// aliased by the histograms, the wide histogram, the list and its count
+__host__ __device__ constexpr int sel_words(int KPT) {
+    return 33 * 32 * KPT > SEL_HIST_WORDS + SEL_WIDE_BINS + SEL_LIST + 4 ? 33 * 32 * KPT
+                                                                        : SEL_HIST_WORDS + SEL_WIDE_BINS + SEL_LIST + 4;
+}
 // Up to this many keys per thread the returns load as per-thread float4 runs; above it, as coalesced
 // scalar rows transposed through LDS (a thread's float4 run at KPT 32 puts 64 lines under every wave
 // load instruction). A/B: -DMBRL_SELECT_VEC_MAX=64 is the r04 choice.
@@ -488,7 +496,7 @@ __device__ __forceinline__ void select_reg_body(const float* __restrict__ costs,
                                                 uint32_t* sel_smem, Emit emit) {
     uint32_t(*hist)[16][257] = reinterpret_cast<uint32_t(*)[16][257]>(sel_smem);  // [2][16][257], aliases keys
     __shared__ uint32_t scan_ws[16];
-    __shared__ uint32_t sel[2];
+    __shared__ uint32_t sel[3];   // bucket, keys before it, keys in it
     CSTAMP(0);
     const int tid = threadIdx.x, wave = tid >> 6;
     const int n0 = tid * KPT;
@@ -555,9 +563,8 @@ __device__ __forceinline__ void select_reg_body(const float* __restrict__ costs,
             key[k] = n < N ? sel_smem[n + (n >> 5)] : 0xFFFFFFFFu;
         }
     }
-    // leading bits every key shares (block min / max): their radix passes would select the one
-    // populated bucket, so the first pass starts at the first byte that differs (returns of one plan
-    // usually share sign and exponent: one pass of four saved)
+    // leading bits every key shares (block min / max): returns of one plan usually share sign and
+    // exponent, so the first digit starts at the first bit in which the keys differ
     uint32_t kmin = 0xFFFFFFFFu, kmax = 0u;
 #pragma unroll
     for (int k = 0; k < KPT; ++k)
@@ -570,36 +577,90 @@ __device__ __forceinline__ void select_reg_body(const float* __restrict__ costs,
     __shared__ uint32_t mm_ws[2][16];
     if ((tid & 63) == 0) { mm_ws[0][wave] = kmin; mm_ws[1][wave] = kmax; }
     __syncthreads();   // also: every thread has taken its keys out of sel_smem (non-vector path)
+    uint32_t* wide = sel_smem + SEL_HIST_WORDS;          // [SEL_WIDE_BINS] the first pass's histogram
+    uint32_t* list = wide + SEL_WIDE_BINS;               // [SEL_LIST] its bucket's keys, then
+    uint32_t* list_n = list + SEL_LIST;                  // their count
+    for (int i = tid; i < SEL_WIDE_BINS; i += 1024) wide[i] = 0;
+    for (int i = tid; i < 16 * 257; i += 1024) (&hist[0][0][0])[i] = 0;
+    if (tid == 0) *list_n = 0;
 #pragma unroll
     for (int w = 0; w < 16; ++w) { kmin = min(kmin, mm_ws[0][w]); kmax = max(kmax, mm_ws[1][w]); }
-    const int skip = (kmin == kmax ? 32 : __clz(kmin ^ kmax)) >> 3;   // whole shared bytes (0..4)
-    // radix passes over the remaining 8-bit digits; the histogram buffer of pass p+1 is cleared
-    // during pass p, and the bucket search is a 256-entry scan by waves 0-3 only: 3 barriers per pass
+    const int lead = kmin == kmax ? 32 : __clz(kmin ^ kmax);   // leading bits every key shares
+    uint32_t mask = lead == 0 ? 0u : (lead >= 32 ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> lead));
+    uint32_t prefix = kmin & mask, kk = (uint32_t)K;
+    int rem = 32 - lead;                                 // bits below the shared ones still to resolve
     CSTAMP(1);
-    const uint32_t hi = skip == 0 ? 0u : (skip >= 4 ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> (8 * skip)));
-    uint32_t prefix = kmin & hi, mask = hi, kk = (uint32_t)K;
-    for (int i = tid; i < 16 * 257; i += 1024) (&hist[0][0][0])[i] = 0;
     __syncthreads();
-    int buf = 0;
-    for (int shift = 24 - 8 * skip; shift >= 0; shift -= 8, buf ^= 1) {
-        // returns cluster (most candidates share the leading digits): when every pending lane of a
-        // wave has the same digit, one lane adds the count; otherwise plain per-lane atomics (more
-        // aggregation rounds cost more VALU issue than the contention they save). Rows padded to
-        // 257: no cross-wave bank collisions on a shared digit.
+    // (1) one wide pass over the first SEL_WIDE_BITS differing bits: 2048 bins, one shared histogram
+    // (plan returns spread over most of them, so the K-th key's bucket holds a handful of keys)
+    bool listed = false;
+    if (rem > 0) {
+        const int wb = min(SEL_WIDE_BITS, rem), wshift = rem - wb;
+        const uint32_t wmask = (1u << wb) - 1u;
 #pragma unroll
-        for (int k = 0; k < KPT; ++k) {
-            const bool pending = n0 + k < N && (key[k] & mask) == prefix;
-            const uint32_t dig = (key[k] >> shift) & 255u;
+        for (int k = 0; k < KPT; ++k)
+            if (n0 + k < N) atomicAdd(&wide[(key[k] >> wshift) & wmask], 1u);
+        __syncthreads();
+        const uint32_t h0 = wide[2 * tid], h1 = wide[2 * tid + 1];
+        uint32_t tot;
+        const uint32_t b0 = block_exclusive_scan(h0 + h1, scan_ws, &tot);
+        if (b0 < kk && b0 + h0 >= kk) { sel[0] = 2u * tid; sel[1] = b0; sel[2] = h0; }
+        else if (b0 + h0 < kk && b0 + h0 + h1 >= kk) { sel[0] = 2u * tid + 1u; sel[1] = b0 + h0; sel[2] = h1; }
+        __syncthreads();
+        prefix |= sel[0] << wshift;
+        mask |= wmask << wshift;
+        kk -= sel[1];
+        rem = wshift;
+        CSTAMP(2);
+        // (2) the bucket's keys (sel[2] of them) into an LDS list: the later passes read it, not the
+        // KPT keys of every thread
+        if (rem > 0 && sel[2] <= (uint32_t)SEL_LIST) {
+#pragma unroll
+            for (int k = 0; k < KPT; ++k) {
+                const bool pend = n0 + k < N && (key[k] & mask) == prefix;
+                const uint64_t act = __ballot(pend);
+                if (act != 0) {
+                    const int leader = __builtin_ctzll(act);
+                    uint32_t base = 0;
+                    if ((tid & 63) == leader) base = atomicAdd(list_n, (uint32_t)__popcll(act));
+                    base = (uint32_t)__shfl((int)base, leader, 64);
+                    if (pend) list[base + (uint32_t)__popcll(act & ((1ull << (tid & 63)) - 1ull))] = key[k];
+                }
+            }
+            listed = true;
+            __syncthreads();
+        }
+        CSTAMP(3);
+    }
+    // (3) 8-bit radix passes over the remaining bits: over the list (a few keys, at most SEL_LIST / 1024
+    // per thread), or over every thread's KPT keys when the bucket was too large to list. Per-wave
+    // histograms (rows padded to 257: no cross-wave bank collisions on a shared digit); the buffer of pass
+    // p+1 is cleared during pass p; the bucket search is a 256-entry scan by waves 0-3.
+    const uint32_t nl = listed ? *list_n : 0u;
+    int buf = 0;
+    while (rem > 0) {
+        const int db = min(8, rem), shift = rem - db;
+        const uint32_t dmask = (1u << db) - 1u;
+        auto count = [&](uint32_t kv, bool valid) {
+            const bool pending = valid && (kv & mask) == prefix;
+            const uint32_t dig = (kv >> shift) & dmask;
             const uint64_t act = __ballot(pending);
             if (act != 0) {
                 const int leader = __builtin_ctzll(act);
                 const uint32_t d0 = __shfl(dig, leader, 64);
-                if (__ballot(pending && dig == d0) == act) {
+                if (__ballot(pending && dig == d0) == act) {   // clustered: one add per wave
                     if ((int)(tid & 63) == leader) atomicAdd(&hist[buf][wave][d0], (uint32_t)__popcll(act));
                 } else if (pending) {
                     atomicAdd(&hist[buf][wave][dig], 1u);
                 }
             }
+        };
+        if (listed) {
+            for (uint32_t i0 = 0; i0 < nl; i0 += 1024)   // block-uniform trip count
+                count(i0 + tid < nl ? list[i0 + tid] : 0u, i0 + tid < nl);
+        } else {
+#pragma unroll
+            for (int k = 0; k < KPT; ++k) count(key[k], n0 + k < N);
         }
         for (int i = tid; i < 16 * 257; i += 1024) (&hist[buf ^ 1][0][0])[i] = 0;
         __syncthreads();
@@ -623,31 +684,36 @@ __device__ __forceinline__ void select_reg_body(const float* __restrict__ costs,
         }
         __syncthreads();
         prefix |= sel[0] << shift;
-        mask |= 0xFFu << shift;
+        mask |= dmask << shift;
         kk -= sel[1];
-        CSTAMP(2 + (24 - shift) / 8);
+        rem = shift;
+        buf ^= 1;
     }
-    uint32_t eq = 0;
-#pragma unroll
-    for (int k = 0; k < KPT; ++k) eq += (n0 + k < N && key[k] == prefix);
-    uint32_t tot;
-    uint32_t eq_before = block_exclusive_scan(eq, scan_ws, &tot);
-    bool take[KPT];
-    uint32_t cnt = 0;
-#pragma unroll
-    for (int k = 0; k < KPT; ++k) {
-        take[k] = false;
-        if (n0 + k < N) {
-            if (key[k] < prefix) take[k] = true;
-            else if (key[k] == prefix) { take[k] = eq_before < kk; ++eq_before; }
-        }
-        cnt += take[k];
-    }
-    uint32_t pos = block_exclusive_scan(cnt, scan_ws, &tot);
+    CSTAMP(4);
+    // prefix = the K-th smallest key; the elites are every key below it and the first kk keys equal to
+    // it (lowest index first). One packed scan gives each thread both counts before it: (below << 16) |
+    // equal (N <= 32768, so neither half carries), and an elite's place in ascending index order is
+    // below-before + min(equal-before, kk).
+    uint32_t lt = 0, eq = 0;
 #pragma unroll
     for (int k = 0; k < KPT; ++k)
-        if (take[k] && pos < (uint32_t)K) emit(pos++, n0 + k);
-    CSTAMP(6);
+        if (n0 + k < N) { lt += key[k] < prefix; eq += key[k] == prefix; }
+    uint32_t tot;
+    const uint32_t ex = block_exclusive_scan((lt << 16) | eq, scan_ws, &tot);
+    uint32_t lt_b = ex >> 16, eq_b = ex & 0xFFFFu;
+#pragma unroll
+    for (int k = 0; k < KPT; ++k) {
+        if (n0 + k >= N) continue;
+        if (key[k] < prefix) {
+            const uint32_t pos = lt_b + min(eq_b, kk);
+            if (pos < (uint32_t)K) emit(pos, n0 + k);
+            ++lt_b;
+        } else if (key[k] == prefix) {
+            if (eq_b < kk && lt_b + eq_b < (uint32_t)K) emit(lt_b + eq_b, n0 + k);
+            ++eq_b;
+        }
+    }
+    CSTAMP(5);
 }
 
 template <int KPT>
@@ -662,7 +728,7 @@ __global__ void __launch_bounds__(1024) select_reg_kernel(const float* __restric
                          [&](uint32_t pos, int n) { elite_idx[pos] = n; });
 }
 
-static size_t select_reg_lds(int KPT) { return 4 * (size_t)max(33 * 32 * KPT, SEL_HIST_WORDS); }
+static size_t select_reg_lds(int KPT) { return 4 * (size_t)sel_words(KPT); }
 
 // ------------------------------------------------------------------------------------------------
 // CEM refit. gather: regenerate every elite's a_t from the counter RNG into aelite[t][e][a].
@@ -868,7 +934,7 @@ struct UpdateArgs {
 };
 
 __host__ __device__ inline size_t update_lds_words(int KPT, int a, int K) {
-    const size_t sel = (size_t)(33 * 32 * KPT > SEL_HIST_WORDS ? 33 * 32 * KPT : SEL_HIST_WORDS);
+    const size_t sel = (size_t)sel_words(KPT);
     const size_t ref = refit_rows_floats(a, K);
     return (((size_t)K + 3) & ~(size_t)3) + 2 * (((size_t)a + 3) & ~(size_t)3) + (sel > ref ? sel : ref);
 }
@@ -1459,6 +1525,8 @@ int mbrl_set_option(int32_t option, int32_t value) {
         case MBRL_OPT_GD_HOP: ok = value >= 0 && value <= 3; break;
         case MBRL_OPT_PAIR_L2: ok = value >= 0 && value <= 2; break;
         case MBRL_OPT_DEBUG_SHARD_FAIL: ok = value >= 0 && value <= 1 << 20; break;
+        case MBRL_OPT_DEBUG_SHARD_FAIL_RANK: ok = value >= 0 && value <= 1 << 20; break;
+        case MBRL_OPT_SHARD_EMULATE: ok = value >= 0 && value <= 2; break;
         default: ok = value == 0 || value == 1; break;
     }
     if (!ok) return fail(MBRL_EINVAL, "option %d: value %d not allowed", option, value);
@@ -1737,8 +1805,11 @@ int mbrl_train_grads(const mbrl_train_model* model, const mbrl_train_data* data,
     if (ws_bytes < need) return fail(MBRL_EWORKSPACE, "train_grads: workspace %zu < %zu bytes", ws_bytes, need);
     TrainTensors w{model->weight, model->bias, model->weight_grad, model->bias_grad,
                    data->states, data->actions, data->next_states, data->rewards};
-    return hip_check(launch_train_grads(t, w, batch_idx, batch, loss_out, static_cast<float*>(workspace),
-                                        reinterpret_cast<hipStream_t>(stream)), "train_grads");
+    const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (int rc = hip_check(hipMemsetAsync(workspace, 0, train_counter_bytes(t, batch), st), "train_grads counters"))
+        return rc;
+    return hip_check(launch_train_grads(t, w, batch_idx, batch, loss_out, static_cast<float*>(workspace), st),
+                     "train_grads");
 }
 
 int mbrl_train_epoch(const mbrl_train_model* model, const mbrl_train_data* data, const int64_t* order, int64_t rows,
@@ -1768,6 +1839,9 @@ int mbrl_train_epoch(const mbrl_train_model* model, const mbrl_train_data* data,
                    data->states, data->actions, data->next_states, data->rewards};
     const int arith = g_opt[MBRL_OPT_ADAM_ARITH].load(std::memory_order_relaxed);
     const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    // the tickets and band counters start the epoch at zero whatever the workspace held
+    if (int rc = hip_check(hipMemsetAsync(workspace, 0, train_counter_bytes(t, bs), st), "train_epoch counters"))
+        return rc;
     std::vector<mbrl_adam_tensor> table(tensors, tensors + count);
     const int64_t batches = (rows + batch_size - 1) / batch_size;
     // the Adam step rides in the backward launches when the table is the model's layers in order
@@ -1998,6 +2072,8 @@ struct Rccl {
     ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int);
     ncclResult_t (*comm_destroy)(ncclComm_t);
     ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t);
+    ncclResult_t (*group_start)();
+    ncclResult_t (*group_end)();
     std::string error;   // why the library could not be loaded ("" when it was)
 };
 
@@ -2022,6 +2098,8 @@ static const Rccl& rccl() {
         r.comm_init_rank = reinterpret_cast<decltype(r.comm_init_rank)>(sym("ncclCommInitRank"));
         r.comm_destroy = reinterpret_cast<decltype(r.comm_destroy)>(sym("ncclCommDestroy"));
         r.all_gather = reinterpret_cast<decltype(r.all_gather)>(sym("ncclAllGather"));
+        r.group_start = reinterpret_cast<decltype(r.group_start)>(sym("ncclGroupStart"));
+        r.group_end = reinterpret_cast<decltype(r.group_end)>(sym("ncclGroupEnd"));
     });
     return r;
 }
@@ -2064,9 +2142,26 @@ int mbrl_comm_destroy(mbrl_comm_t comm) {
     return nccl_check(rccl().comm_destroy(reinterpret_cast<ncclComm_t>(comm)), "ncclCommDestroy");
 }
 
+// MBRL_OPT_SHARD_EMULATE 2 (timing): the all-gather's rank-major buffer in one launch -- this rank's
+// slot from its own costs, every other slot from the costs a mode-1 plan kept for this iteration --
+// and the gathered status words (this rank's own, the others clear).
+__global__ void emu_gather_kernel(const float* __restrict__ local, const float* __restrict__ kept, int G, int rank,
+                                  size_t slot, const unsigned* __restrict__ own_status, float* __restrict__ gathered,
+                                  unsigned* __restrict__ peer) {
+    const size_t total = (size_t)G * slot, lo = (size_t)rank * slot;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x)
+        gathered[i] = (i >= lo && i < lo + slot) ? local[i - lo] : kept[i];
+    if (blockIdx.x == 0)
+        for (int r = threadIdx.x; r < G; r += blockDim.x) peer[r] = r == rank ? *own_status : 0u;
+}
+
 struct ShardWs {
     float *local, *gathered, *costs, *actions, *mu[2], *sigma[2], *aelite, *states, *s0;
-    float* emu_actions;   // MBRL_OPT_SHARD_EMULATE: the other ranks' proposals, one shard at a time
+    float* emu_actions;   // MBRL_OPT_SHARD_EMULATE 1: the other ranks' proposals, one shard at a time (taken
+                          // in mode 2 as well, so both modes place emu_kept alike)
+    float* emu_kept;      // MBRL_OPT_SHARD_EMULATE: [I][G][E][Nl] every iteration's gathered costs (mode 1
+                          // writes them, mode 2 reads the other ranks' slots back)
+    unsigned* peer;       // [G] the ranks' status words, gathered with the last iteration's costs
     void* pair;
     unsigned long long* xchg;
     unsigned* status;
@@ -2076,7 +2171,7 @@ struct ShardWs {
     size_t bytes;
 };
 
-static bool shard_emulated() { return g_opt[MBRL_OPT_SHARD_EMULATE].load(std::memory_order_relaxed) == 1; }
+static int shard_emulation() { return g_opt[MBRL_OPT_SHARD_EMULATE].load(std::memory_order_relaxed); }
 
 static ShardWs shard_ws(const Geometry& g, const mbrl_cem_params* p, int G, void* base) {
     ShardWs w{};
@@ -2100,7 +2195,10 @@ static ShardWs shard_ws(const Geometry& g, const mbrl_cem_params* p, int G, void
     w.keys = (uint32_t*)take((size_t)p->N * 4);
     w.s0 = (float*)take((size_t)g.s * 4);
     w.pair = take(pair_area_bytes(g, Nl));
-    w.emu_actions = (float*)take(shard_emulated() && G > 1 ? (size_t)p->H * Nl * g.a * 4 : 0);
+    w.peer = (unsigned*)take((size_t)G * 4);
+    const int emu = shard_emulation();
+    w.emu_actions = (float*)take(emu != 0 && G > 1 ? (size_t)p->H * Nl * g.a * 4 : 0);
+    w.emu_kept = (float*)take(emu != 0 && G > 1 ? (size_t)p->iterations * g.E * p->N * 4 : 0);
     w.bytes = o;
     return w;
 }
@@ -2124,9 +2222,11 @@ static int plan_sharded_body(const mbrl_mlp_shape* shape, const void* packed, co
     Geometry g;
     int rc = shape_geometry(shape, &g);
     if (rc) return rc;
-    // comm == NULL with MBRL_OPT_SHARD_EMULATE (tests): this call computes every other rank's shard
-    // itself and writes the rank-major buffer the all-gather would have delivered
-    const bool emulate = comm == nullptr && shard_emulated();
+    // comm == NULL with MBRL_OPT_SHARD_EMULATE (tests, timing): this call fills the rank-major buffer the
+    // all-gather would have delivered itself (mode 1: every other rank's shard rolled out here; mode 2:
+    // the other ranks' costs a mode-1 plan kept)
+    const int emu_mode = comm == nullptr ? shard_emulation() : 0;
+    const bool emulate = emu_mode != 0;
     if (!p || (!comm && !emulate)) return fail(MBRL_EINVAL, "plan_sharded: NULL params or comm");
     if (p->N < 1 || p->H < 1 || p->K < 1 || p->K > p->N || p->iterations < 1)
         return fail(MBRL_EINVAL, "bad CEM params N=%d H=%d K=%d I=%d", p->N, p->H, p->K, p->iterations);
@@ -2136,19 +2236,26 @@ static int plan_sharded_body(const mbrl_mlp_shape* shape, const void* packed, co
         return fail(MBRL_EINVAL, "plan_sharded: packed/s0/actions_out/states_out/workspace NULL");
     const ShardWs w = shard_ws(g, p, nranks, workspace);
     if (ws_bytes < w.bytes) return fail(MBRL_EWORKSPACE, "workspace %zu < %zu", ws_bytes, w.bytes);
+    if (emulate && nranks > 1 && !w.emu_kept)
+        return fail(MBRL_EINVAL, "plan_sharded: the workspace was sized without MBRL_OPT_SHARD_EMULATE");
     if ((rc = pair_forced_check(g, p->N / nranks))) return rc;
     if ((rc = rollout_validate(g, norm, cost))) return rc;
     if (!emulate && (rc = rccl_ready())) return rc;
     const int N = p->N, Nl = N / nranks, H = p->H, a = g.a, E = g.E;
     const int off = rank * Nl;   // this rank's global candidates [off, off + Nl)
+    const size_t slot = (size_t)E * Nl;   // one rank's floats in the gathered buffer
     const bool fuse = update_kpt(N, p->K, a) != 0 && g_opt[MBRL_OPT_UNFUSED_UPDATE].load(std::memory_order_relaxed) == 0;
     const bool fuse_draw = fuse && update_samples(Nl, a);
+    // injected failure (tests): iteration fail_it on rank fail_rank (the calling rank unless one is named)
+    const int fail_it = g_opt[MBRL_OPT_DEBUG_SHARD_FAIL].load(std::memory_order_relaxed) - 1;
+    const int fail_opt = g_opt[MBRL_OPT_DEBUG_SHARD_FAIL_RANK].load(std::memory_order_relaxed);
+    const int fail_rank = fail_opt == 0 ? rank : fail_opt - 1;
     // From here on the ranks must issue the same collectives: a launch that fails on this rank does not
     // end the call. Its remaining compute launches are skipped, but it still joins every remaining
-    // all-gather -- with its local costs poisoned to NaN (all bits set), so its peers neither wait on it
-    // nor take its shard's candidates as elites -- and the first error is returned at the end. (An
-    // abort of the communicator would not help: ncclCommAbort acts on the calling rank only, and peers
-    // already inside an all-gather would wait on it.)
+    // all-gather -- with its local costs poisoned to NaN (all bits set) and its status word set, which
+    // the last iteration's all-gather hands to every peer -- and the first error is returned at the
+    // end. (An abort of the communicator would not help: ncclCommAbort acts on the calling rank only,
+    // and peers already inside an all-gather would wait on it.)
     int err = MBRL_OK;
     std::string err_msg;
     auto step = [&](int r) {
@@ -2158,9 +2265,11 @@ static int plan_sharded_body(const mbrl_mlp_shape* shape, const void* packed, co
         }
         return err == MBRL_OK;
     };
+    unsigned* own_status = w.status + 1;   // [0] is the trajectory kernel's; zeroed with it below
     // one first launch: distribution rows, the workspace copy of s0, iteration 0's proposals of this
-    // shard (global candidates [off, off + Nl)), the hand-off words zeroed (mbrl_cem_plan)
+    // shard (global candidates [off, off + Nl)), the hand-off words and this rank's status zeroed
     const InitZero z = plan_zero(g, Nl, w.pair, w.xchg, w.xchg_bytes, w.status);
+    if (!z.ptr[1]) step(hip_check(hipMemsetAsync(own_status, 0, sizeof(unsigned), stream), "status memset"));
     hipLaunchKernelGGL(cem_init_kernel, dim3(H * (fuse_draw ? draw_slices(H, 1, Nl, a) : 1), 1), dim3(1024), 0, stream,
                        p->seed, p->init_mu, p->init_sigma, p->lo, p->hi, H, a, Nl, w.mu[0], w.sigma[0],
                        fuse_draw ? w.actions : nullptr, s0_in, g.s, w.s0, off, z);
@@ -2170,9 +2279,11 @@ static int plan_sharded_body(const mbrl_mlp_shape* shape, const void* packed, co
         sp0.seed = p->seed; sp0.iteration = 0; sp0.mu = w.mu[0]; sp0.sigma = w.sigma[0]; sp0.lo = p->lo; sp0.hi = p->hi;
         step(sample_impl(&sp0, H, a, Nl, off, w.actions, stream));
     }
+    bool poisoned = false;   // this rank's local costs and status word carry its failure
     unsigned pair_epoch = 0;
     int cur = 0;
     for (int it = 0; it < p->iterations; ++it) {
+        const bool last = it + 1 == p->iterations;
         mbrl_sampler sp{};
         sp.seed = p->seed; sp.iteration = it; sp.mu = w.mu[cur]; sp.sigma = w.sigma[cur]; sp.lo = p->lo; sp.hi = p->hi;
         if (err == MBRL_OK && rollout_events && rollout_events[2 * it])
@@ -2180,34 +2291,67 @@ static int plan_sharded_body(const mbrl_mlp_shape* shape, const void* packed, co
         if (err == MBRL_OK)
             step(rollout_impl(g, packed, norm, cost, w.s0, 0, w.actions, nullptr, Nl, H, 0, w.local, nullptr, nullptr,
                               stream, pair_area_bytes(g, Nl) ? w.pair : nullptr, z.ptr[0] ? &pair_epoch : nullptr));
-        if (err == MBRL_OK && g_opt[MBRL_OPT_DEBUG_SHARD_FAIL].load(std::memory_order_relaxed) == it + 1)
+        if (err == MBRL_OK && it == fail_it && fail_rank == rank)
             step(fail(MBRL_EHIP, "plan_sharded: injected launch failure at iteration %d (MBRL_OPT_DEBUG_SHARD_FAIL)", it));
         if (err == MBRL_OK && rollout_events && rollout_events[2 * it + 1])
             step(hip_check(hipEventRecord(reinterpret_cast<hipEvent_t>(rollout_events[2 * it + 1]), stream), "event"));
-        // the one collective of an iteration: every rank's [E][Nl] costs, rank-major
+        if (err != MBRL_OK && !poisoned) {
+            // NaN costs sort last on every rank (MBRL_NAN_LAST); the status word tells the peers. If even
+            // these fail the rank still joins the collectives (and returns its first error).
+            poisoned = true;
+            const int m1 = hip_check(hipMemsetAsync(w.local, 0xFF, slot * 4, stream), "poison memset");
+            const int m2 = hip_check(hipMemsetAsync(own_status, 0x01, sizeof(unsigned), stream), "status memset");
+            if (m1 || m2) err_msg += std::string("; then ") + g_err;
+        }
+        // the one collective of an iteration: every rank's [E][Nl] costs, rank-major; the last one also
+        // gathers the ranks' status words (grouped: one RCCL launch)
         if (!emulate) {
-            if (err != MBRL_OK)   // NaN costs sort last on every rank (MBRL_NAN_LAST)
-                (void)hipMemsetAsync(w.local, 0xFF, (size_t)E * Nl * 4, stream);
-            step(nccl_check(rccl().all_gather(w.local, w.gathered, (size_t)E * Nl, ncclFloat,
-                                              reinterpret_cast<ncclComm_t>(comm), stream), "ncclAllGather"));
+            const Rccl& R = rccl();
+            ncclComm_t c = reinterpret_cast<ncclComm_t>(comm);
+            if (last) step(nccl_check(R.group_start(), "ncclGroupStart"));
+            step(nccl_check(R.all_gather(w.local, w.gathered, slot, ncclFloat, c, stream), "ncclAllGather"));
+            if (last) {
+                step(nccl_check(R.all_gather(own_status, w.peer, 1, ncclUint32, c, stream), "ncclAllGather status"));
+                step(nccl_check(R.group_end(), "ncclGroupEnd"));
+            }
+        } else if (err == MBRL_OK && nranks == 1) {
+            step(hip_check(hipMemcpyAsync(w.gathered, w.local, slot * 4, hipMemcpyDeviceToDevice, stream), "gather"));
+            if (last) step(hip_check(hipMemcpyAsync(w.peer, own_status, 4, hipMemcpyDeviceToDevice, stream), "status"));
+        } else if (err == MBRL_OK && emu_mode == 2) {
+            float* kept = w.emu_kept + (size_t)it * nranks * slot;
+            hipLaunchKernelGGL(emu_gather_kernel, dim3(256), dim3(256), 0, stream, w.local, kept, nranks, rank, slot,
+                               own_status, w.gathered, w.peer);
+            step(hip_check(hipGetLastError(), "emulated gather"));
         } else if (err == MBRL_OK) {
             // rank r's slot: its proposals of this iteration (drawn at its global offset from this
             // iteration's mu / sigma, as its own previous update or initial draw made them) rolled out
             for (int r = 0; r < nranks && err == MBRL_OK; ++r) {
-                float* slot = w.gathered + (size_t)r * E * Nl;
+                float* sl = w.gathered + (size_t)r * slot;
                 if (r == rank) {
-                    step(hip_check(hipMemcpyAsync(slot, w.local, (size_t)E * Nl * 4, hipMemcpyDeviceToDevice, stream),
+                    step(hip_check(hipMemcpyAsync(sl, w.local, slot * 4, hipMemcpyDeviceToDevice, stream),
                                    "emulated gather"));
+                } else if (fail_rank == r && fail_it >= 0 && it >= fail_it) {   // an emulated peer's failure
+                    step(hip_check(hipMemsetAsync(sl, 0xFF, slot * 4, stream), "emulated peer poison"));
                 } else if (step(sample_impl(&sp, H, a, Nl, r * Nl, w.emu_actions, stream))) {
-                    step(rollout_impl(g, packed, norm, cost, w.s0, 0, w.emu_actions, nullptr, Nl, H, 0, slot, nullptr,
+                    step(rollout_impl(g, packed, norm, cost, w.s0, 0, w.emu_actions, nullptr, Nl, H, 0, sl, nullptr,
                                       nullptr, stream, pair_area_bytes(g, Nl) ? w.pair : nullptr,
                                       z.ptr[0] ? &pair_epoch : nullptr));
                 }
             }
+            if (last && err == MBRL_OK) {
+                step(hip_check(hipMemsetAsync(w.peer, 0, (size_t)nranks * 4, stream), "emulated status"));
+                if (fail_rank != rank && fail_rank < nranks && fail_it >= 0)
+                    step(hip_check(hipMemsetAsync(w.peer + fail_rank, 0x01, 4, stream), "emulated peer status"));
+                step(hip_check(hipMemcpyAsync(w.peer + rank, own_status, 4, hipMemcpyDeviceToDevice, stream),
+                               "emulated status"));
+            }
+            if (err == MBRL_OK)   // kept for mode 2
+                step(hip_check(hipMemcpyAsync(w.emu_kept + (size_t)it * nranks * slot, w.gathered, nranks * slot * 4,
+                                              hipMemcpyDeviceToDevice, stream), "emulated keep"));
         }
         if (err != MBRL_OK) continue;   // only the all-gathers remain for this rank
         float* costs = w.gathered;
-        if (E > 1) {   // (one rank: the identity)
+        if (E > 1 && nranks > 1) {   // (one rank: the identity)
             hipLaunchKernelGGL(shard_costs_kernel, dim3(256), dim3(256), 0, stream, w.gathered, nranks, E, Nl, w.costs);
             costs = w.costs;
         }
@@ -2216,7 +2360,6 @@ static int plan_sharded_body(const mbrl_mlp_shape* shape, const void* packed, co
                                           hipMemcpyDeviceToDevice, stream), "cost record"));
         int64_t* elites = elite_hist ? elite_hist + (size_t)it * p->K : w.elites;
         float* rets = returns_hist ? returns_hist + (size_t)it * N : nullptr;
-        const bool last = it + 1 == p->iterations;
         if (err != MBRL_OK) continue;
         if (fuse) {
             UpdateArgs U{};
@@ -2252,7 +2395,31 @@ static int plan_sharded_body(const mbrl_mlp_shape* shape, const void* packed, co
         hipLaunchKernelGGL(member_mean_kernel, dim3((Hs + 255) / 256), dim3(256), 0, stream, w.states, E, Hs,
                            states_out);
     }
-    return hip_check(hipGetLastError(), "sharded plan launch");
+    if ((rc = hip_check(hipGetLastError(), "sharded plan launch"))) return rc;
+    if (nranks == 1) return MBRL_OK;   // no peers: enqueue only, as mbrl_cem_plan
+    // the peers' status words (gathered with the last iteration's costs): one copy behind the plan's
+    // last launch and one stream synchronisation
+    static thread_local unsigned* peer_host = nullptr;
+    static thread_local int peer_cap = 0;
+    if (peer_cap < nranks) {
+        if (peer_host) (void)hipHostFree(peer_host);
+        peer_host = nullptr;
+        peer_cap = 0;
+        if ((rc = hip_check(hipHostMalloc(reinterpret_cast<void**>(&peer_host), (size_t)nranks * 4), "hipHostMalloc")))
+            return rc;
+        peer_cap = nranks;
+    }
+    if ((rc = hip_check(hipMemcpyAsync(peer_host, w.peer, (size_t)nranks * 4, hipMemcpyDeviceToHost, stream),
+                        "peer status copy")))
+        return rc;
+    if ((rc = hip_check(hipStreamSynchronize(stream), "plan synchronise"))) return rc;
+    std::string failed;
+    for (int r = 0; r < nranks; ++r)
+        if (peer_host[r] && r != rank) failed += (failed.empty() ? "" : ", ") + std::to_string(r);
+    if (!failed.empty())
+        return fail(MBRL_EPEER, "plan_sharded: rank(s) %s failed during this plan (each returns its own error); "
+                                "this rank's outputs are void", failed.c_str());
+    return MBRL_OK;
 }
 
 int mbrl_cem_plan_sharded(const mbrl_mlp_shape* shape, const void* packed, const mbrl_norm* norm,

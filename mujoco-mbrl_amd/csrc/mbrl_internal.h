@@ -415,6 +415,7 @@ struct TrainTensors {
 };
 size_t train_ws_floats(const TrainShape& t, int batch);
 size_t train_status_offset(const TrainShape& t, int batch);   // bytes: the fused step's status word
+size_t train_counter_bytes(const TrainShape& t, int batch);   // the tickets and band counters (offset 0)
 // adam (optional): the step of every layer's weight and bias (linear1.weight, linear1.bias, ...)
 // folded into the backward launches, bit-identical to a separate mbrl_adam_step after the gradient.
 // With the layer-0 fold one layer's step cannot ride in this step's launches: it comes back in

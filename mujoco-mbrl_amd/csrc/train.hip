@@ -1752,9 +1752,11 @@ static TrainWs train_ws(const TrainShape& t, int batch, float* base) {
     // (the short last one lays out its data areas for its own size) finds the tickets, the sticky
     // status word and the band counters where the others left them, zero between launches; the band
     // counters sized for the fused step's largest batch (FUSED_MAX_BANDS)
+    // (tickets and band counters first: every training call zeroes them in one memset on entry, see
+    // train_counter_bytes; the status word and the serial behind them keep their values)
     w.tickets = reinterpret_cast<unsigned*>(take(3 * ((W + TT - 1) / TT)));
-    w.status = reinterpret_cast<unsigned*>(take(1));
     w.bands = reinterpret_cast<unsigned*>(take(32 * FUSED_MAX_BANDS));
+    w.status = reinterpret_cast<unsigned*>(take(1));
     w.serial = reinterpret_cast<unsigned*>(take(1));
     for (int l = 0; l < t.L; ++l) w.act[l] = take(R * W);
     w.dh[0] = take(R * W);
@@ -1776,6 +1778,15 @@ static TrainWs train_ws(const TrainShape& t, int batch, float* base) {
 }
 
 size_t train_ws_floats(const TrainShape& t, int batch) { return train_ws(t, batch, nullptr).floats; }
+
+// Bytes at the start of the workspace holding the fused step's arrival tickets and band counters. Their
+// protocol leaves them zero between launches, but a workspace that was never zeroed, or a step whose
+// bounded wait timed out, would leave counts behind: mbrl_train_grads / mbrl_train_epoch clear them
+// once per call. The sticky status word and the fold's serial lie behind them and are kept.
+size_t train_counter_bytes(const TrainShape& t, int batch) {
+    float* base = reinterpret_cast<float*>(static_cast<uintptr_t>(64));
+    return (size_t)(reinterpret_cast<char*>(train_ws(t, batch, base).status) - reinterpret_cast<char*>(base));
+}
 
 size_t train_status_offset(const TrainShape& t, int batch) {
     float* base = reinterpret_cast<float*>(static_cast<uintptr_t>(64));   // any aligned base: offsets only

@@ -24,9 +24,10 @@ MBRL_EINVAL = -1
 MBRL_EUNSUPPORTED = -2
 MBRL_EHIP = -3
 MBRL_EWORKSPACE = -4
+MBRL_EPEER = -5          # mbrl_cem_plan_sharded: another rank failed during the plan (ABI v13)
 MBRL_COST_GOAL_STATE = 0
 MBRL_COST_MODEL_REWARD = 1
-ABI_VERSION = 12
+ABI_VERSION = 13
 MBRL_NAN_LAST = 0
 MBRL_NAN_FIRST = 1
 MBRL_PRECISION_F32 = 0
@@ -38,7 +39,8 @@ OPTIONS = {"rollout_tile": 0, "split_tile": 1, "debug_traj_abort": 2, "gd_single
            "unfused_update": 5, "adam_arith": 6, "xcd_map": 7, "train_tile": 8, "train_no_fold": 9,
            "rollout_pair": 10, "shard_emulate": 11, "debug_pair_abort": 12,
            "traj_hop": 13, "gd_hop": 14, "pair_l2": 15,
-           "train_xcd": 16, "train_split": 17, "debug_shard_fail": 18, "train_fo": 19}
+           "train_xcd": 16, "train_split": 17, "debug_shard_fail": 18, "train_fo": 19,
+           "debug_shard_fail_rank": 20}
 
 
 def precision_code(name):
@@ -206,6 +208,8 @@ def source_digest():
     pkg = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     files = sorted(glob.glob(os.path.join(pkg, "csrc", "*.hip")) + glob.glob(os.path.join(pkg, "csrc", "*.h")),
                    key=lambda f: os.path.relpath(f, pkg))
+    if not any(f.endswith(".hip") for f in files):
+        return None
     files.append(os.path.join(os.path.dirname(pkg), "include", "mbrl_cem.h"))
     if not all(os.path.exists(f) for f in files):
         return None
@@ -217,10 +221,12 @@ def source_digest():
 
 
 def build_info():
-    """(the loaded library's source digest, whether it equals the tree's)."""
+    """(the loaded library's source digest, whether it equals the tree's: None when the tree has no
+    sources to compare with, e.g. an installed or prebuilt library)."""
     info = load().mbrl_build_info().decode()
     built = dict(kv.split("=", 1) for kv in info.split())["src"]
-    return built, built == source_digest()
+    tree = source_digest()
+    return built, (None if tree is None else built == tree)
 
 
 def check(rc, what):

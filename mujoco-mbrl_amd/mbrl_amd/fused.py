@@ -232,6 +232,12 @@ def _value_stamp(v, out):
         out.append(v)
     elif isinstance(v, torch.Tensor):
         out.append((id(v), v.data_ptr(), v._version))
+    elif isinstance(v, np.ndarray):       # mutable in place with no version: stamped by content
+        out.append((id(v), v.dtype.str, v.shape, v.tobytes()))
+    elif t is list or t is tuple:         # (goal / weights / statistics given as Python sequences)
+        out.append((id(v), len(v)))
+        for x in v:
+            _value_stamp(x, out)
     else:
         out.append(id(v))
 

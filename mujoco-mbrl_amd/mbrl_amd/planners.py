@@ -365,8 +365,9 @@ class CEMPlanner(ModelPlanner):
                     if res.pop("_host", False):
                         return res
                 else:
-                    res = _cem_fused_sharded(prob, initial_state.to(device=dev, dtype=torch.float32).contiguous(),
-                                             st, ws)
+                    res = _cem_fused_sharded(prob, initial_state, st, ws)
+                    if res.pop("_host", False):
+                        return res
             else:
                 a = st["adim"]
                 if a is None:
@@ -729,41 +730,71 @@ def _cem_sharded_native(prob, s0, st, world, rank, comm=_OWN_COMM):
     """mbrl_cem_plan_sharded: this rank's shard of the plan, every iteration's all-gather included, in
     one C-ABI call on the current stream (the result is the single-GPU plan's, on every rank).
     comm: the library's RCCL communicator for the default group (default), or None under
-    _lib.option("shard_emulate", 1), where the call computes every rank's shard itself (tests)."""
+    _lib.option("shard_emulate", 1 or 2), where the call fills every rank's slot itself (tests, timing).
+    s0 on the host with neither records nor device outputs asked for: the plan reads s0 from and writes
+    its outputs to mapped host staging (as _cem_plan_host); the call returns after the plan completed
+    (it synchronises once for the peers' status words when world > 1), so no copy launch follows it.
+    A failure on any rank raises RuntimeError on every rank (MBRL_EPEER on the healthy ones); the
+    communicator stays usable."""
     lib = _lib.load()
     dev = prob.device
     md = prob.mdesc
     N, K, H, I = st["N"], st["K"], st["H"], st["I"]
     a, s, E = md["a"], md["s"], md["E"]
-    params = _lib.CemParams(N, H, K, I, st["alpha"], st["lo"], st["hi"], 0.0, st["init_std"], 0,
-                            int(st["seed"]) & 0xFFFFFFFFFFFFFFFF)
-    need = lib.mbrl_cem_plan_sharded_workspace_bytes(fused.ctypes_ref(prob.shape), fused.ctypes_ref(params), world)
-    if need == 0:
-        raise ValueError(f"num_candidates {N} must divide evenly over {world} ranks")
+    pkey = ("sharded", world, N, H, K, I, st["alpha"], st["lo"], st["hi"], st["init_std"],
+            int(st["seed"]) & 0xFFFFFFFFFFFFFFFF, lib.mbrl_get_option(_lib.OPTIONS["shard_emulate"]))
+    hit = prob.plan_cache.get(pkey)
+    if hit is None:
+        params = _lib.CemParams(N, H, K, I, st["alpha"], st["lo"], st["hi"], 0.0, st["init_std"], 0, pkey[10])
+        need = lib.mbrl_cem_plan_sharded_workspace_bytes(fused.ctypes_ref(prob.shape), fused.ctypes_ref(params), world)
+        if need == 0:
+            raise ValueError(f"num_candidates {N} must divide evenly over {world} ranks")
+        if len(prob.plan_cache) > 64:
+            prob.plan_cache.clear()
+        hit = prob.plan_cache[pkey] = (params, fused.ctypes_ref(params), need)
+    params, pref, need = hit
     ws = _workspace(("cem_sharded", str(dev)), need, dev)
     if comm is _OWN_COMM:
         comm = _rccl_comm(dev, world, rank)
-    buf = torch.empty(H * (s + 3 * a), dtype=torch.float32, device=dev)
-    both = buf[:H * (s + a)]
-    states, actions = both[:H * s].view(H, s), both[H * s:].view(H, a)
-    mu, sigma = buf[H * (s + a):H * (s + 2 * a)].view(H, a), buf[H * (s + 2 * a):].view(H, a)
     rec = st["record"]
+    staged = HOST_STAGING and not st["keep"] and not rec and not s0.is_cuda
+    if staged:
+        stage = _staging(dev, H * (s + 3 * a) + s)
+        arr = stage.array
+        o_s0 = H * (s + 3 * a)
+        x = s0.detach() if s0.requires_grad else s0
+        arr[o_s0:o_s0 + s] = x.numpy().reshape(-1) if x.dtype == torch.float32 else x.reshape(-1).to(torch.float32).numpy()
+        o_act, o_mu, o_sg = H * s, H * (s + a), H * (s + 2 * a)
+        at = stage.cached_at((H, s, a), (o_s0, o_mu, o_sg, o_act, 0))
+        p_s0, p_mu, p_sg, p_act, p_st = at
+    else:
+        s0 = s0.to(device=dev, dtype=torch.float32).contiguous()
+        buf = torch.empty(H * (s + 3 * a), dtype=torch.float32, device=dev)
+        both = buf[:H * (s + a)]
+        states, actions = both[:H * s].view(H, s), both[H * s:].view(H, a)
+        mu, sigma = buf[H * (s + a):H * (s + 2 * a)].view(H, a), buf[H * (s + 2 * a):].view(H, a)
+        p_s0, p_mu, p_sg, p_act, p_st = _lib.ptr(s0), _lib.ptr(mu), _lib.ptr(sigma), _lib.ptr(actions), _lib.ptr(states)
     cost_hist = torch.empty((I, E, N), dtype=torch.float32, device=dev) if rec else None
     ret_hist = torch.empty((I, N), dtype=torch.float32, device=dev) if rec else None
     elite_hist = torch.empty((I, K), dtype=torch.int64, device=dev) if rec else None
     pev = st.get("plan_events")
     if pev is not None:
         pev[0].record()
-    rc = lib.mbrl_cem_plan_sharded(fused.ctypes_ref(prob.shape), _lib.ptr(prob.packed), fused.ctypes_ref(prob.norm),
-                                   fused.ctypes_ref(prob.cost), _lib.ptr(s0), fused.ctypes_ref(params), comm, world, rank,
-                                   _lib.ptr(mu), _lib.ptr(sigma), _lib.ptr(actions), _lib.ptr(states),
+    rc = lib.mbrl_cem_plan_sharded(*prob.refs, p_s0, pref, comm, world, rank, p_mu, p_sg, p_act, p_st,
                                    _lib.ptr(cost_hist), _lib.ptr(ret_hist), _lib.ptr(elite_hist), _events(st, I),
                                    _lib.ptr(ws), ws.numel(), _lib.stream_handle(dev))
     if pev is not None and rc == _lib.MBRL_OK:
         pev[1].record()
-    # a failure after the argument checks still joined every all-gather of the plan (include/mbrl_cem.h),
-    # so the communicator stays in step with the other ranks and is kept
+    # a failure after the argument checks still joined every all-gather of the plan, and every rank
+    # learns of it (include/mbrl_cem.h): the communicator stays in step with the other ranks and is kept
     _lib.check(rc, "mbrl_cem_plan_sharded")
+    if staged:
+        if world == 1:     # (with peers the call has synchronised already)
+            torch.cuda.current_stream(dev).synchronize()
+        x = arr[:o_s0].copy()
+        return dict(states=torch.from_numpy(x[:o_act].reshape(H, s)), actions=torch.from_numpy(x[o_act:o_mu].reshape(H, a)),
+                    mu=torch.from_numpy(x[o_mu:o_sg].reshape(H, a)), sigma=torch.from_numpy(x[o_sg:].reshape(H, a)),
+                    _host=True)
     out = dict(states=states, actions=actions, mu=mu, sigma=sigma, _both=both)
     if rec:
         out.update(costs=cost_hist, returns=ret_hist, elites=elite_hist)
@@ -775,7 +806,8 @@ def _cem_fused_sharded(prob, s0, st, world):
     if SHARDED_NATIVE and dist.get_backend() == "nccl" and _rccl_comm(prob.device, world, dist.get_rank()):
         return _cem_sharded_native(prob, s0, st, world, dist.get_rank())
     st = dict(st, E=prob.mdesc["E"], a=prob.mdesc["a"])
-    return cem_sharded_protocol(_FusedShardOps(prob, s0, st), st, world, dist.get_rank())
+    return cem_sharded_protocol(_FusedShardOps(prob, s0.to(device=prob.device, dtype=torch.float32).contiguous(), st),
+                                st, world, dist.get_rank())
 
 
 def _cem_generic(model, cost, s0, st, a, dev):

@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     assert decl == sorted(_lib.EXPORTED)
     for name in decl:
         assert hasattr(lib, name), name
-    assert lib.mbrl_abi_version() == _lib.ABI_VERSION == 12
+    assert lib.mbrl_abi_version() == _lib.ABI_VERSION == 13
 
 
 def test_no_gpu_needed_for_sizing_calls():
@@ -203,3 +203,20 @@ def test_library_was_built_from_this_tree():
     from mbrl_amd import _lib
     built, same = _lib.build_info()
     assert same, f"libmbrl_cem.so was built from sources {built}, the tree holds {_lib.source_digest()}: rebuild"
+
+
+def test_shard_options_and_peer_status_code():
+    """ABI v13: MBRL_OPT_SHARD_EMULATE takes 0 / 1 / 2 (2: the per-rank timing mode) and
+    MBRL_OPT_DEBUG_SHARD_FAIL_RANK names the failing rank; MBRL_EPEER is -5 in the header and here."""
+    from mbrl_amd import _lib
+    lib = _lib.load()
+    code = _lib.OPTIONS["shard_emulate"]
+    for v in (1, 2):
+        with _lib.option("shard_emulate", v):
+            assert lib.mbrl_get_option(code) == v
+    assert lib.mbrl_set_option(code, 3) < 0 and lib.mbrl_get_option(code) == 0
+    with _lib.option("debug_shard_fail_rank", 4):
+        assert lib.mbrl_get_option(_lib.OPTIONS["debug_shard_fail_rank"]) == 4
+    hdr = open(os.path.join(REPO, "include", "mbrl_cem.h")).read()
+    assert "MBRL_EPEER = -5" in hdr and _lib.MBRL_EPEER == -5
+    assert "MBRL_OPT_DEBUG_SHARD_FAIL_RANK = 20" in hdr and "MBRL_OPT_COUNT = 21" in hdr

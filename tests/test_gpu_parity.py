@@ -161,6 +161,26 @@ def test_select_matches_stable_argsort_with_ties_nan_and_signed_zero():
         assert int(am[0]) == ocem.rs_argmin(r), N
 
 
+@pytest.mark.parametrize("N", [1024, 4096, 16384, 32768])
+def test_select_fuzz_distributions(N):
+    """The register-resident selection (wide 11-bit first pass, the bucket's keys listed in LDS, 8-bit
+    passes over the list or over every key when the bucket is too large, one packed compaction scan)
+    against NumPy's stable order on distributions that exercise each branch: plan-like returns in one
+    binade, a narrow cluster (the K-th bucket large), heavy ties, NaN- and signed-zero-heavy sets, a
+    wide spread over binades, all-equal keys; K from 1 to N."""
+    from mbrl_amd import fused
+    rng = np.random.default_rng(N)
+    dists = [lambda: rng.uniform(130, 250, N), lambda: rng.uniform(120, 120.01, N),
+             lambda: rng.integers(0, 7, N), lambda: np.where(rng.random(N) < .4, np.nan, rng.standard_normal(N)),
+             lambda: np.where(rng.random(N) < .5, -0.0, 0.0), lambda: np.exp(rng.uniform(-30, 30, N)),
+             lambda: np.full(N, 3.5)]
+    for i, d in enumerate(dists):
+        r = np.asarray(d(), dtype=np.float32)
+        for K in (1, max(1, N // 10), N // 2 + 1, N):
+            el = fused.select(torch.from_numpy(r).to(DEV).view(1, N), K)
+            assert np.array_equal(el.cpu().numpy(), ocem.select_elites(r, K)), (N, i, K)
+
+
 def test_select_ensemble_mean():
     from mbrl_amd import fused
     rng = np.random.default_rng(1)

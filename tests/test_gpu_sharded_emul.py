@@ -118,3 +118,52 @@ def test_sharded_plan_through_the_c_entry_rejects_bad_calls():
     assert lib.mbrl_comm_init(ident, 2, 2, ctypes.byref(comm)) == _lib.MBRL_EINVAL
     assert lib.mbrl_comm_init(None, 2, 0, ctypes.byref(comm)) == _lib.MBRL_EINVAL
     assert lib.mbrl_comm_destroy(None) == _lib.MBRL_OK
+
+
+def _emulated_mode(prob, st, s0, world, rank, mode, **opts):
+    from mbrl_amd import _lib, planners
+    import contextlib
+    with contextlib.ExitStack() as stack:
+        stack.enter_context(_lib.option("shard_emulate", mode))
+        for k, v in opts.items():
+            stack.enter_context(_lib.option(k, v))
+        stack.enter_context(torch.cuda.device(prob.device))
+        res = planners._cem_sharded_native(prob, s0, st, world, rank, comm=None)
+        torch.cuda.synchronize()
+    return {k: res[k].cpu() for k in KEYS}
+
+
+@pytest.mark.parametrize("cid,N,H,world", [(4, 16384, 30, 8), (5, 32768, 50, 8), (3, 4096, 30, 4)],
+                         ids=["c4_G8", "c5_G8", "c3_G4"])
+def test_timing_emulation_runs_one_ranks_work_bit_identically(cid, N, H, world):
+    """MBRL_OPT_SHARD_EMULATE = 2 (the per-rank timing mode, tools/rank_split.py): the other ranks'
+    slots come from the costs a mode-1 plan kept, in one launch per iteration, so the call runs one
+    rank's own work only -- and, kept costs being the same problem's, every output equals the single-GPU
+    plan's bit for bit (the selection still runs over all N with K = N / 10)."""
+    prob, st, s0 = _problem(cid, N, H)
+    ref = _single(prob, st, s0)
+    _assert_same(_emulated_mode(prob, st, s0, world, 0, 1), ref, (cid, world, "mode 1"))
+    for rank in (0, world // 2, world - 1):
+        _assert_same(_emulated_mode(prob, st, s0, world, rank, 2), ref, (cid, world, rank, "mode 2"))
+
+
+@pytest.mark.parametrize("cid,N,H,world", [(4, 16384, 30, 8), (5, 32768, 50, 8), (2, 1024, 20, 4)],
+                         ids=["c4_G8", "c5_G8", "c2_G4"])
+def test_a_failed_peer_is_reported_on_every_rank(cid, N, H, world):
+    """A launch failure on one rank (injected at iteration 1 in an emulated peer's slot: its costs
+    poisoned and its status word set, as the failing rank itself does) makes every other rank id return
+    MBRL_EPEER -- not a plan over N - N/G candidates (planners.py:184 chooses over all N) -- and the
+    failing rank id its own error. The next plan is the single-GPU plan again, bit for bit."""
+    from mbrl_amd import _lib
+    prob, st, s0 = _problem(cid, N, H)
+    ref = _single(prob, st, s0)
+    bad = 1
+    for rank in range(world):
+        with pytest.raises(RuntimeError) as ei:
+            _emulated_mode(prob, st, s0, world, rank, 1, debug_shard_fail=2, debug_shard_fail_rank=bad + 1)
+        msg = str(ei.value)
+        if rank == bad:
+            assert f"({_lib.MBRL_EHIP})" in msg and "injected launch failure at iteration 1" in msg, msg
+        else:
+            assert f"({_lib.MBRL_EPEER})" in msg and f"rank(s) {bad} failed during this plan" in msg, msg
+    _assert_same(_emulated_mode(prob, st, s0, world, 0, 1), ref, (cid, world, "after"))

@@ -1,5 +1,5 @@
 """Diagnostic: phase times of select_reg_kernel from the -DMBRL_STAMPS build (thread 0's
-s_memrealtime, 100 MHz). make -C mujoco-mbrl_amd diag && python tools/select_stamps.py [N]"""
+s_memrealtime, 100 MHz). make -C mujoco-mbrl_amd diag && python tools/select_stamps.py [N [lo hi]]"""
 import ctypes
 import os
 import sys
@@ -21,7 +21,8 @@ def main():
     dev = torch.device("cuda", 0)
     buf = torch.zeros(8, dtype=torch.int64, device=dev)
     assert lib.mbrl_diag_set_cem_stamps(buf.data_ptr()) == 0
-    costs = torch.from_numpy(np.random.default_rng(0).uniform(120, 123, N).astype(np.float32)).to(dev).view(1, N)
+    lo, hi = (float(sys.argv[2]), float(sys.argv[3])) if len(sys.argv) > 3 else (120.0, 123.0)
+    costs = torch.from_numpy(np.random.default_rng(0).uniform(lo, hi, N).astype(np.float32)).to(dev).view(1, N)
     ws = torch.empty(1 << 20, dtype=torch.uint8, device=dev)
     rows = []
     for _ in range(20):
@@ -29,8 +30,8 @@ def main():
         torch.cuda.synchronize()
         rows.append(buf.cpu().numpy().copy())
     st = np.array(rows[5:], dtype=np.float64)
-    d = np.diff(st[:, :7], axis=1).mean(0) / 100.0
-    names = ["load+keys", "pass 24", "pass 16", "pass 8", "pass 0", "compaction"]
+    d = np.diff(st[:, :6], axis=1).mean(0) / 100.0
+    names = ["load+keys+minmax", "wide pass", "list", "8-bit passes", "compaction"]
     print(f"select_reg N={N}: us per phase (thread 0, mean of 15)")
     for n, v in zip(names, d):
         print(f"  {n:12s} {v:7.2f}")
