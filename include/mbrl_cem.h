@@ -192,7 +192,11 @@ enum {
                                        other ranks see it as a peer failure; under MBRL_OPT_SHARD_EMULATE a
                                        call with another rank id fails that rank's emulated slot); 0: the
                                        calling rank's, whatever its id */
-    MBRL_OPT_COUNT = 21
+    MBRL_OPT_UPDATE_SPLIT = 21,     /* (ABI v13) plans' per-iteration update as two launches that share out the
+                                       elites' regeneration (select + regenerate, then refit + draw): 0 auto
+                                       (K ceil(a/4) >= 2048 Philox blocks per row), 1 never, 2 always (A/B,
+                                       tests; same bits) */
+    MBRL_OPT_COUNT = 22
 };
 int mbrl_set_option(int32_t option, int32_t value);
 int mbrl_get_option(int32_t option);

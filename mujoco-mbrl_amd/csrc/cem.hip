@@ -28,11 +28,8 @@ static thread_local std::string g_err;
 
 // mbrl_set_option switches (include/mbrl_cem.h MBRL_OPT_*); 0 = automatic.
 static std::atomic<int> g_opt[MBRL_OPT_COUNT];
-// MBRL_OPT_ROLLOUT_PAIR = 0 (auto) takes column-split pairs for small plans when this is set
-#ifndef MBRL_PAIR_AUTO
-#define MBRL_PAIR_AUTO 1
-#endif
-static constexpr bool kPairAuto = MBRL_PAIR_AUTO;
+// MBRL_OPT_ROLLOUT_PAIR = 0 (auto) takes column-split pairs for small plans (2 = never, the A/B)
+static constexpr bool kPairAuto = true;
 // traj_coop_kernel hand-off mode under MBRL_OPT_TRAJ_HOP = 0 (TrajArgs.hop_mode)
 static constexpr int kTrajHopDefault = 2;
 
@@ -372,7 +369,8 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* l
 __device__ unsigned long long* g_cem_stamps;
 #define CSTAMP(k)                                                                      \
     do {                                                                               \
-        if (threadIdx.x == 0 && g_cem_stamps) g_cem_stamps[k] = __builtin_amdgcn_s_memrealtime(); \
+        if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0 && g_cem_stamps)                \
+            g_cem_stamps[k] = __builtin_amdgcn_s_memrealtime();                                       \
     } while (0)
 #else
 #define CSTAMP(k) \
@@ -466,123 +464,115 @@ __global__ void __launch_bounds__(1024) select_kernel(const float* __restrict__ 
     }
 }
 
-// Register-resident variant for N <= 1024 * KPT: thread t owns candidates [t*KPT, t*KPT + KPT)
-// (contiguous, so the compaction scan yields ascending indices). Returns are computed and stored
-// coalesced (candidate n by thread n % 1024) into LDS keys, then each thread takes its KPT keys from
-// LDS; the LDS key array is reused for the per-wave radix histograms afterwards.
+// Register-resident selection for N <= 1024 * KPT. Wave w owns candidates [64 KPT w, 64 KPT (w + 1)) and
+// every load is coalesced: with 16-byte aligned rows (N and member_stride multiples of 4) lane l holds
+// groups of four, group g at 64 KPT w + 256 g + 4 l (one float4 per lane, a contiguous KB per wave load
+// instruction), else single keys at 64 KPT w + 64 g + l. A thread's keys are therefore not contiguous;
+// the elites' ascending-index positions come from ballots over the lanes (in order) and the waves'
+// totals (one barrier), so no key moves between threads.
+// Passes: one wide pass over the first SEL_WIDE_BITS bits in which the keys differ (one shared
+// histogram), the K-th key's bucket listed in LDS, 8-bit passes over that list (or over every key when
+// the bucket is too large to list), then the compaction.
 constexpr int SEL_HIST_WORDS = 2 * 16 * 257;   // two buffers of per-wave 8-bit digit histograms
 constexpr int SEL_WIDE_BITS = 11, SEL_WIDE_BINS = 1 << SEL_WIDE_BITS;   // the first (wide) pass
 constexpr int SEL_LIST = 2048;                  // keys of the wide pass's bucket kept in LDS
-// LDS words of the register-resident selection: the coalesced key staging of the non-vector load,
-// aliased by the histograms, the wide histogram, the list and its count
-__host__ __device__ constexpr int sel_words(int KPT) {
-    return 33 * 32 * KPT > SEL_HIST_WORDS + SEL_WIDE_BINS + SEL_LIST + 4 ? 33 * 32 * KPT
-                                                                        : SEL_HIST_WORDS + SEL_WIDE_BINS + SEL_LIST + 4;
-}
-// Up to this many keys per thread the returns load as per-thread float4 runs; above it, as coalesced
-// scalar rows transposed through LDS (a thread's float4 run at KPT 32 puts 64 lines under every wave
-// load instruction). A/B: -DMBRL_SELECT_VEC_MAX=64 is the r04 choice.
-#ifndef MBRL_SELECT_VEC_MAX
-#define MBRL_SELECT_VEC_MAX 64
-#endif
+// LDS words of the register-resident selection: the histograms, the wide histogram, the list, its count
+__host__ __device__ constexpr int sel_words(int) { return SEL_HIST_WORDS + SEL_WIDE_BINS + SEL_LIST + 4; }
 
 // Segmented over blockIdx.x (independent problems of N candidates each, batched planning): segment
 // b reads costs[e * member_stride + b * N + n] and writes elite_idx[b * K ..] (local indices) and
 // returns_out[b * N ..].
-// The body is shared with cem_update_kernel; emit(pos, n) receives the elites in ascending index.
+// The body is shared with cem_update_kernel; emit(pos, n) receives each elite with its place in
+// ascending candidate order.
 template <int KPT, typename Emit>
 __device__ __forceinline__ void select_reg_body(const float* __restrict__ costs, int E, int N, int K, int nan_policy,
                                                 float* __restrict__ returns_out, int member_stride,
                                                 uint32_t* sel_smem, Emit emit) {
-    uint32_t(*hist)[16][257] = reinterpret_cast<uint32_t(*)[16][257]>(sel_smem);  // [2][16][257], aliases keys
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    uint32_t(*hist)[16][257] = reinterpret_cast<uint32_t(*)[16][257]>(sel_smem);  // [2][16][257]
     __shared__ uint32_t scan_ws[16];
     __shared__ uint32_t sel[3];   // bucket, keys before it, keys in it
     CSTAMP(0);
-    const int tid = threadIdx.x, wave = tid >> 6;
-    const int n0 = tid * KPT;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const bool vec = KPT >= 4 && (N & 3) == 0 && (member_stride & 3) == 0;
+    const int lv = 64 * KPT * wave + 4 * lane, ls = 64 * KPT * wave + lane;
+    // candidate of this lane's key j (ascending in (wave, j / VW, lane, j % VW): the global order)
+    auto idx = [&](int j) { return vec ? lv + 256 * (j >> 2) + (j & 3) : ls + 64 * j; };
+    // idx rises with j, so this lane's keys below N are its first nv (one register, not KPT predicates)
+    const int nv = vec ? 4 * max(0, min(KPT / 4, (N - lv + 255) / 256)) : max(0, min(KPT, (N - ls + 63) / 64));
     uint32_t key[KPT];
-    // KPT in [4, MBRL_SELECT_VEC_MAX] with 16-byte aligned rows: each thread loads its own contiguous
-    // KPT returns as float4 (no LDS transpose); the member sum keeps the same per-candidate order, so
-    // the bits are the same either way
-    const bool vec = KPT >= 4 && KPT <= MBRL_SELECT_VEC_MAX && (N & 3) == 0 && (member_stride & 3) == 0;
-    if (vec) {
-        typedef float f4 __attribute__((ext_vector_type(4)));
-        constexpr int G4 = KPT >= 4 ? KPT / 4 : 1;
-        f4 r4[G4];
+    {
+        float r[KPT];   // every load in flight before the first use; the member sum keeps its order
+        if (vec) {
+            constexpr int G4 = KPT >= 4 ? KPT / 4 : 1;
 #pragma unroll
-        for (int j = 0; j < G4; ++j)
-            r4[j] = n0 + 4 * j < N ? *reinterpret_cast<const f4*>(costs + n0 + 4 * j) : f4{0.f, 0.f, 0.f, 0.f};
-        for (int e = 1; e < E; ++e)
+            for (int g = 0; g < G4; ++g) {
+                const int n = lv + 256 * g;
+                const f4 v = n < N ? *reinterpret_cast<const f4*>(costs + n) : f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int j = 0; j < G4; ++j)
-                if (n0 + 4 * j < N) {
-                    const f4 c = *reinterpret_cast<const f4*>(costs + (size_t)e * member_stride + n0 + 4 * j);
+                for (int i = 0; i < 4; ++i) r[4 * g + i] = v[i];
+            }
+            for (int e = 1; e < E; ++e)
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) r4[j][i] = __fadd_rn(r4[j][i], c[i]);
+                for (int g = 0; g < G4; ++g) {
+                    const int n = lv + 256 * g;
+                    if (n < N) {
+                        const f4 c = *reinterpret_cast<const f4*>(costs + (size_t)e * member_stride + n);
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) r[4 * g + i] = __fadd_rn(r[4 * g + i], c[i]);
+                    }
                 }
 #pragma unroll
-        for (int j = 0; j < G4; ++j) {
-            if (n0 + 4 * j < N) {
+            for (int g = 0; g < G4; ++g) {
+                const int n = lv + 256 * g;
                 f4 v;
 #pragma unroll
-                for (int i = 0; i < 4; ++i) v[i] = E > 1 ? __fdiv_rn(r4[j][i], (float)E) : r4[j][i];
-                if (returns_out) *reinterpret_cast<f4*>(returns_out + n0 + 4 * j) = v;
+                for (int i = 0; i < 4; ++i) v[i] = E > 1 ? __fdiv_rn(r[4 * g + i], (float)E) : r[4 * g + i];
+                if (returns_out && n < N) *reinterpret_cast<f4*>(returns_out + n) = v;
 #pragma unroll
-                for (int i = 0; i < 4; ++i) key[4 * j + i] = order_key(v[i], nan_policy);
-            } else {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) key[4 * j + i] = 0xFFFFFFFFu;
+                for (int i = 0; i < 4; ++i) key[4 * g + i] = n < N ? order_key(v[i], nan_policy) : 0xFFFFFFFFu;
             }
-        }
-    } else {
-        float r[KPT];                                   // every load in flight before the first use
+        } else {
 #pragma unroll
-        for (int k = 0; k < KPT; ++k) {
-            const int n = tid + 1024 * k;
-            r[k] = n < N ? costs[n] : 0.f;
-        }
-        for (int e = 1; e < E; ++e)
-#pragma unroll
-            for (int k = 0; k < KPT; ++k) {
-                const int n = tid + 1024 * k;
-                if (n < N) r[k] = __fadd_rn(r[k], costs[(size_t)e * member_stride + n]);
+            for (int j = 0; j < KPT; ++j) {
+                const int n = ls + 64 * j;
+                r[j] = n < N ? costs[n] : 0.f;
             }
+            for (int e = 1; e < E; ++e)
 #pragma unroll
-        for (int k = 0; k < KPT; ++k) {
-            const int n = tid + 1024 * k;
-            if (n < N) {
-                const float v = E > 1 ? __fdiv_rn(r[k], (float)E) : r[k];
-                if (returns_out) returns_out[n] = v;
-                sel_smem[n + (n >> 5)] = order_key(v, nan_policy);  // one pad word per 32: conflict-free reads
+                for (int j = 0; j < KPT; ++j) {
+                    const int n = ls + 64 * j;
+                    if (n < N) r[j] = __fadd_rn(r[j], costs[(size_t)e * member_stride + n]);
+                }
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                const int n = ls + 64 * j;
+                const float v = E > 1 ? __fdiv_rn(r[j], (float)E) : r[j];
+                if (returns_out && n < N) returns_out[n] = v;
+                key[j] = n < N ? order_key(v, nan_policy) : 0xFFFFFFFFu;
             }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < KPT; ++k) {
-            const int n = n0 + k;
-            key[k] = n < N ? sel_smem[n + (n >> 5)] : 0xFFFFFFFFu;
         }
     }
     // leading bits every key shares (block min / max): returns of one plan usually share sign and
     // exponent, so the first digit starts at the first bit in which the keys differ
     uint32_t kmin = 0xFFFFFFFFu, kmax = 0u;
 #pragma unroll
-    for (int k = 0; k < KPT; ++k)
-        if (n0 + k < N) { kmin = min(kmin, key[k]); kmax = max(kmax, key[k]); }
+    for (int j = 0; j < KPT; ++j)
+        if (j < nv) { kmin = min(kmin, key[j]); kmax = max(kmax, key[j]); }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
         kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, o, 64));
         kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o, 64));
     }
     __shared__ uint32_t mm_ws[2][16];
-    if ((tid & 63) == 0) { mm_ws[0][wave] = kmin; mm_ws[1][wave] = kmax; }
-    __syncthreads();   // also: every thread has taken its keys out of sel_smem (non-vector path)
+    if (lane == 0) { mm_ws[0][wave] = kmin; mm_ws[1][wave] = kmax; }
     uint32_t* wide = sel_smem + SEL_HIST_WORDS;          // [SEL_WIDE_BINS] the first pass's histogram
     uint32_t* list = wide + SEL_WIDE_BINS;               // [SEL_LIST] its bucket's keys, then
     uint32_t* list_n = list + SEL_LIST;                  // their count
     for (int i = tid; i < SEL_WIDE_BINS; i += 1024) wide[i] = 0;
     for (int i = tid; i < 16 * 257; i += 1024) (&hist[0][0][0])[i] = 0;
     if (tid == 0) *list_n = 0;
+    __syncthreads();
 #pragma unroll
     for (int w = 0; w < 16; ++w) { kmin = min(kmin, mm_ws[0][w]); kmax = max(kmax, mm_ws[1][w]); }
     const int lead = kmin == kmax ? 32 : __clz(kmin ^ kmax);   // leading bits every key shares
@@ -590,7 +580,6 @@ __device__ __forceinline__ void select_reg_body(const float* __restrict__ costs,
     uint32_t prefix = kmin & mask, kk = (uint32_t)K;
     int rem = 32 - lead;                                 // bits below the shared ones still to resolve
     CSTAMP(1);
-    __syncthreads();
     // (1) one wide pass over the first SEL_WIDE_BITS differing bits: 2048 bins, one shared histogram
     // (plan returns spread over most of them, so the K-th key's bucket holds a handful of keys)
     bool listed = false;
@@ -598,8 +587,8 @@ __device__ __forceinline__ void select_reg_body(const float* __restrict__ costs,
         const int wb = min(SEL_WIDE_BITS, rem), wshift = rem - wb;
         const uint32_t wmask = (1u << wb) - 1u;
 #pragma unroll
-        for (int k = 0; k < KPT; ++k)
-            if (n0 + k < N) atomicAdd(&wide[(key[k] >> wshift) & wmask], 1u);
+        for (int j = 0; j < KPT; ++j)
+            if (j < nv) atomicAdd(&wide[(key[j] >> wshift) & wmask], 1u);
         __syncthreads();
         const uint32_t h0 = wide[2 * tid], h1 = wide[2 * tid + 1];
         uint32_t tot;
@@ -616,15 +605,17 @@ __device__ __forceinline__ void select_reg_body(const float* __restrict__ costs,
         // KPT keys of every thread
         if (rem > 0 && sel[2] <= (uint32_t)SEL_LIST) {
 #pragma unroll
-            for (int k = 0; k < KPT; ++k) {
-                const bool pend = n0 + k < N && (key[k] & mask) == prefix;
+            for (int j = 0; j < KPT; ++j) {
+                const bool pend = j < nv && (key[j] & mask) == prefix;
                 const uint64_t act = __ballot(pend);
                 if (act != 0) {
                     const int leader = __builtin_ctzll(act);
                     uint32_t base = 0;
-                    if ((tid & 63) == leader) base = atomicAdd(list_n, (uint32_t)__popcll(act));
+                    if (lane == leader) base = atomicAdd(list_n, (uint32_t)__popcll(act));
                     base = (uint32_t)__shfl((int)base, leader, 64);
-                    if (pend) list[base + (uint32_t)__popcll(act & ((1ull << (tid & 63)) - 1ull))] = key[k];
+                    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
+                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+                    if (pend) list[base + below] = key[j];
                 }
             }
             listed = true;
@@ -649,7 +640,7 @@ __device__ __forceinline__ void select_reg_body(const float* __restrict__ costs,
                 const int leader = __builtin_ctzll(act);
                 const uint32_t d0 = __shfl(dig, leader, 64);
                 if (__ballot(pending && dig == d0) == act) {   // clustered: one add per wave
-                    if ((int)(tid & 63) == leader) atomicAdd(&hist[buf][wave][d0], (uint32_t)__popcll(act));
+                    if (lane == leader) atomicAdd(&hist[buf][wave][d0], (uint32_t)__popcll(act));
                 } else if (pending) {
                     atomicAdd(&hist[buf][wave][dig], 1u);
                 }
@@ -660,7 +651,7 @@ __device__ __forceinline__ void select_reg_body(const float* __restrict__ costs,
                 count(i0 + tid < nl ? list[i0 + tid] : 0u, i0 + tid < nl);
         } else {
 #pragma unroll
-            for (int k = 0; k < KPT; ++k) count(key[k], n0 + k < N);
+            for (int j = 0; j < KPT; ++j) count(key[j], j < nv);
         }
         for (int i = tid; i < 16 * 257; i += 1024) (&hist[buf ^ 1][0][0])[i] = 0;
         __syncthreads();
@@ -672,9 +663,9 @@ __device__ __forceinline__ void select_reg_body(const float* __restrict__ costs,
 #pragma unroll
             for (int o = 1; o < 64; o <<= 1) {
                 const uint32_t y = __shfl_up(incl, o, 64);
-                if ((tid & 63) >= o) incl += y;
+                if (lane >= o) incl += y;
             }
-            if ((tid & 63) == 63) scan_ws[wave] = incl;
+            if (lane == 63) scan_ws[wave] = incl;
         }
         __syncthreads();
         if (tid < 256) {
@@ -691,26 +682,70 @@ __device__ __forceinline__ void select_reg_body(const float* __restrict__ costs,
     }
     CSTAMP(4);
     // prefix = the K-th smallest key; the elites are every key below it and the first kk keys equal to
-    // it (lowest index first). One packed scan gives each thread both counts before it: (below << 16) |
-    // equal (N <= 32768, so neither half carries), and an elite's place in ascending index order is
-    // below-before + min(equal-before, kk).
-    uint32_t lt = 0, eq = 0;
+    // it in candidate order. An elite's place in that order is (keys below it before it) + min(equal
+    // keys before it, kk). Keys past N are all ones and follow every real key in the order, so they
+    // can only tie with a K-th key of all ones after the kk real ones: no validity test is needed here.
+    auto below = [&](uint64_t b) {   // set bits of b in lanes before this one
+        return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+    };
+    constexpr int VW = KPT >= 4 ? 4 : 1;   // keys of one lane that are adjacent in the order
+    const int vw = vec ? VW : 1;
+    uint32_t wl = 0, we = 0;   // this wave's keys below / equal to the prefix
 #pragma unroll
-    for (int k = 0; k < KPT; ++k)
-        if (n0 + k < N) { lt += key[k] < prefix; eq += key[k] == prefix; }
-    uint32_t tot;
-    const uint32_t ex = block_exclusive_scan((lt << 16) | eq, scan_ws, &tot);
-    uint32_t lt_b = ex >> 16, eq_b = ex & 0xFFFFu;
+    for (int j = 0; j < KPT; ++j) {
+        wl += (uint32_t)__popcll(__ballot(key[j] < prefix));
+        we += (uint32_t)__popcll(__ballot(key[j] == prefix));
+    }
+    if (lane == 0) scan_ws[wave] = (wl << 16) | we;   // N <= 32768: neither half carries
+    __syncthreads();
+    uint32_t before = 0;
+    for (int w = 0; w < wave; ++w) before += scan_ws[w];
+    uint32_t lt_b = before >> 16, eq_b = before & 0xFFFFu;   // keys of earlier groups (wave-uniform)
 #pragma unroll
-    for (int k = 0; k < KPT; ++k) {
-        if (n0 + k >= N) continue;
-        if (key[k] < prefix) {
-            const uint32_t pos = lt_b + min(eq_b, kk);
-            if (pos < (uint32_t)K) emit(pos, n0 + k);
-            ++lt_b;
-        } else if (key[k] == prefix) {
-            if (eq_b < kk && lt_b + eq_b < (uint32_t)K) emit(lt_b + eq_b, n0 + k);
-            ++eq_b;
+    for (int g = 0; g < KPT / VW; ++g) {
+        // the group's keys in candidate order: lanes ascending, and inside a lane its vw keys
+        uint64_t bl[VW], be[VW];
+        uint32_t ll = 0, le = 0;   // this group's keys before this lane's
+#pragma unroll
+        for (int i = 0; i < VW; ++i) {
+            bl[i] = __ballot(key[VW * g + i] < prefix);
+            be[i] = __ballot(key[VW * g + i] == prefix);
+            ll += below(bl[i]);
+            le += below(be[i]);
+        }
+        if (vw == VW) {
+#pragma unroll
+            for (int i = 0; i < VW; ++i) {
+                const uint32_t k = key[VW * g + i];
+                if (k < prefix) {
+                    const uint32_t pos = lt_b + ll + min(eq_b + le, kk);
+                    if (pos < (uint32_t)K) emit(pos, idx(VW * g + i));
+                    ++ll;
+                } else if (k == prefix) {
+                    if (eq_b + le < kk && lt_b + ll + eq_b + le < (uint32_t)K) emit(lt_b + ll + eq_b + le, idx(VW * g + i));
+                    ++le;
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < VW; ++i) {
+                lt_b += (uint32_t)__popcll(bl[i]);
+                eq_b += (uint32_t)__popcll(be[i]);
+            }
+        } else {
+            // single keys (VW keys of a lane are VW separate groups of the order): group by group
+#pragma unroll
+            for (int i = 0; i < VW; ++i) {
+                const uint32_t k = key[VW * g + i];
+                const uint32_t l1 = below(bl[i]), e1 = below(be[i]);
+                if (k < prefix) {
+                    const uint32_t pos = lt_b + l1 + min(eq_b + e1, kk);
+                    if (pos < (uint32_t)K) emit(pos, idx(VW * g + i));
+                } else if (k == prefix) {
+                    if (eq_b + e1 < kk && lt_b + l1 + eq_b + e1 < (uint32_t)K) emit(lt_b + l1 + eq_b + e1, idx(VW * g + i));
+                }
+                lt_b += (uint32_t)__popcll(bl[i]);
+                eq_b += (uint32_t)__popcll(be[i]);
+            }
         }
     }
     CSTAMP(5);
@@ -811,39 +846,21 @@ __host__ __device__ inline size_t refit_rows_floats(int a, int K) {
 // Row t of the refit (mu, sigma, outputs already offset to the problem; NULL outputs are skipped): eidx
 // = the K elites' global candidate indices in LDS (visible after refit_rows' first barrier). With
 // `next` (LDS [2][a4]) the new mu_t, sigma_t are also left there for the next proposal draw.
-__device__ __forceinline__ void refit_rows(int t, const uint32_t* eidx, float* smem, uint64_t seed, int iteration,
-                                           const float* __restrict__ mu, const float* __restrict__ sigma, float lo,
-                                           float hi, int a, int K, float alpha, float oma, float* __restrict__ mu_out,
-                                           float* __restrict__ sigma_out, float* __restrict__ fin_mu,
-                                           float* __restrict__ fin_sigma, float* __restrict__ fin_actions,
-                                           float* next) {
+// The chunked sums of refit_rows over the elites' actions already in LDS (ael = smem [K][a]) and this
+// row's mu, sigma staged in musg: mean, population variance, the alpha-smoothed mu', sigma' and the
+// outputs. Ends on a barrier.
+__device__ __forceinline__ void refit_sums(int t, float* smem, float lo, float hi, int a, int K, float alpha, float oma,
+                                           float* __restrict__ mu_out, float* __restrict__ sigma_out,
+                                           float* __restrict__ fin_mu, float* __restrict__ fin_sigma,
+                                           float* __restrict__ fin_actions, float* next) {
 #pragma clang fp contract(off)
-    const int G = (a + 3) >> 2;
     const int nch = (K + ELITE_CHUNK - 1) / ELITE_CHUNK;
     const int a4 = (a + 3) & ~3;
     float* ael = smem;                                   // [K][a]
     float* part = smem + (((size_t)K * a + 3) & ~(size_t)3);   // [nch][a]
     float* mean = part + (((size_t)nch * a + 3) & ~(size_t)3);  // [a]
-    float* musg = mean + a4;                                     // [2][a]: this step's mu, sigma
-    // stage every global operand first (all loads in flight together), then compute from LDS
-    for (int d = threadIdx.x; d < a; d += blockDim.x) {
-        musg[d] = mu[t * a + d];
-        musg[a4 + d] = sigma[t * a + d];
-    }
-    __syncthreads();
-    const float* smu = musg;
-    const float* ssg = musg + a4;
-    for (int idx = threadIdx.x; idx < K * G; idx += blockDim.x) {
-        const int e = idx / G, g = idx - (idx / G) * G;
-        float z[4];
-        cem_normal4(seed, eidx[e], (uint32_t)t, (uint32_t)iteration, (uint32_t)g, z);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int d = 4 * g + j;
-            if (d < a) ael[(size_t)e * a + d] = cem_action(smu[d], ssg[d], z[j], lo, hi);
-        }
-    }
-    __syncthreads();
+    const float* smu = mean + a4;                               // [2][a]: this step's mu, sigma
+    const float* ssg = smu + a4;
     for (int pass = 0; pass < 2; ++pass) {
         for (int idx = threadIdx.x; idx < nch * a; idx += blockDim.x) {
             const int c = idx / a, d = idx - (idx / a) * a;
@@ -886,6 +903,54 @@ __device__ __forceinline__ void refit_rows(int t, const uint32_t* eidx, float* s
         }
         __syncthreads();
     }
+}
+
+// Row t's mu, sigma into LDS (musg, behind the mean) -- refit_rows' and the split update's first step.
+__device__ __forceinline__ void refit_stage_row(int t, float* smem, const float* __restrict__ mu,
+                                                const float* __restrict__ sigma, int a, int K) {
+    const int nch = (K + ELITE_CHUNK - 1) / ELITE_CHUNK;
+    const int a4 = (a + 3) & ~3;
+    float* musg = smem + (((size_t)K * a + 3) & ~(size_t)3) + (((size_t)nch * a + 3) & ~(size_t)3) + a4;
+    for (int d = threadIdx.x; d < a; d += blockDim.x) {
+        musg[d] = mu[t * a + d];
+        musg[a4 + d] = sigma[t * a + d];
+    }
+}
+
+// Elites [e0, e1)'s actions of row t regenerated from the counter RNG (bit-identical to the sampled
+// ones): into dst[e][a] (LDS or global). smu / ssg: this row's mu, sigma.
+__device__ __forceinline__ void regen_elites(int t, const uint32_t* eidx, int e0, int e1, uint64_t seed, int iteration,
+                                             const float* smu, const float* ssg, float lo, float hi, int a,
+                                             float* __restrict__ dst) {
+#pragma clang fp contract(off)
+    const int G = (a + 3) >> 2;
+    for (int idx = threadIdx.x; idx < (e1 - e0) * G; idx += blockDim.x) {
+        const int e = e0 + idx / G, g = idx - (idx / G) * G;
+        float z[4];
+        cem_normal4(seed, eidx[e], (uint32_t)t, (uint32_t)iteration, (uint32_t)g, z);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int d = 4 * g + j;
+            if (d < a) dst[(size_t)e * a + d] = cem_action(smu[d], ssg[d], z[j], lo, hi);
+        }
+    }
+}
+
+__device__ __forceinline__ void refit_rows(int t, const uint32_t* eidx, float* smem, uint64_t seed, int iteration,
+                                           const float* __restrict__ mu, const float* __restrict__ sigma, float lo,
+                                           float hi, int a, int K, float alpha, float oma, float* __restrict__ mu_out,
+                                           float* __restrict__ sigma_out, float* __restrict__ fin_mu,
+                                           float* __restrict__ fin_sigma, float* __restrict__ fin_actions,
+                                           float* next) {
+    const int nch = (K + ELITE_CHUNK - 1) / ELITE_CHUNK;
+    const int a4 = (a + 3) & ~3;
+    const float* musg = smem + (((size_t)K * a + 3) & ~(size_t)3) + (((size_t)nch * a + 3) & ~(size_t)3) + a4;
+    // stage every global operand first (all loads in flight together), then compute from LDS
+    refit_stage_row(t, smem, mu, sigma, a, K);
+    __syncthreads();
+    regen_elites(t, eidx, 0, K, seed, iteration, musg, musg + a4, lo, hi, a, smem);
+    __syncthreads();
+    refit_sums(t, smem, lo, hi, a, K, alpha, oma, mu_out, sigma_out, fin_mu, fin_sigma, fin_actions, next);
 }
 
 __global__ void __launch_bounds__(REFIT_THREADS) refit_fused_kernel(
@@ -931,12 +996,36 @@ struct UpdateArgs {
     float *fin_mu, *fin_sigma, *fin_actions;   // last iteration: plan outputs (or NULL)
     float* next_actions;         // [H][B*draw_n][a] proposals of iteration + 1, or NULL
     int draw_off, draw_n;        // problem b draws candidates b*N + draw_off + [0, draw_n) (a plan: 0, N)
+    float* ael;                  // split update (B == 1): [H][K][a] the elites' actions between its launches
 };
 
 __host__ __device__ inline size_t update_lds_words(int KPT, int a, int K) {
     const size_t sel = (size_t)sel_words(KPT);
     const size_t ref = refit_rows_floats(a, K);
     return (((size_t)K + 3) & ~(size_t)3) + 2 * (((size_t)a + 3) & ~(size_t)3) + (sel > ref ? sel : ref);
+}
+
+// Row t of the next iteration's proposals for candidate slice j of S, from mu', sigma' in LDS (next).
+__device__ __forceinline__ void update_draw(const UpdateArgs& U, int t, int j, int S, int b, uint32_t nbase,
+                                            const float* next) {
+    const int a = U.a, a4 = (a + 3) & ~3;
+    const int G = (a + 3) >> 2;
+    const int Dn = U.draw_n;
+    const size_t row = (size_t)gridDim.y * Dn;
+    const uint32_t cbase = nbase + (uint32_t)U.draw_off;   // global candidate of local index 0
+    const int NS = (Dn + S - 1) / S, n0 = j * NS, n1 = min(Dn, n0 + NS);
+    for (int idx = threadIdx.x; idx < (n1 - n0) * G; idx += 1024) {
+        const int n = n0 + idx / G, g = idx - (idx / G) * G;
+        float z[4];
+        cem_normal4(U.seed, cbase + (uint32_t)n, (uint32_t)t, (uint32_t)(U.iteration + 1), (uint32_t)g, z);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int d = 4 * g + q;
+            if (d < a)
+                U.next_actions[((size_t)t * row + (size_t)b * Dn + n) * a + d] =
+                    cem_action(next[d], next[a4 + d], z[q], U.lo, U.hi);
+        }
+    }
 }
 
 template <int KPT>
@@ -958,31 +1047,66 @@ __global__ void __launch_bounds__(1024) cem_update_kernel(const UpdateArgs U) {
                              if (eo) eo[pos] = n;
                          });
     __syncthreads();   // eidx complete; the selection's LDS becomes the refit's
+    CSTAMP(6);
     const size_t rb = (size_t)b * U.H * a;
     const bool w = j == 0;   // slice 0 of the row writes its refit
     refit_rows(t, eidx, reinterpret_cast<float*>(work), U.seed, U.iteration, U.mu + rb, U.sigma + rb, U.lo, U.hi, a,
                K, U.alpha, U.oma, w ? U.mu_out + rb : nullptr, w ? U.sigma_out + rb : nullptr,
                (w && U.fin_mu) ? U.fin_mu + rb : nullptr, (w && U.fin_sigma) ? U.fin_sigma + rb : nullptr,
                (w && U.fin_actions) ? U.fin_actions + rb : nullptr, U.next_actions ? next : nullptr);
-    if (U.next_actions) {   // refit_rows ended on a barrier: next[] is visible
-        const int G = (a + 3) >> 2;
-        const int Dn = U.draw_n;
-        const size_t row = (size_t)gridDim.y * Dn;
-        const uint32_t cbase = nbase + (uint32_t)U.draw_off;   // global candidate of local index 0
-        const int NS = (Dn + S - 1) / S, n0 = j * NS, n1 = min(Dn, n0 + NS);
-        for (int idx = threadIdx.x; idx < (n1 - n0) * G; idx += 1024) {
-            const int n = n0 + idx / G, g = idx - (idx / G) * G;
-            float z[4];
-            cem_normal4(U.seed, cbase + (uint32_t)n, (uint32_t)t, (uint32_t)(U.iteration + 1), (uint32_t)g, z);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int d = 4 * g + q;
-                if (d < a)
-                    U.next_actions[((size_t)t * row + (size_t)b * Dn + n) * a + d] =
-                        cem_action(next[d], next[a4 + d], z[q], U.lo, U.hi);
-            }
-        }
+    CSTAMP(7);
+    if (U.next_actions) update_draw(U, t, j, S, b, nbase, next);   // refit_rows ended on a barrier
+}
+
+// The same update as two launches (the split update): the regeneration of the K elites'
+// actions -- K ceil(a / 4) Philox blocks per row, repeated by each of the row's S workgroups in
+// cem_update_kernel -- is shared out: launch 1 (select + regenerate) has workgroup (t, j) select, then
+// regenerate elites [j K / S, (j + 1) K / S) of row t into U.ael; launch 2 (refit + draw) has every
+// workgroup of row t read the row's K elites back, then run the same chunked sums and the draw. The
+// kernel boundary is the only hand-off. Bit-identical to cem_update_kernel: the same values in the
+// same order.
+template <int KPT>
+__global__ void __launch_bounds__(1024) cem_select_regen_kernel(const UpdateArgs U) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t usmem[];
+    const int S = gridDim.x / U.H;
+    const int t = blockIdx.x / S, j = blockIdx.x - (blockIdx.x / S) * S;
+    const bool lead = t == 0 && j == 0;
+    const int K = U.K, N = U.N, a = U.a, a4 = (a + 3) & ~3;
+    uint32_t* eidx = usmem;                                                  // [K] global candidate index
+    float* row = reinterpret_cast<float*>(usmem + ((K + 3) & ~3));          // [2][a4] mu_t, sigma_t
+    uint32_t* work = usmem + ((K + 3) & ~3) + 2 * a4;
+    int64_t* eo = (U.elite_out && lead) ? U.elite_out : nullptr;
+    float* ro = (U.returns_out && lead) ? U.returns_out : nullptr;
+    for (int d = threadIdx.x; d < a; d += 1024) {
+        row[d] = U.mu[t * a + d];
+        row[a4 + d] = U.sigma[t * a + d];
     }
+    select_reg_body<KPT>(U.costs, U.E, N, K, MBRL_NAN_LAST, ro, U.member_stride, work,
+                         [&](uint32_t pos, int n) {
+                             eidx[pos] = (uint32_t)n;
+                             if (eo) eo[pos] = n;
+                         });
+    __syncthreads();   // eidx complete (and the row staged)
+    const int KS = (K + S - 1) / S, e0 = min(K, j * KS), e1 = min(K, e0 + KS);
+    regen_elites(t, eidx, e0, e1, U.seed, U.iteration, row, row + a4, U.lo, U.hi, a, U.ael + (size_t)t * K * a);
+}
+
+__global__ void __launch_bounds__(1024) cem_refit_draw_kernel(const UpdateArgs U) {
+    extern __shared__ __attribute__((aligned(16))) float fsmem[];
+    const int S = gridDim.x / U.H;
+    const int t = blockIdx.x / S, j = blockIdx.x - (blockIdx.x / S) * S;
+    const int K = U.K, a = U.a, a4 = (a + 3) & ~3;
+    float* next = fsmem;                  // [2][a4] mu', sigma' of row t
+    float* work = fsmem + 2 * a4;         // refit_rows' layout: [K][a] elites, partials, mean, mu / sigma
+    const float* src = U.ael + (size_t)t * K * a;
+    for (int i = threadIdx.x; i < K * a; i += 1024) work[i] = src[i];
+    refit_stage_row(t, work, U.mu, U.sigma, a, K);
+    __syncthreads();
+    const bool w = j == 0;   // slice 0 of the row writes its refit
+    refit_sums(t, work, U.lo, U.hi, a, K, U.alpha, U.oma, w ? U.mu_out : nullptr, w ? U.sigma_out : nullptr,
+               (w && U.fin_mu) ? U.fin_mu : nullptr, (w && U.fin_sigma) ? U.fin_sigma : nullptr,
+               (w && U.fin_actions) ? U.fin_actions : nullptr, U.next_actions ? next : nullptr);
+    if (U.next_actions) update_draw(U, t, j, S, 0, 0u, next);
 }
 
 // The plan's first launch: workgroup (t * S + j, b) sets row t of problem b's distribution to
@@ -1474,9 +1598,45 @@ static int draw_slices(int H, int B, int N, int a) {
     return s < 1 ? 1 : (int)s;
 }
 
+// The split update (two launches, cem_select_regen_kernel + cem_refit_draw_kernel) where the elites'
+// regeneration is worth sharing out: at least SPLIT_MIN_BLOCKS Philox blocks per row (walker's K =
+// 1638: 3276 blocks, ~10 us of one workgroup's VALU; cheetah's 818 would save less than the launch
+// boundary costs). MBRL_OPT_UPDATE_SPLIT: 0 auto, 1 never, 2 wherever scratch is given (tests, A/B).
+constexpr long SPLIT_MIN_BLOCKS = 2048;
+
+static bool update_split(const UpdateArgs& U, int B) {
+    const int o = g_opt[MBRL_OPT_UPDATE_SPLIT].load(std::memory_order_relaxed);
+    if (o == 1 || B != 1 || !U.ael) return false;
+    return o == 2 || (long)U.K * ((U.a + 3) / 4) >= SPLIT_MIN_BLOCKS;
+}
+
+static int update_split_impl(const UpdateArgs& U, int kpt, hipStream_t stream) {
+    // workgroups per row: the draw's slices, and at least ~256 workgroups in all for the regeneration
+    const int Sd = U.next_actions ? draw_slices(U.H, 1, U.draw_n, U.a) : 1;
+    const int S = std::max(Sd, std::max(1, 256 / U.H));
+    const int a4 = (U.a + 3) & ~3;
+    const size_t lds_a = ((((size_t)U.K + 3) & ~(size_t)3) + 2 * a4 + (size_t)sel_words(kpt)) * 4;
+    const size_t lds_b = (2 * a4 + refit_rows_floats(U.a, U.K)) * 4;
+    if (lds_b + 1024 > 160 * 1024) return fail(MBRL_EUNSUPPORTED, "split update: K=%d a=%d exceeds LDS", U.K, U.a);
+#define MBRL_SPLIT_A(KPT)                                                                                       \
+    if (kpt == KPT) {                                                                                           \
+        hipError_t err = ensure_dynamic_lds(reinterpret_cast<const void*>(&cem_select_regen_kernel<KPT>), (int)lds_a); \
+        if (err != hipSuccess) return hip_check(err, "split update attribute");                                 \
+        hipLaunchKernelGGL(cem_select_regen_kernel<KPT>, dim3(U.H * S), dim3(1024), lds_a, stream, U);          \
+    }
+    MBRL_SPLIT_A(1) MBRL_SPLIT_A(2) MBRL_SPLIT_A(4) MBRL_SPLIT_A(8) MBRL_SPLIT_A(16) MBRL_SPLIT_A(32)
+#undef MBRL_SPLIT_A
+    if (int rc = hip_check(hipGetLastError(), "split update launch 1")) return rc;
+    hipError_t err = ensure_dynamic_lds(reinterpret_cast<const void*>(&cem_refit_draw_kernel), (int)lds_b);
+    if (err != hipSuccess) return hip_check(err, "split update attribute");
+    hipLaunchKernelGGL(cem_refit_draw_kernel, dim3(U.H * S), dim3(1024), lds_b, stream, U);
+    return hip_check(hipGetLastError(), "split update launch 2");
+}
+
 static int update_impl(const UpdateArgs& U, int B, hipStream_t stream) {
     const int kpt = update_kpt(U.N, U.K, U.a);
     if (!kpt) return fail(MBRL_EUNSUPPORTED, "update: N=%d K=%d a=%d not fusable", U.N, U.K, U.a);
+    if (update_split(U, B)) return update_split_impl(U, kpt, stream);
     const size_t lds = update_lds_words(kpt, U.a, U.K) * 4;
     const int S = U.next_actions ? draw_slices(U.H, B, U.draw_n, U.a) : 1;
 #define MBRL_UPD(KPT)                                                                                            \
@@ -1527,6 +1687,7 @@ int mbrl_set_option(int32_t option, int32_t value) {
         case MBRL_OPT_DEBUG_SHARD_FAIL: ok = value >= 0 && value <= 1 << 20; break;
         case MBRL_OPT_DEBUG_SHARD_FAIL_RANK: ok = value >= 0 && value <= 1 << 20; break;
         case MBRL_OPT_SHARD_EMULATE: ok = value >= 0 && value <= 2; break;
+        case MBRL_OPT_UPDATE_SPLIT: ok = value >= 0 && value <= 2; break;
         default: ok = value == 0 || value == 1; break;
     }
     if (!ok) return fail(MBRL_EINVAL, "option %d: value %d not allowed", option, value);
@@ -2037,6 +2198,7 @@ int mbrl_cem_plan(const mbrl_mlp_shape* shape, const void* packed, const mbrl_no
             U.fin_mu = last ? mu : nullptr; U.fin_sigma = last ? sigma : nullptr; U.fin_actions = last ? actions_out : nullptr;
             U.next_actions = (fuse_draw && !last) ? w.actions : nullptr;
             U.draw_off = 0; U.draw_n = p->N;
+            U.ael = w.aelite;   // (scratch of the split update)
             rc = update_impl(U, 1, stream);
         } else {
             rc = select_impl(costs, g.E, p->N, p->K, MBRL_NAN_LAST, elites, rets, w.keys, align256((size_t)p->N * 4), stream);
@@ -2371,6 +2533,7 @@ static int plan_sharded_body(const mbrl_mlp_shape* shape, const void* packed, co
             U.fin_mu = last ? mu : nullptr; U.fin_sigma = last ? sigma : nullptr; U.fin_actions = last ? actions_out : nullptr;
             U.next_actions = (fuse_draw && !last) ? w.actions : nullptr;   // this rank's shard of iteration it + 1
             U.draw_off = off; U.draw_n = Nl;
+            U.ael = w.aelite;   // (scratch of the split update)
             step(update_impl(U, 1, stream));
         } else if (step(select_impl(costs, E, N, p->K, MBRL_NAN_LAST, elites, rets, w.keys, align256((size_t)N * 4),
                                     stream))) {

@@ -33,40 +33,19 @@
 
 #include "mbrl_internal.h"
 
-// Waves per workgroup for the rollout: 8 (two per SIMD, T/2 tiles each) for R = 1, 4 for R = 2 (the
-// 8-wave output partials would push R = 2 past 160 KiB of LDS). -DMBRL_ROLLOUT_NW=4 forces 4.
-// Weight stream through buffer_load (SGPR descriptor + 32-bit offsets); -DMBRL_GLOBAL_LOAD for the
-// global_load form. Measured on cheetah, rollout ms (tools/variants.sh, r01):
-//   global 4 waves 1.083 | buffer 4 waves 1.044 | global 8 waves 1.171 | buffer 8 waves 1.035
-#ifndef MBRL_ROLLOUT_NW
-#define MBRL_ROLLOUT_NW 8
-#endif
-#ifndef MBRL_GLOBAL_LOAD
-#define MBRL_BUFFER_LOAD 1
-#endif
+// Waves per workgroup for the rollout: 8 (two per SIMD, T/2 tiles each) for R = 1, and for R = 2 where
+// the aliased output partials fit LDS; else 4. The weight stream goes through buffer_load (SGPR
+// descriptor + 32-bit offsets). Measured on cheetah, rollout ms (r01; the other forms were removed in
+// r06): global 4 waves 1.083 | buffer 4 waves 1.044 | global 8 waves 1.171 | buffer 8 waves 1.035
 // State slots per lane (ceil(s / 16)) up to which the 8/16-candidate epilogues keep their per-lane
 // parameter copies in registers; wider states read them from LDS (the copies spilled on humanoid).
 #ifndef MBRL_EPI_REG_SLOTS
 #define MBRL_EPI_REG_SLOTS 2
 #endif
-// Hidden-layer hand-offs by per-wave LDS flags instead of workgroup barriers.
-// Off: parity-green but 3-35 % slower than the barriers (profiles/r03_ab_layer_flags.txt) -- every
-// flag poll is an LDS load the wave must drain its prefetched B reads for (s_waitcnt lgkmcnt(0)).
-#ifndef MBRL_LAYER_FLAGS
-#define MBRL_LAYER_FLAGS 0
-#endif
 // Timing ablation only (results are garbage): -DMBRL_PAIR_DIAG=1 keeps the column-split pairs' LDS
 // hand-off flow but drops every cross-workgroup store, poll and load.
 #ifndef MBRL_PAIR_DIAG
 #define MBRL_PAIR_DIAG 0
-#endif
-// Issue priority of the two waves that share a SIMD (8-wave kernels; MI355X_MICROARCH.md "Two waves
-// per SIMD"): 0 none; 1 the younger half (waves 4-7) at s_setprio 1 for the whole launch; 2 the two
-// halves trade priority every K chunk, so neither finishes a layer alone; 3 every wave steps its
-// priority down 3 -> 2 -> 1 -> 0 at fixed chunks of each hidden layer (no branch), so the wave that
-// reaches a step first yields issue slots to the one behind it until that one reaches it too.
-#ifndef MBRL_PRIO
-#define MBRL_PRIO 0
 #endif
 
 namespace mbrl {
@@ -74,25 +53,6 @@ namespace mbrl {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 #define MBRL_PIN() __builtin_amdgcn_sched_barrier(0)
-
-// Optional (-DMBRL_INTERLEAVE): spread a chunk's T weight loads (and the next A read) between its
-// 4*T*R MFMAs with sched_group_barrier. Off by default: with the 4-deep ring the compiler's own
-// order (loads issued as one burst at the chunk head) is 2 % faster (tools/variants.sh, r01).
-// Masks: 0x8 MFMA, 0x20 VMEM read, 0x100 DS read.
-template <int T, int R>
-__device__ __forceinline__ void interleave_loads() {
-#ifndef MBRL_INTERLEAVE
-    return;
-#endif
-    __builtin_amdgcn_sched_group_barrier(0x008, 2 * R, 0);
-    __builtin_amdgcn_sched_group_barrier(0x100, R, 0);
-#pragma unroll
-    for (int q = 0; q < T; ++q) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 2 * R, 0);
-        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 2 * R, 0);
-    }
-}
 
 // Diagnostic build only (make diag, -DMBRL_STAMPS): per-wave s_memtime sums per kernel segment,
 // written to a buffer set by mbrl_diag_set_stamps(). The timed kernel never contains stamps.
@@ -113,20 +73,8 @@ __device__ unsigned long long* g_mbrl_stamps;
     } while (0)
 #endif
 
-template <int T>
-__device__ __forceinline__ void load_chunk(f32x4 (&b)[T], const f32x4* __restrict__ p) {
-#ifdef MBRL_DIAG_NOLOAD  // timing ablation only: no weight stream (results are garbage)
-    (void)p;
-#pragma unroll
-    for (int j = 0; j < T; ++j) asm volatile("" : "+v"(b[j]));
-#else
-#pragma unroll
-    for (int j = 0; j < T; ++j) b[j] = p[j * 64];
-#endif
-}
-
-// -DMBRL_BUFFER_LOAD variant: the same stream through buffer_load_dwordx4 (SGPR descriptor, 32-bit
-// per-lane offsets: one VGPR of address per load instead of two).
+// The weight stream through buffer_load_dwordx4 (SGPR descriptor, 32-bit per-lane offsets: one VGPR of
+// address per load instead of a global_load's two).
 template <int T>
 __device__ __forceinline__ void load_chunk_buf(f32x4 (&b)[T], __amdgpu_buffer_rsrc_t rsrc, unsigned voff) {
 #ifdef MBRL_DIAG_NOLOAD  // timing ablation only: no weight stream (results are garbage)
@@ -226,31 +174,6 @@ __device__ __forceinline__ void hidden_store_nobar(const f32x4 (&acc)[R][T], con
             v = __builtin_elementwise_max(v, zero);
             *reinterpret_cast<f32x4*>(out + (16 * r + (lane & 15)) * lda + wave * 16 * T + 16 * j + 4 * (lane >> 4)) = v;
         }
-}
-
-// hidden_store without the barrier; then this wave's count of finished layer stores is published
-// in LDS (lflag[wave]) once its own ds_writes have completed (s_waitcnt lgkmcnt(0)).
-template <int T, int R>
-__device__ __forceinline__ void hidden_store_flag(const f32x4 (&acc)[R][T], const f32x4 (&bias)[T], float* out,
-                                                  int lda, int wave, int lane, uint32_t* lflag, uint32_t count) {
-    const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-#pragma unroll
-        for (int j = 0; j < T; ++j) {
-            f32x4 v = acc[r][j] + bias[j];
-            v = __builtin_elementwise_max(v, zero);
-            *reinterpret_cast<f32x4*>(out + (16 * r + (lane & 15)) * lda + wave * 16 * T + 16 * j + 4 * (lane >> 4)) = v;
-        }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (lane == 0) *reinterpret_cast<volatile uint32_t*>(lflag + wave) = count;
-    asm volatile("" ::: "memory");
-}
-
-// Block until wave p has published at least `need` layer stores (its columns of the layer input).
-__device__ __forceinline__ void wait_layer(const uint32_t* lflag, int p, uint32_t need) {
-    while (*reinterpret_cast<const volatile uint32_t*>(lflag + p) < need) __builtin_amdgcn_s_sleep(1);
-    asm volatile("" ::: "memory");
 }
 
 template <int T>
@@ -449,10 +372,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
     constexpr int NT = 64 * NW;
     static_assert(TW >= 1 && TW * NW == 4 * T, "tiles per wave");
     constexpr bool RING = K0C_T > 0;
-#ifndef MBRL_RING_NB
-#define MBRL_RING_NB 4   // A/B of the prefetch depth only (2 also satisfies the ring layout)
-#endif
-    constexpr int NB = RING ? MBRL_RING_NB : 2;
+    constexpr int NB = RING ? 4 : 2;        // weight ring slots: 3 chunks ahead (2 slots: 0.5-1.2 % slower, r03)
     constexpr int SS = RING ? NOT_T : 1;    // register state slots per lane (ceil(s / 16) <= NOT); generic: LDS
     // per-lane epilogue parameter copies in registers (else the same values from LDS): not at 32
     // candidates x 8 waves, whose MFMA loop already takes the whole 256-VGPR budget
@@ -460,13 +380,6 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
     static_assert(!RING || ((K0C_T + NOT_T) % NB == 0 && K0C_T % 2 == 0 && NOT_T % 2 == 0), "ring layout");
     static_assert(!PAIR || (NW == 8 && R == 1 && RING && T % 2 == 0), "column-split pairs: 8 waves, 16 rows");
     constexpr bool L0DUP = PAIR && K0C_T == 2;   // PAIR: layer 0 computed by both halves (below)
-    // hidden-layer hand-offs by per-wave flags (hidden_store_flag / wait_layer): a wave starts layer
-    // l + 1 as soon as the producers of its first K chunks have stored layer l, so the waves that win
-    // the MFMA arbitration run ahead instead of idling at a barrier. Layer l + 1 consumes every wave's
-    // layer-l columns before it stores, and a wave stores layer l only after reading all of layer l's
-    // input, so no buffer is overwritten while another wave still reads it (the ping-pong invariant
-    // the barriers kept).
-    constexpr bool LFLAGS = RING && MBRL_LAYER_FLAGS;
     // LDS row strides: compile-time for the ring instances (make_geometry: lda = max(Wpad, 16 K0C) + 4,
     // pw = 16 NOT + 4; the launcher checks them), so every LDS address of a row block, partial or
     // slot is one base register plus an immediate offset. With runtime strides hipcc hoisted one
@@ -476,7 +389,6 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
     constexpr int PWC = 16 * NOT_T + 4;
     const int lda = RING ? LDAC : A.lda;
     const int pw = RING ? PWC : A.pw;
-    uint32_t nstore = 0;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const LdsMap L = lds_map(A, smem, M);
     uint32_t* const lflag = L.lflag;
@@ -738,20 +650,16 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
     const f32x4* wb = reinterpret_cast<const f32x4*>(member) + cw * TW * 64 + lane;
     const int cs = 4 * T * 64;
     const int C = A.chunks_per_step;
-#ifdef MBRL_BUFFER_LOAD
     (void)wb;
     const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(member), 0, (int)(A.stream_floats * sizeof(float)), 0x00020000);
     const unsigned lane_off = (unsigned)((cw * TW * 64 + lane) * 16);
 #ifdef MBRL_DIAG_SAMECHUNK  // timing ablation only: every load re-reads chunk 0 (L1 hits; results garbage)
+    (void)C;
 #define MBRL_LOAD_CHUNK(DST, G) load_chunk_buf<TW>(DST, wrsrc, lane_off + 0u * (unsigned)(G))
 #else
 #define MBRL_LOAD_CHUNK(DST, G) \
     load_chunk_buf<TW>(DST, wrsrc, lane_off + (unsigned)(((G) < C ? (G) : (G) - C) * cs * 16))
-#endif
-#else
-    auto chunk_ptr = [&](int g) { return wb + (size_t)(g < C ? g : g - C) * cs; };
-#define MBRL_LOAD_CHUNK(DST, G) load_chunk<TW>(DST, chunk_ptr(G))
 #endif
 
     f32x4 ring[NB][TW];
@@ -766,15 +674,9 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
     [[maybe_unused]] const int ocw0 = PAIR ? 4 * (half ^ 1) + wave : 0;
     [[maybe_unused]] f32x4 w0p[L0DUP ? K0C_T : 1][TW];
     if constexpr (L0DUP) {
-#ifdef MBRL_BUFFER_LOAD
         const unsigned poff = (unsigned)((ocw0 * TW * 64 + lane) * 16);
 #pragma unroll
         for (int kc = 0; kc < K0C_T; ++kc) load_chunk_buf<TW>(w0p[kc], wrsrc, poff + (unsigned)(kc * cs * 16));
-#else
-#pragma unroll
-        for (int kc = 0; kc < K0C_T; ++kc)
-            load_chunk<TW>(w0p[kc], reinterpret_cast<const f32x4*>(member) + ocw0 * TW * 64 + lane + (size_t)kc * cs);
-#endif
     }
     int pwl = -1;   // PAIR: first partner K chunk of the current hidden layer (-1: no hand-off to wait for)
     float total[R];  // return of row epi_row(r, wave, lane), held by the 16 lanes of that row
@@ -791,30 +693,13 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
 #define MBRL_HIDDEN_CHUNK(SLOT, KC, NK, IN)                                          \
     do {                                                                             \
         MBRL_LOAD_CHUNK(ring[((SLOT) + NB - 1) % NB], g + NB - 1);                   \
-        if (LFLAGS && (KC) + 1 < (NK) && ((KC) + 1) % TW == 0)                        \
-            wait_layer(lflag, (((KC) + 1 + rof / 16) % (NK)) / TW, nstore);            \
         if (PAIR && (KC) + 1 == pwl) lds_wait_ge(lflag, 4 * ++xneed);               \
-        if (MBRL_PRIO == 2 && NW == 8) {                                             \
-            if (young != (((KC) & 1) != 0)) __builtin_amdgcn_s_setprio(1);          \
-            else __builtin_amdgcn_s_setprio(0);                                      \
-        }                                                                            \
-        if (MBRL_PRIO == 3 && NW == 8 && (NK) >= 16) {                               \
-            if ((KC) == 0) __builtin_amdgcn_s_setprio(3);                            \
-            if ((KC) == (NK) / 2) __builtin_amdgcn_s_setprio(2);                     \
-            if ((KC) == 3 * (NK) / 4) __builtin_amdgcn_s_setprio(1);                 \
-            if ((KC) == 7 * (NK) / 8) __builtin_amdgcn_s_setprio(0);                 \
-        }                                                                            \
         if ((KC) + 1 < (NK)) read_a<R>(aAB[((KC) + 1) & 1], IN, lda, (KC) + 1, lane); \
         mma_hidden<TW, R>(acc, aAB[(KC) & 1], ring[SLOT]);                           \
-        interleave_loads<TW, R>();                                                   \
         MBRL_PIN();                                                                  \
         ++g;                                                                         \
     } while (0)
 
-    [[maybe_unused]] const bool young = NW == 8 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256;
-    if constexpr (MBRL_PRIO == 1 && NW == 8) {
-        if (young) __builtin_amdgcn_s_setprio(1);
-    }
     for (int tp = 0; tp < A.H * npass; ++tp) {
         const int t = A.reward ? (tp >> 1) : tp;
         const int pass = A.reward ? (tp & 1) : 0;
@@ -834,7 +719,6 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
                 MBRL_LOAD_CHUNK(ring[((kc % NB) + NB - 1) % NB], g + NB - 1);
                 if (kc + 1 < K0C_T) read_a<R>(aAB[(kc + 1) & 1], actX, lda, kc + 1, lane);
                 if (16 * kc < A.s + A.a) mma_hidden<TW, R>(acc, aAB[kc & 1], ring[kc % NB]);
-                interleave_loads<TW, R>();
                 MBRL_PIN();
                 ++g;
             }
@@ -858,8 +742,6 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
                 for (int kc = 0; kc < K0C_T; ++kc)
                     if (16 * kc < A.s + A.a) mma_hidden<TW, R>(acc, aAB[kc & 1], w0p[kc]);
                 hidden_store<TW, R>(acc, bias, actY, lda, ocw0, lane);
-            } else if constexpr (LFLAGS) {
-                hidden_store_flag<TW, R>(acc, bias, actY, lda, cw, lane, lflag, ++nstore);
             } else {
                 hidden_store<TW, R>(acc, bias, actY, lda, cw, lane);
             }
@@ -873,7 +755,6 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
             load_bias<TW>(bias, L.hbias + l * A.Wpad, cw, lane);
             constexpr int KH = 4 * T;  // 4T % NB == 0: every hidden layer starts on the same slot
             constexpr int S0 = RING ? K0C_T % NB : 0;
-            if constexpr (LFLAGS) wait_layer(lflag, (rof / 16) / TW, nstore);
             pwl = (L0DUP && l == 1) ? -1 : pwait;                   // layer 0's partner columns are local
             // K position kc reads chunk kc + rof/16 (kc < 2T) or kc - rof/16 (kc >= 2T): two bases
             const float* const inLo = in + rof;
@@ -882,10 +763,7 @@ __global__ void __launch_bounds__(64 * NW, 1) rollout_kernel(const RolloutArgs A
 #pragma unroll
             for (int kc = 0; kc < KH; ++kc) MBRL_HIDDEN_CHUNK((S0 + kc) % NB, kc, KH, (kc + 1 < KH / 2 ? inLo : inHi));
             STAMP(2);
-            if (l + 1 < A.L) {
-                if constexpr (LFLAGS) hidden_store_flag<TW, R>(acc, bias, out, lda, cw, lane, lflag, ++nstore);
-                else hidden_store<TW, R>(acc, bias, out, lda, cw, lane);
-            }
+            if (l + 1 < A.L) hidden_store<TW, R>(acc, bias, out, lda, cw, lane);
             STAMP(3);
             float* tmp = in; in = out; out = tmp;
         }
@@ -1080,10 +958,10 @@ static hipError_t launch_rollout_t(const RolloutArgs& A, hipStream_t stream) {
     // two waves per SIMD (8 waves, T/2 tiles each) where the tile count and LDS allow it: always for
     // R = 1; for R = 2 when the launcher asks (A.nw == 8: the aliased partials fit LDS)
     // (16 waves, T/4 tiles each, measured 8 % slower than 8: the 128-VGPR budget spills)
-    if constexpr (R == 2 && T >= 2 && MBRL_ROLLOUT_NW >= 8) {
+    if constexpr (R == 2 && T >= 2) {
         if (A.nw == 8) return launch_rollout_tn<T, R, 8>(A, stream);
     }
-    constexpr int NW = (T >= 2 && R == 1 && MBRL_ROLLOUT_NW >= 8) ? 8 : 4;
+    constexpr int NW = (T >= 2 && R == 1) ? 8 : 4;
     return launch_rollout_tn<T, R, NW>(A, stream);
 }
 
@@ -1193,21 +1071,13 @@ __global__ void __launch_bounds__(64 * m8_waves(T, NOT_T), 1) rollout_m8_kernel(
     // chunk 2o, odd blocks 2o + 1: no idle half); wider outputs pair two tiles per K chunk
     constexpr bool KPAIR = NOT8 == 1;
     constexpr int NOC = KPAIR ? 2 : 4 * NOP;
-#ifdef MBRL_M8_NB
-    constexpr int NB = MBRL_M8_NB;           // A/B override
-#else
     constexpr int NB = 4;                    // ring slots (16 VGPRs each), 3 chunks ahead: 1 % faster than 8
-#endif                                       // (walker 2048-candidate shard, tools/ab.sh, r01)
+                                             // (walker 2048-candidate shard, tools/ab.sh, r01)
     constexpr int DUM = (NB - (K0C_T + NOC) % NB) % NB;
     constexpr int TW16 = T / 2;              // the 16-candidate kernel's K chunks per output partial
     constexpr int NPW = (FPW / 16) / TW16;   // its partials inside this wave's own chunks
     constexpr int SS = NOT_T;
     static_assert(KH % NB == 0 && (T == 4 || T == 8), "m8 geometry");
-    // hidden-layer hand-offs by per-wave flags, as in rollout_kernel (wave w produces K chunks
-    // [CPW w, CPW (w + 1)) of the next layer)
-    constexpr bool LFLAGS = MBRL_LAYER_FLAGS;
-    constexpr int CPW = FPW / 16;
-    uint32_t nstore = 0;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const LdsMap L = lds_map(A, smem, M);
     uint32_t* const lflag = L.lflag;
@@ -1353,17 +1223,8 @@ __global__ void __launch_bounds__(64 * m8_waves(T, NOT_T), 1) rollout_m8_kernel(
             *reinterpret_cast<f32x4*>(out + cand * lda + FPW * wave + 32 * u + 4 * (lane >> 3)) = v;
         }
     };
-    // a stored layer another wave reads: publish it (flags) or wait for every wave (barrier)
-    auto publish_layer = [&]() {
-        if constexpr (LFLAGS) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            ++nstore;
-            if (lane == 0) *reinterpret_cast<volatile uint32_t*>(lflag + wave) = nstore;
-            asm volatile("" ::: "memory");
-        } else {
-            __syncthreads();
-        }
-    };
+    // a stored layer another wave reads: wait for every wave (barrier)
+    auto publish_layer = [&]() { __syncthreads(); };
     auto load_bias8 = [&](const float* hb) {
 #pragma unroll
         for (int u = 0; u < TPW; ++u)
@@ -1374,25 +1235,15 @@ __global__ void __launch_bounds__(64 * m8_waves(T, NOT_T), 1) rollout_m8_kernel(
         for (int u = 0; u < TPW; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
     };
 // one hidden-type chunk: refill the slot chunk c-1 vacated, read the next chunk's B, MFMAs of chunk c
-#define M8_CHUNK(SLOT, KC, NK, IN, FL)                                      \
+#define M8_CHUNK(SLOT, KC, NK, IN)                                          \
     do {                                                                    \
         M8_LOAD(((SLOT) + NB - 1) % NB, g + NB - 1);                         \
-        if (LFLAGS && (FL) && (KC) + 1 < (NK) && ((KC) + 1) % CPW == 0)      \
-            wait_layer(lflag, (((KC) + 1 + rofc) % (NK)) / CPW, nstore);     \
-        if (MBRL_PRIO == 2 && NW == 8) {                                    \
-            if (young != (((KC) & 1) != 0)) __builtin_amdgcn_s_setprio(1); \
-            else __builtin_amdgcn_s_setprio(0);                             \
-        }                                                                   \
         if ((KC) + 1 < (NK)) read_b(bb[((KC) + 1) & 1], IN, 16 * ((KC) + 1)); \
         mma_pair(ring[SLOT], bb[(KC) & 1]);                                 \
         MBRL_PIN();                                                         \
         ++g;                                                                \
     } while (0)
 
-    [[maybe_unused]] const bool young = NW == 8 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256;
-    if constexpr (MBRL_PRIO == 1 && NW == 8) {
-        if (young) __builtin_amdgcn_s_setprio(1);
-    }
     for (int t = 0; t < A.H; ++t) {
         int g = 0;
         if (actw && t + 1 < A.H) fetch_a(t + 1);
@@ -1413,7 +1264,7 @@ __global__ void __launch_bounds__(64 * m8_waves(T, NOT_T), 1) rollout_m8_kernel(
             ++g;
         } else {
 #pragma unroll
-            for (int kc = 0; kc < K0C_T; ++kc) M8_CHUNK(kc % NB, kc, K0C_T, actX, false);
+            for (int kc = 0; kc < K0C_T; ++kc) M8_CHUNK(kc % NB, kc, K0C_T, actX);
         }
         STAMP(0);
         store_layer(actY);
@@ -1424,13 +1275,12 @@ __global__ void __launch_bounds__(64 * m8_waves(T, NOT_T), 1) rollout_m8_kernel(
         for (int l = 1; l < A.L; ++l) {
             zero_acc8();
             load_bias8(L.hbias + l * A.Wpad);
-            if constexpr (LFLAGS) wait_layer(lflag, rofc / CPW, nstore);
             // the half-rotated K order (rollout_kernel): position kc reads chunk (kc + rofc) mod KH
             const float* const inLo = in + 16 * rofc;
             const float* const inHi = in - 16 * rofc;
             read_b(bb[0], inLo, 0);
 #pragma unroll
-            for (int kc = 0; kc < KH; ++kc) M8_CHUNK((K0C_T + kc) % NB, kc, KH, (kc + 1 < KH / 2 ? inLo : inHi), true);
+            for (int kc = 0; kc < KH; ++kc) M8_CHUNK((K0C_T + kc) % NB, kc, KH, (kc + 1 < KH / 2 ? inLo : inHi));
             STAMP(2);
             store_layer(out);
             if (l + 1 < A.L) publish_layer();   // the last hidden layer is read back by its own wave only

@@ -322,15 +322,7 @@ __device__ __forceinline__ f32x4 load_operand(const GemmLaunch& L, const Operand
     return v;
 }
 
-// The second of a wave's two K chunks through LDS (MBRL_TRAIN_GLDS): load_operand's elements, issued as
-// direct-to-LDS loads (global_load_lds: no VGPR destination) into the wave's own 1 KB fragment slot, so
-// both chunks travel together at the 16-wave budget of 128 VGPRs; read back with the same predicates.
-// A whole-row 16-byte load where load_operand would take one (every lane's 4 columns inside K), else one
-// 4-byte load per element; a lane with nothing to read points at the operand's first element and its
-// value is replaced on the way back. The LDS destination is the slot base + lane x size (wave-uniform base).
-#ifndef MBRL_TRAIN_GLDS
-#define MBRL_TRAIN_GLDS 0
-#endif
+// Whether a lane's 4 columns of chunk kb lie inside K on a row-contiguous operand: one 16-byte load.
 template <int KIND>
 __device__ __forceinline__ bool staged_vec(const Operand& o, int kb, int K) {
     return KIND == OP_DIRECT && o.vec && kb + 16 <= K;
@@ -372,42 +364,6 @@ __device__ __forceinline__ f32x4 mask_raw(const Operand& o, int i, int kb, int k
 #pragma unroll
         for (int e = 0; e < 4; ++e)
             if (!(k0 + e < K)) v[e] = 0.0f;
-    return v;
-}
-
-template <int KIND>
-__device__ __forceinline__ void stage_operand(const GemmLaunch& L, const Operand& o, int i, int kb, int k0, int K,
-                                              float* slot) {
-    const bool row_ok = i < o.rows && i != o.ones_row;
-    if (staged_vec<KIND>(o, kb, K)) {
-        const float* g = row_ok ? storage_row(o, i) + k0 : o.p0;
-        __builtin_amdgcn_global_load_lds(g, slot, 16, 0, 0);
-        return;
-    }
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        const float* g = o.p0;
-        if (row_ok && k0 + e < K) {
-            if constexpr (KIND == OP_DIRECT) g = storage_row(o, i) + k0 + e;
-            else g = storage_row(o, k0 + e) + i;
-        }
-        __builtin_amdgcn_global_load_lds(g, slot + 64 * e, 4, 0, 0);
-    }
-}
-
-template <int KIND>
-__device__ __forceinline__ f32x4 read_staged(const Operand& o, int i, int kb, int k0, int K, const float* slot, int lane) {
-    f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
-    if (i >= o.rows) return v;
-    if (i == o.ones_row) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = k0 + e < K ? 1.0f : 0.0f;
-        return v;
-    }
-    if (staged_vec<KIND>(o, kb, K)) return *reinterpret_cast<const f32x4*>(slot + 4 * lane);
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-        if (k0 + e < K) v[e] = slot[64 * e + lane];
     return v;
 }
 
@@ -535,53 +491,6 @@ __device__ __forceinline__ void gemm_tile(const GemmLaunch& L, int tile, float (
     constexpr int GROUP = NW == 16 ? (TMX == 2 ? 1 : 2) : NW == 8 ? 2 : 4;   // TMX 2 at 16 waves: the 128-VGPR budget
     int g0 = kb0;
     constexpr bool RAW = AK != OP_GATHER && BK != OP_GATHER;   // branch-free loads (load_raw / mask_raw)
-    if constexpr (NW == 16 && TMX == 2 && RAW && MBRL_TRAIN_GLDS) {
-        if (kb1 - kb0 > 16 && kb1 - kb0 <= 32) {
-            // the wave's two chunks at once: the first into registers, the second into LDS (its own
-            // slot of red, which it overwrites with its partials only after reading it back); the
-            // first chunk's use waits for both (vmcnt(0)), so the two latencies overlap
-            float* const slot = &red[wave][0][0];
-            const int kb = kb0 + 16;
-            // the LDS-bound loads first: they are branch-free, while the register loads' per-element
-            // guards become branches whose join points hipcc closes with vmcnt(0) -- which then also
-            // waits for these, already in flight
-#pragma unroll
-            for (int x = 0; x < 2 * TMX; ++x) stage_operand<AK>(L, D.A, m0 + 16 * x + c, kb, kb + 4 * q, D.K, slot + 256 * x);
-#pragma unroll
-            for (int y = 0; y < 2; ++y)
-                stage_operand<BK>(L, D.B, n0 + 16 * y + c, kb, kb + 4 * q, D.K, slot + 256 * (2 * TMX + y));
-            f32x4 a[2 * TMX], b[2];
-#pragma unroll
-            for (int x = 0; x < 2 * TMX; ++x) a[x] = load_raw<AK>(D.A, m0 + 16 * x + c, kb0, kb0 + 4 * q, D.K);
-#pragma unroll
-            for (int y = 0; y < 2; ++y) b[y] = load_raw<BK>(D.B, n0 + 16 * y + c, kb0, kb0 + 4 * q, D.K);
-#pragma unroll
-            for (int x = 0; x < 2 * TMX; ++x) a[x] = mask_raw<AK>(D.A, m0 + 16 * x + c, kb0, kb0 + 4 * q, D.K, a[x]);
-#pragma unroll
-            for (int y = 0; y < 2; ++y) b[y] = mask_raw<BK>(D.B, n0 + 16 * y + c, kb0, kb0 + 4 * q, D.K, b[y]);
-#pragma unroll
-            for (int s = 0; s < 4; ++s)
-#pragma unroll
-                for (int x = 0; x < 2 * TMX; ++x)
-#pragma unroll
-                    for (int y = 0; y < 2; ++y)
-                        acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[x][s], b[y][s], acc[x][y], 0, 0, 0);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-            for (int x = 0; x < 2 * TMX; ++x) a[x] = read_staged<AK>(D.A, m0 + 16 * x + c, kb, kb + 4 * q, D.K, slot + 256 * x, lane);
-#pragma unroll
-            for (int y = 0; y < 2; ++y)
-                b[y] = read_staged<BK>(D.B, n0 + 16 * y + c, kb, kb + 4 * q, D.K, slot + 256 * (2 * TMX + y), lane);
-#pragma unroll
-            for (int s = 0; s < 4; ++s)
-#pragma unroll
-                for (int x = 0; x < 2 * TMX; ++x)
-#pragma unroll
-                    for (int y = 0; y < 2; ++y)
-                        acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[x][s], b[y][s], acc[x][y], 0, 0, 0);
-            g0 = kb1;
-        }
-    }
     for (; g0 < kb1; g0 += 16 * GROUP) {
         f32x4 a[GROUP][2 * TMX], b[GROUP][2];
 #pragma unroll

@@ -40,7 +40,7 @@ OPTIONS = {"rollout_tile": 0, "split_tile": 1, "debug_traj_abort": 2, "gd_single
            "rollout_pair": 10, "shard_emulate": 11, "debug_pair_abort": 12,
            "traj_hop": 13, "gd_hop": 14, "pair_l2": 15,
            "train_xcd": 16, "train_split": 17, "debug_shard_fail": 18, "train_fo": 19,
-           "debug_shard_fail_rank": 20}
+           "debug_shard_fail_rank": 20, "update_split": 21}
 
 
 def precision_code(name):

@@ -219,4 +219,16 @@ def test_shard_options_and_peer_status_code():
         assert lib.mbrl_get_option(_lib.OPTIONS["debug_shard_fail_rank"]) == 4
     hdr = open(os.path.join(REPO, "include", "mbrl_cem.h")).read()
     assert "MBRL_EPEER = -5" in hdr and _lib.MBRL_EPEER == -5
-    assert "MBRL_OPT_DEBUG_SHARD_FAIL_RANK = 20" in hdr and "MBRL_OPT_COUNT = 21" in hdr
+    assert "MBRL_OPT_DEBUG_SHARD_FAIL_RANK = 20" in hdr and "MBRL_OPT_COUNT = 22" in hdr
+
+
+def test_every_compile_time_variant_still_compiles():
+    """The kept compile-time variants (stamp builds and the rollout's timing ablations, Makefile
+    `variants`) compile against the current sources, so none of them rots unseen."""
+    import shutil
+    if shutil.which("hipcc") is None and not os.path.exists("/opt/rocm/bin/hipcc"):
+        pytest.skip("no hipcc")
+    r = subprocess.run(["make", "-s", "-C", os.path.join(REPO, "mujoco-mbrl_amd"), "variants"],
+                       capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert " error" not in r.stderr, r.stderr[-2000:]

@@ -124,3 +124,30 @@ def test_cem_update_abi_against_the_oracle_random_shapes(case):
     assert np.array_equal(mu_o.cpu().numpy(), m2) and np.array_equal(sg_o.cpu().numpy(), s2)
     nref = cem_actions(m2, s2, -1.0, 1.0, seed, it + 1, np.arange(off, off + cnt))
     assert np.array_equal(nxt.cpu().numpy(), nref)
+
+
+# the split update (cem_select_regen_kernel + cem_refit_draw_kernel: the elites' regeneration shared
+# out over the row's workgroups) forced on and off: walker at full N (where auto takes it), cheetah,
+# cartpole, the reward head, degenerate sizes (one candidate; every candidate an elite; K < S)
+@pytest.mark.parametrize("cid,N,H,K,I", [(4, 16384, 6, None, 3), (3, 4096, 30, None, 3), (2, 1024, 20, None, 3),
+                                          (6, 512, 8, None, 2), (3, 1, 2, 1, 2), (3, 17, 3, 17, 2), (2, 33, 4, 5, 3)])
+def test_split_update_plan_equals_one_launch_update(cid, N, H, K, I):
+    from mbrl_amd import CEMPlanner, _lib
+    p = ocem.synth_problem(cid, N=N, H=H)
+    _, model_fn, cost_fn, sample_action = build(p)
+    kw = dict(num_candidates=N, num_iterations=I)
+    if K is not None:
+        kw["num_elites"] = K
+    out = {}
+    for split in (0, 1, 2):
+        with _lib.option("update_split", split):
+            out[split] = CEMPlanner.plan_detailed(torch.from_numpy(p["s0"]), model_fn, cost_fn, sample_action, H,
+                                                  seed=p["rng_seed"], record=True, **kw)
+    for split in (0, 2):
+        for k in ("returns", "elites", "mu", "sigma", "actions", "states"):
+            a, b = out[split][k], out[1][k]
+            if isinstance(a, (list, tuple)):
+                for it, (x, y) in enumerate(zip(a, b)):
+                    assert torch.equal(torch.as_tensor(x), torch.as_tensor(y)), (split, k, it)
+            else:
+                assert torch.equal(torch.as_tensor(a), torch.as_tensor(b)), (split, k)

@@ -167,3 +167,13 @@ def test_a_failed_peer_is_reported_on_every_rank(cid, N, H, world):
         else:
             assert f"({_lib.MBRL_EPEER})" in msg and f"rank(s) {bad} failed during this plan" in msg, msg
     _assert_same(_emulated_mode(prob, st, s0, world, 0, 1), ref, (cid, world, "after"))
+
+
+def test_sharded_plan_with_the_split_update_forced_both_ways():
+    """The sharded plan's update over all N (walker N = 16384 at G = 8: K = 1638, where auto splits it)
+    with the split update forced off and on: every rank id equal to the single-GPU plan."""
+    prob, st, s0 = _problem(4, 16384, 30)
+    ref = _single(prob, st, s0)
+    for split in (1, 2):
+        for rank in (0, 7):
+            _assert_same(_emulated_mode(prob, st, s0, 8, rank, 1, update_split=split), ref, ("split", split, rank))

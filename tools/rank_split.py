@@ -30,31 +30,38 @@ sys.path[:0] = [REPO, os.path.join(REPO, "mujoco-mbrl_amd")]
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-from bench import ITERATIONS, TimingEvent  # noqa: E402
+from bench import ITERATIONS, MEASURED_IT, TimingEvent  # noqa: E402
 from mbrl_amd import CEMPlanner, _lib, fused, planners, synthetic  # noqa: E402
 
 ALLGATHER_US = (10.0, 25.0, 40.0)
+T1_MS = None   # --t1-ms: the single-GPU plan's time given (profiling runs time the rank's plan only)
 
 
 def _time(fn, plans, warmup):
+    """fn(plan_events, rollout_events): warm-up, then `plans` timed calls; the plan's device span and
+    iteration MEASURED_IT's rollout launch from fence-free events (as bench.py)."""
     for _ in range(warmup):
-        fn()
+        fn(None, None)
     torch.cuda.synchronize()
     pev = [(TimingEvent(), TimingEvent()) for _ in range(plans)]
-    for a, b in pev:
-        a.record()
-        b.record()
+    rev = [[(TimingEvent(), TimingEvent()) if it == MEASURED_IT else None for it in range(ITERATIONS)]
+           for _ in range(plans)]
+    for pair in pev + [r[MEASURED_IT] for r in rev]:
+        pair[0].record()
+        pair[1].record()
     torch.cuda.synchronize()
     walls = []
     t0 = time.perf_counter()
     for k in range(plans):
         t = time.perf_counter()
-        fn(pev[k])
+        fn(pev[k], rev[k])
         walls.append(time.perf_counter() - t)
     elapsed = time.perf_counter() - t0
     torch.cuda.synchronize()
     span = float(np.mean([a.elapsed_time(b) for a, b in pev]))
-    return dict(ms_per_plan=elapsed / plans * 1e3, plan_gpu_ms=span, wall_median_ms=float(np.median(walls)) * 1e3)
+    roll = float(np.mean([r[MEASURED_IT][0].elapsed_time(r[MEASURED_IT][1]) for r in rev]))
+    return dict(ms_per_plan=elapsed / plans * 1e3, plan_gpu_ms=span, wall_median_ms=float(np.median(walls)) * 1e3,
+                rollout_ms=roll)
 
 
 def row(cid, world, n_total, plans, warmup, dev, mode):
@@ -70,13 +77,14 @@ def row(cid, world, n_total, plans, warmup, dev, mode):
     s0_host = p["s0"].cpu().float()
     s0_dev = s0_host.to(dev)
 
-    def single(pev=None):
-        return planners._cem_fused_single(prob, s0_host, dict(st, plan_events=pev))
+    def single(pev, rev):
+        return planners._cem_fused_single(prob, s0_host, dict(st, plan_events=pev, events=rev))
 
     rank = world - 1   # every rank does the same work; the last one's shard is the last candidates
 
-    def sharded(pev=None):
-        return planners._cem_sharded_native(prob, s0_host, dict(st, plan_events=pev), world, rank, comm=None)
+    def sharded(pev, rev):
+        return planners._cem_sharded_native(prob, s0_host, dict(st, plan_events=pev, events=rev), world, rank,
+                                            comm=None)
 
     # bit-identity first: mode 1 (keeps the gathered costs), then mode 2, against the single-GPU plan
     ref = planners._cem_fused_single(prob, s0_dev, st_rec)
@@ -87,7 +95,7 @@ def row(cid, world, n_total, plans, warmup, dev, mode):
         for k in ("elites", "mu", "sigma", "actions", "states"):
             assert torch.equal(torch.as_tensor(got[k]).cpu(), torch.as_tensor(ref[k]).cpu()), (cid, world, k)
         t_rank = _time(sharded, plans, warmup)
-    t_one = _time(single, plans, warmup)
+    t_one = _time(single, plans, warmup) if T1_MS is None else dict(ms_per_plan=T1_MS, given=True)
     out = dict(config=cid, workload=cfg["name"], mode=mode, gpus=world, rank=rank, N=n_total,
                candidates_per_rank=n_total // world, K=K, H=H, E=E, rank_plan=t_rank, single_gpu_plan=t_one,
                bit_identical=True, allgather_us_assumed=list(ALLGATHER_US))
@@ -110,7 +118,14 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--n-local", type=int, default=None, help="weak mode: candidates per rank (default config N)")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--t1-ms", type=float, default=None, help="strong mode: the single-GPU plan's ms (not timed)")
+    ap.add_argument("--option", action="append", default=[], help="NAME=VALUE: an mbrl_set_option for the run (A/B)")
     args = ap.parse_args()
+    for o in args.option:
+        name, val = o.split("=")
+        _lib.load().mbrl_set_option(_lib.OPTIONS[name], int(val))
+    global T1_MS
+    T1_MS = args.t1_ms
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     f = open(args.out, "a") if args.out else None
@@ -132,14 +147,25 @@ def main():
                         num_candidates=n_local, num_elites=n_local // 10, num_iterations=ITERATIONS,
                         seed=p["rng_seed"], device=dev))
                     s0 = p["s0"].cpu().float()
-                    base_one = _time(lambda pev=None: planners._cem_fused_single(prob, s0, dict(st, plan_events=pev)),
+                    base_one = _time(lambda pev, rev: planners._cem_fused_single(prob, s0, dict(st, plan_events=pev,
+                                                                                                 events=rev)),
                                      plans, min(args.warmup, plans))
                 r["one_gpu_n_local_plan"] = base_one
                 r["projected_weak_efficiency"] = {
                     f"{a:g}us": base_one["ms_per_plan"] / (r["rank_plan"]["ms_per_plan"] + ITERATIONS * a / 1e3)
                     for a in ALLGATHER_US}
+            if args.option:
+                r["options"] = args.option
             line = json.dumps(r)
             print(line, flush=True)
+            # a bench.py-shaped line for tools/plan_timeline.py (rocprofv3 runs of this tool)
+            rp = r["rank_plan"]
+            flop = r["candidates_per_rank"] * r["H"] * synthetic.flop_per_candidate_step(cfg)
+            print(json.dumps({"metric": "rank plan", "ms_per_step": rp["ms_per_plan"],
+                              "config": {"workload": f"{cfg['name']} N={r['N']} G={world} rank {r['rank']}",
+                                         "candidates_per_gpu": r["candidates_per_rank"]},
+                              "roofline": {"avg_launch_ms": rp["rollout_ms"],
+                                           "frac": flop / (rp["rollout_ms"] * 1e-3) / 1e12 / 157.3}}), flush=True)
             if f:
                 f.write(line + "\n")
                 f.flush()
