@@ -704,26 +704,43 @@ __device__ __forceinline__ void select_reg_body(const float* __restrict__ costs,
 #pragma unroll
     for (int g = 0; g < KPT / VW; ++g) {
         // the group's keys in candidate order: lanes ascending, and inside a lane its vw keys
-        uint64_t bl[VW], be[VW];
-        uint32_t ll = 0, le = 0;   // this group's keys before this lane's
+        uint64_t bl[VW], be[VW], beany = 0;
 #pragma unroll
         for (int i = 0; i < VW; ++i) {
             bl[i] = __ballot(key[VW * g + i] < prefix);
             be[i] = __ballot(key[VW * g + i] == prefix);
-            ll += below(bl[i]);
-            le += below(be[i]);
+            beany |= be[i];
         }
         if (vw == VW) {
+            uint32_t ll = 0;   // this group's keys below the prefix in lanes before this one
 #pragma unroll
-            for (int i = 0; i < VW; ++i) {
-                const uint32_t k = key[VW * g + i];
-                if (k < prefix) {
-                    const uint32_t pos = lt_b + ll + min(eq_b + le, kk);
-                    if (pos < (uint32_t)K) emit(pos, idx(VW * g + i));
-                    ++ll;
-                } else if (k == prefix) {
-                    if (eq_b + le < kk && lt_b + ll + eq_b + le < (uint32_t)K) emit(lt_b + ll + eq_b + le, idx(VW * g + i));
-                    ++le;
+            for (int i = 0; i < VW; ++i) ll += below(bl[i]);
+            if (beany == 0) {
+                // (the usual group: no key equal to the K-th, so every elite here is below it)
+                const uint32_t base = lt_b + ll + min(eq_b, kk);
+                uint32_t own = 0;
+#pragma unroll
+                for (int i = 0; i < VW; ++i)
+                    if (key[VW * g + i] < prefix) {
+                        if (base + own < (uint32_t)K) emit(base + own, idx(VW * g + i));
+                        ++own;
+                    }
+            } else {
+                uint32_t le = 0;
+#pragma unroll
+                for (int i = 0; i < VW; ++i) le += below(be[i]);
+#pragma unroll
+                for (int i = 0; i < VW; ++i) {
+                    const uint32_t k = key[VW * g + i];
+                    if (k < prefix) {
+                        const uint32_t pos = lt_b + ll + min(eq_b + le, kk);
+                        if (pos < (uint32_t)K) emit(pos, idx(VW * g + i));
+                        ++ll;
+                    } else if (k == prefix) {
+                        if (eq_b + le < kk && lt_b + ll + eq_b + le < (uint32_t)K)
+                            emit(lt_b + ll + eq_b + le, idx(VW * g + i));
+                        ++le;
+                    }
                 }
             }
 #pragma unroll
@@ -881,8 +898,18 @@ __device__ __forceinline__ void refit_sums(int t, float* smem, float lo, float h
         __syncthreads();
         if ((int)threadIdx.x < a) {
             const int d = threadIdx.x;
+            // the chunk partials in sequence, eight LDS reads in flight at a time (the same additions
+            // in the same order: a dependent read per partial cost ~2 us per pass at walker's 52 chunks)
             float tot = part[d];
-            for (int c = 1; c < nch; ++c) tot = __fadd_rn(tot, part[c * a + d]);
+            int c = 1;
+            for (; c + 8 <= nch; c += 8) {
+                float v[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) v[q] = part[(c + q) * a + d];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) tot = __fadd_rn(tot, v[q]);
+            }
+            for (; c < nch; ++c) tot = __fadd_rn(tot, part[c * a + d]);
             const float m = __fdiv_rn(tot, (float)K);
             if (pass == 0) {
                 mean[d] = m;
@@ -1312,7 +1339,8 @@ static int rollout_validate(const Geometry& g, const mbrl_norm* norm, const mbrl
 static int rollout_impl(const Geometry& g, const void* packed, const mbrl_norm* norm, const mbrl_cost* cost,
                         const float* s0, int s0_per_cand, const float* actions, const mbrl_sampler* sampler,
                         int N, int H, int n_offset, float* costs, float* actions_out, float* states_out,
-                        hipStream_t stream, void* pair_area = nullptr, unsigned* pair_epoch = nullptr) {
+                        hipStream_t stream, void* pair_area = nullptr, unsigned* pair_epoch = nullptr,
+                        const unsigned** pair_status_out = nullptr) {
     if (!packed || !s0 || !costs) return fail(MBRL_EINVAL, "packed, s0 and costs must be non-NULL");
     if (N < 1 || H < 1) return fail(MBRL_EINVAL, "N=%d H=%d must be >= 1", N, H);
     if (!actions && !sampler) return fail(MBRL_EINVAL, "need either actions or a sampler");
@@ -1426,6 +1454,13 @@ static int rollout_impl(const Geometry& g, const void* packed, const mbrl_norm* 
                 P.pair_base = (P.pair_epoch - 1) * qs;
                 const hipError_t err = launch_rollout_pair(P, g.T, stream);
                 if (err == hipSuccess && dpa == 2) return MBRL_OK;   // tests: the pair launch's own results
+                if (err == hipSuccess && pair_status_out && P.pair_prezeroed) {
+                    // the caller checks the plan's pair status word once, after the plan (a sharded plan
+                    // with peers: it redoes the whole plan without pairs if any hand-off timed out), so
+                    // no gated redo launch follows each pair launch
+                    *pair_status_out = P.pair_flags + (size_t)2 * ntiles * g.E * 32;
+                    return MBRL_OK;
+                }
                 if (err == hipSuccess) {
                     // A pair's halves wait on each other, and a plain launch does not promise that both
                     // are resident (another stream may hold CUs): a wait that timed out raised the status
@@ -2308,13 +2343,17 @@ int mbrl_comm_destroy(mbrl_comm_t comm) {
 // slot from its own costs, every other slot from the costs a mode-1 plan kept for this iteration --
 // and the gathered status words (this rank's own, the others clear).
 __global__ void emu_gather_kernel(const float* __restrict__ local, const float* __restrict__ kept, int G, int rank,
-                                  size_t slot, const unsigned* __restrict__ own_status, float* __restrict__ gathered,
+                                  size_t slot, const unsigned* __restrict__ own_status,
+                                  const unsigned* __restrict__ own_pair, float* __restrict__ gathered,
                                   unsigned* __restrict__ peer) {
     const size_t total = (size_t)G * slot, lo = (size_t)rank * slot;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x)
         gathered[i] = (i >= lo && i < lo + slot) ? local[i - lo] : kept[i];
     if (blockIdx.x == 0)
-        for (int r = threadIdx.x; r < G; r += blockDim.x) peer[r] = r == rank ? *own_status : 0u;
+        for (int r = threadIdx.x; r < G; r += blockDim.x) {
+            peer[r] = r == rank ? *own_status : 0u;
+            peer[G + r] = (r == rank && own_pair) ? *own_pair : 0u;
+        }
 }
 
 struct ShardWs {
@@ -2323,7 +2362,8 @@ struct ShardWs {
                           // in mode 2 as well, so both modes place emu_kept alike)
     float* emu_kept;      // MBRL_OPT_SHARD_EMULATE: [I][G][E][Nl] every iteration's gathered costs (mode 1
                           // writes them, mode 2 reads the other ranks' slots back)
-    unsigned* peer;       // [G] the ranks' status words, gathered with the last iteration's costs
+    unsigned* peer;       // [2G] the ranks' status words, then their pair status words, gathered with the
+                          // last iteration's costs
     void* pair;
     unsigned long long* xchg;
     unsigned* status;
@@ -2357,7 +2397,7 @@ static ShardWs shard_ws(const Geometry& g, const mbrl_cem_params* p, int G, void
     w.keys = (uint32_t*)take((size_t)p->N * 4);
     w.s0 = (float*)take((size_t)g.s * 4);
     w.pair = take(pair_area_bytes(g, Nl));
-    w.peer = (unsigned*)take((size_t)G * 4);
+    w.peer = (unsigned*)take((size_t)2 * G * 4);
     const int emu = shard_emulation();
     w.emu_actions = (float*)take(emu != 0 && G > 1 ? (size_t)p->H * Nl * g.a * 4 : 0);
     w.emu_kept = (float*)take(emu != 0 && G > 1 ? (size_t)p->iterations * g.E * p->N * 4 : 0);
@@ -2380,7 +2420,8 @@ static int plan_sharded_body(const mbrl_mlp_shape* shape, const void* packed, co
                              const mbrl_cost* cost, const float* s0_in, const mbrl_cem_params* p, mbrl_comm_t comm,
                              int32_t nranks, int32_t rank, float* mu, float* sigma, float* actions_out,
                              float* states_out, float* cost_hist, float* returns_hist, int64_t* elite_hist,
-                             mbrl_event_t* rollout_events, void* workspace, size_t ws_bytes, hipStream_t stream) {
+                             mbrl_event_t* rollout_events, void* workspace, size_t ws_bytes, hipStream_t stream,
+                             bool allow_pairs = true) {
     Geometry g;
     int rc = shape_geometry(shape, &g);
     if (rc) return rc;
@@ -2428,10 +2469,17 @@ static int plan_sharded_body(const mbrl_mlp_shape* shape, const void* packed, co
         return err == MBRL_OK;
     };
     unsigned* own_status = w.status + 1;   // [0] is the trajectory kernel's; zeroed with it below
+    unsigned* zero_word = w.status + 2;    // stays 0: the pair status gathered when no pair launch ran
+    // With peers the plan checks its column-split pair launches once, after the plan (the pair status
+    // word, gathered with the last iteration's costs): any hand-off that timed out on any rank sends
+    // every rank through the whole plan again without pairs. No gated redo launch per iteration.
+    void* const pair_ws = allow_pairs ? w.pair : nullptr;
+    const unsigned* pair_status = nullptr;
+    const unsigned** const defer = nranks > 1 ? &pair_status : nullptr;
     // one first launch: distribution rows, the workspace copy of s0, iteration 0's proposals of this
     // shard (global candidates [off, off + Nl)), the hand-off words and this rank's status zeroed
     const InitZero z = plan_zero(g, Nl, w.pair, w.xchg, w.xchg_bytes, w.status);
-    if (!z.ptr[1]) step(hip_check(hipMemsetAsync(own_status, 0, sizeof(unsigned), stream), "status memset"));
+    if (!z.ptr[1]) step(hip_check(hipMemsetAsync(own_status, 0, 2 * sizeof(unsigned), stream), "status memset"));
     hipLaunchKernelGGL(cem_init_kernel, dim3(H * (fuse_draw ? draw_slices(H, 1, Nl, a) : 1), 1), dim3(1024), 0, stream,
                        p->seed, p->init_mu, p->init_sigma, p->lo, p->hi, H, a, Nl, w.mu[0], w.sigma[0],
                        fuse_draw ? w.actions : nullptr, s0_in, g.s, w.s0, off, z);
@@ -2452,7 +2500,8 @@ static int plan_sharded_body(const mbrl_mlp_shape* shape, const void* packed, co
             step(hip_check(hipEventRecord(reinterpret_cast<hipEvent_t>(rollout_events[2 * it]), stream), "event"));
         if (err == MBRL_OK)
             step(rollout_impl(g, packed, norm, cost, w.s0, 0, w.actions, nullptr, Nl, H, 0, w.local, nullptr, nullptr,
-                              stream, pair_area_bytes(g, Nl) ? w.pair : nullptr, z.ptr[0] ? &pair_epoch : nullptr));
+                              stream, pair_area_bytes(g, Nl) ? pair_ws : nullptr, z.ptr[0] ? &pair_epoch : nullptr,
+                              defer));
         if (err == MBRL_OK && it == fail_it && fail_rank == rank)
             step(fail(MBRL_EHIP, "plan_sharded: injected launch failure at iteration %d (MBRL_OPT_DEBUG_SHARD_FAIL)", it));
         if (err == MBRL_OK && rollout_events && rollout_events[2 * it + 1])
@@ -2474,6 +2523,8 @@ static int plan_sharded_body(const mbrl_mlp_shape* shape, const void* packed, co
             step(nccl_check(R.all_gather(w.local, w.gathered, slot, ncclFloat, c, stream), "ncclAllGather"));
             if (last) {
                 step(nccl_check(R.all_gather(own_status, w.peer, 1, ncclUint32, c, stream), "ncclAllGather status"));
+                step(nccl_check(R.all_gather(pair_status ? pair_status : zero_word, w.peer + nranks, 1, ncclUint32, c,
+                                             stream), "ncclAllGather pair status"));
                 step(nccl_check(R.group_end(), "ncclGroupEnd"));
             }
         } else if (err == MBRL_OK && nranks == 1) {
@@ -2482,7 +2533,7 @@ static int plan_sharded_body(const mbrl_mlp_shape* shape, const void* packed, co
         } else if (err == MBRL_OK && emu_mode == 2) {
             float* kept = w.emu_kept + (size_t)it * nranks * slot;
             hipLaunchKernelGGL(emu_gather_kernel, dim3(256), dim3(256), 0, stream, w.local, kept, nranks, rank, slot,
-                               own_status, w.gathered, w.peer);
+                               own_status, pair_status, w.gathered, w.peer);
             step(hip_check(hipGetLastError(), "emulated gather"));
         } else if (err == MBRL_OK) {
             // rank r's slot: its proposals of this iteration (drawn at its global offset from this
@@ -2496,16 +2547,19 @@ static int plan_sharded_body(const mbrl_mlp_shape* shape, const void* packed, co
                     step(hip_check(hipMemsetAsync(sl, 0xFF, slot * 4, stream), "emulated peer poison"));
                 } else if (step(sample_impl(&sp, H, a, Nl, r * Nl, w.emu_actions, stream))) {
                     step(rollout_impl(g, packed, norm, cost, w.s0, 0, w.emu_actions, nullptr, Nl, H, 0, sl, nullptr,
-                                      nullptr, stream, pair_area_bytes(g, Nl) ? w.pair : nullptr,
+                                      nullptr, stream, pair_area_bytes(g, Nl) ? pair_ws : nullptr,
                                       z.ptr[0] ? &pair_epoch : nullptr));
                 }
             }
             if (last && err == MBRL_OK) {
-                step(hip_check(hipMemsetAsync(w.peer, 0, (size_t)nranks * 4, stream), "emulated status"));
+                step(hip_check(hipMemsetAsync(w.peer, 0, (size_t)2 * nranks * 4, stream), "emulated status"));
                 if (fail_rank != rank && fail_rank < nranks && fail_it >= 0)
                     step(hip_check(hipMemsetAsync(w.peer + fail_rank, 0x01, 4, stream), "emulated peer status"));
                 step(hip_check(hipMemcpyAsync(w.peer + rank, own_status, 4, hipMemcpyDeviceToDevice, stream),
                                "emulated status"));
+                if (pair_status)
+                    step(hip_check(hipMemcpyAsync(w.peer + nranks + rank, pair_status, 4, hipMemcpyDeviceToDevice,
+                                                  stream), "emulated pair status"));
             }
             if (err == MBRL_OK)   // kept for mode 2
                 step(hip_check(hipMemcpyAsync(w.emu_kept + (size_t)it * nranks * slot, w.gathered, nranks * slot * 4,
@@ -2560,28 +2614,38 @@ static int plan_sharded_body(const mbrl_mlp_shape* shape, const void* packed, co
     }
     if ((rc = hip_check(hipGetLastError(), "sharded plan launch"))) return rc;
     if (nranks == 1) return MBRL_OK;   // no peers: enqueue only, as mbrl_cem_plan
-    // the peers' status words (gathered with the last iteration's costs): one copy behind the plan's
-    // last launch and one stream synchronisation
+    // the peers' status and pair status words (gathered with the last iteration's costs): one copy
+    // behind the plan's last launch and one stream synchronisation
     static thread_local unsigned* peer_host = nullptr;
     static thread_local int peer_cap = 0;
-    if (peer_cap < nranks) {
+    if (peer_cap < 2 * nranks) {
         if (peer_host) (void)hipHostFree(peer_host);
         peer_host = nullptr;
         peer_cap = 0;
-        if ((rc = hip_check(hipHostMalloc(reinterpret_cast<void**>(&peer_host), (size_t)nranks * 4), "hipHostMalloc")))
+        if ((rc = hip_check(hipHostMalloc(reinterpret_cast<void**>(&peer_host), (size_t)2 * nranks * 4),
+                            "hipHostMalloc")))
             return rc;
-        peer_cap = nranks;
+        peer_cap = 2 * nranks;
     }
-    if ((rc = hip_check(hipMemcpyAsync(peer_host, w.peer, (size_t)nranks * 4, hipMemcpyDeviceToHost, stream),
+    if ((rc = hip_check(hipMemcpyAsync(peer_host, w.peer, (size_t)2 * nranks * 4, hipMemcpyDeviceToHost, stream),
                         "peer status copy")))
         return rc;
     if ((rc = hip_check(hipStreamSynchronize(stream), "plan synchronise"))) return rc;
     std::string failed;
-    for (int r = 0; r < nranks; ++r)
+    bool pair_timeout = false;
+    for (int r = 0; r < nranks; ++r) {
         if (peer_host[r] && r != rank) failed += (failed.empty() ? "" : ", ") + std::to_string(r);
+        if (peer_host[nranks + r]) pair_timeout = true;
+    }
     if (!failed.empty())
         return fail(MBRL_EPEER, "plan_sharded: rank(s) %s failed during this plan (each returns its own error); "
                                 "this rank's outputs are void", failed.c_str());
+    // a column-split hand-off timed out on some rank (its tile's costs were invalid): every rank sees
+    // the same gathered words, so every rank runs the plan again, without pairs (same bits)
+    if (pair_timeout && allow_pairs)
+        return plan_sharded_body(shape, packed, norm, cost, s0_in, p, comm, nranks, rank, mu, sigma, actions_out,
+                                 states_out, cost_hist, returns_hist, elite_hist, rollout_events, workspace, ws_bytes,
+                                 stream, false);
     return MBRL_OK;
 }
 

@@ -177,3 +177,18 @@ def test_sharded_plan_with_the_split_update_forced_both_ways():
     for split in (1, 2):
         for rank in (0, 7):
             _assert_same(_emulated_mode(prob, st, s0, 8, rank, 1, update_split=split), ref, ("split", split, rank))
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_a_timed_out_pair_handoff_redoes_the_plan_without_pairs(mode):
+    """With peers the sharded plan checks its column-split pair launches once, after the plan (the pair
+    status word gathered with the last iteration's costs) instead of a gated redo launch behind every
+    pair launch. A hand-off that times out (MBRL_OPT_DEBUG_PAIR_ABORT = 1: the pair kernel gives up at
+    once) sends every rank through the plan again on 8-candidate tiles: the result is still the
+    single-GPU plan, bit for bit (walker N = 16384 at G = 8: 2048 candidates per rank, pairs)."""
+    prob, st, s0 = _problem(4, 16384, 30)
+    ref = _single(prob, st, s0)
+    _emulated_mode(prob, st, s0, 8, 0, 1)   # keeps the gathered costs for mode 2
+    for rank in (0, 5):
+        got = _emulated_mode(prob, st, s0, 8, rank, mode, debug_pair_abort=1)
+        _assert_same(got, ref, ("pair abort", mode, rank))
