@@ -354,6 +354,46 @@ def train_line(dev, W=512, epochs=50):
                 steps=steps)
 
 
+def rank_projection(dev, cfg_id, world, n_total, plans, warmup, allowances_us=(10.0, 25.0, 40.0)):
+    """One rank's real share of a `world`-GPU plan, timed on this GPU: under
+    the library's timing emulation (MBRL_OPT_SHARD_EMULATE = 2) mbrl_cem_plan_sharded runs exactly rank
+    world-1's work -- its shard's rollout, the update over ALL n_total candidates with K = n_total/10,
+    its own draw, the trajectory -- and fills the other ranks' slots of the all-gather from the costs a
+    mode-1 plan kept (one launch per iteration). The result is checked bit-identical to the single-GPU
+    plan first. The all-gather itself cannot run on one GPU: its time is an assumption, reported at
+    each value of `allowances_us` per iteration."""
+    from mbrl_amd import CEMPlanner, _lib, fused, planners, synthetic
+    p = synthetic.make_problem(cfg_id)
+    cfg = p["cfg"]
+    md, cd = fused.describe(p["model"], p["cost"], dev)
+    prob = fused.device_problem(md, cd, dev)
+    kw = dict(num_candidates=n_total, num_elites=n_total // 10, num_iterations=ITERATIONS, seed=p["rng_seed"],
+              device=dev)
+    st = CEMPlanner._settings(p["sample_action"], cfg["H"], kw)
+    st_rec = CEMPlanner._settings(p["sample_action"], cfg["H"], dict(kw, record=True))
+    s0 = p["s0"].cpu().float()
+    rank = world - 1
+    ref = planners._cem_fused_single(prob, s0.to(dev), st_rec)
+    with _lib.option("shard_emulate", 1):
+        planners._cem_sharded_native(prob, s0.to(dev), st_rec, world, 0, comm=None)
+    with _lib.option("shard_emulate", 2):
+        got = planners._cem_sharded_native(prob, s0.to(dev), st_rec, world, rank, comm=None)
+        same = all(torch.equal(torch.as_tensor(got[k]).cpu(), torch.as_tensor(ref[k]).cpu())
+                   for k in ("elites", "mu", "sigma", "actions", "states"))
+        for _ in range(warmup):
+            planners._cem_sharded_native(prob, s0, st, world, rank, comm=None)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(plans):
+            planners._cem_sharded_native(prob, s0, st, world, rank, comm=None)
+        torch.cuda.synchronize(dev)
+        ms = (time.perf_counter() - t0) / plans * 1e3
+    return dict(gpus=world, rank=rank, candidates_total=n_total, candidates_per_rank=n_total // world,
+                elites=n_total // 10, rank_ms_per_plan=ms, bit_identical_to_single_gpu_plan=same,
+                allgather_us_assumed=list(allowances_us),
+                rank_ms_with_allgather={f"{a:g}us": ms + ITERATIONS * a / 1e3 for a in allowances_us})
+
+
 def parity_sample(prob, res, n=256):
     from oracle import cem as ocem
     from oracle.philox import cem_actions
@@ -597,6 +637,27 @@ def main():
             plan_gpu_ms=timed.plan_gpu_ms if world > 1 else plan_gpu_ms,
             rollout_avg_launch_ms=h_rollout_s * 1e3,
             rollout_frac=h_flop / h_rollout_s / 1e12 / PEAK_FP32_MFMA_TFLOPS)
+    if rank == 0 and world == 1 and not args.no_strong and not args.strong and args.config == 3:
+        # the 8-GPU figures projected from one GPU: one rank's real work timed under the library's timing
+        # emulation, with an assumed all-gather time (rank_projection): walker N=16384 split over 8
+        # (strong, BASELINE configs[3]) against the walker single-GPU plan of `strong`, and the headline
+        # weak-scaled to 8 GPUs (4096 per GPU, N = 32768, K = 3276 on every rank) against this line
+        proj = {}
+        wk = rank_projection(dev, 4, 8, 16384, plans=args.steps, warmup=args.warmup)
+        t1 = out["strong"]["ms_per_step"]
+        wk["single_gpu_ms_per_plan"] = t1
+        wk["projected_speedup"] = {k: t1 / v for k, v in wk["rank_ms_with_allgather"].items()}
+        proj["walker_strong_8"] = wk
+        hw = rank_projection(dev, 3, 8, 8 * cfg["N"], plans=args.steps, warmup=args.warmup)
+        t1 = out["ms_per_step"]
+        hw["single_gpu_ms_per_plan"] = t1
+        hw["projected_weak_efficiency"] = {k: t1 / v for k, v in hw["rank_ms_with_allgather"].items()}
+        hw["projected_value_8gpu"] = {k: ITERATIONS * 8 * cfg["N"] * H / (v * 1e-3)
+                                      for k, v in hw["rank_ms_with_allgather"].items()}
+        proj["cheetah_weak_8"] = hw
+        proj["note"] = ("projections on ONE GPU: a rank's own work under MBRL_OPT_SHARD_EMULATE=2 (DESIGN.md §5), "
+                        "the all-gather's time assumed; the measured multi-GPU line is the driver's SCALE run")
+        out["projection_8gpu"] = proj
     if rank == 0 and world == 1 and not args.no_train:   # (single-GPU runs only: no rank waits on it)
         out["train"] = train_line(dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -68,3 +68,67 @@ def test_one_thread_two_streams_in_flight():
             outs.append(_plan(prob, 2048, return_device=True))
     torch.cuda.synchronize()
     assert all(_same(o, ref) for o in outs)
+
+
+def test_training_beside_plans_on_another_stream():
+    """the fused training step's bounded in-launch waits assume its workgroups are
+    co-resident; plans with cross-workgroup kernels (column-split pairs, the cooperative trajectory) on
+    another stream can hold CUs. Training on one thread and stream while another thread plans: the
+    plans equal the plan made alone, and training either equals training alone bit for bit or raises
+    the status word's RuntimeError -- it never returns wrong parameters silently."""
+    import numpy as np
+    from mbrl_amd import data, models, synthetic
+    prob = synthetic.make_problem(3)
+    ref_plan = _plan(prob, 2048)
+
+    def make():
+        rng = np.random.Generator(np.random.PCG64(5))
+        rolls = []
+        for _ in range(6):
+            st = rng.standard_normal((201, 17)).astype(np.float32)
+            rolls.append(data.Rollout(states=list(torch.from_numpy(st)), observations=list(torch.from_numpy(st)),
+                                      actions=list(torch.from_numpy(rng.uniform(-1, 1, (200, 6)).astype(np.float32))),
+                                      rewards=list(torch.from_numpy(rng.standard_normal(200).astype(np.float32)))))
+        ds = data.TransitionsDataset(rollouts=rolls)
+        ds.set_data_mode("state_only")
+        torch.manual_seed(0)
+        m = models.Model(17, 6, hidden_units=512).to(DEV)
+        return m, ds, torch.optim.Adam(m.parameters(), lr=1e-3)
+
+    def train(m, ds, opt):
+        np.random.seed(3)
+        m.train_model(ds, opt, batch_size=512, num_epochs=10)
+        torch.cuda.synchronize()
+        return [p.detach().cpu().clone() for p in m.parameters()]
+
+    alone = train(*make())
+    out, errors, plans = {}, [], []
+
+    def trainer():
+        try:
+            with torch.cuda.stream(torch.cuda.Stream(DEV)):
+                out["params"] = train(*make())
+        except RuntimeError as e:
+            out["raised"] = str(e)
+        except Exception as e:          # pragma: no cover
+            errors.append(repr(e))
+
+    def planner():
+        try:
+            with torch.cuda.stream(torch.cuda.Stream(DEV)):
+                for _ in range(20):
+                    plans.append(_plan(prob, 2048))
+        except Exception as e:          # pragma: no cover
+            errors.append(repr(e))
+
+    threads = [threading.Thread(target=trainer), threading.Thread(target=planner)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=300)
+    assert not errors, errors
+    assert plans and all(_same(p, ref_plan) for p in plans)
+    if "raised" in out:
+        assert "bounded wait timed out" in out["raised"], out["raised"]
+    else:
+        assert all(torch.equal(a, b) for a, b in zip(out["params"], alone))
