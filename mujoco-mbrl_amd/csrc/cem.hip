@@ -590,40 +590,11 @@ __device__ __forceinline__ void select_reg_body(const float* __restrict__ costs,
         for (int j = 0; j < KPT; ++j)
             if (j < nv) atomicAdd(&wide[(key[j] >> wshift) & wmask], 1u);
         __syncthreads();
-        // the bucket search by wave 0 alone (one barrier): lane l sums bins [32 l, 32 l + 32), a wave
-        // scan finds the lane holding the kk-th key, and that lane walks its 32 bins
-        if (wave == 0) {
-            typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-            const u4* wl4 = reinterpret_cast<const u4*>(wide + 32 * lane);
-            uint32_t lsum = 0;
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const u4 v = wl4[q];
-                lsum += (v[0] + v[1]) + (v[2] + v[3]);
-            }
-            uint32_t incl = lsum;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t y = __shfl_up(incl, o, 64);
-                if (lane >= o) incl += y;
-            }
-            uint32_t b = incl - lsum;
-            if (b < kk && incl >= kk) {
-                bool found = false;
-#pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    const u4 v = wl4[q];
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        if (!found && b + v[i] >= kk) {
-                            sel[0] = (uint32_t)(32 * lane + 4 * q + i); sel[1] = b; sel[2] = v[i];
-                            found = true;
-                        }
-                        b += v[i];
-                    }
-                }
-            }
-        }
+        const uint32_t h0 = wide[2 * tid], h1 = wide[2 * tid + 1];
+        uint32_t tot;
+        const uint32_t b0 = block_exclusive_scan(h0 + h1, scan_ws, &tot);
+        if (b0 < kk && b0 + h0 >= kk) { sel[0] = 2u * tid; sel[1] = b0; sel[2] = h0; }
+        else if (b0 + h0 < kk && b0 + h0 + h1 >= kk) { sel[0] = 2u * tid + 1u; sel[1] = b0 + h0; sel[2] = h1; }
         __syncthreads();
         prefix |= sel[0] << wshift;
         mask |= wmask << wshift;
