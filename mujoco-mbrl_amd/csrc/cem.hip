@@ -587,8 +587,8 @@ __device__ __forceinline__ void select_reg_body(const float* __restrict__ costs,
         const int wb = min(SEL_WIDE_BITS, rem), wshift = rem - wb;
         const uint32_t wmask = (1u << wb) - 1u;
 #pragma unroll
-        for (int j = 0; j < KPT; ++j)
-            if (j < nv) atomicAdd(&wide[(key[j] >> wshift) & wmask], 1u);
+        for (int j = 0; j < KPT; ++j)   // (keys past N into a dummy bin: no branch per key)
+            atomicAdd(&wide[j < nv ? (key[j] >> wshift) & wmask : SEL_WIDE_BINS + SEL_LIST + 1], 1u);
         __syncthreads();
         const uint32_t h0 = wide[2 * tid], h1 = wide[2 * tid + 1];
         uint32_t tot;
@@ -704,85 +704,74 @@ __device__ __forceinline__ void select_reg_body(const float* __restrict__ costs,
     CSTAMP(4);
     // prefix = the K-th smallest key; the elites are every key below it and the first kk keys equal to
     // it in candidate order. An elite's place in that order is (keys below it before it) + min(equal
-    // keys before it, kk). Keys past N are all ones and follow every real key in the order, so they
-    // can only tie with a K-th key of all ones after the kk real ones: no validity test is needed here.
+    // keys before it, kk) -- below K by construction. Keys past N are all ones and follow every real key
+    // in the order, so they can only tie with a K-th key of all ones after the kk real ones: no validity
+    // test is needed here. Counts are packed (below << 16 | equal; N <= 32768, so neither half carries)
+    // and kept in VALU registers; one conditional store per key is the only branch (the scalar unit,
+    // shared by the CU's 16 waves, was the bottleneck of a ballot-per-key compaction).
     auto below = [&](uint64_t b) {   // set bits of b in lanes before this one
         return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
     };
+    auto cnt2 = [&](uint32_t k) { return ((uint32_t)(k < prefix) << 16) | (uint32_t)(k == prefix); };
     constexpr int VW = KPT >= 4 ? 4 : 1;   // keys of one lane that are adjacent in the order
     const int vw = vec ? VW : 1;
-    uint32_t wl = 0, we = 0;   // this wave's keys below / equal to the prefix
+    {
+        uint32_t c = 0;
 #pragma unroll
-    for (int j = 0; j < KPT; ++j) {
-        wl += (uint32_t)__popcll(__ballot(key[j] < prefix));
-        we += (uint32_t)__popcll(__ballot(key[j] == prefix));
+        for (int j = 0; j < KPT; ++j) c += cnt2(key[j]);
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o, 64);
+        if (lane == 0) scan_ws[wave] = c;   // this wave's keys below / equal to the prefix, packed
     }
-    if (lane == 0) scan_ws[wave] = (wl << 16) | we;   // N <= 32768: neither half carries
     __syncthreads();
-    uint32_t before = 0;
-    for (int w = 0; w < wave; ++w) before += scan_ws[w];
-    uint32_t lt_b = before >> 16, eq_b = before & 0xFFFFu;   // keys of earlier groups (wave-uniform)
+    uint32_t run = 0;   // packed counts of the keys before this wave's current group (wave-uniform)
+    for (int w = 0; w < wave; ++w) run += scan_ws[w];
 #pragma unroll
     for (int g = 0; g < KPT / VW; ++g) {
-        // the group's keys in candidate order: lanes ascending, and inside a lane its vw keys
-        uint64_t bl[VW], be[VW], beany = 0;
-#pragma unroll
-        for (int i = 0; i < VW; ++i) {
-            bl[i] = __ballot(key[VW * g + i] < prefix);
-            be[i] = __ballot(key[VW * g + i] == prefix);
-            beany |= be[i];
-        }
+        // the group's keys in candidate order: lanes ascending, and inside a lane its vw keys (one
+        // group of VW keys per lane), or VW groups of single keys (vw = 1)
         if (vw == VW) {
-            uint32_t ll = 0;   // this group's keys below the prefix in lanes before this one
-#pragma unroll
-            for (int i = 0; i < VW; ++i) ll += below(bl[i]);
-            if (beany == 0) {
-                // (the usual group: no key equal to the K-th, so every elite here is below it)
-                const uint32_t base = lt_b + ll + min(eq_b, kk);
-                uint32_t own = 0;
-#pragma unroll
-                for (int i = 0; i < VW; ++i)
-                    if (key[VW * g + i] < prefix) {
-                        if (base + own < (uint32_t)K) emit(base + own, idx(VW * g + i));
-                        ++own;
-                    }
-            } else {
-                uint32_t le = 0;
-#pragma unroll
-                for (int i = 0; i < VW; ++i) le += below(be[i]);
-#pragma unroll
-                for (int i = 0; i < VW; ++i) {
-                    const uint32_t k = key[VW * g + i];
-                    if (k < prefix) {
-                        const uint32_t pos = lt_b + ll + min(eq_b + le, kk);
-                        if (pos < (uint32_t)K) emit(pos, idx(VW * g + i));
-                        ++ll;
-                    } else if (k == prefix) {
-                        if (eq_b + le < kk && lt_b + ll + eq_b + le < (uint32_t)K)
-                            emit(lt_b + ll + eq_b + le, idx(VW * g + i));
-                        ++le;
-                    }
-                }
-            }
+            // counts of the group's keys in lanes before this one: ballots and mbcnt (VALU only)
+            uint64_t bl[VW], be[VW], beany = 0;
+            uint32_t before = 0, tot = 0;
 #pragma unroll
             for (int i = 0; i < VW; ++i) {
-                lt_b += (uint32_t)__popcll(bl[i]);
-                eq_b += (uint32_t)__popcll(be[i]);
+                bl[i] = __ballot(key[VW * g + i] < prefix);
+                be[i] = __ballot(key[VW * g + i] == prefix);
+                beany |= be[i];
+                before += below(bl[i]) << 16;
+                tot += (uint32_t)__popcll(bl[i]) << 16;
             }
-        } else {
-            // single keys (VW keys of a lane are VW separate groups of the order): group by group
+            if (beany != 0) {   // (rare: keys equal to the K-th in this group)
+#pragma unroll
+                for (int i = 0; i < VW; ++i) {
+                    before += below(be[i]);
+                    tot += (uint32_t)__popcll(be[i]);
+                }
+            }
+            uint32_t at = run + before;
 #pragma unroll
             for (int i = 0; i < VW; ++i) {
                 const uint32_t k = key[VW * g + i];
-                const uint32_t l1 = below(bl[i]), e1 = below(be[i]);
-                if (k < prefix) {
-                    const uint32_t pos = lt_b + l1 + min(eq_b + e1, kk);
-                    if (pos < (uint32_t)K) emit(pos, idx(VW * g + i));
-                } else if (k == prefix) {
-                    if (eq_b + e1 < kk && lt_b + l1 + eq_b + e1 < (uint32_t)K) emit(lt_b + l1 + eq_b + e1, idx(VW * g + i));
-                }
-                lt_b += (uint32_t)__popcll(bl[i]);
-                eq_b += (uint32_t)__popcll(be[i]);
+                const uint32_t lb = at >> 16, eb = at & 0xFFFFu;
+                const bool lt = k < prefix, eq = k == prefix;
+                const bool take = lt || (eq && eb < kk);
+                const uint32_t pos = lb + (lt ? min(eb, kk) : eb);
+                if (take) emit(pos, idx(VW * g + i));
+                at += cnt2(k);
+            }
+            run += tot;
+        } else {
+#pragma unroll
+            for (int i = 0; i < VW; ++i) {
+                const uint32_t k = key[VW * g + i];
+                const bool lt = k < prefix, eq = k == prefix;
+                const uint64_t bl = __ballot(lt), be = __ballot(eq);
+                const uint32_t lb = (run >> 16) + below(bl), eb = (run & 0xFFFFu) + below(be);
+                const bool take = lt || (eq && eb < kk);
+                const uint32_t pos = lb + (lt ? min(eb, kk) : eb);
+                if (take) emit(pos, idx(VW * g + i));
+                run += ((uint32_t)__popcll(bl) << 16) + (uint32_t)__popcll(be);
             }
         }
     }
