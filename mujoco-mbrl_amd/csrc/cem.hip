@@ -501,7 +501,23 @@ __device__ __forceinline__ void select_reg_body(const float* __restrict__ costs,
     // idx rises with j, so this lane's keys below N are its first nv (one register, not KPT predicates)
     const int nv = vec ? 4 * max(0, min(KPT / 4, (N - lv + 255) / 256)) : max(0, min(KPT, (N - ls + 63) / 64));
     uint32_t key[KPT];
-    {
+    if (vec && E == 1) {
+        // (the plans' usual case) branch-free: every lane loads from a valid address -- its own group,
+        // or the row's first where it has none -- and the keys past N are set to all ones by a select
+        constexpr int G4 = KPT >= 4 ? KPT / 4 : 1;
+        f4 v[G4];
+#pragma unroll
+        for (int g = 0; g < G4; ++g) v[g] = *reinterpret_cast<const f4*>(costs + (lv + 256 * g < N ? lv + 256 * g : 0));
+        if (returns_out) {
+#pragma unroll
+            for (int g = 0; g < G4; ++g)
+                if (lv + 256 * g < N) *reinterpret_cast<f4*>(returns_out + lv + 256 * g) = v[g];
+        }
+#pragma unroll
+        for (int g = 0; g < G4; ++g)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) key[4 * g + i] = 4 * g < nv ? order_key(v[g][i], nan_policy) : 0xFFFFFFFFu;
+    } else {
         float r[KPT];   // every load in flight before the first use; the member sum keeps its order
         if (vec) {
             constexpr int G4 = KPT >= 4 ? KPT / 4 : 1;
