@@ -1,0 +1,15 @@
+# r06: selection with the branch-free load -- tests, select / update timing and stamps -- then the rank
+# projections and the bench line
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r06g
+rm -rf $O; mkdir -p $O
+timeout -k 10 700 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_fused_update.py tests/test_gpu_sharded_emul.py tests/test_gpu_m8.py tests/test_gpu_fuzz.py -k "select or fused or split or timing or peer or pair or full_size or fuzz or m8" > $O/t.log 2>&1 || { echo TESTS FAILED; tail -30 $O/t.log; exit 1; }
+tail -1 $O/t.log
+timeout -k 10 120 python tools/select_bench.py > $O/select_bench.json 2>&1 || exit 1
+for n in 4096 16384 32768; do timeout -k 10 120 python tools/select_stamps.py $n 130 250 >> $O/select_stamps.txt 2>&1 || exit 1; done
+timeout -k 10 120 python tools/update_bench.py --stamps > $O/update_bench.jsonl 2>&1 || exit 1
+timeout -k 10 300 python tools/rank_split.py --mode strong --configs 4 --gpus 8 --out $O/strong_c4g8.jsonl > $O/rs.log 2>&1 || exit 1
+timeout -k 10 300 python tools/rank_split.py --mode weak --configs 3 --gpus 8 --out $O/weak_c3g8.jsonl >> $O/rs.log 2>&1 || exit 1
+timeout -k 10 500 python bench.py > $O/bench.log 2>&1 || { tail -5 $O/bench.log; exit 1; }
+tail -1 $O/bench.log > $O/bench.json
