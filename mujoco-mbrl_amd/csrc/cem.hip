@@ -14,6 +14,7 @@
 #include <set>
 #include <string>
 #include <tuple>
+#include <type_traits>
 #include <vector>
 #include <algorithm>
 
@@ -332,28 +333,59 @@ __global__ void pack_bias_kernel(const float* __restrict__ b, int n_real, int n_
 // ------------------------------------------------------------------------------------------------
 // Block scan helper (exclusive), blockDim.x multiple of 64, <= 1024
 // ------------------------------------------------------------------------------------------------
+// Cross-lane moves as DPP operand modifiers (VALU, no LDS round trip as __shfl's ds_bpermute takes).
+// Lanes whose source is outside the row, or whose row is not in ROWS, read 0.
+template <int CTRL, int ROWS = 0xF>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xF, false);
+}
+
+// Inclusive prefix sum over the wave: in-row shifts by 1, 2, 4, 8, then the row broadcasts.
+__device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t x) {
+    x += dpp_u32<0x111>(x);        // row_shr:1
+    x += dpp_u32<0x112>(x);        // row_shr:2
+    x += dpp_u32<0x114>(x);        // row_shr:4
+    x += dpp_u32<0x118>(x);        // row_shr:8
+    x += dpp_u32<0x142, 0xA>(x);   // row_bcast:15 (rows 1 and 3)
+    x += dpp_u32<0x143, 0xC>(x);   // row_bcast:31 (rows 2 and 3)
+    return x;
+}
+
+// Wave minimum / maximum: every lane of a row gets the row's (quad swaps, half mirror, mirror), then the
+// four rows' through readlane.
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
+    x = min(x, dpp_u32<0xB1>(x));
+    x = min(x, dpp_u32<0x4E>(x));
+    x = min(x, dpp_u32<0x141>(x));
+    x = min(x, dpp_u32<0x140>(x));
+    return min(min((uint32_t)__builtin_amdgcn_readlane((int)x, 0), (uint32_t)__builtin_amdgcn_readlane((int)x, 16)),
+               min((uint32_t)__builtin_amdgcn_readlane((int)x, 32), (uint32_t)__builtin_amdgcn_readlane((int)x, 48)));
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
+    x = max(x, dpp_u32<0xB1>(x));
+    x = max(x, dpp_u32<0x4E>(x));
+    x = max(x, dpp_u32<0x141>(x));
+    x = max(x, dpp_u32<0x140>(x));
+    return max(max((uint32_t)__builtin_amdgcn_readlane((int)x, 0), (uint32_t)__builtin_amdgcn_readlane((int)x, 16)),
+               max((uint32_t)__builtin_amdgcn_readlane((int)x, 32), (uint32_t)__builtin_amdgcn_readlane((int)x, 48)));
+}
+
+// The lanes' predicate as a 64-bit mask straight from the compare (HIP's __ballot goes through a
+// select and a second compare).
+__device__ __forceinline__ uint64_t wave_ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+
 __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* lds_waves, uint32_t* total) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    uint32_t x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
+    const uint32_t x = wave_inclusive_scan(v);
     if (lane == 63) lds_waves[wave] = x;
     __syncthreads();
-    if (wave == 0) {
-        uint32_t w = lane < nw ? lds_waves[lane] : 0u;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(w, o, 64);
-            if (lane >= o) w += y;
-        }
-        if (lane < nw) lds_waves[lane] = w;  // inclusive wave prefix
+    uint32_t before = 0, all = 0;   // every wave sums the wave totals itself (broadcast reads)
+    for (int w = 0; w < nw; ++w) {
+        const uint32_t t = lds_waves[w];
+        before += w < wave ? t : 0u;
+        all += t;
     }
-    __syncthreads();
-    const uint32_t before = wave > 0 ? lds_waves[wave - 1] : 0u;
-    *total = lds_waves[nw - 1];
+    *total = all;
     __syncthreads();
     return before + x - v;
 }
@@ -372,9 +404,21 @@ __device__ unsigned long long* g_cem_stamps;
         if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0 && g_cem_stamps)                \
             g_cem_stamps[k] = __builtin_amdgcn_s_memrealtime();                                       \
     } while (0)
+// ... and per workgroup of the split update's two kernels (iteration i, kernel q, workgroup b, point k):
+// start, after the selection / the sums, end (mbrl_diag_set_cem_wg_stamps, tools/split_stamps.py).
+__device__ unsigned long long* g_cem_wg_stamps;   // [8][2][1024][4]
+#define WGSTAMP(q, k)                                                                                     \
+    do {                                                                                                  \
+        if (threadIdx.x == 0 && blockIdx.x < 1024 && g_cem_wg_stamps)                                     \
+            g_cem_wg_stamps[(((U.iteration & 7) * 2 + (q)) * 1024 + blockIdx.x) * 4 + (k)] =              \
+                __builtin_amdgcn_s_memrealtime();                                                         \
+    } while (0)
 #else
 #define CSTAMP(k) \
     do {          \
+    } while (0)
+#define WGSTAMP(q, k) \
+    do {              \
     } while (0)
 #endif
 
@@ -571,15 +615,19 @@ __device__ __forceinline__ void select_reg_body(const float* __restrict__ costs,
     }
     // leading bits every key shares (block min / max): returns of one plan usually share sign and
     // exponent, so the first digit starts at the first bit in which the keys differ
+    // every key of the wave below N (idx rises with the lane): the passes below skip the per-key test
+    const bool wfull = __builtin_amdgcn_readlane(nv, 63) == KPT;
     uint32_t kmin = 0xFFFFFFFFu, kmax = 0u;
+    if (wfull) {
 #pragma unroll
-    for (int j = 0; j < KPT; ++j)
-        if (j < nv) { kmin = min(kmin, key[j]); kmax = max(kmax, key[j]); }
+        for (int j = 0; j < KPT; ++j) { kmin = min(kmin, key[j]); kmax = max(kmax, key[j]); }
+    } else {
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, o, 64));
-        kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o, 64));
+        for (int j = 0; j < KPT; ++j)
+            if (j < nv) { kmin = min(kmin, key[j]); kmax = max(kmax, key[j]); }
     }
+    kmin = wave_min_u32(kmin);
+    kmax = wave_max_u32(kmax);
     __shared__ uint32_t mm_ws[2][16];
     if (lane == 0) { mm_ws[0][wave] = kmin; mm_ws[1][wave] = kmax; }
     uint32_t* wide = sel_smem + SEL_HIST_WORDS;          // [SEL_WIDE_BINS] the first pass's histogram
@@ -594,6 +642,7 @@ __device__ __forceinline__ void select_reg_body(const float* __restrict__ costs,
     const int lead = kmin == kmax ? 32 : __clz(kmin ^ kmax);   // leading bits every key shares
     uint32_t mask = lead == 0 ? 0u : (lead >= 32 ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> lead));
     uint32_t prefix = kmin & mask, kk = (uint32_t)K;
+    uint32_t eqn = (uint32_t)N;                          // keys equal to prefix once it is resolved
     int rem = 32 - lead;                                 // bits below the shared ones still to resolve
     CSTAMP(1);
     // (1) one wide pass over the first SEL_WIDE_BITS differing bits: 2048 bins, one shared histogram
@@ -602,9 +651,14 @@ __device__ __forceinline__ void select_reg_body(const float* __restrict__ costs,
     if (rem > 0) {
         const int wb = min(SEL_WIDE_BITS, rem), wshift = rem - wb;
         const uint32_t wmask = (1u << wb) - 1u;
+        auto wide_count = [&](auto check) {   // (keys past N into a dummy bin: no branch per key)
 #pragma unroll
-        for (int j = 0; j < KPT; ++j)   // (keys past N into a dummy bin: no branch per key)
-            atomicAdd(&wide[j < nv ? (key[j] >> wshift) & wmask : SEL_WIDE_BINS + SEL_LIST + 1], 1u);
+            for (int j = 0; j < KPT; ++j)
+                atomicAdd(&wide[(!decltype(check)::value || j < nv) ? (key[j] >> wshift) & wmask
+                                                                   : SEL_WIDE_BINS + SEL_LIST + 1], 1u);
+        };
+        if (wfull) wide_count(std::false_type{});
+        else wide_count(std::true_type{});
         __syncthreads();
         const uint32_t h0 = wide[2 * tid], h1 = wide[2 * tid + 1];
         uint32_t tot;
@@ -615,45 +669,52 @@ __device__ __forceinline__ void select_reg_body(const float* __restrict__ costs,
         prefix |= sel[0] << wshift;
         mask |= wmask << wshift;
         kk -= sel[1];
+        const uint32_t bsz = sel[2];   // (a register: wave 0 rewrites sel below)
+        eqn = bsz;
         rem = wshift;
         CSTAMP(2);
         // (2) the bucket's keys (sel[2] of them) into an LDS list: the later passes read it, not the
         // KPT keys of every thread
-        if (rem > 0 && sel[2] <= (uint32_t)SEL_LIST) {
+        if (rem > 0 && bsz <= (uint32_t)SEL_LIST) {
+            auto list_keys = [&](auto check) {
 #pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                const bool pend = j < nv && (key[j] & mask) == prefix;
-                const uint64_t act = __ballot(pend);
-                if (act != 0) {
-                    const int leader = __builtin_ctzll(act);
-                    uint32_t base = 0;
-                    if (lane == leader) base = atomicAdd(list_n, (uint32_t)__popcll(act));
-                    base = (uint32_t)__shfl((int)base, leader, 64);
-                    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
-                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
-                    if (pend) list[base + below] = key[j];
+                for (int j = 0; j < KPT; ++j) {
+                    const bool pend = (!decltype(check)::value || j < nv) && (key[j] & mask) == prefix;
+                    const uint64_t act = wave_ballot(pend);
+                    if (act != 0) {
+                        const int leader = __builtin_ctzll(act);
+                        uint32_t base = 0;
+                        if (lane == leader) base = atomicAdd(list_n, (uint32_t)__popcll(act));
+                        base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
+                        const uint32_t below = __builtin_amdgcn_mbcnt_hi(
+                            (uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+                        if (pend) list[base + below] = key[j];
+                    }
                 }
-            }
+            };
+            if (wfull) list_keys(std::false_type{});
+            else list_keys(std::true_type{});
             listed = true;
             __syncthreads();
             // a bucket of at most 64 keys (the usual case): wave 0 ranks them directly -- the kk-th
             // smallest is the key with (keys below it) < kk <= (keys not above it) -- in place of the
             // remaining 8-bit passes and their barriers
-            if (sel[2] <= 64u) {
-                const uint32_t nb = sel[2];
+            if (bsz <= 64u) {
+                const uint32_t nb = (uint32_t)__builtin_amdgcn_readfirstlane((int)bsz);
                 if (wave == 0) {
                     const uint32_t x = (uint32_t)lane < nb ? list[lane] : 0xFFFFFFFFu;
                     uint32_t lt = 0, le = 0;
-                    for (uint32_t j = 0; j < nb; ++j) {
-                        const uint32_t y = (uint32_t)__shfl((int)x, (int)j, 64);
+                    for (uint32_t j = 0; j < nb; ++j) {   // key j to every lane (readlane: no LDS trip)
+                        const uint32_t y = (uint32_t)__builtin_amdgcn_readlane((int)x, (int)j);
                         lt += y < x;
                         le += y <= x;
                     }
-                    if ((uint32_t)lane < nb && lt < kk && le >= kk) { sel[0] = x; sel[1] = kk - lt; }
+                    if ((uint32_t)lane < nb && lt < kk && le >= kk) { sel[0] = x; sel[1] = kk - lt; sel[2] = le - lt; }
                 }
                 __syncthreads();
                 prefix = sel[0];
                 kk = sel[1];
+                eqn = sel[2];
                 mask = 0xFFFFFFFFu;
                 rem = 0;
             }
@@ -672,11 +733,11 @@ __device__ __forceinline__ void select_reg_body(const float* __restrict__ costs,
         auto count = [&](uint32_t kv, bool valid) {
             const bool pending = valid && (kv & mask) == prefix;
             const uint32_t dig = (kv >> shift) & dmask;
-            const uint64_t act = __ballot(pending);
+            const uint64_t act = wave_ballot(pending);
             if (act != 0) {
                 const int leader = __builtin_ctzll(act);
                 const uint32_t d0 = __shfl(dig, leader, 64);
-                if (__ballot(pending && dig == d0) == act) {   // clustered: one add per wave
+                if (wave_ballot(pending && dig == d0) == act) {   // clustered: one add per wave
                     if (lane == leader) atomicAdd(&hist[buf][wave][d0], (uint32_t)__popcll(act));
                 } else if (pending) {
                     atomicAdd(&hist[buf][wave][dig], 1u);
@@ -696,30 +757,71 @@ __device__ __forceinline__ void select_reg_body(const float* __restrict__ costs,
         if (tid < 256) {
 #pragma unroll
             for (int w = 0; w < 16; ++w) h += hist[buf][w][tid];
-            incl = h;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t y = __shfl_up(incl, o, 64);
-                if (lane >= o) incl += y;
-            }
+            incl = wave_inclusive_scan(h);
             if (lane == 63) scan_ws[wave] = incl;
         }
         __syncthreads();
         if (tid < 256) {
             uint32_t before = incl - h;
             for (int w = 0; w < wave; ++w) before += scan_ws[w];
-            if (before < kk && before + h >= kk) { sel[0] = (uint32_t)tid; sel[1] = before; }
+            if (before < kk && before + h >= kk) { sel[0] = (uint32_t)tid; sel[1] = before; sel[2] = h; }
         }
         __syncthreads();
         prefix |= sel[0] << shift;
         mask |= dmask << shift;
         kk -= sel[1];
+        eqn = sel[2];
         rem = shift;
         buf ^= 1;
     }
     CSTAMP(4);
     // prefix = the K-th smallest key; the elites are every key below it and the first kk keys equal to
-    // it in candidate order. An elite's place in that order is (keys below it before it) + min(equal
+    // it in candidate order.
+    // (a) Every key equal to it is an elite (eqn == kk: the K-th key unique, or all its ties taken --
+    // the usual case): the elites are the keys <= prefix. Their flags go to an LDS bitmap in candidate
+    // order (a lane's four adjacent keys are a nibble, eight lanes' nibbles one word, OR-ed by DPP;
+    // or one ballot per key, two words, in the single-key layout), and thread t emits the set bits of
+    // word t after a block scan of the words' counts: ~3 VALU ops per key instead of ~20.
+    // Keys past N are all ones; prefix is not (checked), so they are never flagged.
+    if (eqn == kk && prefix != 0xFFFFFFFFu) {
+        uint32_t* bits = &hist[0][0][0];   // [32 KPT] (the 8-bit passes are done with it)
+        auto ballot_words = [&]() {
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                const uint64_t m = wave_ballot(key[j] <= prefix);
+                if (lane < 2) bits[((ls - lane + 64 * j) >> 5) + lane] = (uint32_t)(m >> (32 * lane));
+            }
+        };
+        if constexpr (KPT >= 4) {
+            if (vec) {
+#pragma unroll
+                for (int g = 0; g < KPT / 4; ++g) {
+                    uint32_t nib = 0;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) nib |= (uint32_t)(key[4 * g + i] <= prefix) << i;
+                    nib <<= 4 * (lane & 7);
+                    nib |= dpp_u32<0xB1>(nib);    // quad_perm [1,0,3,2]
+                    nib |= dpp_u32<0x4E>(nib);    // quad_perm [2,3,0,1]
+                    nib |= dpp_u32<0x141>(nib);   // row_half_mirror: the other quad of the eight
+                    if ((lane & 7) == 0) bits[(lv + 256 * g) >> 5] = nib;
+                }
+            } else {
+                ballot_words();
+            }
+        } else {
+            ballot_words();
+        }
+        __syncthreads();
+        uint32_t m = tid < (N + 31) >> 5 ? bits[tid] : 0u, tot;
+        uint32_t pos = block_exclusive_scan((uint32_t)__popc(m), scan_ws, &tot);
+        while (m != 0u) {
+            emit(pos++, 32 * tid + __builtin_ctz(m));
+            m &= m - 1u;
+        }
+        CSTAMP(5);
+        return;
+    }
+    // (b) Otherwise an elite's place in that order is (keys below it before it) + min(equal
     // keys before it, kk) -- below K by construction. Keys past N are all ones and follow every real key
     // in the order, so they can only tie with a K-th key of all ones after the kk real ones: no validity
     // test is needed here. Counts are packed (below << 16 | equal; N <= 32768, so neither half carries)
@@ -735,9 +837,8 @@ __device__ __forceinline__ void select_reg_body(const float* __restrict__ costs,
         uint32_t c = 0;
 #pragma unroll
         for (int j = 0; j < KPT; ++j) c += cnt2(key[j]);
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o, 64);
-        if (lane == 0) scan_ws[wave] = c;   // this wave's keys below / equal to the prefix, packed
+        c = wave_inclusive_scan(c);
+        if (lane == 63) scan_ws[wave] = c;   // this wave's keys below / equal to the prefix, packed
     }
     __syncthreads();
     uint32_t run = 0;   // packed counts of the keys before this wave's current group (wave-uniform)
@@ -752,8 +853,8 @@ __device__ __forceinline__ void select_reg_body(const float* __restrict__ costs,
             uint32_t before = 0, tot = 0;
 #pragma unroll
             for (int i = 0; i < VW; ++i) {
-                bl[i] = __ballot(key[VW * g + i] < prefix);
-                be[i] = __ballot(key[VW * g + i] == prefix);
+                bl[i] = wave_ballot(key[VW * g + i] < prefix);
+                be[i] = wave_ballot(key[VW * g + i] == prefix);
                 beany |= be[i];
                 before += below(bl[i]) << 16;
                 tot += (uint32_t)__popcll(bl[i]) << 16;
@@ -782,7 +883,7 @@ __device__ __forceinline__ void select_reg_body(const float* __restrict__ costs,
             for (int i = 0; i < VW; ++i) {
                 const uint32_t k = key[VW * g + i];
                 const bool lt = k < prefix, eq = k == prefix;
-                const uint64_t bl = __ballot(lt), be = __ballot(eq);
+                const uint64_t bl = wave_ballot(lt), be = wave_ballot(eq);
                 const uint32_t lb = (run >> 16) + below(bl), eb = (run & 0xFFFFu) + below(be);
                 const bool take = lt || (eq && eb < kk);
                 const uint32_t pos = lb + (lt ? min(eb, kk) : eb);
@@ -1130,6 +1231,7 @@ __global__ void __launch_bounds__(1024) cem_select_regen_kernel(const UpdateArgs
     uint32_t* work = usmem + ((K + 3) & ~3) + 2 * a4;
     int64_t* eo = (U.elite_out && lead) ? U.elite_out : nullptr;
     float* ro = (U.returns_out && lead) ? U.returns_out : nullptr;
+    WGSTAMP(0, 0);
     for (int d = threadIdx.x; d < a; d += 1024) {
         row[d] = U.mu[t * a + d];
         row[a4 + d] = U.sigma[t * a + d];
@@ -1140,8 +1242,13 @@ __global__ void __launch_bounds__(1024) cem_select_regen_kernel(const UpdateArgs
                              if (eo) eo[pos] = n;
                          });
     __syncthreads();   // eidx complete (and the row staged)
+    WGSTAMP(0, 1);
     const int KS = (K + S - 1) / S, e0 = min(K, j * KS), e1 = min(K, e0 + KS);
     regen_elites(t, eidx, e0, e1, U.seed, U.iteration, row, row + a4, U.lo, U.hi, a, U.ael + (size_t)t * K * a);
+#ifdef MBRL_STAMPS
+    __syncthreads();
+    WGSTAMP(0, 2);
+#endif
 }
 
 __global__ void __launch_bounds__(1024) cem_refit_draw_kernel(const UpdateArgs U) {
@@ -1151,6 +1258,7 @@ __global__ void __launch_bounds__(1024) cem_refit_draw_kernel(const UpdateArgs U
     const int K = U.K, a = U.a, a4 = (a + 3) & ~3;
     float* next = fsmem;                  // [2][a4] mu', sigma' of row t
     float* work = fsmem + 2 * a4;         // refit_rows' layout: [K][a] elites, partials, mean, mu / sigma
+    WGSTAMP(1, 0);
     const float* src = U.ael + (size_t)t * K * a;
     for (int i = threadIdx.x; i < K * a; i += 1024) work[i] = src[i];
     refit_stage_row(t, work, U.mu, U.sigma, a, K);
@@ -1159,7 +1267,12 @@ __global__ void __launch_bounds__(1024) cem_refit_draw_kernel(const UpdateArgs U
     refit_sums(t, work, U.lo, U.hi, a, K, U.alpha, U.oma, w ? U.mu_out : nullptr, w ? U.sigma_out : nullptr,
                (w && U.fin_mu) ? U.fin_mu : nullptr, (w && U.fin_sigma) ? U.fin_sigma : nullptr,
                (w && U.fin_actions) ? U.fin_actions : nullptr, U.next_actions ? next : nullptr);
+    WGSTAMP(1, 1);
     if (U.next_actions) update_draw(U, t, j, S, 0, 0u, next);
+#ifdef MBRL_STAMPS
+    __syncthreads();
+    WGSTAMP(1, 2);
+#endif
 }
 
 // The plan's first launch: workgroup (t * S + j, b) sets row t of problem b's distribution to
@@ -1674,7 +1787,10 @@ static bool update_split(const UpdateArgs& U, int B) {
 static int update_split_impl(const UpdateArgs& U, int kpt, hipStream_t stream) {
     // workgroups per row: the draw's slices, and at least ~256 workgroups in all for the regeneration
     const int Sd = U.next_actions ? draw_slices(U.H, 1, U.draw_n, U.a) : 1;
-    const int S = std::max(Sd, std::max(1, 256 / U.H));
+    int S = std::max(Sd, std::max(1, 256 / U.H));
+#ifdef MBRL_STAMPS
+    if (const char* e = getenv("MBRL_DIAG_SPLIT_S")) S = std::max(Sd, atoi(e));   // (diagnostic A/B)
+#endif
     const int a4 = (U.a + 3) & ~3;
     const size_t lds_a = ((((size_t)U.K + 3) & ~(size_t)3) + 2 * a4 + (size_t)sel_words(kpt)) * 4;
     const size_t lds_b = (2 * a4 + refit_rows_floats(U.a, U.K)) * 4;
@@ -2375,6 +2491,10 @@ __global__ void emu_gather_kernel(const float* __restrict__ local, const float* 
     const size_t total = (size_t)G * slot, lo = (size_t)rank * slot;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x)
         gathered[i] = (i >= lo && i < lo + slot) ? local[i - lo] : kept[i];
+#ifdef MBRL_STAMPS
+    if (threadIdx.x == 0 && g_cem_wg_stamps)   // (diagnostic) a workgroup's end, last writer wins
+        g_cem_wg_stamps[8 * 2 * 1024 * 4 - 1] = __builtin_amdgcn_s_memrealtime();
+#endif
     if (blockIdx.x == 0)
         for (int r = threadIdx.x; r < G; r += blockDim.x) {
             peer[r] = r == rank ? *own_status : 0u;
@@ -2688,6 +2808,9 @@ int mbrl_cem_plan_sharded(const mbrl_mlp_shape* shape, const void* packed, const
 #ifdef MBRL_STAMPS
 int mbrl_diag_set_cem_stamps(void* buf) {
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(mbrl::g_cem_stamps), &buf, sizeof(buf));
+}
+int mbrl_diag_set_cem_wg_stamps(void* buf) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(mbrl::g_cem_wg_stamps), &buf, sizeof(buf));
 }
 #endif
 

@@ -161,13 +161,14 @@ def test_select_matches_stable_argsort_with_ties_nan_and_signed_zero():
         assert int(am[0]) == ocem.rs_argmin(r), N
 
 
-@pytest.mark.parametrize("N", [1024, 4096, 16384, 32768])
+@pytest.mark.parametrize("N", [1024, 4096, 16384, 32768, 4094, 16381])
 def test_select_fuzz_distributions(N):
     """The register-resident selection (wide 11-bit first pass, the bucket's keys listed in LDS, 8-bit
-    passes over the list or over every key when the bucket is too large, one packed compaction scan)
-    against NumPy's stable order on distributions that exercise each branch: plan-like returns in one
-    binade, a narrow cluster (the K-th bucket large), heavy ties, NaN- and signed-zero-heavy sets, a
-    wide spread over binades, all-equal keys; K from 1 to N."""
+    passes over the list or over every key when the bucket is too large; the bitmap compaction when
+    every key equal to the K-th is an elite, the packed-count compaction when ties are cut) against
+    NumPy's stable order on distributions that exercise each branch: plan-like returns in one binade, a
+    narrow cluster (the K-th bucket large), heavy ties, NaN- and signed-zero-heavy sets, a wide spread
+    over binades, all-equal keys; K from 1 to N; N not a multiple of 4 for the single-key layout."""
     from mbrl_amd import fused
     rng = np.random.default_rng(N)
     dists = [lambda: rng.uniform(130, 250, N), lambda: rng.uniform(120, 120.01, N),
