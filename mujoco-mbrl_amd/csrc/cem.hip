@@ -639,9 +639,17 @@ __device__ __forceinline__ void select_reg_body(const float* __restrict__ costs,
     __syncthreads();
 #pragma unroll
     for (int w = 0; w < 16; ++w) { kmin = min(kmin, mm_ws[0][w]); kmax = max(kmax, mm_ws[1][w]); }
-    const int lead = kmin == kmax ? 32 : __clz(kmin ^ kmax);   // leading bits every key shares
+    // keys relative to the smallest (order kept: every key is >= kmin, no wrap): the passes then
+    // resolve the bits of (key - kmin), so the wide pass's 2048 bins span [kmin, kmax] whatever bit
+    // boundaries the range straddles (plan returns of one binade sit in a few % of its mantissa range:
+    // with bins over the bits below the shared ones, walker's K-th bucket held 200-500 keys, now ~10)
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) key[j] -= kmin;
+    const uint32_t kpad = 0xFFFFFFFFu - kmin;            // keys past N (all ones before the shift)
+    const uint32_t range = kmax - kmin;
+    const int lead = range == 0 ? 32 : __clz(range);     // leading bits every shifted key shares (zero)
     uint32_t mask = lead == 0 ? 0u : (lead >= 32 ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> lead));
-    uint32_t prefix = kmin & mask, kk = (uint32_t)K;
+    uint32_t prefix = 0u, kk = (uint32_t)K;
     uint32_t eqn = (uint32_t)N;                          // keys equal to prefix once it is resolved
     int rem = 32 - lead;                                 // bits below the shared ones still to resolve
     CSTAMP(1);
@@ -782,8 +790,8 @@ __device__ __forceinline__ void select_reg_body(const float* __restrict__ costs,
     // order (a lane's four adjacent keys are a nibble, eight lanes' nibbles one word, OR-ed by DPP;
     // or one ballot per key, two words, in the single-key layout), and thread t emits the set bits of
     // word t after a block scan of the words' counts: ~3 VALU ops per key instead of ~20.
-    // Keys past N are all ones; prefix is not (checked), so they are never flagged.
-    if (eqn == kk && prefix != 0xFFFFFFFFu) {
+    // Keys past N are kpad, the largest shifted key; prefix is not (checked), so they are never flagged.
+    if (eqn == kk && prefix != kpad) {
         uint32_t* bits = &hist[0][0][0];   // [32 KPT] (the 8-bit passes are done with it)
         auto ballot_words = [&]() {
 #pragma unroll
@@ -822,8 +830,8 @@ __device__ __forceinline__ void select_reg_body(const float* __restrict__ costs,
         return;
     }
     // (b) Otherwise an elite's place in that order is (keys below it before it) + min(equal
-    // keys before it, kk) -- below K by construction. Keys past N are all ones and follow every real key
-    // in the order, so they can only tie with a K-th key of all ones after the kk real ones: no validity
+    // keys before it, kk) -- below K by construction. Keys past N are kpad and follow every real key
+    // in the order, so they can only tie with a K-th key of kpad after the kk real ones: no validity
     // test is needed here. Counts are packed (below << 16 | equal; N <= 32768, so neither half carries)
     // and kept in VALU registers; one conditional store per key is the only branch (the scalar unit,
     // shared by the CU's 16 waves, was the bottleneck of a ballot-per-key compaction).
@@ -980,11 +988,21 @@ __global__ void refit_kernel(const float* __restrict__ aelite, int a, int K, flo
 constexpr int REFIT_THREADS = 1024;
 constexpr size_t REFIT_LDS_MAX = 96 * 1024;
 
-// LDS floats refit_rows works in: [K][a] elite actions, [nch][a] chunk partials, mean, this row's mu, sigma.
+// The elites' actions in LDS: [K][a] with one spare row after every chunk of ELITE_CHUNK elites, so a
+// chunk starts 33 a floats after the previous one and the chunk sums' lanes -- lane (c, d) reads
+// elite 32 c + q, dimension d -- fall on consecutive banks (at 32 a they all shared a bank, ~10-way).
+__host__ __device__ inline int ael_pos(int e, int d, int a) { return (e + e / ELITE_CHUNK) * a + d; }
+__host__ __device__ inline size_t ael_floats(int a, int K) {
+    const size_t nch = (size_t)(K + ELITE_CHUNK - 1) / ELITE_CHUNK;
+    return (((size_t)K + nch) * a + 3) & ~(size_t)3;
+}
+
+// LDS floats refit_rows works in: the elite actions (ael_pos), [nch][a] chunk partials, mean, this
+// row's mu, sigma.
 __host__ __device__ inline size_t refit_rows_floats(int a, int K) {
     const size_t nch = (size_t)(K + ELITE_CHUNK - 1) / ELITE_CHUNK;
     const size_t a4 = ((size_t)a + 3) & ~(size_t)3;
-    return (((size_t)K * a + 3) & ~(size_t)3) + ((nch * a + 3) & ~(size_t)3) + 3 * a4;
+    return ael_floats(a, K) + ((nch * a + 3) & ~(size_t)3) + 3 * a4;
 }
 
 // Row t of the refit (mu, sigma, outputs already offset to the problem; NULL outputs are skipped): eidx
@@ -1000,29 +1018,40 @@ __device__ __forceinline__ void refit_sums(int t, float* smem, float lo, float h
 #pragma clang fp contract(off)
     const int nch = (K + ELITE_CHUNK - 1) / ELITE_CHUNK;
     const int a4 = (a + 3) & ~3;
-    float* ael = smem;                                   // [K][a]
-    float* part = smem + (((size_t)K * a + 3) & ~(size_t)3);   // [nch][a]
+    float* ael = smem;                                   // ael_pos layout
+    float* part = smem + ael_floats(a, K);               // [nch][a]
     float* mean = part + (((size_t)nch * a + 3) & ~(size_t)3);  // [a]
     const float* smu = mean + a4;                               // [2][a]: this step's mu, sigma
     const float* ssg = smu + a4;
-    for (int pass = 0; pass < 2; ++pass) {
+    CSTAMP(8);
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {   // (unrolled: each pass's code has no pass test)
         for (int idx = threadIdx.x; idx < nch * a; idx += blockDim.x) {
             const int c = idx / a, d = idx - (idx / a) * a;
             const int e0 = c * ELITE_CHUNK, n = min(K - e0, ELITE_CHUNK);
             const float md = pass == 1 ? mean[d] : 0.f;
             float v[ELITE_CHUNK];
 #pragma unroll
-            for (int q = 0; q < ELITE_CHUNK; ++q) v[q] = q < n ? ael[(size_t)(e0 + q) * a + d] : 0.f;
-            float acc = 0.f;
+            for (int q = 0; q < ELITE_CHUNK; ++q) v[q] = q < n ? ael[(size_t)(e0 + c + q) * a + d] : 0.f;
+            if (pass == 1)   // the squared deviations first: off the dependent chain of additions
 #pragma unroll
-            for (int q = 0; q < ELITE_CHUNK; ++q) {
-                float x = v[q];
-                if (pass == 1) { const float df = __fadd_rn(x, -md); x = __fmul_rn(df, df); }
-                if (q < n) acc = q == 0 ? x : __fadd_rn(acc, x);
+                for (int q = 0; q < ELITE_CHUNK; ++q) {
+                    const float df = __fadd_rn(v[q], -md);
+                    v[q] = __fmul_rn(df, df);
+                }
+            float acc = v[0];
+            if (n == ELITE_CHUNK) {   // every chunk but the last: 31 dependent additions, no predicate
+#pragma unroll
+                for (int q = 1; q < ELITE_CHUNK; ++q) acc = __fadd_rn(acc, v[q]);
+            } else {
+#pragma unroll
+                for (int q = 1; q < ELITE_CHUNK; ++q)
+                    if (q < n) acc = __fadd_rn(acc, v[q]);
             }
             part[c * a + d] = acc;
         }
         __syncthreads();
+        CSTAMP(9 + 2 * pass);
         if ((int)threadIdx.x < a) {
             const int d = threadIdx.x;
             // the chunk partials in sequence, eight LDS reads in flight at a time (the same additions
@@ -1056,6 +1085,7 @@ __device__ __forceinline__ void refit_sums(int t, float* smem, float lo, float h
             }
         }
         __syncthreads();
+        CSTAMP(10 + 2 * pass);
     }
 }
 
@@ -1064,7 +1094,7 @@ __device__ __forceinline__ void refit_stage_row(int t, float* smem, const float*
                                                 const float* __restrict__ sigma, int a, int K) {
     const int nch = (K + ELITE_CHUNK - 1) / ELITE_CHUNK;
     const int a4 = (a + 3) & ~3;
-    float* musg = smem + (((size_t)K * a + 3) & ~(size_t)3) + (((size_t)nch * a + 3) & ~(size_t)3) + a4;
+    float* musg = smem + ael_floats(a, K) + (((size_t)nch * a + 3) & ~(size_t)3) + a4;
     for (int d = threadIdx.x; d < a; d += blockDim.x) {
         musg[d] = mu[t * a + d];
         musg[a4 + d] = sigma[t * a + d];
@@ -1072,10 +1102,11 @@ __device__ __forceinline__ void refit_stage_row(int t, float* smem, const float*
 }
 
 // Elites [e0, e1)'s actions of row t regenerated from the counter RNG (bit-identical to the sampled
-// ones): into dst[e][a] (LDS or global). smu / ssg: this row's mu, sigma.
+// ones): into dst, [e][a] (global: the split update's hand-off) or in the ael_pos layout (LDS, padded).
+// smu / ssg: this row's mu, sigma.
 __device__ __forceinline__ void regen_elites(int t, const uint32_t* eidx, int e0, int e1, uint64_t seed, int iteration,
                                              const float* smu, const float* ssg, float lo, float hi, int a,
-                                             float* __restrict__ dst) {
+                                             float* __restrict__ dst, bool padded) {
 #pragma clang fp contract(off)
     const int G = (a + 3) >> 2;
     for (int idx = threadIdx.x; idx < (e1 - e0) * G; idx += blockDim.x) {
@@ -1085,7 +1116,7 @@ __device__ __forceinline__ void regen_elites(int t, const uint32_t* eidx, int e0
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int d = 4 * g + j;
-            if (d < a) dst[(size_t)e * a + d] = cem_action(smu[d], ssg[d], z[j], lo, hi);
+            if (d < a) dst[padded ? (size_t)ael_pos(e, d, a) : (size_t)e * a + d] = cem_action(smu[d], ssg[d], z[j], lo, hi);
         }
     }
 }
@@ -1098,11 +1129,11 @@ __device__ __forceinline__ void refit_rows(int t, const uint32_t* eidx, float* s
                                            float* next) {
     const int nch = (K + ELITE_CHUNK - 1) / ELITE_CHUNK;
     const int a4 = (a + 3) & ~3;
-    const float* musg = smem + (((size_t)K * a + 3) & ~(size_t)3) + (((size_t)nch * a + 3) & ~(size_t)3) + a4;
+    const float* musg = smem + ael_floats(a, K) + (((size_t)nch * a + 3) & ~(size_t)3) + a4;
     // stage every global operand first (all loads in flight together), then compute from LDS
     refit_stage_row(t, smem, mu, sigma, a, K);
     __syncthreads();
-    regen_elites(t, eidx, 0, K, seed, iteration, musg, musg + a4, lo, hi, a, smem);
+    regen_elites(t, eidx, 0, K, seed, iteration, musg, musg + a4, lo, hi, a, smem, true);
     __syncthreads();
     refit_sums(t, smem, lo, hi, a, K, alpha, oma, mu_out, sigma_out, fin_mu, fin_sigma, fin_actions, next);
 }
@@ -1244,7 +1275,7 @@ __global__ void __launch_bounds__(1024) cem_select_regen_kernel(const UpdateArgs
     __syncthreads();   // eidx complete (and the row staged)
     WGSTAMP(0, 1);
     const int KS = (K + S - 1) / S, e0 = min(K, j * KS), e1 = min(K, e0 + KS);
-    regen_elites(t, eidx, e0, e1, U.seed, U.iteration, row, row + a4, U.lo, U.hi, a, U.ael + (size_t)t * K * a);
+    regen_elites(t, eidx, e0, e1, U.seed, U.iteration, row, row + a4, U.lo, U.hi, a, U.ael + (size_t)t * K * a, false);
 #ifdef MBRL_STAMPS
     __syncthreads();
     WGSTAMP(0, 2);
@@ -1260,9 +1291,32 @@ __global__ void __launch_bounds__(1024) cem_refit_draw_kernel(const UpdateArgs U
     float* work = fsmem + 2 * a4;         // refit_rows' layout: [K][a] elites, partials, mean, mu / sigma
     WGSTAMP(1, 0);
     const float* src = U.ael + (size_t)t * K * a;
-    for (int i = threadIdx.x; i < K * a; i += 1024) work[i] = src[i];
+    const int n = K * a, ca = ELITE_CHUNK * a;   // flat index f = e a + d lands at f + (f / ca) a (ael_pos)
+    if ((n & 3) == 0) {
+        // 16-byte loads, up to four per thread in flight before the first LDS store
+        typedef float f4 __attribute__((ext_vector_type(4)));
+        const f4* s4 = reinterpret_cast<const f4*>(src);
+        const int n4 = n >> 2;
+        for (int i0 = threadIdx.x; i0 < n4; i0 += 4 * 1024) {
+            f4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (i0 + u * 1024 < n4) v[u] = s4[i0 + u * 1024];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (i0 + u * 1024 < n4)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int f = 4 * (i0 + u * 1024) + k;
+                        work[f + (f / ca) * a] = v[u][k];
+                    }
+        }
+    } else {
+        for (int f = threadIdx.x; f < n; f += 1024) work[f + (f / ca) * a] = src[f];
+    }
     refit_stage_row(t, work, U.mu, U.sigma, a, K);
     __syncthreads();
+    WGSTAMP(1, 3);
     const bool w = j == 0;   // slice 0 of the row writes its refit
     refit_sums(t, work, U.lo, U.hi, a, K, U.alpha, U.oma, w ? U.mu_out : nullptr, w ? U.sigma_out : nullptr,
                (w && U.fin_mu) ? U.fin_mu : nullptr, (w && U.fin_sigma) ? U.fin_sigma : nullptr,

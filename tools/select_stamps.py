@@ -19,7 +19,7 @@ def main():
     lib = _lib.load()
     lib.mbrl_diag_set_cem_stamps.argtypes = [ctypes.c_void_p]
     dev = torch.device("cuda", 0)
-    buf = torch.zeros(8, dtype=torch.int64, device=dev)
+    buf = torch.zeros(16, dtype=torch.int64, device=dev)
     assert lib.mbrl_diag_set_cem_stamps(buf.data_ptr()) == 0
     lo, hi = (float(sys.argv[2]), float(sys.argv[3])) if len(sys.argv) > 3 else (120.0, 123.0)
     costs = torch.from_numpy(np.random.default_rng(0).uniform(lo, hi, N).astype(np.float32)).to(dev).view(1, N)

@@ -30,7 +30,9 @@ def main():
     dev = torch.device("cuda", 0)
     lib = _lib.load()
     buf = torch.zeros(8 * 2 * 1024 * 4, dtype=torch.int64, device=dev)
+    sel = torch.zeros(16, dtype=torch.int64, device=dev)   # workgroup 0: selection (CSTAMP 0-5), sums (8-12)
     lib.mbrl_diag_set_cem_wg_stamps.argtypes = [ctypes.c_void_p]
+    lib.mbrl_diag_set_cem_stamps.argtypes = [ctypes.c_void_p]
     p = synthetic.make_problem(cid)
     cfg = p["cfg"]
     N = cfg["N"]
@@ -41,23 +43,35 @@ def main():
     s0 = p["s0"].cpu().float()
     with _lib.option("shard_emulate", 1):
         planners._cem_sharded_native(prob, s0.to(dev), st, world, 0, comm=None)
-    rows = []
+    rows, sels = [], []
     with _lib.option("shard_emulate", 2):
         for k in range(12):
             assert lib.mbrl_diag_set_cem_wg_stamps(buf.data_ptr() if k >= 2 else None) == 0
+            assert lib.mbrl_diag_set_cem_stamps(sel.data_ptr() if k >= 2 else None) == 0
             buf.zero_()
+            sel.zero_()
             torch.cuda.synchronize()
             planners._cem_sharded_native(prob, s0, st, world, world - 1, comm=None)
             torch.cuda.synchronize()
             if k >= 2:
                 rows.append(buf.view(8, 2, 1024, 4).cpu().numpy().copy())
+                sels.append(sel.cpu().numpy().copy())
     assert lib.mbrl_diag_set_cem_wg_stamps(None) == 0
+    assert lib.mbrl_diag_set_cem_stamps(None) == 0
+    d = np.diff(np.array(sels, dtype=np.float64)[:, :6], axis=1).mean(0) / 100.0
+    sel_phases = dict(zip(["load+minmax", "wide", "list", "passes", "compaction"], [round(float(x), 2) for x in d]))
+    sm = np.array(sels, dtype=np.float64)[:, 8:13]
+    d = np.diff(sm, axis=1).mean(0) / 100.0
+    sums_phases = dict(zip(["pass0 chunk sums", "pass0 sequential", "pass1 chunk sums", "pass1 sequential"],
+                           [round(float(x), 2) for x in d]))
+    print(json.dumps({"last_iteration_selection_phases_us": sel_phases,
+                      "last_iteration_sums_phases_us (refit_draw workgroup 0)": sums_phases}), flush=True)
     out = dict(config=cid, workload=cfg["name"], N=N, gpus=world, rank=world - 1, plans=len(rows), iterations={},
-               split_s=os.environ.get("MBRL_DIAG_SPLIT_S", "auto"))
-    names = (("select_regen", "select", "regen"), ("refit_draw", "sums", "draw"))
+               split_s=os.environ.get("MBRL_DIAG_SPLIT_S", "auto"), last_iteration_selection_phases_us=sel_phases)
+    names = (("select_regen", "select", "regen", None), ("refit_draw", "sums", "draw", "staged"))
     for it in range(ITERATIONS):
         per = {}
-        for q, (kern, p1, p2) in enumerate(names):
+        for q, (kern, p1, p2, p3) in enumerate(names):
             acc = []
             for r in rows:
                 st_ = r[it, q]
@@ -69,11 +83,15 @@ def main():
                 acc.append(dict(wgs=int(used.sum()), start_spread=s[:, 0].max() - t0,
                                 p1_med=np.median(s[:, 1] - s[:, 0]), p1_max=(s[:, 1] - s[:, 0]).max(),
                                 p2_med=np.median(s[:, 2] - s[:, 1]) if (s[:, 2] > 0).all() else None,
+                                p3_med=np.median(s[:, 3] - s[:, 0]) if (s[:, 3] > 0).all() else None,
                                 span=(s[:, 2].max() if (s[:, 2] > 0).all() else s[:, 1].max()) - t0))
             if acc:
                 per[kern] = {"wgs": acc[0]["wgs"]}
                 for key, label in (("start_spread", "start_spread"), ("p1_med", p1 + "_median"),
-                                   ("p1_max", p1 + "_max"), ("p2_med", p2 + "_median"), ("span", "span")):
+                                   ("p1_max", p1 + "_max"), ("p2_med", p2 + "_median"), ("span", "span"),
+                                   ("p3_med", (p3 or "") + "_from_start_median")):
+                    if key == "p3_med" and p3 is None:
+                        continue
                     vals = [a[key] for a in acc if a[key] is not None]
                     per[kern][label] = round(float(np.mean(vals)), 2) if vals else None
         gaps = []

@@ -28,7 +28,7 @@ def main():
     cases = [tuple(args[i:i + 5]) for i in range(0, len(args), 5)] if args else CASES
     dev = torch.device("cuda", 0)
     lib = _lib.load()
-    buf = torch.zeros(8, dtype=torch.int64, device=dev)
+    buf = torch.zeros(16, dtype=torch.int64, device=dev)
     if STAMPS:
         lib.mbrl_diag_set_cem_stamps.argtypes = [ctypes.c_void_p]
         assert lib.mbrl_diag_set_cem_stamps(buf.data_ptr()) == 0
