@@ -15,7 +15,8 @@ import re
 import sys
 
 FAMILIES = [("rollout", r"rollout(_m8|_split)?_kernel<"), ("update", r"cem_update_kernel"), ("sample", r"sample_kernel"),
-            ("select", r"select(_reg)?_kernel"), ("refit", r"refit|gather_elites|finalize_kernel"),
+            ("select", r"select(_reg)?_kernel|select_regen"), ("allgather_emulated", r"emu_gather_kernel"),
+            ("refit", r"refit|gather_elites|finalize_kernel"),
             ("trajectory", r"traj(_coop|_reg)?_kernel|member_mean"), ("fill", r"fill2_kernel|cem_init_kernel"),
             ("memset", r"fillBuffer|[Mm]emset")]
 

@@ -10,8 +10,10 @@ single-GPU plan before timing.
 
 Per row: the rank's wall time per plan (host s0 in, host results out, as bench.py's plans) and its device
 span; the single-GPU plan of the full N timed the same way beside it; projected speed-up =
-T1 / (T_rank + I * allgather_us). The all-gather itself cannot run on one GPU: its allowance is an
-ASSUMPTION, reported at 10 / 25 / 40 us per iteration (RCCL all-gather of 8 x 16-64 KB over xGMI).
+T1 / (T_rank + I * allgather_us), both timed without timing events (ms_per_plan; the evented loop that
+gives the device span and the rollout launch is ms_per_plan_with_events). The all-gather itself cannot
+run on one GPU: its allowance is an ASSUMPTION, reported at 10 / 25 / 40 us per iteration (RCCL
+all-gather of 8 x 16-64 KB over xGMI).
 
   strong rows (--mode strong): config N split over G ranks (walker N=16384: 2048 per rank at G=8).
   weak rows   (--mode weak):   n_local per rank fixed (cheetah 4096), N = G * n_local, K = N/10.
@@ -60,8 +62,15 @@ def _time(fn, plans, warmup):
     torch.cuda.synchronize()
     span = float(np.mean([a.elapsed_time(b) for a, b in pev]))
     roll = float(np.mean([r[MEASURED_IT][0].elapsed_time(r[MEASURED_IT][1]) for r in rev]))
-    return dict(ms_per_plan=elapsed / plans * 1e3, plan_gpu_ms=span, wall_median_ms=float(np.median(walls)) * 1e3,
-                rollout_ms=roll)
+    # the same plans again with no timing events (each record leaves the GPU idle a few us, 4 per plan
+    # above): the production-like figure the projection uses, for T1 and the rank alike
+    t0 = time.perf_counter()
+    for k in range(plans):
+        fn(None, None)
+    torch.cuda.synchronize()
+    plain = (time.perf_counter() - t0) / plans * 1e3
+    return dict(ms_per_plan=plain, ms_per_plan_with_events=elapsed / plans * 1e3, plan_gpu_ms=span,
+                wall_median_ms=float(np.median(walls)) * 1e3, rollout_ms=roll)
 
 
 def row(cid, world, n_total, plans, warmup, dev, mode):
@@ -103,6 +112,10 @@ def row(cid, world, n_total, plans, warmup, dev, mode):
         base = out["t1_ms"] = t_one["ms_per_plan"]   # the full-N plan on one GPU
         out["projected_speedup"] = {f"{a:g}us": base / (t_rank["ms_per_plan"] + ITERATIONS * a / 1e3)
                                     for a in ALLGATHER_US}
+        if "ms_per_plan_with_events" in t_one:
+            out["projected_speedup_with_events"] = {
+                f"{a:g}us": t_one["ms_per_plan_with_events"] / (t_rank["ms_per_plan_with_events"] + ITERATIONS * a / 1e3)
+                for a in ALLGATHER_US}
     else:
         # weak: per-GPU work fixed; efficiency = (single GPU at n_local) / (rank's plan at N = G n_local)
         out["projected_weak_efficiency"] = {}
