@@ -1733,15 +1733,11 @@ static int traj_impl(const Geometry& g, const void* packed, const mbrl_norm* nor
         const int hop = g_opt[MBRL_OPT_TRAJ_HOP].load(std::memory_order_relaxed);
         T.hop_mode = hop == 0 ? kTrajHopDefault : hop - 1;
         const hipError_t err = launch_traj_coop(T, g.E, xchg, status, stream);
-        if (err != hipErrorCooperativeLaunchTooLarge) {   // too large: the grid cannot be co-resident
-            int rc = hip_check(err, "trajectory launch");
-            if (rc) return rc;
-            // The cooperative kernel needs its P*E workgroups co-resident; if a hand-off ever timed
-            // out (another process holding CUs, say) it set `status` and gave up. The single-workgroup
-            // kernel then recomputes the states; otherwise its E workgroups read the status word and exit.
-            T.gate = status;
-        }
-        T.debug_abort = 0;
+        // The cooperative kernel needs its P*E workgroups co-resident; if a hand-off ever times out
+        // (another process holding CUs, say) it sets `status` and each member's workgroup 0 computes
+        // the states alone inside the same launch (traj.hip traj_single).
+        if (err != hipErrorCooperativeLaunchTooLarge) return hip_check(err, "trajectory launch");
+        T.debug_abort = 0;   // too large: the grid cannot be co-resident; one workgroup per member
     }
     return hip_check(launch_traj(T, g.E, stream), "trajectory launch");
 }
@@ -1841,10 +1837,7 @@ static bool update_split(const UpdateArgs& U, int B) {
 static int update_split_impl(const UpdateArgs& U, int kpt, hipStream_t stream) {
     // workgroups per row: the draw's slices, and at least ~256 workgroups in all for the regeneration
     const int Sd = U.next_actions ? draw_slices(U.H, 1, U.draw_n, U.a) : 1;
-    int S = std::max(Sd, std::max(1, 256 / U.H));
-#ifdef MBRL_STAMPS
-    if (const char* e = getenv("MBRL_DIAG_SPLIT_S")) S = std::max(Sd, atoi(e));   // (diagnostic A/B)
-#endif
+    const int S = std::max(Sd, std::max(1, 256 / U.H));
     const int a4 = (U.a + 3) & ~3;
     const size_t lds_a = ((((size_t)U.K + 3) & ~(size_t)3) + 2 * a4 + (size_t)sel_words(kpt)) * 4;
     const size_t lds_b = (2 * a4 + refit_rows_floats(U.a, U.K)) * 4;

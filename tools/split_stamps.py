@@ -5,7 +5,8 @@ done, end) and cem_refit_draw_kernel (start, sums done, end), from rank 7's emul
 spread, median / max of each phase, and the span (first start to last end); the gap from the emulated
 gather's end to the selection's first start (the launch of cem_select_regen_kernel, last iteration) and
 from the selection's last end to the sums' first start (the kernel boundary between the two). Times in us
-(100 MHz clock). MBRL_DIAG_SPLIT_S=S (diagnostic library only) overrides the workgroups per row.
+(100 MHz clock). (profiles/r06/split_stamps_j_s*.jsonl came from a diagnostic build whose S -- the
+workgroups per row -- an environment variable overrode; that override is gone.)
 Usage: python tools/split_stamps.py [config] [gpus]"""
 import json
 import os
@@ -67,7 +68,7 @@ def main():
     print(json.dumps({"last_iteration_selection_phases_us": sel_phases,
                       "last_iteration_sums_phases_us (refit_draw workgroup 0)": sums_phases}), flush=True)
     out = dict(config=cid, workload=cfg["name"], N=N, gpus=world, rank=world - 1, plans=len(rows), iterations={},
-               split_s=os.environ.get("MBRL_DIAG_SPLIT_S", "auto"), last_iteration_selection_phases_us=sel_phases)
+               last_iteration_selection_phases_us=sel_phases)
     names = (("select_regen", "select", "regen", None), ("refit_draw", "sums", "draw", "staged"))
     for it in range(ITERATIONS):
         per = {}
@@ -106,7 +107,7 @@ def main():
                     if r.reshape(-1)[-1] > 0]
             per["gap_gather_end_to_select_start"] = round(float(np.mean(lead)), 2) if lead else None
         out["iterations"][it] = per
-        print(json.dumps({"iteration": it, "split_s": out["split_s"], **per}), flush=True)
+        print(json.dumps({"iteration": it, **per}), flush=True)
     print(json.dumps(out))
 
 
