@@ -1733,11 +1733,18 @@ static int traj_impl(const Geometry& g, const void* packed, const mbrl_norm* nor
         const int hop = g_opt[MBRL_OPT_TRAJ_HOP].load(std::memory_order_relaxed);
         T.hop_mode = hop == 0 ? kTrajHopDefault : hop - 1;
         const hipError_t err = launch_traj_coop(T, g.E, xchg, status, stream);
-        // The cooperative kernel needs its P*E workgroups co-resident; if a hand-off ever times out
-        // (another process holding CUs, say) it sets `status` and each member's workgroup 0 computes
-        // the states alone inside the same launch (traj.hip traj_single).
-        if (err != hipErrorCooperativeLaunchTooLarge) return hip_check(err, "trajectory launch");
-        T.debug_abort = 0;   // too large: the grid cannot be co-resident; one workgroup per member
+        if (err != hipErrorCooperativeLaunchTooLarge) {   // too large: the grid cannot be co-resident
+            int rc = hip_check(err, "trajectory launch");
+            if (rc) return rc;
+            // The cooperative kernel needs its P*E workgroups co-resident; if a hand-off ever timed
+            // out (another process holding CUs, say) it set `status` and gave up. The single-workgroup
+            // kernel then recomputes the states; otherwise its E workgroups read the status word and exit.
+            // (Run inside the cooperative launch instead, the fallback's registers raised the kernel's
+            // from 107 to 161 VGPRs: one workgroup per CU, and two plans' trajectories on one XCD then
+            // waited on each other until the hand-off timeout.)
+            T.gate = status;
+        }
+        T.debug_abort = 0;
     }
     return hip_check(launch_traj(T, g.E, stream), "trajectory launch");
 }

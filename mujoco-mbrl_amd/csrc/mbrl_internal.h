@@ -321,7 +321,8 @@ struct TrajArgs {
     const float* s0;
     const float* actions;  // [H][a]
     float* states_out;     // [E][H][s]
-    int debug_abort;       // traj_coop_kernel: give up at once (tests of its in-launch fallback; MBRL_DEBUG_TRAJ_ABORT)
+    const unsigned* gate;  // traj_kernel: when non-NULL, run only if *gate != 0 (the coop kernel gave up)
+    int debug_abort;       // traj_coop_kernel: give up at once (tests of the fallback; MBRL_DEBUG_TRAJ_ABORT)
     int prezeroed;         // traj_coop_kernel: the granules and status word were zeroed by the plan's first launch
     // traj_coop_kernel hand-off placement (MBRL_OPT_TRAJ_HOP): 0 = a (P, E) grid, agent-scope (sc1)
     // granules; 1 = a 1-D grid of 8 P workgroups where member e's P share blockIdx % 8 == e (one XCD

@@ -28,12 +28,11 @@ __device__ __forceinline__ float wave_sum64(float v) {
     return v;
 }
 
-// y[0..Wpad) = relu(W x + b) with W^T [in][Wpad]; x in LDS, part scratch [KS][Wpad] (NT threads).
-template <int NT>
+// y[0..Wpad) = relu(W x + b) with W^T [in][Wpad]; x in LDS, part scratch [KS][Wpad].
 __device__ __forceinline__ void traj_dense_relu(const float* __restrict__ wt, const float* __restrict__ bias,
                                                 int in, int Wpad, const float* x, float* part, float* y) {
     const int G4 = Wpad / 4;
-    const int KS = NT / G4;                      // NT = 1024: Wpad <= 1024 -> KS >= 4; NT = 512: Wpad <= 512
+    const int KS = TRAJ_THREADS / G4;            // Wpad <= 1024 -> KS >= 4
     const int tid = threadIdx.x;
     const int g4 = tid % G4, ks = tid / G4;
     const int per = (in + KS - 1) / KS;
@@ -48,7 +47,7 @@ __device__ __forceinline__ void traj_dense_relu(const float* __restrict__ wt, co
     }
     *reinterpret_cast<f32x4*>(part + ks * Wpad + 4 * g4) = acc;
     __syncthreads();
-    for (int n = tid; n < Wpad; n += NT) {
+    for (int n = tid; n < Wpad; n += TRAJ_THREADS) {
         float v = bias[n];
         for (int j = 0; j < KS; ++j) v += part[j * Wpad + n];
         y[n] = fmaxf(v, 0.0f);
@@ -56,16 +55,11 @@ __device__ __forceinline__ void traj_dense_relu(const float* __restrict__ wt, co
     __syncthreads();
 }
 
-// LDS floats of traj_single: layer input, layer output, partials, the output layer's result.
-__host__ __device__ inline size_t traj_single_floats(int s, int a, int Wpad) {
-    const int K0 = s + a, xdim = K0 > Wpad ? K0 : Wpad;
-    return (size_t)((xdim + 3) & ~3) + Wpad + 4096 + ((s + 3) & ~3);
-}
-
-// Member e's whole trajectory on one workgroup of NT threads: traj_kernel, and the cooperative
-// kernel's own fallback (its workgroup 0 of the member, when a hand-off timed out).
-template <int NT>
-__device__ void traj_single(const TrajArgs& A, int e, float* smem) {
+__global__ void __launch_bounds__(TRAJ_THREADS) traj_kernel(const TrajArgs A) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    // fallback behind the cooperative kernel: only when that one gave up (status word set)
+    if (A.gate != nullptr && *A.gate == 0u) return;
+    const int e = blockIdx.x;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int K0 = A.s + A.a;
     const int xdim = K0 > A.Wpad ? K0 : A.Wpad;
@@ -77,34 +71,34 @@ __device__ void traj_single(const TrajArgs& A, int e, float* smem) {
     const float* bias = member + A.bias_off;
     const float* tw = member + A.tw_base;
 
-    for (int d = tid; d < A.s; d += NT) {
+    for (int d = tid; d < A.s; d += TRAJ_THREADS) {
         const float sv = A.s0[d];
         x[d] = A.norm_s ? (sv - A.obs_mean[d]) / A.obs_std[d] : sv;
     }
     for (int t = 0; t < A.H; ++t) {
-        for (int d = tid; d < A.a; d += NT) {
+        for (int d = tid; d < A.a; d += TRAJ_THREADS) {
             const float av = A.actions[t * A.a + d];
             x[A.s + d] = A.norm_a ? (av - A.act_mean[d]) / A.act_std[d] : av;
         }
         __syncthreads();
-        traj_dense_relu<NT>(tw + A.tw_off[0], bias, K0, A.Wpad, x, part, y);
+        traj_dense_relu(tw + A.tw_off[0], bias, K0, A.Wpad, x, part, y);
         float* cur = y;
         float* nxt = x;
         for (int l = 1; l < A.L; ++l) {
-            traj_dense_relu<NT>(tw + A.tw_off[l], bias + l * A.Wpad, A.W, A.Wpad, cur, part, nxt);
+            traj_dense_relu(tw + A.tw_off[l], bias + l * A.Wpad, A.W, A.Wpad, cur, part, nxt);
             float* tmp = cur; cur = nxt; nxt = tmp;
         }
         // output layer: one wave per row n, W row-major
         const float* wo = tw + A.tw_off[A.L];
         const float* bo = bias + A.L * A.Wpad;
-        for (int n = wave; n < A.s; n += NT / 64) {
+        for (int n = wave; n < A.s; n += TRAJ_THREADS / 64) {
             float v = 0.f;
             for (int k = lane; k < A.W; k += 64) v += wo[(size_t)n * A.W + k] * cur[k];
             v = wave_sum64(v);
             if (lane == 0) out[n] = v + bo[n];
         }
         __syncthreads();
-        for (int d = tid; d < A.s; d += NT) {
+        for (int d = tid; d < A.s; d += TRAJ_THREADS) {
             const float sn = A.unnorm_s ? out[d] * A.obs_std[d] + A.obs_mean[d] : out[d];
             A.states_out[((size_t)e * A.H + t) * A.s + d] = sn;
             x[d] = A.norm_s ? (sn - A.obs_mean[d]) / A.obs_std[d] : sn;
@@ -114,13 +108,10 @@ __device__ void traj_single(const TrajArgs& A, int e, float* smem) {
     }
 }
 
-__global__ void __launch_bounds__(TRAJ_THREADS) traj_kernel(const TrajArgs A) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    traj_single<TRAJ_THREADS>(A, blockIdx.x, smem);
-}
-
 hipError_t launch_traj(const TrajArgs& A, int E, hipStream_t stream) {
-    const size_t lds = traj_single_floats(A.s, A.a, A.Wpad) * sizeof(float);
+    const int K0 = A.s + A.a;
+    const int xdim = K0 > A.Wpad ? K0 : A.Wpad;
+    const size_t lds = ((size_t)((xdim + 3) & ~3) + A.Wpad + 4096 + ((A.s + 3) & ~3)) * sizeof(float);
     hipLaunchKernelGGL(traj_kernel, dim3(E), dim3(TRAJ_THREADS), lds, stream, A);
     return hipGetLastError();
 }
@@ -236,12 +227,8 @@ __global__ void __launch_bounds__(COOP_THREADS) traj_coop_kernel(const TrajArgs 
     const float* tw = member + A.tw_base;
     gu64* xchg = (gu64*)(xchg_all + (size_t)e * 2 * Wp);
 
-    // A timed-out hand-off (or the test hook) sets `status`; the member's workgroup 0 then computes the
-    // whole trajectory alone (traj_single, in its own LDS) and the others exit -- no second launch
-    // stands behind this kernel on every plan.
     if (A.debug_abort) {                       // test hook: behave as a timed-out hand-off
         if (tid == 0) atomicOr(status, 1u);
-        if (p == 0) traj_single<COOP_THREADS>(A, e, smem);
         return;
     }
     // ---- one-time staging ----------------------------------------------------------------------
@@ -325,10 +312,7 @@ __global__ void __launch_bounds__(COOP_THREADS) traj_coop_kernel(const TrajArgs 
             if (lane == 0) l2_flag = same ? 1 : 0;
         }
         __syncthreads();
-        if (abort_flag) {
-            if (p == 0) traj_single<COOP_THREADS>(A, e, smem);
-            return;
-        }
+        if (abort_flag) return;
     } else if (tid == 0) {
         l2_flag = 0;
     }
@@ -396,10 +380,7 @@ __global__ void __launch_bounds__(COOP_THREADS) traj_coop_kernel(const TrajArgs 
             }
             __syncthreads();
             TSTAMP(2);
-            if (abort_flag) {
-                if (p == 0) traj_single<COOP_THREADS>(A, e, smem);
-                return;
-            }
+            if (abort_flag) return;
             float* tmp = cur; cur = nxt; nxt = tmp;
         }
         // output layer (redundant): half-wave g owns rows g + 16 mm; the lane holding a row's sum
@@ -447,9 +428,7 @@ template <int K0R, int SM, int WI>
 static hipError_t launch_coop_variant(const TrajArgs& A_in, int E, u64* xchg, unsigned* status, hipStream_t stream) {
     hipError_t err = ensure_dynamic_lds(reinterpret_cast<const void*>(&traj_coop_kernel<K0R, SM, WI>), 160 * 1024);
     if (err != hipSuccess) return err;
-    // (at least traj_single's footprint: the fallback runs in the same LDS)
-    const size_t lds = std::max(coop_lds(A_in.s, A_in.a, A_in.W, A_in.Wpad, A_in.L, A_in.H, K0R).total,
-                                traj_single_floats(A_in.s, A_in.a, A_in.Wpad) * sizeof(float));
+    const size_t lds = coop_lds(A_in.s, A_in.a, A_in.W, A_in.Wpad, A_in.L, A_in.H, K0R).total;
     const int P = A_in.Wpad / COOP_ROWS;
     if (!grid_fits(reinterpret_cast<const void*>(&traj_coop_kernel<K0R, SM, WI>), COOP_THREADS, lds, P * E))
         return hipErrorCooperativeLaunchTooLarge;

@@ -587,7 +587,7 @@ def test_trajectory_states_match_oracle(cid, H, over):
 @pytest.mark.parametrize("cid,H", [(3, 12), (5, 7)])
 def test_trajectory_fallback_when_the_cooperative_kernel_gives_up(cid, H):
     """MBRL_OPT_DEBUG_TRAJ_ABORT makes the cooperative kernel behave as a timed-out hand-off (it sets
-    the status word); each member's workgroup 0 must then produce the states alone, in the same launch."""
+    the status word and exits); the gated single-workgroup kernel behind it must then produce the states."""
     from mbrl_amd import _lib, fused
     with _lib.option("debug_traj_abort", 1):
         _trajectory_fallback(fused, cid, H)
