@@ -991,10 +991,16 @@ constexpr size_t REFIT_LDS_MAX = 96 * 1024;
 // The elites' actions in LDS: [K][a] with one spare row after every chunk of ELITE_CHUNK elites, so a
 // chunk starts 33 a floats after the previous one and the chunk sums' lanes -- lane (c, d) reads
 // elite 32 c + q, dimension d -- fall on consecutive banks (at 32 a they all shared a bank, ~10-way).
+// The last chunk is padded to 32 rows of -0.0 (ael_pad): x + (-0.0) == x for every x, so every chunk
+// sums 32 values with no per-element predicate and the same bits as a sum over its real elites.
 __host__ __device__ inline int ael_pos(int e, int d, int a) { return (e + e / ELITE_CHUNK) * a + d; }
 __host__ __device__ inline size_t ael_floats(int a, int K) {
     const size_t nch = (size_t)(K + ELITE_CHUNK - 1) / ELITE_CHUNK;
-    return (((size_t)K + nch) * a + 3) & ~(size_t)3;
+    return (nch * (ELITE_CHUNK + 1) * a + 3) & ~(size_t)3;
+}
+__device__ __forceinline__ void ael_pad(float* ael, int a, int K) {
+    const int nch = (K + ELITE_CHUNK - 1) / ELITE_CHUNK, np = nch * ELITE_CHUNK - K;
+    for (int i = threadIdx.x; i < np * a; i += blockDim.x) ael[ael_pos(K + i / a, i % a, a)] = -0.0f;
 }
 
 // LDS floats refit_rows works in: the elite actions (ael_pos), [nch][a] chunk partials, mean, this
@@ -1031,23 +1037,18 @@ __device__ __forceinline__ void refit_sums(int t, float* smem, float lo, float h
             const int e0 = c * ELITE_CHUNK, n = min(K - e0, ELITE_CHUNK);
             const float md = pass == 1 ? mean[d] : 0.f;
             float v[ELITE_CHUNK];
+            const float* src = ael + (e0 + c) * a + d;   // ael_pos(e0, d); the chunk's rows a floats apart
 #pragma unroll
-            for (int q = 0; q < ELITE_CHUNK; ++q) v[q] = q < n ? ael[(size_t)(e0 + c + q) * a + d] : 0.f;
-            if (pass == 1)   // the squared deviations first: off the dependent chain of additions
+            for (int q = 0; q < ELITE_CHUNK; ++q) v[q] = src[q * a];   // (padding rows: -0.0)
+            if (pass == 1)   // the squared deviations first, off the dependent chain; padding stays -0.0
 #pragma unroll
                 for (int q = 0; q < ELITE_CHUNK; ++q) {
                     const float df = __fadd_rn(v[q], -md);
-                    v[q] = __fmul_rn(df, df);
+                    v[q] = q < n ? __fmul_rn(df, df) : -0.0f;
                 }
             float acc = v[0];
-            if (n == ELITE_CHUNK) {   // every chunk but the last: 31 dependent additions, no predicate
 #pragma unroll
-                for (int q = 1; q < ELITE_CHUNK; ++q) acc = __fadd_rn(acc, v[q]);
-            } else {
-#pragma unroll
-                for (int q = 1; q < ELITE_CHUNK; ++q)
-                    if (q < n) acc = __fadd_rn(acc, v[q]);
-            }
+            for (int q = 1; q < ELITE_CHUNK; ++q) acc = __fadd_rn(acc, v[q]);   // 31 dependent additions
             part[c * a + d] = acc;
         }
         __syncthreads();
@@ -1132,6 +1133,7 @@ __device__ __forceinline__ void refit_rows(int t, const uint32_t* eidx, float* s
     const float* musg = smem + ael_floats(a, K) + (((size_t)nch * a + 3) & ~(size_t)3) + a4;
     // stage every global operand first (all loads in flight together), then compute from LDS
     refit_stage_row(t, smem, mu, sigma, a, K);
+    ael_pad(smem, a, K);
     __syncthreads();
     regen_elites(t, eidx, 0, K, seed, iteration, musg, musg + a4, lo, hi, a, smem, true);
     __syncthreads();
@@ -1315,6 +1317,7 @@ __global__ void __launch_bounds__(1024) cem_refit_draw_kernel(const UpdateArgs U
         for (int f = threadIdx.x; f < n; f += 1024) work[f + (f / ca) * a] = src[f];
     }
     refit_stage_row(t, work, U.mu, U.sigma, a, K);
+    ael_pad(work, a, K);
     __syncthreads();
     WGSTAMP(1, 3);
     const bool w = j == 0;   // slice 0 of the row writes its refit
