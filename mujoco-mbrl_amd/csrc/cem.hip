@@ -791,7 +791,9 @@ __device__ __forceinline__ void select_reg_body(const float* __restrict__ costs,
     // or one ballot per key, two words, in the single-key layout), and thread t emits the set bits of
     // word t after a block scan of the words' counts: ~3 VALU ops per key instead of ~20.
     // Keys past N are kpad, the largest shifted key; prefix is not (checked), so they are never flagged.
-    if (eqn == kk && prefix != kpad) {
+    // (From KPT = 8: at 4 keys per lane and fewer the scan and barrier of (a) cost more than (b)'s
+    // per-key work -- 1.35 against 0.76 us at N = 4096.)
+    if (KPT >= 8 && eqn == kk && prefix != kpad) {
         uint32_t* bits = &hist[0][0][0];   // [32 KPT] (the 8-bit passes are done with it)
         auto ballot_words = [&]() {
 #pragma unroll
